@@ -1,0 +1,105 @@
+/* vc_msm.h -- C ABI of the MI355X vector-commitment MSM engine (libvkzg.so).
+ *
+ * This is the drop-in boundary for the reference's hot path. A Rust
+ * `impl VectorCommitment` (reference: /root/reference/vector-commit/src/lib.rs:70-174)
+ * calls these entry points over `extern "C"` in place of `utils::inner_product`
+ * (vector-commit/src/utils.rs:16-19) and of the arithmetic inside `commit` /
+ * `prove_point`; see INTEGRATION.md for the binding a maintainer adds.
+ *
+ * Conventions
+ *   - All functions are synchronous at the ABI (device work is finished and, for
+ *     host outputs, copied back before return) and return 0 (VC_OK) or a negative
+ *     VC_E_* status; vc_strerror() names it.  Nothing here panics.
+ *   - Field elements: canonical (non-Montgomery) little-endian u64 limbs.
+ *     BN254 Fq / all scalar fields / Bandersnatch Fq: 4 limbs; BLS12-381 Fq: 6 limbs.
+ *   - Affine points: x limbs then y limbs (2*NL u64), plus one u8 per point that is 1
+ *     for the identity (its x, y are ignored).  Twisted-Edwards identity is (0, 1).
+ *   - Scalars: 4 u64 limbs each.  `mont` = 0: canonical and < r;  `mont` = 1:
+ *     arkworks' internal Montgomery form (the engine converts on the device).
+ *   - The caller owns every host buffer; a vc_ctx owns its device copies.
+ *   - A vc_ctx serialises calls internally (one mutex); share it across threads freely
+ *     (the reference's multiproof bound needs UniversalParams: Sync, multiproof.rs:96).
+ */
+#ifndef VC_MSM_H
+#define VC_MSM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* curves (the reference instantiates only BN254, vector-commit/Cargo.toml:15) */
+#define VC_CURVE_BN254 0        /* BN254 G1, y^2 = x^3 + 3 (ark-bn254)              */
+#define VC_CURVE_BLS12_381 1    /* BLS12-381 G1, y^2 = x^3 + 4                      */
+#define VC_CURVE_BANDERSNATCH 2 /* twisted Edwards a=-5 over BLS12-381 Fr           */
+
+/* status codes */
+#define VC_OK 0
+#define VC_E_INVALID (-1)     /* bad argument (null pointer, size, unknown curve)  */
+#define VC_E_HIP (-2)         /* HIP runtime error                                 */
+#define VC_E_OOM (-3)         /* device allocation failed                          */
+#define VC_E_TABLE (-4)       /* unknown / incompatible base table id              */
+#define VC_E_RANGE (-5)       /* offset + n beyond the base table                  */
+#define VC_E_NOT_ON_CURVE (-6)/* an uploaded base is not on the curve              */
+#define VC_E_NO_DEVICE (-7)   /* no usable gfx950 device                           */
+#define VC_E_DOMAIN (-8)      /* evaluation point outside what the call supports   */
+
+typedef struct vc_ctx vc_ctx;
+
+const char* vc_strerror(int status);
+int vc_version(void);
+
+/* Context: one device, one stream. device = HIP ordinal. */
+int vc_ctx_create(int curve, int device, vc_ctx** out);
+void vc_ctx_destroy(vc_ctx* ctx);
+int vc_ctx_curve(const vc_ctx* ctx);
+/* Launch on an external stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own. */
+int vc_ctx_set_stream(vc_ctx* ctx, void* hip_stream);
+/* Per-kernel device timing (HIP events around each launch on the ctx stream). */
+int vc_ctx_enable_timing(vc_ctx* ctx, int on);
+/* name: "msm_accumulate", "msm_digits", ... ; returns total ms and launch count */
+int vc_ctx_kernel_time(vc_ctx* ctx, const char* name, double* total_ms, long* launches);
+int vc_ctx_reset_timing(vc_ctx* ctx);
+
+/* Base tables ---------------------------------------------------------------
+ * Upload n affine bases once (validated on the device: VC_E_NOT_ON_CURVE).
+ * Replaces the reference's `IPAUniversalParams::g` (ipa/mod.rs:22-28) and
+ * `KZGKey::lagrange_commitments` (kzg/mod.rs:28-40). */
+int vc_bases_upload(vc_ctx* ctx, const uint64_t* affine_xy, const uint8_t* inf, size_t n,
+                    int* table_id);
+int vc_bases_count(vc_ctx* ctx, int table_id, size_t* n);
+/* Synthetic bases s_i*G with s_i = H(seed, i) mod r, generated on the device (bench input
+ * generation; the reference generates its CRS at setup, kzg_point_generator.rs:32-43). */
+int vc_bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* table_id);
+int vc_bases_download(vc_ctx* ctx, int table_id, uint64_t* affine_xy, uint8_t* inf);
+
+/* MSM: out = sum_i scalars[i] * bases[offset + i]  (utils::inner_product, utils.rs:16-19).
+ * `zip` truncation of the reference (Appendix B.9) is the caller's n. */
+int vc_msm(vc_ctx* ctx, int table_id, size_t offset, const uint64_t* scalars, size_t n, int mont,
+           uint64_t* out_xy, uint8_t* out_inf);
+/* Same with scalars already resident in device memory (4 u64 per scalar). */
+int vc_msm_device(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars, size_t n,
+                  int mont, uint64_t* out_xy, uint8_t* out_inf);
+/* Partial MSM for sharding across GPUs: returns the un-normalised accumulator (projective,
+ * curve-specific words, see vc_point_words) so ranks can all-gather and add. */
+int vc_point_words(int curve);
+int vc_msm_device_partial(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars,
+                          size_t n, int mont, uint32_t* out_acc);
+/* Sum k partial accumulators (host) and normalise to canonical affine. */
+int vc_partials_sum(int curve, const uint32_t* accs, size_t k, uint64_t* out_xy, uint8_t* out_inf);
+
+/* Batched width-w commits against one table: out[j] = sum_i s[j*w+i] * bases[i].
+ * (IPA::commit ipa/mod.rs:130-135, verkle Node::gen_commitment node.rs:243-271) */
+int vc_msm_batch(vc_ctx* ctx, int table_id, size_t width, const uint64_t* scalars, size_t batch,
+                 int mont, uint64_t* out_xy, uint8_t* out_inf);
+int vc_msm_batch_device(vc_ctx* ctx, int table_id, size_t width, const void* d_scalars,
+                        size_t batch, int mont, void* d_out_xy, uint8_t* d_out_inf);
+/* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 16]. */
+int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VC_MSM_H */

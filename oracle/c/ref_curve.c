@@ -1,0 +1,433 @@
+/* ORACLE (test infrastructure + CPU baseline only; never linked into the product).
+ *
+ * Plain-C restatement of the reference MSM `utils::inner_product`
+ * (/root/reference/vector-commit/src/utils.rs:16-19):
+ *     a.iter().zip(b).map(|(P, s)| P * s).sum()
+ * i.e. one full double-and-add scalar multiplication per term (arkworks 0.4
+ * `sw_double_and_add_projective` / `mul_bigint`: MSB-first over the canonical
+ * scalar bits, leading zeros skipped, general projective add of the base), then a
+ * sequential fold from zero.  64-bit-limb Montgomery (CIOS) field arithmetic
+ * with unsigned __int128, like arkworks' own backend.
+ *
+ * Compiled once per curve (-DCURVE_BN254 / -DCURVE_BLS12_381 / -DCURVE_BANDERSNATCH)
+ * into oracle/_build/libref_oracle.so; symbols are prefixed with the curve name.
+ * Optional pthread split of the terms (the sum is commutative, so the affine
+ * result is identical to the sequential fold); cores used = nthreads.
+ *
+ * Pinned by tests/test_oracle.py against the Python big-int oracle
+ * (oracle/pyoracle), itself pinned by generator / r*G = O KATs.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <pthread.h>
+
+typedef unsigned __int128 u128;
+typedef uint64_t u64;
+
+#if defined(CURVE_BN254)
+#define NL 4
+#define PFX(x) bn254_##x
+#define SW 1
+#define COEFF_B 3
+static const u64 P_[NL] = {0x3c208c16d87cfd47ULL, 0x97816a916871ca8dULL, 0xb85045b68181585dULL, 0x30644e72e131a029ULL};
+#elif defined(CURVE_BLS12_381)
+#define NL 6
+#define PFX(x) bls12_381_##x
+#define SW 1
+#define COEFF_B 4
+static const u64 P_[NL] = {0xb9feffffffffaaabULL, 0x1eabfffeb153ffffULL, 0x6730d2a0f6b0f624ULL,
+                           0x64774b84f38512bfULL, 0x4b1ba7b6434bacd7ULL, 0x1a0111ea397fe69aULL};
+#elif defined(CURVE_BANDERSNATCH)
+#define NL 4
+#define PFX(x) bandersnatch_##x
+#define SW 0
+/* base field = BLS12-381 Fr */
+static const u64 P_[NL] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL, 0x73eda753299d7d48ULL};
+/* d = 45022363124591815672509500913686876175488063829319466900776701791074614335719, a = -5 */
+static const u64 D_CANON[NL] = {0xb369f2f5188d58e7ULL, 0xcb66677177e54f92ULL, 0xc66e3bf86be3b6d8ULL, 0x6389c12633c267cbULL};
+#else
+#error "define a curve"
+#endif
+
+typedef struct { u64 v[NL]; } fe;
+
+static u64 INV_;   /* -p^{-1} mod 2^64 */
+static fe R2_;     /* R^2 mod p */
+static fe ONE_;    /* R mod p (Montgomery one) */
+static int inited_;
+
+static int geq_p(const u64* a) {
+    for (int i = NL - 1; i >= 0; i--) {
+        if (a[i] > P_[i]) return 1;
+        if (a[i] < P_[i]) return 0;
+    }
+    return 1;
+}
+static void sub_p(u64* a) {
+    u64 br = 0;
+    for (int i = 0; i < NL; i++) {
+        u128 d = (u128)a[i] - P_[i] - br;
+        a[i] = (u64)d;
+        br = (u64)(d >> 64) ? 1 : 0;
+    }
+}
+static void fadd(fe* r, const fe* a, const fe* b) {
+    u64 c = 0;
+    u64 t[NL];
+    for (int i = 0; i < NL; i++) {
+        u128 s = (u128)a->v[i] + b->v[i] + c;
+        t[i] = (u64)s;
+        c = (u64)(s >> 64);
+    }
+    if (c || geq_p(t)) sub_p(t);
+    memcpy(r->v, t, sizeof t);
+}
+static void fsub(fe* r, const fe* a, const fe* b) {
+    u64 br = 0;
+    u64 t[NL];
+    for (int i = 0; i < NL; i++) {
+        u128 d = (u128)a->v[i] - b->v[i] - br;
+        t[i] = (u64)d;
+        br = (u64)(d >> 64) ? 1 : 0;
+    }
+    if (br) {
+        u64 c = 0;
+        for (int i = 0; i < NL; i++) {
+            u128 s = (u128)t[i] + P_[i] + c;
+            t[i] = (u64)s;
+            c = (u64)(s >> 64);
+        }
+    }
+    memcpy(r->v, t, sizeof t);
+}
+static void fmul(fe* r, const fe* a, const fe* b) {
+    u64 t[NL + 2];
+    memset(t, 0, sizeof t);
+    for (int i = 0; i < NL; i++) {
+        u64 C = 0;
+        for (int j = 0; j < NL; j++) {
+            u128 s = (u128)a->v[j] * b->v[i] + t[j] + C;
+            t[j] = (u64)s;
+            C = (u64)(s >> 64);
+        }
+        u128 s = (u128)t[NL] + C;
+        t[NL] = (u64)s;
+        t[NL + 1] = (u64)(s >> 64);
+        u64 m = t[0] * INV_;
+        s = (u128)m * P_[0] + t[0];
+        C = (u64)(s >> 64);
+        for (int j = 1; j < NL; j++) {
+            s = (u128)m * P_[j] + t[j] + C;
+            t[j - 1] = (u64)s;
+            C = (u64)(s >> 64);
+        }
+        s = (u128)t[NL] + C;
+        t[NL - 1] = (u64)s;
+        t[NL] = t[NL + 1] + (u64)(s >> 64);
+    }
+    if (t[NL] || geq_p(t)) sub_p(t);
+    memcpy(r->v, t, NL * sizeof(u64));
+}
+static int fiszero(const fe* a) {
+    u64 o = 0;
+    for (int i = 0; i < NL; i++) o |= a->v[i];
+    return o == 0;
+}
+static int feq(const fe* a, const fe* b) { return memcmp(a->v, b->v, sizeof a->v) == 0; }
+static void to_mont(fe* r, const u64* canon) {
+    fe a;
+    memcpy(a.v, canon, sizeof a.v);
+    fmul(r, &a, &R2_);
+}
+static void from_mont(u64* canon, const fe* a) {
+    fe one = {{0}};
+    one.v[0] = 1;
+    fe t;
+    fmul(&t, a, &one);
+    memcpy(canon, t.v, sizeof t.v);
+}
+/* a^(p-2) */
+static void finv(fe* r, const fe* a) {
+    u64 e[NL];
+    memcpy(e, P_, sizeof e);
+    e[0] -= 2; /* p is odd and > 2: no borrow */
+    fe acc = ONE_;
+    for (int i = NL - 1; i >= 0; i--)
+        for (int b = 63; b >= 0; b--) {
+            fmul(&acc, &acc, &acc);
+            if ((e[i] >> b) & 1) fmul(&acc, &acc, a);
+        }
+    *r = acc;
+}
+static void init(void) {
+    if (inited_) return;
+    u64 inv = 1;
+    for (int i = 0; i < 7; i++) inv *= 2 - P_[0] * inv;
+    INV_ = (u64)0 - inv;
+    /* R mod p and R^2 mod p by doubling */
+    fe x = {{0}};
+    x.v[0] = 1;
+    for (int i = 0; i < 64 * NL * 2; i++) {
+        fadd(&x, &x, &x);
+        if (i == 64 * NL - 1) ONE_ = x;
+    }
+    R2_ = x;
+    inited_ = 1;
+}
+
+#if SW
+/* ------------------------------------------------ short Weierstrass a=0, Jacobian */
+typedef struct { fe x, y, z; } pt;
+static void pzero(pt* p) { memset(p, 0, sizeof *p); p->y = ONE_; }
+static int piszero(const pt* p) { return fiszero(&p->z); }
+static void pdbl(pt* r, const pt* p) {
+    if (piszero(p)) { *r = *p; return; }
+    fe A, B, C, D, E, F, t;
+    fmul(&A, &p->x, &p->x);
+    fmul(&B, &p->y, &p->y);
+    fmul(&C, &B, &B);
+    fadd(&t, &p->x, &B);
+    fmul(&t, &t, &t);
+    fsub(&t, &t, &A);
+    fsub(&t, &t, &C);
+    fadd(&D, &t, &t);
+    fadd(&E, &A, &A);
+    fadd(&E, &E, &A);
+    fmul(&F, &E, &E);
+    pt o;
+    fsub(&o.x, &F, &D);
+    fsub(&o.x, &o.x, &D);
+    fsub(&t, &D, &o.x);
+    fmul(&t, &E, &t);
+    fe c8;
+    fadd(&c8, &C, &C);
+    fadd(&c8, &c8, &c8);
+    fadd(&c8, &c8, &c8);
+    fsub(&o.y, &t, &c8);
+    fmul(&o.z, &p->y, &p->z);
+    fadd(&o.z, &o.z, &o.z);
+    *r = o;
+}
+static void padd(pt* r, const pt* p, const pt* q) {
+    if (piszero(p)) { *r = *q; return; }
+    if (piszero(q)) { *r = *p; return; }
+    fe z1z1, z2z2, u1, u2, s1, s2, t;
+    fmul(&z1z1, &p->z, &p->z);
+    fmul(&z2z2, &q->z, &q->z);
+    fmul(&u1, &p->x, &z2z2);
+    fmul(&u2, &q->x, &z1z1);
+    fmul(&t, &q->z, &z2z2);
+    fmul(&s1, &p->y, &t);
+    fmul(&t, &p->z, &z1z1);
+    fmul(&s2, &q->y, &t);
+    if (feq(&u1, &u2)) {
+        if (feq(&s1, &s2)) { pdbl(r, p); return; }
+        pzero(r);
+        return;
+    }
+    fe h, i, j, rr, v;
+    fsub(&h, &u2, &u1);
+    fadd(&i, &h, &h);
+    fmul(&i, &i, &i);
+    fmul(&j, &h, &i);
+    fsub(&rr, &s2, &s1);
+    fadd(&rr, &rr, &rr);
+    fmul(&v, &u1, &i);
+    pt o;
+    fmul(&o.x, &rr, &rr);
+    fsub(&o.x, &o.x, &j);
+    fsub(&o.x, &o.x, &v);
+    fsub(&o.x, &o.x, &v);
+    fsub(&t, &v, &o.x);
+    fmul(&t, &rr, &t);
+    fmul(&s1, &s1, &j);
+    fadd(&s1, &s1, &s1);
+    fsub(&o.y, &t, &s1);
+    fadd(&t, &p->z, &q->z);
+    fmul(&t, &t, &t);
+    fsub(&t, &t, &z1z1);
+    fsub(&t, &t, &z2z2);
+    fmul(&o.z, &t, &h);
+    *r = o;
+}
+static void pload(pt* r, const u64* xy, int inf) {
+    if (inf) { pzero(r); return; }
+    to_mont(&r->x, xy);
+    to_mont(&r->y, xy + NL);
+    r->z = ONE_;
+}
+static void pstore(u64* xy, uint8_t* inf, const pt* p) {
+    if (piszero(p)) {
+        memset(xy, 0, 2 * NL * sizeof(u64));
+        *inf = 1;
+        return;
+    }
+    fe zi, zi2, zi3, x, y;
+    finv(&zi, &p->z);
+    fmul(&zi2, &zi, &zi);
+    fmul(&zi3, &zi2, &zi);
+    fmul(&x, &p->x, &zi2);
+    fmul(&y, &p->y, &zi3);
+    from_mont(xy, &x);
+    from_mont(xy + NL, &y);
+    *inf = 0;
+}
+#else
+/* ------------------------------------------------ twisted Edwards a=-5, extended (X,Y,T,Z) */
+typedef struct { fe x, y, t, z; } pt;
+static fe D_;
+static void pzero(pt* p) { memset(p, 0, sizeof *p); p->y = ONE_; p->z = ONE_; }
+static void padd(pt* r, const pt* p, const pt* q) {
+    /* add-2008-hwcd (unified, complete for a non-square, d non-square) */
+    fe A, B, C, Dd, E, F, G, H, t1, t2;
+    fmul(&A, &p->x, &q->x);
+    fmul(&B, &p->y, &q->y);
+    fmul(&C, &p->t, &q->t);
+    fmul(&C, &C, &D_);
+    fmul(&Dd, &p->z, &q->z);
+    fadd(&t1, &p->x, &p->y);
+    fadd(&t2, &q->x, &q->y);
+    fmul(&E, &t1, &t2);
+    fsub(&E, &E, &A);
+    fsub(&E, &E, &B);
+    fsub(&F, &Dd, &C);
+    fadd(&G, &Dd, &C);
+    /* H = B - a*A = B + 5A */
+    fadd(&t1, &A, &A);
+    fadd(&t1, &t1, &t1);
+    fadd(&t1, &t1, &A);
+    fadd(&H, &B, &t1);
+    pt o;
+    fmul(&o.x, &E, &F);
+    fmul(&o.y, &G, &H);
+    fmul(&o.t, &E, &H);
+    fmul(&o.z, &F, &G);
+    *r = o;
+}
+static void pdbl(pt* r, const pt* p) { padd(r, p, p); }
+static void pload(pt* r, const u64* xy, int inf) {
+    if (inf) { pzero(r); return; }
+    to_mont(&r->x, xy);
+    to_mont(&r->y, xy + NL);
+    fmul(&r->t, &r->x, &r->y);
+    r->z = ONE_;
+}
+static void pstore(u64* xy, uint8_t* inf, const pt* p) {
+    fe zi, x, y;
+    finv(&zi, &p->z);
+    fmul(&x, &p->x, &zi);
+    fmul(&y, &p->y, &zi);
+    from_mont(xy, &x);
+    from_mont(xy + NL, &y);
+    /* identity is (0, 1); y is canonical here */
+    u64 one_c[NL] = {1};
+    *inf = (fiszero(&x) && memcmp(xy + NL, one_c, sizeof one_c) == 0) ? 1 : 0;
+}
+#endif
+
+/* arkworks mul_bigint: MSB-first, leading zeros skipped */
+static void pmul(pt* r, const pt* base, const u64* k /*4 limbs canonical*/) {
+    pt acc;
+    pzero(&acc);
+    int started = 0;
+    for (int i = 3; i >= 0; i--)
+        for (int b = 63; b >= 0; b--) {
+            int bit = (k[i] >> b) & 1;
+            if (!started && !bit) continue;
+            started = 1;
+            pdbl(&acc, &acc);
+            if (bit) padd(&acc, &acc, base);
+        }
+    *r = acc;
+}
+
+typedef struct {
+    const u64* bases;
+    const uint8_t* inf;
+    const u64* scalars;
+    size_t lo, hi;
+    pt acc;
+} job_t;
+
+static void* run_job(void* arg) {
+    job_t* j = (job_t*)arg;
+    pt acc;
+    pzero(&acc);
+    for (size_t i = j->lo; i < j->hi; i++) {
+        pt b, m;
+        pload(&b, j->bases + i * 2 * NL, j->inf ? j->inf[i] : 0);
+        pmul(&m, &b, j->scalars + i * 4);
+        padd(&acc, &acc, &m);
+    }
+    j->acc = acc;
+    return NULL;
+}
+
+/* naive MSM; bases: n x (x[NL], y[NL]) canonical LE u64; scalars: n x 4 u64 canonical (< r) */
+int PFX(ref_msm)(const u64* bases, const uint8_t* inf, const u64* scalars, size_t n, int nthreads,
+                 u64* out_xy, uint8_t* out_inf) {
+    init();
+#if !SW
+    to_mont(&D_, D_CANON);
+#endif
+    if (nthreads < 1) nthreads = 1;
+    if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
+    job_t* jobs = (job_t*)calloc(nthreads, sizeof(job_t));
+    pthread_t* th = (pthread_t*)calloc(nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].bases = bases;
+        jobs[t].inf = inf;
+        jobs[t].scalars = scalars;
+        jobs[t].lo = n * t / nthreads;
+        jobs[t].hi = n * (t + 1) / nthreads;
+    }
+    if (nthreads == 1) run_job(&jobs[0]);
+    else {
+        for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, run_job, &jobs[t]);
+        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    }
+    pt acc;
+    pzero(&acc);
+    for (int t = 0; t < nthreads; t++) padd(&acc, &acc, &jobs[t].acc);
+    pstore(out_xy, out_inf, &acc);
+    free(jobs);
+    free(th);
+    return 0;
+}
+
+/* on-curve check of canonical affine points (used to validate generated inputs) */
+int PFX(ref_on_curve)(const u64* bases, size_t n) {
+    init();
+#if !SW
+    to_mont(&D_, D_CANON);
+#endif
+    for (size_t i = 0; i < n; i++) {
+        fe x, y, x2, y2, l, r;
+        to_mont(&x, bases + i * 2 * NL);
+        to_mont(&y, bases + i * 2 * NL + NL);
+        fmul(&x2, &x, &x);
+        fmul(&y2, &y, &y);
+#if SW
+        fe b = {{0}};
+        b.v[0] = COEFF_B;
+        to_mont(&b, b.v);
+        fmul(&l, &x2, &x);
+        fadd(&l, &l, &b);
+        if (!feq(&l, &y2)) return 0;
+        (void)r;
+#else
+        /* -5 x^2 + y^2 == 1 + d x^2 y^2 */
+        fe five = {{0}};
+        five.v[0] = 5;
+        to_mont(&five, five.v);
+        fmul(&l, &x2, &five);
+        fsub(&l, &y2, &l);
+        fmul(&r, &x2, &y2);
+        fmul(&r, &r, &D_);
+        fadd(&r, &r, &ONE_);
+        if (!feq(&l, &r)) return 0;
+#endif
+    }
+    return 1;
+}

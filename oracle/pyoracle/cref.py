@@ -1,0 +1,88 @@
+"""ORACLE (test infrastructure only) -- ctypes binding of oracle/_build/libref_oracle.so (C restatement)."""
+import ctypes
+import os
+
+import numpy as np
+
+from .curves import CURVES
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_build", "libref_oracle.so")
+NL = {"bn254": 4, "bls12_381": 6, "bandersnatch": 4}
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle C library missing: run `make -C oracle`")
+        _lib = ctypes.CDLL(LIB_PATH)
+    return _lib
+
+
+def ints_to_limbs(vals, nl):
+    out = np.zeros((len(vals), nl), dtype=np.uint64)
+    for i, v in enumerate(vals):
+        v = int(v)
+        for j in range(nl):
+            out[i, j] = (v >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
+    return out
+
+
+def limbs_to_int(row):
+    return sum(int(x) << (64 * j) for j, x in enumerate(row))
+
+
+def points_to_array(curve_name, pts):
+    nl = NL[curve_name]
+    arr = np.zeros((len(pts), 2 * nl), dtype=np.uint64)
+    inf = np.zeros(len(pts), dtype=np.uint8)
+    for i, P in enumerate(pts):
+        if P is None:
+            inf[i] = 1
+            continue
+        arr[i, :nl] = ints_to_limbs([P[0]], nl)[0]
+        arr[i, nl:] = ints_to_limbs([P[1]], nl)[0]
+    return arr, inf
+
+
+def array_to_point(curve_name, xy, inf):
+    nl = NL[curve_name]
+    c = CURVES[curve_name]
+    if inf:
+        return c.identity()
+    return (limbs_to_int(xy[:nl]), limbs_to_int(xy[nl:]))
+
+
+def msm_arrays(curve_name, bases, inf, scalars, nthreads=1):
+    """bases: (n, 2*NL) uint64 canonical; scalars: (n, 4) uint64 canonical. Returns (xy, inf)."""
+    nl = NL[curve_name]
+    n = scalars.shape[0]
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    infp = None
+    if inf is not None:
+        inf = np.ascontiguousarray(inf, dtype=np.uint8)
+        infp = inf.ctypes.data_as(ctypes.c_void_p)
+    out = np.zeros(2 * nl, dtype=np.uint64)
+    oinf = np.zeros(1, dtype=np.uint8)
+    fn = getattr(lib(), curve_name + "_ref_msm")
+    fn.restype = ctypes.c_int
+    fn(bases.ctypes.data_as(ctypes.c_void_p), infp, scalars.ctypes.data_as(ctypes.c_void_p),
+       ctypes.c_size_t(n), ctypes.c_int(nthreads), out.ctypes.data_as(ctypes.c_void_p),
+       oinf.ctypes.data_as(ctypes.c_void_p))
+    return out, int(oinf[0])
+
+
+def msm(curve_name, pts, scalars, nthreads=1):
+    arr, inf = points_to_array(curve_name, pts)
+    sc = ints_to_limbs(scalars, 4)
+    xy, oi = msm_arrays(curve_name, arr, inf, sc, nthreads)
+    return array_to_point(curve_name, xy, oi)
+
+
+def on_curve(curve_name, bases):
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    fn = getattr(lib(), curve_name + "_ref_on_curve")
+    return bool(fn(bases.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(bases.shape[0])))

@@ -1,0 +1,335 @@
+// Base tables: upload (canonical -> Montgomery, on-curve validation), synthetic generation
+// (s_i * G on the device), download. Replaces the reference's CRS storage
+// (IPAUniversalParams::g, ipa/mod.rs:22-28; KZGKey::lagrange_commitments, kzg/mod.rs:28-40),
+// which arkworks keeps as projective Montgomery points; the engine keeps affine
+// Montgomery (64 B BN254, 96 B BLS12-381, 96 B Bandersnatch (x, y, d*x*y)).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+#include "ec.hpp"
+
+namespace vk {
+
+template <class C>
+struct Gen;
+template <>
+struct Gen<BN254G1> {
+    VK_HD static uint32_t x(int i) { return i == 0 ? 1u : 0u; }
+    VK_HD static uint32_t y(int i) { return i == 0 ? 2u : 0u; }
+};
+template <>
+struct Gen<BLS381G1> {
+    VK_HD static uint32_t x(int i) {
+        constexpr uint32_t v[] = {0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu,
+                                  0x9774b905u, 0xc3688c4fu, 0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u};
+        return v[i];
+    }
+    VK_HD static uint32_t y(int i) {
+        constexpr uint32_t v[] = {0x46c5e7e1u, 0x0caa2329u, 0xa2888ae4u, 0xd03cc744u, 0x2c04b3edu, 0x00db18cbu,
+                                  0xd5d00af6u, 0xfcf5e095u, 0x741d8ae4u, 0xa09e30edu, 0xe3aaa0f1u, 0x08b3f481u};
+        return v[i];
+    }
+};
+template <>
+struct Gen<Bandersnatch> {
+    VK_HD static uint32_t x(int i) {
+        constexpr uint32_t v[] = {0xa252ae18u, 0xe1e71866u, 0xad998465u, 0x2b79c022u,
+                                  0x7bbe42f3u, 0x74371177u, 0x2c0b34c5u, 0x29c132ccu};
+        return v[i];
+    }
+    VK_HD static uint32_t y(int i) {
+        constexpr uint32_t v[] = {0xcc974166u, 0x5e3167b6u, 0xeee46460u, 0x358cad81u,
+                                  0xbadcd586u, 0x157d8b50u, 0xda123e0fu, 0x2a6c669eu};
+        return v[i];
+    }
+};
+
+// ------------------------------------------------------------------ on-curve + conversions
+template <class C>
+__device__ __forceinline__ bool on_curve(const fe<typename C::F>& x, const fe<typename C::F>& y) {
+    using F = typename C::F;
+    fe<F> x2 = fe_sqr<F>(x), y2 = fe_sqr<F>(y);
+    if constexpr (!C::is_te) {
+        fe<F> b = fe_zero<F>();
+        b.v[0] = (uint32_t)C::COEFF_B;
+        b = fe_to_mont<F>(b);
+        return fe_eq<F>(fe_add<F>(fe_mul<F>(x2, x), b), y2);
+    } else {
+        fe<F> lhs = fe_sub<F>(y2, fe_mul_small<F, 5>(x2));
+        fe<F> rhs = fe_add<F>(fe_one<F>(), fe_mul<F>(fe_mul<F>(x2, y2), C::d()));
+        return fe_eq<F>(lhs, rhs);
+    }
+}
+
+template <class C>
+__device__ __forceinline__ typename C::Aff make_aff(const fe<typename C::F>& x, const fe<typename C::F>& y) {
+    typename C::Aff a;
+    a.x = x;
+    a.y = y;
+    if constexpr (C::is_te) a.kt = fe_mul<typename C::F>(fe_mul<typename C::F>(x, y), C::d());
+    return a;
+}
+
+template <class C>
+__global__ void k_upload(const uint32_t* __restrict__ xy, const uint8_t* __restrict__ inf, uint32_t n,
+                         typename C::Aff* __restrict__ out, uint8_t* __restrict__ out_inf,
+                         uint32_t* __restrict__ bad) {
+    using F = typename C::F;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<F> x, y;
+#pragma unroll
+    for (int k = 0; k < F::N; k++) {
+        x.v[k] = xy[(size_t)i * 2 * F::N + k];
+        y.v[k] = xy[(size_t)i * 2 * F::N + F::N + k];
+    }
+    uint8_t isinf = inf ? inf[i] : 0;
+    if (isinf) {
+        x = fe_zero<F>();
+        y = C::is_te ? fe_one<F>() : fe_zero<F>();
+    } else {
+        // canonical range check (x, y < p): reduce_once leaves values >= p changed
+        if (!fe_eq<F>(fe_reduce_once<F>(x), x) || !fe_eq<F>(fe_reduce_once<F>(y), y)) {
+            atomicOr(bad, 1u);
+            return;
+        }
+        x = fe_to_mont<F>(x);
+        y = fe_to_mont<F>(y);
+        if (!on_curve<C>(x, y)) atomicOr(bad, 1u);
+    }
+    out[i] = make_aff<C>(x, y);
+    out_inf[i] = isinf;
+}
+
+template <class C>
+__global__ void k_download(const typename C::Aff* __restrict__ in, const uint8_t* __restrict__ inf,
+                           uint32_t n, uint32_t* __restrict__ xy) {
+    using F = typename C::F;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<F> x = fe_from_mont<F>(in[i].x), y = fe_from_mont<F>(in[i].y);
+    if (inf[i]) {
+        x = fe_zero<F>();
+        y = fe_zero<F>();
+    }
+#pragma unroll
+    for (int k = 0; k < F::N; k++) {
+        xy[(size_t)i * 2 * F::N + k] = x.v[k];
+        xy[(size_t)i * 2 * F::N + F::N + k] = y.v[k];
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t& s) {
+    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// P_i = s_i * G with s_i from splitmix64(seed, i), s_i < 2^(bits-2); affine via one inversion
+template <class C>
+__global__ void k_random(uint64_t seed, uint32_t n, int sbits, typename C::Aff* __restrict__ out,
+                         uint8_t* __restrict__ out_inf) {
+    using F = typename C::F;
+    using Acc = typename C::Acc;
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t st = seed * 0x100000001b3ull + i;
+    uint64_t s[4];
+    for (int k = 0; k < 4; k++) s[k] = splitmix64(st);
+    int topbits = sbits - 2 - 192;  // bits used in the top limb
+    s[3] &= (topbits >= 64) ? ~0ull : ((1ull << topbits) - 1);
+    s[0] |= 1;  // never zero
+    typename C::Aff g;
+    fe<F> gx, gy;
+#pragma unroll
+    for (int k = 0; k < F::N; k++) {
+        gx.v[k] = Gen<C>::x(k);
+        gy.v[k] = Gen<C>::y(k);
+    }
+    gx = fe_to_mont<F>(gx);
+    gy = fe_to_mont<F>(gy);
+    g = make_aff<C>(gx, gy);
+    Acc acc = C::zero();
+    for (int b = 255; b >= 0; b--) {
+        acc = C::dbl(acc);
+        if ((s[b >> 6] >> (b & 63)) & 1) acc = C::madd(acc, g, false);
+    }
+    fe<F> x, y;
+    C::to_aff(acc, x, y);
+    out[i] = make_aff<C>(x, y);
+    out_inf[i] = 0;
+}
+
+// ------------------------------------------------------------------ host entry points
+template <class C>
+static int upload_t(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id) {
+    using Aff = typename C::Aff;
+    using F = typename C::F;
+    Table* t = new Table();
+    t->curve = ctx->curve;
+    t->n = n;
+    int st = t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff));
+    if (st == VC_OK) st = t->inf.ensure(std::max<size_t>(n, 1));
+    DevBuf dxy, dinf, dbad;
+    if (st == VC_OK) st = dxy.ensure(std::max<size_t>(n, 1) * 2 * F::N * 4);
+    if (st == VC_OK) st = dinf.ensure(std::max<size_t>(n, 1));
+    if (st == VC_OK) st = dbad.ensure(4);
+    if (st != VC_OK) {
+        delete t;
+        return st;
+    }
+    auto fail = [&](int code) {
+        delete t;
+        return code;
+    };
+    if (n > 0) {
+        if (hipMemcpyAsync(dxy.p, xy, n * 2 * F::N * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            return fail(VC_E_HIP);
+        if (inf) {
+            if (hipMemcpyAsync(dinf.p, inf, n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+                return fail(VC_E_HIP);
+        }
+        if (hipMemsetAsync(dbad.p, 0, 4, ctx->stream) != hipSuccess) return fail(VC_E_HIP);
+        hipLaunchKernelGGL(k_upload<C>, dim3((n + 255) / 256), dim3(256), 0, ctx->stream,
+                           dxy.as<uint32_t>(), inf ? dinf.as<uint8_t>() : nullptr, (uint32_t)n,
+                           t->bases.as<Aff>(), t->inf.as<uint8_t>(), dbad.as<uint32_t>());
+        uint32_t bad = 0;
+        if (hipMemcpyAsync(&bad, dbad.p, 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+            return fail(VC_E_HIP);
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(VC_E_HIP);
+        if (bad) return fail(VC_E_NOT_ON_CURVE);
+    }
+    ctx->tables.push_back(t);
+    *id = (int)ctx->tables.size() - 1;
+    return VC_OK;
+}
+
+template <class C, class Fr>
+static int random_t(vc_ctx* ctx, uint64_t seed, size_t n, int* id) {
+    using Aff = typename C::Aff;
+    Table* t = new Table();
+    t->curve = ctx->curve;
+    t->n = n;
+    int st = t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff));
+    if (st == VC_OK) st = t->inf.ensure(std::max<size_t>(n, 1));
+    if (st != VC_OK) {
+        delete t;
+        return st;
+    }
+    if (n > 0) {
+        hipLaunchKernelGGL(k_random<C>, dim3((n + 127) / 128), dim3(128), 0, ctx->stream, seed,
+                           (uint32_t)n, Fr::BITS, t->bases.as<Aff>(), t->inf.as<uint8_t>());
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+            delete t;
+            return VC_E_HIP;
+        }
+    }
+    ctx->tables.push_back(t);
+    *id = (int)ctx->tables.size() - 1;
+    return VC_OK;
+}
+
+template <class C>
+static int download_t(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf) {
+    using F = typename C::F;
+    if (t->n == 0) return VC_OK;
+    DevBuf d;
+    VK_TRY(d.ensure(t->n * 2 * F::N * 4));
+    hipLaunchKernelGGL(k_download<C>, dim3((t->n + 255) / 256), dim3(256), 0, ctx->stream,
+                       t->bases.as<typename C::Aff>(), t->inf.as<uint8_t>(), (uint32_t)t->n,
+                       d.as<uint32_t>());
+    VK_CHECK_HIP(hipGetLastError());
+    VK_CHECK_HIP(hipMemcpyAsync(xy, d.p, t->n * 2 * F::N * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (inf) VK_CHECK_HIP(hipMemcpyAsync(inf, t->inf.p, t->n, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+int bases_upload(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id) {
+    switch (ctx->curve) {
+        case VC_CURVE_BN254: return upload_t<BN254G1>(ctx, xy, inf, n, id);
+        case VC_CURVE_BLS12_381: return upload_t<BLS381G1>(ctx, xy, inf, n, id);
+        case VC_CURVE_BANDERSNATCH: return upload_t<Bandersnatch>(ctx, xy, inf, n, id);
+    }
+    return VC_E_INVALID;
+}
+int bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id) {
+    switch (ctx->curve) {
+        case VC_CURVE_BN254: return random_t<BN254G1, BN254Fr>(ctx, seed, n, id);
+        case VC_CURVE_BLS12_381: return random_t<BLS381G1, BLS381Fr>(ctx, seed, n, id);
+        case VC_CURVE_BANDERSNATCH: return random_t<Bandersnatch, BandFr>(ctx, seed, n, id);
+    }
+    return VC_E_INVALID;
+}
+int bases_download(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf) {
+    switch (t->curve) {
+        case VC_CURVE_BN254: return download_t<BN254G1>(ctx, t, xy, inf);
+        case VC_CURVE_BLS12_381: return download_t<BLS381G1>(ctx, t, xy, inf);
+        case VC_CURVE_BANDERSNATCH: return download_t<Bandersnatch>(ctx, t, xy, inf);
+    }
+    return VC_E_INVALID;
+}
+
+// ------------------------------------------------------------------ host point helpers
+template <class C>
+static int acc_to_affine_t(const uint32_t* accw, uint64_t* out_xy, uint8_t* out_inf) {
+    using F = typename C::F;
+    typename C::Acc a;
+    memcpy(&a, accw, sizeof a);
+    fe<F> x, y;
+    bool fin = C::to_aff(a, x, y);
+    if (!fin) {
+        memset(out_xy, 0, 2 * F::N * 4);
+        if (C::is_te) out_xy[0 + F::N / 2] = 1;  // y = 1
+        *out_inf = 1;
+        return VC_OK;
+    }
+    x = fe_from_mont<F>(x);
+    y = fe_from_mont<F>(y);
+    memcpy(out_xy, x.v, F::N * 4);
+    memcpy(reinterpret_cast<uint32_t*>(out_xy) + F::N, y.v, F::N * 4);
+    *out_inf = 0;
+    return VC_OK;
+}
+template <class C>
+static int acc_sum_t(const uint32_t* accs, size_t k, uint32_t* out) {
+    typename C::Acc r = C::zero();
+    for (size_t i = 0; i < k; i++) {
+        typename C::Acc a;
+        memcpy(&a, accs + i * (sizeof(a) / 4), sizeof a);
+        r = C::add(r, a);
+    }
+    memcpy(out, &r, sizeof r);
+    return VC_OK;
+}
+int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out_inf) {
+    switch (curve) {
+        case VC_CURVE_BN254: return acc_to_affine_t<BN254G1>(acc, out_xy, out_inf);
+        case VC_CURVE_BLS12_381: return acc_to_affine_t<BLS381G1>(acc, out_xy, out_inf);
+        case VC_CURVE_BANDERSNATCH: return acc_to_affine_t<Bandersnatch>(acc, out_xy, out_inf);
+    }
+    return VC_E_INVALID;
+}
+int acc_sum(int curve, const uint32_t* accs, size_t k, uint32_t* out) {
+    switch (curve) {
+        case VC_CURVE_BN254: return acc_sum_t<BN254G1>(accs, k, out);
+        case VC_CURVE_BLS12_381: return acc_sum_t<BLS381G1>(accs, k, out);
+        case VC_CURVE_BANDERSNATCH: return acc_sum_t<Bandersnatch>(accs, k, out);
+    }
+    return VC_E_INVALID;
+}
+int point_words(int curve) {
+    switch (curve) {
+        case VC_CURVE_BN254: return BN254G1::ACC_WORDS;
+        case VC_CURVE_BLS12_381: return BLS381G1::ACC_WORDS;
+        case VC_CURVE_BANDERSNATCH: return Bandersnatch::ACC_WORDS;
+    }
+    return 0;
+}
+int aff_limbs64(int curve) { return curve == VC_CURVE_BLS12_381 ? 6 : 4; }
+
+}  // namespace vk

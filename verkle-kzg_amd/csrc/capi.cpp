@@ -1,0 +1,299 @@
+// extern "C" entry points of libvkzg.so (declared in include/vc_msm.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ctx.hpp"
+
+namespace vk {
+
+hipError_t& last_hip_error() {
+    static thread_local hipError_t e = hipSuccess;
+    return e;
+}
+
+int DevBuf::ensure(size_t bytes) {
+    if (bytes <= cap && p) return VC_OK;
+    release();
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        p = nullptr;
+        cap = 0;
+        return VC_E_OOM;
+    }
+    cap = bytes;
+    return VC_OK;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+}  // namespace vk
+
+hipEvent_t vc_ctx::get_event() {
+    if (!event_pool.empty()) {
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+void vc_ctx::timer_begin(const char*, hipEvent_t* a) {
+    *a = get_event();
+    (void)hipEventRecord(*a, stream);
+}
+
+void vc_ctx::timer_end(const char* name, hipEvent_t a) {
+    hipEvent_t b = get_event();
+    (void)hipEventRecord(b, stream);
+    pending.push_back({a, b, name});
+}
+
+void vc_ctx::collect_timers() {
+    for (auto& p : pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            auto& slot = ktime[p.name];
+            slot.first += ms;
+            slot.second += 1;
+        }
+        event_pool.push_back(p.a);
+        event_pool.push_back(p.b);
+    }
+    pending.clear();
+}
+
+namespace {
+
+struct Guard {
+    vc_ctx* c;
+    std::lock_guard<std::mutex> lk;
+    explicit Guard(vc_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); }
+    ~Guard() {
+        if (c->timing) c->collect_timers();
+    }
+};
+
+bool valid_curve(int c) { return c == VC_CURVE_BN254 || c == VC_CURVE_BLS12_381 || c == VC_CURVE_BANDERSNATCH; }
+
+}  // namespace
+
+extern "C" {
+
+const char* vc_strerror(int s) {
+    switch (s) {
+        case VC_OK: return "ok";
+        case VC_E_INVALID: return "invalid argument";
+        case VC_E_HIP: return hipGetErrorString(vk::last_hip_error());
+        case VC_E_OOM: return "device out of memory";
+        case VC_E_TABLE: return "unknown or incompatible base table";
+        case VC_E_RANGE: return "range beyond the base table";
+        case VC_E_NOT_ON_CURVE: return "base point not on the curve (or not canonical)";
+        case VC_E_NO_DEVICE: return "no usable HIP device";
+        case VC_E_DOMAIN: return "evaluation point outside the supported domain";
+    }
+    return "unknown status";
+}
+
+int vc_version(void) { return 1; }
+
+int vc_ctx_create(int curve, int device, vc_ctx** out) {
+    if (!out || !valid_curve(curve)) return VC_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VC_E_NO_DEVICE;
+    if (device < 0 || device >= ndev) return VC_E_INVALID;
+    VK_CHECK_HIP(hipSetDevice(device));
+    vc_ctx* c = new vc_ctx();
+    c->curve = curve;
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        vk::last_hip_error() = e;
+        delete c;
+        return VC_E_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return VC_OK;
+}
+
+void vc_ctx_destroy(vc_ctx* ctx) {
+    if (!ctx) return;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        (void)hipSetDevice(ctx->device);
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        for (auto* t : ctx->tables) delete t;
+        ctx->tables.clear();
+        for (auto& b : ctx->ws) b.release();
+        for (auto& p : ctx->pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+        if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    }
+    delete ctx;
+}
+
+int vc_ctx_curve(const vc_ctx* ctx) { return ctx ? ctx->curve : VC_E_INVALID; }
+
+int vc_ctx_set_stream(vc_ctx* ctx, void* s) {
+    if (!ctx) return VC_E_INVALID;
+    Guard g(ctx);
+    ctx->stream = s ? reinterpret_cast<hipStream_t>(s) : ctx->own_stream;
+    return VC_OK;
+}
+
+int vc_ctx_enable_timing(vc_ctx* ctx, int on) {
+    if (!ctx) return VC_E_INVALID;
+    Guard g(ctx);
+    ctx->timing = on != 0;
+    return VC_OK;
+}
+
+int vc_ctx_kernel_time(vc_ctx* ctx, const char* name, double* total_ms, long* launches) {
+    if (!ctx || !name) return VC_E_INVALID;
+    Guard g(ctx);
+    auto it = ctx->ktime.find(name);
+    if (total_ms) *total_ms = it == ctx->ktime.end() ? 0.0 : it->second.first;
+    if (launches) *launches = it == ctx->ktime.end() ? 0 : it->second.second;
+    return VC_OK;
+}
+
+int vc_ctx_reset_timing(vc_ctx* ctx) {
+    if (!ctx) return VC_E_INVALID;
+    Guard g(ctx);
+    ctx->ktime.clear();
+    return VC_OK;
+}
+
+int vc_bases_upload(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id) {
+    if (!ctx || !id || (n > 0 && !xy) || n >= 0x7fffffffu) return VC_E_INVALID;
+    Guard g(ctx);
+    return vk::bases_upload(ctx, xy, inf, n, id);
+}
+
+int vc_bases_count(vc_ctx* ctx, int id, size_t* n) {
+    if (!ctx || !n) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    *n = t->n;
+    return VC_OK;
+}
+
+int vc_bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id) {
+    if (!ctx || !id || n >= 0x7fffffffu) return VC_E_INVALID;
+    Guard g(ctx);
+    return vk::bases_random(ctx, seed, n, id);
+}
+
+int vc_bases_download(vc_ctx* ctx, int id, uint64_t* xy, uint8_t* inf) {
+    if (!ctx || !xy) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    return vk::bases_download(ctx, t, xy, inf);
+}
+
+int vc_point_words(int curve) { return valid_curve(curve) ? vk::point_words(curve) : VC_E_INVALID; }
+
+static int msm_device_acc(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont,
+                          uint32_t* acc) {
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    if (offset > t->n || n > t->n - offset) return VC_E_RANGE;
+    if (n > 0 && !d_sc) return VC_E_INVALID;
+    return vk::msm_run(ctx, t, offset, d_sc, n, mont, acc);
+}
+
+int vc_msm_device_partial(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont,
+                          uint32_t* out_acc) {
+    if (!ctx || !out_acc) return VC_E_INVALID;
+    Guard g(ctx);
+    return msm_device_acc(ctx, id, offset, d_sc, n, mont, out_acc);
+}
+
+int vc_msm_device(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont,
+                  uint64_t* out_xy, uint8_t* out_inf) {
+    if (!ctx || !out_xy || !out_inf) return VC_E_INVALID;
+    Guard g(ctx);
+    std::vector<uint32_t> acc(vk::point_words(ctx->curve));
+    VK_TRY(msm_device_acc(ctx, id, offset, d_sc, n, mont, acc.data()));
+    return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
+}
+
+int vc_msm(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n, int mont,
+           uint64_t* out_xy, uint8_t* out_inf) {
+    if (!ctx || !out_xy || !out_inf || (n > 0 && !scalars)) return VC_E_INVALID;
+    Guard g(ctx);
+    if (n > 0) {
+        VK_TRY(ctx->ws[vk::WS_SCALARS].ensure(n * 32));
+        VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[vk::WS_SCALARS].p, scalars, n * 32, hipMemcpyHostToDevice,
+                                    ctx->stream));
+    }
+    std::vector<uint32_t> acc(vk::point_words(ctx->curve));
+    VK_TRY(msm_device_acc(ctx, id, offset, ctx->ws[vk::WS_SCALARS].p, n, mont, acc.data()));
+    return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
+}
+
+int vc_partials_sum(int curve, const uint32_t* accs, size_t k, uint64_t* out_xy, uint8_t* out_inf) {
+    if (!valid_curve(curve) || (k > 0 && !accs) || !out_xy || !out_inf) return VC_E_INVALID;
+    std::vector<uint32_t> acc(vk::point_words(curve));
+    VK_TRY(vk::acc_sum(curve, accs, k, acc.data()));
+    return vk::acc_to_affine(curve, acc.data(), out_xy, out_inf);
+}
+
+int vc_fixed_base_precompute(vc_ctx* ctx, int id, int window_bits) {
+    if (!ctx) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    return vk::fixed_base_precompute(ctx, t, window_bits);
+}
+
+int vc_msm_batch_device(vc_ctx* ctx, int id, size_t width, const void* d_sc, size_t batch, int mont,
+                        void* d_out_xy, uint8_t* d_out_inf) {
+    if (!ctx || (batch > 0 && (!d_sc || !d_out_xy || !d_out_inf)) || width == 0) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    VK_TRY(vk::msm_batch_run(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+int vc_msm_batch(vc_ctx* ctx, int id, size_t width, const uint64_t* scalars, size_t batch, int mont,
+                 uint64_t* out_xy, uint8_t* out_inf) {
+    if (!ctx || (batch > 0 && (!scalars || !out_xy || !out_inf)) || width == 0) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    if (batch == 0) return VC_OK;
+    const size_t nl = (size_t)vk::aff_limbs64(ctx->curve);
+    VK_TRY(ctx->ws[vk::WS_SCALARS].ensure(batch * width * 32));
+    VK_TRY(ctx->ws[vk::WS_MISC].ensure(batch * (2 * nl * 8 + 1)));
+    uint8_t* dxy = ctx->ws[vk::WS_MISC].as<uint8_t>();
+    uint8_t* dinf = dxy + batch * 2 * nl * 8;
+    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[vk::WS_SCALARS].p, scalars, batch * width * 32,
+                                hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(vk::msm_batch_run(ctx, t, width, ctx->ws[vk::WS_SCALARS].p, batch, mont, dxy, dinf));
+    VK_CHECK_HIP(hipMemcpyAsync(out_xy, dxy, batch * 2 * nl * 8, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipMemcpyAsync(out_inf, dinf, batch, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,281 @@
+// Batched fixed-base commits: thousands of width-w commitments against one small CRS
+// (IPA::commit ipa/mod.rs:130-135 at N = 256; verkle Node::gen_commitment node.rs:243-271;
+// the commit phase of prove_multiproof multiproof.rs:151,168). Config 3 of BASELINE.json.
+//
+// MI355X-first design: the bases never change, so each base G_i gets a window table
+//     T[i][w][k] = (k+1) * 2^(c*w) * G_i     (affine, Montgomery; k < 2^(c-1))
+// held in HBM (width 256, c = 8: 67 MB BN254 / 100 MB Bandersnatch -- L3-resident; c = 16:
+// 8.6-13 GB, which only a 288 GB part can afford). A commit is then sum over (i, w) of
+// +-T[i][w][|d_iw|-1]: W mixed adds per base, no doublings, no buckets, no cross-block
+// reduction. TPC lanes share one commit (strided over bases, so scalar loads coalesce)
+// and fold their partial sums with cross-lane shuffles; results are normalised with one
+// workgroup-level batch inversion per 256 commits.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+#include "ec.hpp"
+
+namespace vk {
+
+template <class Fr>
+__device__ __forceinline__ fe<Fr> load_scalar_fb(const uint32_t* __restrict__ sc, size_t i) {
+    const uint4* p = reinterpret_cast<const uint4*>(sc + 8 * i);
+    uint4 a = p[0], b = p[1];
+    fe<Fr> s;
+    s.v[0] = a.x; s.v[1] = a.y; s.v[2] = a.z; s.v[3] = a.w;
+    s.v[4] = b.x; s.v[5] = b.y; s.v[6] = b.z; s.v[7] = b.w;
+    return s;
+}
+
+template <class C>
+__device__ typename C::Acc mul_small_fb(const typename C::Acc& p, uint32_t k) {
+    typename C::Acc r = C::zero();
+    if (k == 0) return r;
+    int top = 31 - __builtin_clz(k);
+    r = p;
+    for (int i = top - 1; i >= 0; i--) {
+        r = C::dbl(r);
+        if ((k >> i) & 1) r = C::add(r, p);
+    }
+    return r;
+}
+
+// Q[i] = 2^(c*w) * G_i for the given window (chained: caller passes the previous window)
+template <class C>
+__global__ void k_fb_shift(typename C::Acc* __restrict__ Q, const typename C::Aff* __restrict__ bases,
+                           uint32_t n, int c, int first) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    typename C::Acc q;
+    if (first) q = C::from_aff(bases[i], false);
+    else {
+        q = Q[i];
+        for (int k = 0; k < c; k++) q = C::dbl(q);
+    }
+    Q[i] = q;
+}
+
+// tmp[i][k] = (k+1) * Q[i], chunks of CH consecutive k per thread
+template <class C>
+__global__ void k_fb_fill(const typename C::Acc* __restrict__ Q, uint32_t n, uint32_t NBk, uint32_t CH,
+                          typename C::Acc* __restrict__ tmp) {
+    uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nch = (NBk + CH - 1) / CH;
+    uint32_t i = gid / nch, ch = gid % nch;
+    if (i >= n) return;
+    typename C::Acc q = Q[i];
+    uint32_t k0 = ch * CH, k1 = min(k0 + CH, NBk);
+    typename C::Acc p = mul_small_fb<C>(q, k0 + 1);
+    for (uint32_t k = k0; k < k1; k++) {
+        tmp[(size_t)i * NBk + k] = p;
+        p = C::add(p, q);
+    }
+}
+
+// ------------------------------------------------------------------ batch normalisation
+// One workgroup normalises 256 consecutive accumulators with one field inversion:
+// prefix/suffix products by LDS scans, inv_j = inv(prod) * prefix_{j-1} * suffix_{j+1}.
+template <class C>
+__device__ __forceinline__ fe<typename C::F> denom(const typename C::Acc& a) {
+    if constexpr (C::is_te) return a.Z;
+    else return a.zzz;
+}
+
+template <class C>
+__global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __restrict__ in, size_t count,
+                                                  typename C::Aff* __restrict__ out_aff,
+                                                  uint32_t* __restrict__ out_canon,
+                                                  uint8_t* __restrict__ out_inf) {
+    using F = typename C::F;
+    __shared__ fe<F> pre[256];
+    __shared__ fe<F> suf[256];
+    size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t tid = threadIdx.x;
+    typename C::Acc a = j < count ? in[j] : C::zero();
+    bool ident = C::is_zero(a);
+    fe<F> z = (j < count && !ident) ? denom<C>(a) : fe_one<F>();
+    if constexpr (!C::is_te) {
+        if (ident) z = fe_one<F>();
+    }
+    pre[tid] = z;
+    suf[tid] = z;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        fe<F> p = pre[tid], s = suf[tid];
+        if (tid >= off) p = fe_mul<F>(pre[tid - off], p);
+        if (tid + off < 256) s = fe_mul<F>(s, suf[tid + off]);
+        __syncthreads();
+        pre[tid] = p;
+        suf[tid] = s;
+        __syncthreads();
+    }
+    __shared__ fe<F> tinv;
+    if (tid == 0) tinv = fe_inv<F>(pre[255]);
+    __syncthreads();
+    fe<F> iz = tinv;
+    if (tid > 0) iz = fe_mul<F>(iz, pre[tid - 1]);
+    if (tid < 255) iz = fe_mul<F>(iz, suf[tid + 1]);
+    if (j >= count) return;
+    fe<F> x, y;
+    if constexpr (C::is_te) {
+        x = fe_mul<F>(a.X, iz);
+        y = fe_mul<F>(a.Y, iz);
+        ident = fe_is_zero<F>(x) && fe_eq<F>(y, fe_one<F>());
+    } else {
+        fe<F> t = fe_mul<F>(iz, a.zz);  // 1/Z
+        x = fe_mul<F>(a.x, fe_sqr<F>(t));
+        y = fe_mul<F>(a.y, iz);
+    }
+    if (out_aff) {
+        typename C::Aff r;
+        r.x = x;
+        r.y = y;
+        if constexpr (C::is_te) r.kt = fe_mul<F>(fe_mul<F>(x, y), C::d());
+        out_aff[j] = r;
+    }
+    if (out_canon) {
+        fe<F> cx = fe_from_mont<F>(x), cy = fe_from_mont<F>(y);
+        if (ident && !C::is_te) {
+            cx = fe_zero<F>();
+            cy = fe_zero<F>();
+        }
+#pragma unroll
+        for (int k = 0; k < F::N; k++) {
+            out_canon[j * 2 * F::N + k] = cx.v[k];
+            out_canon[j * 2 * F::N + F::N + k] = cy.v[k];
+        }
+    }
+    if (out_inf) out_inf[j] = ident ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ the batched commit
+template <class C, class Fr>
+__global__ void __launch_bounds__(256) k_fb_commit(const typename C::Aff* __restrict__ tab,
+                                                  const uint8_t* __restrict__ inf, uint32_t width,
+                                                  int c, int W, const uint32_t* __restrict__ sc,
+                                                  uint32_t batch, int mont, int tpc,
+                                                  typename C::Acc* __restrict__ out) {
+    using Acc = typename C::Acc;
+    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t g = gtid / tpc, sub = gtid % tpc;
+    const uint32_t NBk = 1u << (c - 1);
+    const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
+    Acc acc = C::zero();
+    if (g < batch) {
+        for (uint32_t i = sub; i < width; i += tpc) {
+            if (inf[i]) continue;
+            fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
+            if (mont) s = fe_from_mont<Fr>(s);
+            const typename C::Aff* ti = tab + (size_t)i * W * NBk;
+            uint32_t carry = 0;
+            for (int w = 0; w < W; w++) {
+                uint32_t raw = (s.v[0] & mask) + carry;
+#pragma unroll
+                for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
+                s.v[7] >>= c;
+                carry = raw > half ? 1u : 0u;
+                int32_t d = carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
+                if (d != 0) {
+                    uint32_t a = (uint32_t)(d < 0 ? -d : d) - 1;
+                    acc = C::madd(acc, ti[(size_t)w * NBk + a], d < 0);
+                }
+            }
+        }
+    }
+    // fold the tpc partial sums of one commit (tpc is a power of two <= 64)
+    for (int m = tpc >> 1; m > 0; m >>= 1) {
+        Acc o;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&acc);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+        for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
+        acc = C::add(acc, o);
+    }
+    if (sub == 0 && g < batch) out[g] = acc;
+}
+
+// ------------------------------------------------------------------ host drivers
+template <class C>
+static int fb_precompute_t(vc_ctx* ctx, Table* t, int c) {
+    using Acc = typename C::Acc;
+    using Aff = typename C::Aff;
+    using Fr = typename std::conditional<std::is_same<C, BN254G1>::value, BN254Fr,
+                                         typename std::conditional<std::is_same<C, BLS381G1>::value, BLS381Fr,
+                                                                   BandFr>::type>::type;
+    if (c < 4 || c > 16) return VC_E_INVALID;
+    const uint32_t n = (uint32_t)t->n;
+    const int W = (Fr::BITS + 1 + c - 1) / c;
+    const uint32_t NBk = 1u << (c - 1);
+    if (t->fb_c == c && t->fb.p) return VC_OK;
+    t->fb.release();
+    VK_TRY(t->fb.ensure(std::max<size_t>((size_t)n * W * NBk, 1) * sizeof(Aff)));
+    DevBuf Q, tmp, aff_w;
+    VK_TRY(Q.ensure(std::max<uint32_t>(n, 1) * sizeof(Acc)));
+    VK_TRY(tmp.ensure(std::max<size_t>((size_t)n * NBk, 1) * sizeof(Acc)));
+    VK_TRY(aff_w.ensure(std::max<size_t>((size_t)n * NBk, 1) * sizeof(Aff)));
+    const uint32_t CH = NBk >= 64 ? 64 : NBk;
+    const uint32_t nch = (NBk + CH - 1) / CH;
+    for (int w = 0; w < W; w++) {
+        VK_LAUNCH(ctx, "fb_shift", (k_fb_shift<C>), (n + 255) / 256, 256, 0, Q.as<Acc>(),
+                  t->bases.as<Aff>(), n, c, w == 0 ? 1 : 0);
+        VK_LAUNCH(ctx, "fb_fill", (k_fb_fill<C>), ((size_t)n * nch + 127) / 128, 128, 0, Q.as<Acc>(), n,
+                  NBk, CH, tmp.as<Acc>());
+        size_t cnt = (size_t)n * NBk;
+        VK_LAUNCH(ctx, "fb_normalize", (k_normalize<C>), (cnt + 255) / 256, 256, 0, tmp.as<Acc>(), cnt,
+                  aff_w.as<Aff>(), (uint32_t*)nullptr, (uint8_t*)nullptr);
+        // scatter window w into T[i][w][k]
+        VK_CHECK_HIP(hipMemcpy2DAsync(t->fb.as<Aff>() + (size_t)w * NBk, (size_t)W * NBk * sizeof(Aff),
+                                      aff_w.p, (size_t)NBk * sizeof(Aff), (size_t)NBk * sizeof(Aff), n,
+                                      hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    t->fb_c = c;
+    t->fb_W = W;
+    return VC_OK;
+}
+
+template <class C, class Fr>
+static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
+                       void* d_out_xy, uint8_t* d_out_inf) {
+    using Acc = typename C::Acc;
+    if (width > t->n) return VC_E_RANGE;
+    if (!t->fb.p) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
+    if (batch == 0) return VC_OK;
+    VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
+    int tpc = 16;
+    while (tpc > 1 && (size_t)tpc > width) tpc >>= 1;
+    size_t threads = batch * (size_t)tpc;
+    VK_LAUNCH(ctx, "fb_commit", (k_fb_commit<C, Fr>), (threads + 255) / 256, 256, 0,
+              t->fb.as<typename C::Aff>(), t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, t->fb_W,
+              reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, tpc,
+              ctx->ws[WS_OUT].as<Acc>());
+    VK_LAUNCH(ctx, "fb_normalize_out", (k_normalize<C>), (batch + 255) / 256, 256, 0,
+              ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
+              reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);
+    return VC_OK;
+}
+
+int fixed_base_precompute(vc_ctx* ctx, Table* t, int c) {
+    switch (t->curve) {
+        case VC_CURVE_BN254: return fb_precompute_t<BN254G1>(ctx, t, c);
+        case VC_CURVE_BLS12_381: return fb_precompute_t<BLS381G1>(ctx, t, c);
+        case VC_CURVE_BANDERSNATCH: return fb_precompute_t<Bandersnatch>(ctx, t, c);
+    }
+    return VC_E_INVALID;
+}
+
+int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
+                  void* d_out_xy, uint8_t* d_out_inf) {
+    switch (t->curve) {
+        case VC_CURVE_BN254: return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf);
+        case VC_CURVE_BLS12_381: return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf);
+        case VC_CURVE_BANDERSNATCH: return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf);
+    }
+    return VC_E_INVALID;
+}
+
+}  // namespace vk

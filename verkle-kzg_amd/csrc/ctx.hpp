@@ -1,0 +1,130 @@
+// Engine context: one device, one stream, base tables, grow-only workspaces, kernel timers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/vc_msm.h"
+
+#define VK_CHECK_HIP(expr)                              \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) {                         \
+            vk::last_hip_error() = e_;                  \
+            return e_ == hipErrorOutOfMemory ? VC_E_OOM : VC_E_HIP; \
+        }                                               \
+    } while (0)
+
+#define VK_TRY(expr)            \
+    do {                        \
+        int s_ = (expr);        \
+        if (s_ != VC_OK) return s_; \
+    } while (0)
+
+namespace vk {
+
+hipError_t& last_hip_error();
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes);
+    void release();
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+    ~DevBuf() { release(); }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+};
+
+struct Table {
+    int curve = 0;
+    size_t n = 0;
+    DevBuf bases;  // n x Aff (Montgomery)
+    DevBuf inf;    // n x u8
+    // fixed-base window tables for batched commits
+    int fb_c = 0, fb_W = 0;
+    DevBuf fb;
+};
+
+enum WsSlot {
+    WS_DIGITS = 0,
+    WS_COUNTS,
+    WS_OFFSETS,
+    WS_CURSOR,
+    WS_SORTED,
+    WS_BUCKETS,
+    WS_CARRY,
+    WS_THROUGH,
+    WS_OWNER,
+    WS_OWNER_B,
+    WS_SEG,
+    WS_WIN,
+    WS_SCAN_TMP,
+    WS_SCALARS,
+    WS_OUT,
+    WS_MISC,
+    WS_COUNT_
+};
+
+struct PendingTimer {
+    hipEvent_t a, b;
+    std::string name;
+};
+
+}  // namespace vk
+
+struct vc_ctx {
+    int curve = 0;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    std::mutex mu;
+    std::vector<vk::Table*> tables;
+    vk::DevBuf ws[vk::WS_COUNT_];
+    bool timing = false;
+    std::vector<vk::PendingTimer> pending;
+    std::vector<hipEvent_t> event_pool;
+    std::map<std::string, std::pair<double, long>> ktime;
+
+    hipEvent_t get_event();
+    void timer_begin(const char* name, hipEvent_t* a);
+    void timer_end(const char* name, hipEvent_t a);
+    void collect_timers();  // call after the stream is synchronised
+    vk::Table* table(int id) {
+        if (id < 0 || id >= (int)tables.size() || !tables[id]) return nullptr;
+        return tables[id];
+    }
+};
+
+// launch helper: records HIP events around the launch when timing is on
+#define VK_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                          \
+    do {                                                                             \
+        hipEvent_t ev_a_ = nullptr;                                                  \
+        if ((ctx)->timing) (ctx)->timer_begin(name, &ev_a_);                         \
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), shmem, (ctx)->stream, __VA_ARGS__); \
+        if ((ctx)->timing) (ctx)->timer_end(name, ev_a_);                            \
+        VK_CHECK_HIP(hipGetLastError());                                             \
+    } while (0)
+
+namespace vk {
+// implemented per translation unit with explicit instantiations
+int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
+            uint32_t* out_acc_words /*host, projective, vc_point_words*/);
+int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out_inf);
+int acc_sum(int curve, const uint32_t* accs, size_t k, uint32_t* out);
+int point_words(int curve);
+int aff_limbs64(int curve);  // NL of the base field in u64 limbs
+int bases_upload(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id);
+int bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id);
+int bases_download(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf);
+int fixed_base_precompute(vc_ctx* ctx, Table* t, int c);
+int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
+                  int mont, void* d_out_xy, uint8_t* d_out_inf);
+}  // namespace vk

@@ -1,0 +1,252 @@
+// Prime-field arithmetic for gfx950 (and host, for conversions): Montgomery form over
+// 32-bit limbs. The VALU has no 64x64 multiply; the native wide product is
+// v_mad_u64_u32 (32x32+64 -> 64), so limbs are 32 bits and every product is one mad.
+//
+// Multiplication is "no-carry" CIOS (valid because every modulus here has its top limb
+// < 2^31 - 1: BN254 Fq/Fr, BLS12-381 Fq/Fr, Bandersnatch Fr), fully unrolled so the
+// modulus limbs become instruction literals.
+//
+// Field parameter structs (N, p(i), inv, r2(i), one(i)) are at the bottom.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VK_HD __host__ __device__ __forceinline__
+
+namespace vk {
+
+template <class F>
+struct fe {
+    uint32_t v[F::N];
+};
+
+// ---------------------------------------------------------------- helpers
+template <class F>
+VK_HD fe<F> fe_zero() {
+    fe<F> r;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) r.v[i] = 0;
+    return r;
+}
+template <class F>
+VK_HD fe<F> fe_one() {
+    fe<F> r;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) r.v[i] = F::one(i);
+    return r;
+}
+template <class F>
+VK_HD bool fe_is_zero(const fe<F>& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) o |= a.v[i];
+    return o == 0;
+}
+template <class F>
+VK_HD bool fe_eq(const fe<F>& a, const fe<F>& b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) o |= a.v[i] ^ b.v[i];
+    return o == 0;
+}
+
+// r = a - p if a >= p (a < 2p)
+template <class F>
+VK_HD fe<F> fe_reduce_once(const fe<F>& a) {
+    fe<F> t;
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+        uint64_t d = (uint64_t)a.v[i] - F::p(i) - borrow;
+        t.v[i] = (uint32_t)d;
+        borrow = (uint32_t)(d >> 63);
+    }
+    fe<F> r;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) r.v[i] = borrow ? a.v[i] : t.v[i];
+    return r;
+}
+
+template <class F>
+VK_HD fe<F> fe_add(const fe<F>& a, const fe<F>& b) {
+    fe<F> s;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+        uint64_t t = (uint64_t)a.v[i] + b.v[i] + c;
+        s.v[i] = (uint32_t)t;
+        c = (uint32_t)(t >> 32);
+    }
+    return fe_reduce_once<F>(s);  // a+b < 2p < 2^(32N): no carry out
+}
+
+template <class F>
+VK_HD fe<F> fe_sub(const fe<F>& a, const fe<F>& b) {
+    fe<F> d;
+    uint32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+        uint64_t t = (uint64_t)a.v[i] - b.v[i] - borrow;
+        d.v[i] = (uint32_t)t;
+        borrow = (uint32_t)(t >> 63);
+    }
+    // add back p masked by borrow
+    uint32_t mask = 0u - borrow;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+        uint64_t t = (uint64_t)d.v[i] + (F::p(i) & mask) + c;
+        d.v[i] = (uint32_t)t;
+        c = (uint32_t)(t >> 32);
+    }
+    return d;
+}
+
+template <class F>
+VK_HD fe<F> fe_dbl(const fe<F>& a) {
+    return fe_add<F>(a, a);
+}
+
+template <class F>
+VK_HD fe<F> fe_neg(const fe<F>& a) {
+    return fe_sub<F>(fe_zero<F>(), a);
+}
+
+// no-carry CIOS Montgomery multiplication: r = a*b*2^(-32N) mod p.
+// On the device it is an out-of-line call: a fully inlined 12-limb multiply is ~600
+// instructions, and an EC add holds 10-16 of them -- inlining every one blows the
+// instruction cache (and compile time) for no gain.
+#define VK_MUL_ATTR __host__ __device__ __noinline__
+template <class F>
+VK_MUL_ATTR fe<F> fe_mul(const fe<F> a, const fe<F> b) {
+    constexpr int N = F::N;
+    uint32_t t[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint64_t A = (uint64_t)a.v[0] * b.v[i] + t[0];
+        t[0] = (uint32_t)A;
+        uint32_t m = t[0] * F::inv;
+        uint64_t C = (uint64_t)m * F::p(0) + t[0];
+#pragma unroll
+        for (int j = 1; j < N; j++) {
+            A = (uint64_t)a.v[j] * b.v[i] + t[j] + (A >> 32);
+            C = (uint64_t)m * F::p(j) + (uint32_t)A + (C >> 32);
+            t[j - 1] = (uint32_t)C;
+        }
+        t[N - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+    }
+    fe<F> r;
+#pragma unroll
+    for (int j = 0; j < N; j++) r.v[j] = t[j];
+    return fe_reduce_once<F>(r);
+}
+
+template <class F>
+VK_HD fe<F> fe_sqr(const fe<F>& a) {
+    return fe_mul<F>(a, a);
+}
+
+// canonical -> Montgomery
+template <class F>
+VK_HD fe<F> fe_to_mont(const fe<F>& a) {
+    fe<F> r2;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) r2.v[i] = F::r2(i);
+    return fe_mul<F>(a, r2);
+}
+// Montgomery -> canonical
+template <class F>
+VK_HD fe<F> fe_from_mont(const fe<F>& a) {
+    fe<F> one = fe_zero<F>();
+    one.v[0] = 1;
+    return fe_mul<F>(a, one);
+}
+
+// a^(p-2) (slow; only for rare normalisations)
+template <class F>
+VK_HD fe<F> fe_inv(const fe<F>& a) {
+    // exponent p - 2 with the borrow propagated (BLS12-381 Fr has p[0] == 1)
+    uint32_t e_limbs[F::N];
+    uint32_t borrow = 2;
+    for (int i = 0; i < F::N; i++) {
+        uint64_t d = (uint64_t)F::p(i) - borrow;
+        e_limbs[i] = (uint32_t)d;
+        borrow = (uint32_t)(d >> 63);
+    }
+    fe<F> acc = fe_one<F>();
+    for (int i = F::N - 1; i >= 0; i--) {
+        uint32_t e = e_limbs[i];
+        for (int b = 31; b >= 0; b--) {
+            acc = fe_sqr<F>(acc);
+            if ((e >> b) & 1) acc = fe_mul<F>(acc, a);
+        }
+    }
+    return acc;
+}
+
+// small-constant multiple (k <= 8) via additions
+template <class F, int K>
+VK_HD fe<F> fe_mul_small(const fe<F>& a) {
+    static_assert(K >= 1 && K <= 8, "");
+    if (K == 1) return a;
+    if (K == 2) return fe_dbl<F>(a);
+    if (K == 3) return fe_add<F>(fe_dbl<F>(a), a);
+    if (K == 4) return fe_dbl<F>(fe_dbl<F>(a));
+    if (K == 5) return fe_add<F>(fe_dbl<F>(fe_dbl<F>(a)), a);
+    if (K == 8) return fe_dbl<F>(fe_dbl<F>(fe_dbl<F>(a)));
+    fe<F> r = a;
+    for (int i = 1; i < K; i++) r = fe_add<F>(r, a);
+    return r;
+}
+
+// ---------------------------------------------------------------- parameter sets
+#define VK_LIMBS(...)                                  \
+    {                                                  \
+        constexpr uint32_t v[] = {__VA_ARGS__};        \
+        return v[i];                                   \
+    }
+
+struct BN254Fq {
+    static constexpr int N = 8;
+    static constexpr uint32_t inv = 0xe4866389u;
+    VK_HD static constexpr uint32_t p(int i) VK_LIMBS(0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u, 0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u)
+    VK_HD static constexpr uint32_t r2(int i) VK_LIMBS(0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u, 0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u)
+    VK_HD static constexpr uint32_t one(int i) VK_LIMBS(0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u, 0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u)
+};
+struct BN254Fr {
+    static constexpr int N = 8;
+    static constexpr int BITS = 254;
+    static constexpr uint32_t inv = 0xefffffffu;
+    VK_HD static constexpr uint32_t p(int i) VK_LIMBS(0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u, 0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u)
+    VK_HD static constexpr uint32_t r2(int i) VK_LIMBS(0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u, 0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u)
+    VK_HD static constexpr uint32_t one(int i) VK_LIMBS(0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u, 0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u)
+};
+struct BLS381Fq {
+    static constexpr int N = 12;
+    static constexpr uint32_t inv = 0xfffcfffdu;
+    VK_HD static constexpr uint32_t p(int i) VK_LIMBS(0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau)
+    VK_HD static constexpr uint32_t r2(int i) VK_LIMBS(0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u, 0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, 0x67eb88a9u, 0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u)
+    VK_HD static constexpr uint32_t one(int i) VK_LIMBS(0x0002fffdu, 0x76090000u, 0xc40c0002u, 0xebf4000bu, 0x53c758bau, 0x5f489857u, 0x70525745u, 0x77ce5853u, 0xa256ec6du, 0x5c071a97u, 0xfa80e493u, 0x15f65ec3u)
+};
+// BLS12-381 Fr == Bandersnatch base field
+struct BLS381Fr {
+    static constexpr int N = 8;
+    static constexpr int BITS = 255;
+    static constexpr uint32_t inv = 0xffffffffu;
+    VK_HD static constexpr uint32_t p(int i) VK_LIMBS(0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u, 0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u)
+    VK_HD static constexpr uint32_t r2(int i) VK_LIMBS(0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu, 0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u)
+    VK_HD static constexpr uint32_t one(int i) VK_LIMBS(0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau, 0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u)
+};
+struct BandFr {
+    static constexpr int N = 8;
+    static constexpr int BITS = 253;
+    static constexpr uint32_t inv = 0x5cc063dfu;
+    VK_HD static constexpr uint32_t p(int i) VK_LIMBS(0x2876e7e1u, 0x74fd06b5u, 0x74190471u, 0xff8f8700u, 0x02687600u, 0x0cce7602u, 0xca675f52u, 0x1cfb69d4u)
+    VK_HD static constexpr uint32_t r2(int i) VK_LIMBS(0x58db47cbu, 0xdbb4f5d6u, 0x7fecb938u, 0x40fa7ca2u, 0xc0055ceau, 0xaa9e6daeu, 0xb14aec7du, 0x0ae793ddu)
+    VK_HD static constexpr uint32_t one(int i) VK_LIMBS(0xbc48c0f8u, 0x5817ca56u, 0x5f37dc74u, 0x0383c7fcu, 0xecbc4ff8u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u)
+};
+#undef VK_LIMBS
+
+}  // namespace vk

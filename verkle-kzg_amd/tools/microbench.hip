@@ -1,0 +1,69 @@
+// Field-multiply and v_mad_u64_u32 throughput microbenchmark (gfx950). Prints JSON lines.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "../csrc/ff.hpp"
+using namespace vk;
+
+__global__ void k_mad(uint32_t* out, uint32_t seed, int iters) {
+    uint32_t x = seed + threadIdx.x, y = seed * 3 + blockIdx.x;
+    uint64_t a0 = x, a1 = y, a2 = x ^ y, a3 = x + y, a4 = 5, a5 = 7, a6 = 9, a7 = 11;
+    for (int i = 0; i < iters; i++) {
+#define M(a) a = (uint64_t)(uint32_t)a * x + (a >> 32);
+        M(a0) M(a1) M(a2) M(a3) M(a4) M(a5) M(a6) M(a7)
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
+}
+
+template <class F>
+__global__ void k_fmul(uint32_t* out, uint32_t seed, int iters) {
+    fe<F> a, b, c, d;
+    for (int i = 0; i < F::N; i++) {
+        a.v[i] = seed * (i + 1) + threadIdx.x;
+        b.v[i] = seed ^ (i * 77);
+        c.v[i] = i + blockIdx.x;
+        d.v[i] = seed + i;
+    }
+    a.v[F::N - 1] &= 0xfffff; b.v[F::N - 1] &= 0xfffff; c.v[F::N - 1] &= 0xfffff; d.v[F::N - 1] &= 0xfffff;
+    for (int i = 0; i < iters; i++) {
+        a = fe_mul<F>(a, b);
+        c = fe_mul<F>(c, d);
+        b = fe_mul<F>(b, c);
+        d = fe_mul<F>(d, a);
+    }
+    uint32_t r = 0;
+    for (int i = 0; i < F::N; i++) r ^= a.v[i] ^ b.v[i] ^ c.v[i] ^ d.v[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
+template <class K>
+static double timeit(K kern, int blocks, int iters, uint32_t* out) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
+    hipDeviceSynchronize();
+    hipEventRecord(a);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
+
+int main() {
+    uint32_t* out;
+    int blocks = 256 * 16;
+    hipMalloc(&out, blocks * 256 * 4);
+    double ms = timeit(k_mad, blocks, 4096, out);
+    double mads = (double)blocks * 256 * 4096 * 8;
+    printf("{\"bench\":\"v_mad_u64_u32\",\"ms\":%.3f,\"Gop_per_s\":%.1f}\n", ms, mads / ms / 1e6);
+    ms = timeit(k_fmul<BLS381Fq>, blocks, 256, out);
+    double muls = (double)blocks * 256 * 256 * 4;
+    printf("{\"bench\":\"fe_mul_bls381_fq_12limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
+    ms = timeit(k_fmul<BLS381Fr>, blocks, 256, out);
+    printf("{\"bench\":\"fe_mul_bls381_fr_8limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
+    ms = timeit(k_fmul<BN254Fq>, blocks, 256, out);
+    printf("{\"bench\":\"fe_mul_bn254_fq_8limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
+    return 0;
+}

@@ -1,0 +1,84 @@
+"""ctypes binding of libvkzg.so (C ABI: include/vc_msm.h).
+
+The product path: every call goes to the HIP engine. There is no CPU fallback -- if the
+library is missing this raises, and on a GPU box a failing device raises too.
+"""
+import ctypes
+import os
+import re
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(_PKG)
+LIB_PATH = os.path.join(ROOT, "lib", "libvkzg.so")
+HEADER = os.path.join(os.path.dirname(ROOT), "include", "vc_msm.h")
+
+c_void_p, c_int, c_size_t, c_uint64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
+c_double, c_long, c_char_p = ctypes.c_double, ctypes.c_long, ctypes.c_char_p
+P = ctypes.c_void_p
+
+SIGNATURES = {
+    "vc_strerror": (c_char_p, [c_int]),
+    "vc_version": (c_int, []),
+    "vc_ctx_create": (c_int, [c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "vc_ctx_destroy": (None, [c_void_p]),
+    "vc_ctx_curve": (c_int, [c_void_p]),
+    "vc_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
+    "vc_ctx_enable_timing": (c_int, [c_void_p, c_int]),
+    "vc_ctx_kernel_time": (c_int, [c_void_p, c_char_p, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
+    "vc_ctx_reset_timing": (c_int, [c_void_p]),
+    "vc_bases_upload": (c_int, [c_void_p, P, P, c_size_t, ctypes.POINTER(c_int)]),
+    "vc_bases_count": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
+    "vc_bases_random": (c_int, [c_void_p, c_uint64, c_size_t, ctypes.POINTER(c_int)]),
+    "vc_bases_download": (c_int, [c_void_p, c_int, P, P]),
+    "vc_msm": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_msm_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_point_words": (c_int, [c_int]),
+    "vc_msm_device_partial": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P]),
+    "vc_partials_sum": (c_int, [c_int, P, c_size_t, P, P]),
+    "vc_msm_batch": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_msm_batch_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_fixed_base_precompute": (c_int, [c_void_p, c_int, c_int]),
+}
+
+_lib = None
+
+
+class VCError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        msg = lib().vc_strerror(status)
+        super().__init__(f"{where}: {msg.decode() if msg else status} (status {status})")
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libvkzg.so not built at {LIB_PATH}: run `make -C verkle-kzg_amd` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7. Loading torch
+        # first makes libvkzg.so bind to that copy (same soname), so engine buffers and
+        # torch tensors/streams/RCCL share one runtime. Importing torch does not touch the GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status, where):
+    if status != 0:
+        raise VCError(status, where)
+
+
+def header_functions():
+    """Names of every function declared in include/vc_msm.h."""
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vc_[a-z0-9_]+)\s*\(", src)))

@@ -1,0 +1,202 @@
+"""Python handle on the HIP MSM engine (thin wrapper over include/vc_msm.h).
+
+Layouts follow the C ABI: field elements are canonical little-endian u64 limbs, affine
+points are (x limbs, y limbs) rows plus a u8 identity flag, scalars are 4 u64 limbs.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+
+CURVE_IDS = {"bn254": 0, "bls12_381": 1, "bandersnatch": 2}
+NL = {"bn254": 4, "bls12_381": 6, "bandersnatch": 4}
+# scalar-field moduli (for synthetic data generation and range checks)
+SCALAR_R = {
+    "bn254": 21888242871839275222246405745257275088548364400416034343698204186575808495617,
+    "bls12_381": 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001,
+    "bandersnatch": 13108968793781547619861935127046491459309155893440570251786403306729687672801,
+}
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def ints_to_limbs(vals, nl=4):
+    out = np.zeros((len(vals), nl), dtype=np.uint64)
+    for i, v in enumerate(vals):
+        v = int(v)
+        for j in range(nl):
+            out[i, j] = (v >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
+    return out
+
+
+def limbs_to_int(row):
+    return sum(int(x) << (64 * j) for j, x in enumerate(row))
+
+
+def points_to_arrays(curve, pts):
+    """[(x, y) | None] -> ((n, 2*NL) uint64, (n,) uint8). Edwards identity may be (0, 1)."""
+    nl = NL[curve]
+    arr = np.zeros((len(pts), 2 * nl), dtype=np.uint64)
+    inf = np.zeros(len(pts), dtype=np.uint8)
+    for i, P in enumerate(pts):
+        if P is None:
+            inf[i] = 1
+            continue
+        arr[i, :nl] = ints_to_limbs([P[0]], nl)[0]
+        arr[i, nl:] = ints_to_limbs([P[1]], nl)[0]
+    return arr, inf
+
+
+def arrays_to_points(curve, xy, inf):
+    nl = NL[curve]
+    out = []
+    for i in range(xy.shape[0]):
+        if inf[i]:
+            out.append((0, 1) if curve == "bandersnatch" else None)
+        else:
+            out.append((limbs_to_int(xy[i, :nl]), limbs_to_int(xy[i, nl:])))
+    return out
+
+
+def random_scalars(curve, n, rng):
+    """n scalars below r (top limb drawn below r's top limb): (n, 4) uint64."""
+    r = SCALAR_R[curve]
+    top = r >> 192
+    s = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64, endpoint=False)
+    s[:, 3] = rng.integers(0, top, size=n, dtype=np.uint64)
+    return s
+
+
+class Engine:
+    """One vc_ctx: a curve on one device."""
+
+    def __init__(self, curve, device=0):
+        self.curve = curve
+        self.cid = CURVE_IDS[curve]
+        self.nl = NL[curve]
+        h = ctypes.c_void_p()
+        check(lib().vc_ctx_create(self.cid, device, ctypes.byref(h)), "vc_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().vc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- streams / timing
+    def set_stream(self, stream_handle):
+        check(lib().vc_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)), "vc_ctx_set_stream")
+
+    def enable_timing(self, on=True):
+        check(lib().vc_ctx_enable_timing(self.h, 1 if on else 0), "vc_ctx_enable_timing")
+
+    def reset_timing(self):
+        check(lib().vc_ctx_reset_timing(self.h), "vc_ctx_reset_timing")
+
+    def kernel_time(self, name):
+        ms = ctypes.c_double()
+        cnt = ctypes.c_long()
+        check(lib().vc_ctx_kernel_time(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)),
+              "vc_ctx_kernel_time")
+        return ms.value, cnt.value
+
+    # -------------------------------------------------------------- bases
+    def upload_bases(self, xy, inf=None):
+        xy = np.ascontiguousarray(xy, dtype=np.uint64)
+        assert xy.ndim == 2 and xy.shape[1] == 2 * self.nl
+        if inf is not None:
+            inf = np.ascontiguousarray(inf, dtype=np.uint8)
+            assert inf.shape == (xy.shape[0],)
+        tid = ctypes.c_int()
+        check(lib().vc_bases_upload(self.h, _ptr(xy), _ptr(inf), xy.shape[0], ctypes.byref(tid)),
+              "vc_bases_upload")
+        return tid.value
+
+    def upload_points(self, pts):
+        xy, inf = points_to_arrays(self.curve, pts)
+        return self.upload_bases(xy, inf)
+
+    def random_bases(self, n, seed=0):
+        tid = ctypes.c_int()
+        check(lib().vc_bases_random(self.h, seed, n, ctypes.byref(tid)), "vc_bases_random")
+        return tid.value
+
+    def bases_count(self, table):
+        n = ctypes.c_size_t()
+        check(lib().vc_bases_count(self.h, table, ctypes.byref(n)), "vc_bases_count")
+        return n.value
+
+    def download_bases(self, table):
+        n = self.bases_count(table)
+        xy = np.zeros((n, 2 * self.nl), dtype=np.uint64)
+        inf = np.zeros(n, dtype=np.uint8)
+        check(lib().vc_bases_download(self.h, table, _ptr(xy), _ptr(inf)), "vc_bases_download")
+        return xy, inf
+
+    def fixed_base_precompute(self, table, window_bits=8):
+        check(lib().vc_fixed_base_precompute(self.h, table, window_bits), "vc_fixed_base_precompute")
+
+    # -------------------------------------------------------------- MSM
+    def msm(self, table, scalars, offset=0, mont=False):
+        """scalars: (n, 4) uint64 (or list of ints). Returns ((2*NL,) uint64, inf)."""
+        if not isinstance(scalars, np.ndarray):
+            scalars = ints_to_limbs(scalars, 4)
+        sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+        out = np.zeros(2 * self.nl, dtype=np.uint64)
+        oinf = np.zeros(1, dtype=np.uint8)
+        check(lib().vc_msm(self.h, table, offset, _ptr(sc), sc.shape[0], 1 if mont else 0, _ptr(out),
+                           _ptr(oinf)), "vc_msm")
+        return out, int(oinf[0])
+
+    def msm_point(self, table, scalars, offset=0, mont=False):
+        xy, inf = self.msm(table, scalars, offset, mont)
+        return arrays_to_points(self.curve, xy[None, :], np.array([inf]))[0]
+
+    def msm_device(self, table, d_scalars_ptr, n, offset=0, mont=False):
+        out = np.zeros(2 * self.nl, dtype=np.uint64)
+        oinf = np.zeros(1, dtype=np.uint8)
+        check(lib().vc_msm_device(self.h, table, offset, ctypes.c_void_p(d_scalars_ptr), n,
+                                  1 if mont else 0, _ptr(out), _ptr(oinf)), "vc_msm_device")
+        return out, int(oinf[0])
+
+    def point_words(self):
+        return lib().vc_point_words(self.cid)
+
+    def msm_device_partial(self, table, d_scalars_ptr, n, offset=0, mont=False):
+        acc = np.zeros(self.point_words(), dtype=np.uint32)
+        check(lib().vc_msm_device_partial(self.h, table, offset, ctypes.c_void_p(d_scalars_ptr), n,
+                                          1 if mont else 0, _ptr(acc)), "vc_msm_device_partial")
+        return acc
+
+    def partials_sum(self, accs):
+        accs = np.ascontiguousarray(accs, dtype=np.uint32)
+        out = np.zeros(2 * self.nl, dtype=np.uint64)
+        oinf = np.zeros(1, dtype=np.uint8)
+        check(lib().vc_partials_sum(self.cid, _ptr(accs), accs.shape[0], _ptr(out), _ptr(oinf)),
+              "vc_partials_sum")
+        return out, int(oinf[0])
+
+    def msm_batch(self, table, scalars, width, mont=False):
+        """scalars: (batch*width, 4) uint64. Returns ((batch, 2*NL) uint64, (batch,) uint8)."""
+        sc = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        assert sc.shape[0] % width == 0
+        batch = sc.shape[0] // width
+        out = np.zeros((batch, 2 * self.nl), dtype=np.uint64)
+        oinf = np.zeros(batch, dtype=np.uint8)
+        check(lib().vc_msm_batch(self.h, table, width, _ptr(sc), batch, 1 if mont else 0, _ptr(out),
+                                 _ptr(oinf)), "vc_msm_batch")
+        return out, oinf
+
+    def msm_batch_device(self, table, width, d_scalars_ptr, batch, d_out_xy_ptr, d_out_inf_ptr, mont=False):
+        check(lib().vc_msm_batch_device(self.h, table, width, ctypes.c_void_p(d_scalars_ptr), batch,
+                                        1 if mont else 0, ctypes.c_void_p(d_out_xy_ptr),
+                                        ctypes.c_void_p(d_out_inf_ptr)), "vc_msm_batch_device")
