@@ -1,0 +1,161 @@
+"""CPU tests of the oracle (test infrastructure): curve KATs, C restatement vs Python restatement,
+the committed golden fixtures, and the reference's own round-trip / tamper tests restated
+(ipa/mod.rs:382-421, kzg/mod.rs:278-297, multiproof.rs:261-357)."""
+import json
+import os
+import random
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def P(h):
+    return None if h is None else (int(h[0], 16), int(h[1], 16))
+
+
+def test_curve_kats():
+    from pyoracle.curves import CURVES
+    for C in CURVES.values():
+        assert C.is_on_curve(C.g)
+        assert C.mul(C.g, C.r - 1) == C.neg(C.g)      # r*G = O
+        assert C.add(C.g, C.neg(C.g)) == C.identity()
+    # BN254 generator is (1, 2) (ark-bn254 G1)
+    assert CURVES["bn254"].g == (1, 2)
+
+
+def test_domain_generator():
+    """omega_n = 5^((r-1)/n) has exact order n (precompute.rs:26)."""
+    from pyoracle.protocol import group_gen
+    from pyoracle.curves import BN254
+    w = group_gen(256)
+    assert pow(w, 256, BN254.r) == 1 and pow(w, 128, BN254.r) != 1
+
+
+def test_golden_msm_python_and_c(oracle_c):
+    from pyoracle.curves import CURVES
+    for case in load("msm.json")["cases"]:
+        C = CURVES[case["curve"]]
+        pts = [P(b) for b in case["bases"]]
+        if C.kind == "te":
+            pts = [(0, 1) if p is None else p for p in pts]
+        sc = [int(s, 16) for s in case["scalars"]]
+        want = P(case["expected"])
+        if case["n"] <= 7:
+            assert C.msm(pts, sc) == want
+        got = oracle_c.msm(C.name, pts, sc)
+        if C.kind == "te" and got == (0, 1) and want is None:
+            got = None
+        assert got == want, (case["curve"], case["n"])
+
+
+def test_c_oracle_threads_match(oracle_c):
+    from pyoracle.curves import BLS12_381, random_points
+    rng = random.Random(5)
+    pts = random_points(BLS12_381, 33, rng)
+    sc = [rng.randrange(BLS12_381.r) for _ in pts]
+    assert oracle_c.msm("bls12_381", pts, sc, 1) == oracle_c.msm("bls12_381", pts, sc, 5)
+
+
+def test_golden_transcript():
+    from pyoracle import arkser
+    from pyoracle.curves import BN254
+    g = load("transcript.json")
+    for h in g["hash_to_field"]:
+        assert hex(arkser.hash_to_field(bytes.fromhex(h["msg"]), h["dst"].encode(), BN254.r)) == h["out"]
+    for c in g["compressed"]:
+        p = P(c["point"])
+        assert arkser.ser_point_compressed(p).hex() == c["bytes"]
+        assert hex(arkser.to_data_item(p)) == c["to_data_item"]
+    # compressed flag semantics: bit7 set iff y is the larger root
+    g1 = BN254.g
+    assert arkser.ser_point_compressed(g1)[31] & 0x80 == 0
+    assert arkser.ser_point_compressed(BN254.neg(g1))[31] & 0x80 == 0x80
+
+
+def test_ipa_crs_prefix():
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    g = load("ipa_crs_bn254.json")
+    pts = protocol.ipa_gen_points(8, max_=512)
+    assert [P(h) for h in g["points"][:8]] == pts
+    assert all(BN254.is_on_curve(p) for p in pts)
+    with pytest.raises(ValueError):       # Appendix B.1: default max 256 < N+1 = 257
+        protocol.ipa_gen_points(257)
+
+
+def test_reference_ipa_tests_restated():
+    """ipa/mod.rs:382-421 at N = 32: commit proof round trip + tamper; eval proofs in/out of domain."""
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    crs = [P(h) for h in load("ipa_crs_bn254.json")["points"][:33]]
+    ipa = protocol.IPA(32, points=crs)
+    data = protocol.LagrangeBasis.from_vec(list(range(32)))
+    com = ipa.commit(data)
+    cp = ipa.prove_commitment(com, data)
+    assert ipa.verify_commitment_proof(com, cp)
+    assert not ipa.verify_commitment_proof(BN254.add(com, BN254.g), cp)
+    idx = 13
+    pr = ipa.prove(com, idx, data)
+    assert ipa.verify(com, idx, pr)
+    out = ipa.prove(com, 64, data)
+    assert ipa.verify(com, 64, out)
+    assert not ipa.verify(com, idx, out)
+
+
+def test_reference_kzg_test_restated():
+    """kzg/mod.rs:278-297: CRS 16, data 8: every index verifies, 8..16 give y = 0, index 17 verifies."""
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    rng = random.Random(9)
+    kz = protocol.KZG(16)
+    d = protocol.LagrangeBasis([rng.randrange(BN254.r) for _ in range(8)], 16)
+    c = kz.commit(d)
+    for i in range(16):
+        pr = kz.prove(c, i, d)
+        assert kz.verify(c, i, pr)
+        if i >= 8:
+            assert pr["y"] == 0
+    assert kz.verify(c, 17, kz.prove(c, 17, d))
+
+
+def test_golden_ipa_256_proof_verifies():
+    from pyoracle import protocol
+    crs = [P(h) for h in load("ipa_crs_bn254.json")["points"]]
+    g = load("ipa_256.json")
+    ipa = protocol.IPA(256, points=crs)
+    com = P(g["commitment"])
+    for key in ("proof_in_domain", "proof_out_domain"):
+        pr = g[key]
+        proof = {"l": [P(x) for x in pr["l"]], "r": [P(x) for x in pr["r"]], "tip": int(pr["tip"], 16),
+                 "y": int(pr["y"], 16)}
+        assert ipa.verify(com, pr["point"], proof)
+
+
+def test_golden_multiproof_verifies_and_tamper():
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    crs = [P(h) for h in load("ipa_crs_bn254.json")["points"][:33]]
+    g = load("multiproof_32.json")
+    for name, vc in (("ipa", protocol.IPA(32, points=crs)), ("kzg", protocol.KZG(32))):
+        ent = g[name]
+        vq = [(P(q["commit"]), q["z"], int(q["y"], 16)) for q in ent["queries"]]
+        if name == "ipa":
+            pr = ent["proof"]
+            proof = {"l": [P(x) for x in pr["l"]], "r": [P(x) for x in pr["r"]], "tip": int(pr["tip"], 16),
+                     "y": int(pr["y"], 16)}
+        else:
+            proof = {"proof": P(ent["proof"]["proof"]), "y": int(ent["proof"]["y"], 16)}
+        mp = {"proof": proof, "d": P(ent["d"])}
+        assert protocol.verify_multiproof(vc, vq, mp)
+        bad = dict(mp, d=BN254.add(mp["d"], BN254.g))
+        assert not protocol.verify_multiproof(vc, vq, bad)
+        vq2 = list(vq)
+        vq2[0] = (vq[0][0], vq[0][1], (vq[0][2] + 1) % BN254.r)
+        assert not protocol.verify_multiproof(vc, vq2, mp)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 recipe used for profiles/ (kernel trace + stats, then HBM PMC passes).
+# usage: bash tools_profile.sh <tag> [bench args...]
+set -e
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd /tmp && export TMPDIR=/tmp
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py "$@" > $OUT/bench_trace.json
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $R/bench.py "$@" > $OUT/bench_fetch.json
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $R/bench.py "$@" > $OUT/bench_write.json
+echo profile-done

@@ -116,6 +116,37 @@ VK_HD fe<F> fe_neg(const fe<F>& a) {
 // On the device it is an out-of-line call: a fully inlined 12-limb multiply is ~600
 // instructions, and an EC add holds 10-16 of them -- inlining every one blows the
 // instruction cache (and compile time) for no gain.
+#ifdef VK_MUL_ROLLED
+// experiment switch: inline CIOS with the outer row loop rolled (b shifted per row)
+template <class F>
+VK_HD fe<F> fe_mul(const fe<F>& a, fe<F> b) {
+    constexpr int N = F::N;
+    uint32_t t[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) t[j] = 0;
+#pragma unroll 1
+    for (int i = 0; i < N; i++) {
+        uint32_t bi = b.v[0];
+#pragma unroll
+        for (int k = 0; k < N - 1; k++) b.v[k] = b.v[k + 1];
+        uint64_t A = (uint64_t)a.v[0] * bi + t[0];
+        t[0] = (uint32_t)A;
+        uint32_t m = t[0] * F::inv;
+        uint64_t C = (uint64_t)m * F::p(0) + t[0];
+#pragma unroll
+        for (int j = 1; j < N; j++) {
+            A = (uint64_t)a.v[j] * bi + t[j] + (A >> 32);
+            C = (uint64_t)m * F::p(j) + (uint32_t)A + (C >> 32);
+            t[j - 1] = (uint32_t)C;
+        }
+        t[N - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+    }
+    fe<F> r;
+#pragma unroll
+    for (int j = 0; j < N; j++) r.v[j] = t[j];
+    return fe_reduce_once<F>(r);
+}
+#else
 #define VK_MUL_ATTR __host__ __device__ __noinline__
 template <class F>
 VK_MUL_ATTR fe<F> fe_mul(const fe<F> a, const fe<F> b) {
@@ -142,6 +173,7 @@ VK_MUL_ATTR fe<F> fe_mul(const fe<F> a, const fe<F> b) {
     for (int j = 0; j < N; j++) r.v[j] = t[j];
     return fe_reduce_once<F>(r);
 }
+#endif
 
 template <class F>
 VK_HD fe<F> fe_sqr(const fe<F>& a) {

@@ -9,7 +9,7 @@ import re
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
-LIB_PATH = os.path.join(ROOT, "lib", "libvkzg.so")
+LIB_PATH = os.environ.get("VKZG_LIB") or os.path.join(ROOT, "lib", "libvkzg.so")
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "vc_msm.h")
 
 c_void_p, c_int, c_size_t, c_uint64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
