@@ -1,0 +1,113 @@
+/* vc_scheme.h -- scheme-level C ABI of libvkzg.so: the reference's VectorCommitment
+ * operations (/root/reference/vector-commit/src/lib.rs:70-174) for BN254 G1, with every
+ * MSM / quotient / fold on the GPU and the serial Fiat-Shamir work on the host.
+ *
+ * Field elements (Fr) are 4 canonical little-endian u64 limbs; points are canonical affine
+ * x[4], y[4] + a u8 identity flag (as in vc_msm.h).  All calls are synchronous and return
+ * VC_OK or a VC_E_* status (vc_msm.h).  The reference's `todo!()` batch methods
+ * (prove_batch / verify_batch, ipa/mod.rs:156-189, kzg/mod.rs:156-197) have no counterpart.
+ *
+ * Scope: the protocol layer is instantiated for BN254 (the only curve the reference runs,
+ * vector-commit/Cargo.toml:15).  The MSM / commit engines (vc_msm.h) also serve BLS12-381 G1
+ * and Bandersnatch.
+ */
+#ifndef VC_SCHEME_H
+#define VC_SCHEME_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "vc_msm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- Fiat-Shamir (a12)
+ * TranscriptHasher (transcript.rs:28-62): append(label || compressed(value)); digest(label) =
+ * hash_to_field(state || label) with DefaultFieldHasher<Sha256> and DST = the label given at
+ * creation; then state = ser(out) || label. */
+typedef struct vc_transcript vc_transcript;
+vc_transcript* vc_transcript_new(const char* label);
+vc_transcript* vc_transcript_clone(const vc_transcript* t);
+void vc_transcript_free(vc_transcript* t);
+int vc_transcript_append_bytes(vc_transcript* t, const uint8_t* bytes, size_t n, const char* label);
+int vc_transcript_append_point(vc_transcript* t, const uint64_t* xy, uint8_t inf, const char* label);
+int vc_transcript_append_fr(vc_transcript* t, const uint64_t* fr, const char* label);
+int vc_transcript_append_u64(vc_transcript* t, uint64_t v, const char* label);
+int vc_transcript_digest(vc_transcript* t, const char* label, uint64_t* out_fr);
+/* raw hash_to_field(msg) mod r with the given DST */
+int vc_hash_to_field(const uint8_t* msg, size_t n, const uint8_t* dst, size_t dst_len, uint64_t* out_fr);
+
+/* ---------------------------------------------------------------- serialisation (a13)
+ * arkworks 0.4 compressed SW encoding (32 B) and VCCommitment::to_data_item (lib.rs:56-67). */
+int vc_point_compress(const uint64_t* xy, uint8_t inf, uint8_t* out32);
+/* batched on the device: n points -> n Fr (canonical) */
+int vc_to_data_item_batch(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, uint64_t* out_fr);
+
+/* ---------------------------------------------------------------- CRS (a15)
+ * IPAPointGenerator::gen (ipa_point_generator.rs:51-67): first `num` accepted points of
+ * sha256(seed || le64(i)) -> Affine::from_random_bytes.  VC_E_RANGE if num > max
+ * (PointGeneratorError::OutOfBounds, Appendix B.1). */
+int vc_ipa_crs(const uint8_t* seed, size_t seed_len, size_t max, size_t num, uint64_t* out_xy);
+/* KZG::setup (kzg/mod.rs:115-124): Lagrange SRS L_j = l_j(s) * G over the domain of size
+ * n = next_pow2(max_items), computed on the device; out n points (table uploaded into ctx). */
+int vc_kzg_setup(vc_ctx* ctx, size_t max_items, const uint64_t* secret_fr, int* table_id, size_t* size);
+
+/* ---------------------------------------------------------------- IPA (ipa/mod.rs)
+ * `table` holds the N + 1 CRS points g[0..N], q (IPAUniversalParams::new_from_vec).
+ * Proof layout: L[k], R[k] points (k = log2 N rounds), tip, y. */
+typedef struct {
+    size_t rounds;
+    uint64_t* l_xy; uint8_t* l_inf;   /* rounds x 8 u64, rounds */
+    uint64_t* r_xy; uint8_t* r_inf;
+    uint64_t tip[4];
+    uint64_t y[4];
+} vc_ipa_proof;
+
+int vc_ipa_commit(vc_ctx* ctx, int table, size_t N, const uint64_t* data, size_t batch,
+                  uint64_t* out_xy, uint8_t* out_inf);
+/* prove_point (:137-154 -> low_level_ipa :268-319). transcript may be NULL (fresh "ipa").
+ * Proves `batch` independent openings at once (same N, one CRS): data batch x N, points batch,
+ * commitments batch; transcripts NULL or an array of batch handles (consumed state). */
+int vc_ipa_prove(vc_ctx* ctx, int table, size_t N, const uint64_t* data, const uint64_t* com_xy,
+                 const uint8_t* com_inf, const uint64_t* points, size_t batch,
+                 vc_transcript** transcripts, vc_ipa_proof* proofs);
+/* verify_point (:165-181 -> low_level_verify_ipa :321-360); result 1 = valid, 0 = invalid */
+int vc_ipa_verify(vc_ctx* ctx, int table, size_t N, const uint64_t* com_xy, uint8_t com_inf,
+                  const uint64_t* point, const vc_ipa_proof* proof, vc_transcript* transcript,
+                  int* result);
+
+/* ---------------------------------------------------------------- KZG (kzg/mod.rs)
+ * prove_point (:136-154): y = evaluate(point), q = divide_by_vanishing(index) when
+ * point <= size, else divide_by_vanishing_outside_domain(point); proof = MSM(L, q).
+ * evals may be shorter than the domain (`max`); VC_E_DOMAIN for point == size (the
+ * reference panics there, Appendix B.4). */
+int vc_kzg_prove(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t max,
+                 const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y);
+/* the quotient alone (a5/a6), for parity tests: q (size x 4 u64) and y */
+int vc_kzg_quotient(vc_ctx* ctx, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                    uint64_t* q_out, uint64_t* y);
+
+/* ---------------------------------------------------------------- multiproof (multiproof.rs)
+ * scheme: 0 = IPA (table = N + 1 CRS points), 1 = KZG (table = Lagrange SRS of size N).
+ * queries: data Q x N (Fr), commitments Q, z Q (u64, < N), y Q (Fr).
+ * Output: proof D and the inner proof (IPA proof or KZG (proof point, y)). */
+int vc_multiproof_prove(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* data,
+                        const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                        const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proof,
+                        uint64_t* kzg_proof_xy, uint8_t* kzg_proof_inf, uint64_t* kzg_y);
+/* IPA-scheme verification (verify_multiproof :178-215 + low_level_verify_ipa) */
+int vc_multiproof_verify_ipa(vc_ctx* ctx, int table, size_t N, size_t Q, const uint64_t* com_xy,
+                             const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                             const uint64_t* d_xy, uint8_t d_inf, const vc_ipa_proof* proof, int* result);
+/* KZG-scheme: the (commitment E - D, t) pair verify_point would check with pairings
+ * (out of scope); returned so a caller can run its own pairing check. */
+int vc_multiproof_kzg_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                            const uint64_t* z, const uint64_t* y, const uint64_t* d_xy, uint8_t d_inf,
+                            uint64_t* c_xy, uint8_t* c_inf, uint64_t* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VC_SCHEME_H */

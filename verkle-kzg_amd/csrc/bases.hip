@@ -166,46 +166,52 @@ __global__ void k_random(uint64_t seed, uint32_t n, int sbits, typename C::Aff* 
 
 // ------------------------------------------------------------------ host entry points
 template <class C>
-static int upload_t(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id) {
+static int fill_t(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf, size_t n) {
     using Aff = typename C::Aff;
     using F = typename C::F;
-    Table* t = new Table();
     t->curve = ctx->curve;
     t->n = n;
-    int st = t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff));
-    if (st == VC_OK) st = t->inf.ensure(std::max<size_t>(n, 1));
+    t->fb_c = t->fb_W = 0;  // any fixed-base tables are stale now
+    VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff)));
+    VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
+    if (n == 0) return VC_OK;
     DevBuf dxy, dinf, dbad;
-    if (st == VC_OK) st = dxy.ensure(std::max<size_t>(n, 1) * 2 * F::N * 4);
-    if (st == VC_OK) st = dinf.ensure(std::max<size_t>(n, 1));
-    if (st == VC_OK) st = dbad.ensure(4);
+    VK_TRY(dxy.ensure(n * 2 * F::N * 4));
+    VK_TRY(dinf.ensure(n));
+    VK_TRY(dbad.ensure(4));
+    VK_CHECK_HIP(hipMemcpyAsync(dxy.p, xy, n * 2 * F::N * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (inf) VK_CHECK_HIP(hipMemcpyAsync(dinf.p, inf, n, hipMemcpyHostToDevice, ctx->stream));
+    VK_CHECK_HIP(hipMemsetAsync(dbad.p, 0, 4, ctx->stream));
+    hipLaunchKernelGGL(k_upload<C>, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, dxy.as<uint32_t>(),
+                       inf ? dinf.as<uint8_t>() : nullptr, (uint32_t)n, t->bases.as<Aff>(), t->inf.as<uint8_t>(),
+                       dbad.as<uint32_t>());
+    VK_CHECK_HIP(hipGetLastError());
+    uint32_t bad = 0;
+    VK_CHECK_HIP(hipMemcpyAsync(&bad, dbad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return bad ? VC_E_NOT_ON_CURVE : VC_OK;
+}
+
+template <class C>
+static int upload_t(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id) {
+    Table* t = new Table();
+    int st = fill_t<C>(ctx, t, xy, inf, n);
     if (st != VC_OK) {
         delete t;
         return st;
     }
-    auto fail = [&](int code) {
-        delete t;
-        return code;
-    };
-    if (n > 0) {
-        if (hipMemcpyAsync(dxy.p, xy, n * 2 * F::N * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-            return fail(VC_E_HIP);
-        if (inf) {
-            if (hipMemcpyAsync(dinf.p, inf, n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-                return fail(VC_E_HIP);
-        }
-        if (hipMemsetAsync(dbad.p, 0, 4, ctx->stream) != hipSuccess) return fail(VC_E_HIP);
-        hipLaunchKernelGGL(k_upload<C>, dim3((n + 255) / 256), dim3(256), 0, ctx->stream,
-                           dxy.as<uint32_t>(), inf ? dinf.as<uint8_t>() : nullptr, (uint32_t)n,
-                           t->bases.as<Aff>(), t->inf.as<uint8_t>(), dbad.as<uint32_t>());
-        uint32_t bad = 0;
-        if (hipMemcpyAsync(&bad, dbad.p, 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
-            return fail(VC_E_HIP);
-        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(VC_E_HIP);
-        if (bad) return fail(VC_E_NOT_ON_CURVE);
-    }
     ctx->tables.push_back(t);
     *id = (int)ctx->tables.size() - 1;
     return VC_OK;
+}
+
+int bases_fill(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf, size_t n) {
+    switch (ctx->curve) {
+        case VC_CURVE_BN254: return fill_t<BN254G1>(ctx, t, xy, inf, n);
+        case VC_CURVE_BLS12_381: return fill_t<BLS381G1>(ctx, t, xy, inf, n);
+        case VC_CURVE_BANDERSNATCH: return fill_t<Bandersnatch>(ctx, t, xy, inf, n);
+    }
+    return VC_E_INVALID;
 }
 
 template <class C, class Fr>

@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __rest
         __syncthreads();
     }
     __shared__ fe<F> tinv;
-    if (tid == 0) tinv = fe_inv<F>(pre[255]);
+    if (tid == 0) tinv = fe_inv_bin<F>(pre[255]);
     __syncthreads();
     fe<F> iz = tinv;
     if (tid > 0) iz = fe_mul<F>(iz, pre[tid - 1]);
@@ -243,7 +243,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
                        void* d_out_xy, uint8_t* d_out_inf) {
     using Acc = typename C::Acc;
     if (width > t->n) return VC_E_RANGE;
-    if (!t->fb.p) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
+    if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
     if (batch == 0) return VC_OK;
     VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
     int tpc = 16;
@@ -257,6 +257,30 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
               ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
               reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);
     return VC_OK;
+}
+
+// table <- normalised projective accumulators (device), e.g. a freshly computed SRS
+template <class C>
+static int table_from_acc_t(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) {
+    t->curve = ctx->curve;
+    t->n = n;
+    t->fb_c = t->fb_W = 0;
+    VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(typename C::Aff)));
+    VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
+    if (n == 0) return VC_OK;
+    VK_LAUNCH(ctx, "normalize_table", (k_normalize<C>), (n + 255) / 256, 256, 0,
+              reinterpret_cast<const typename C::Acc*>(d_acc), n, t->bases.as<typename C::Aff>(),
+              (uint32_t*)nullptr, t->inf.as<uint8_t>());
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) {
+    switch (ctx->curve) {
+        case VC_CURVE_BN254: return table_from_acc_t<BN254G1>(ctx, t, d_acc, n);
+        case VC_CURVE_BLS12_381: return table_from_acc_t<BLS381G1>(ctx, t, d_acc, n);
+        case VC_CURVE_BANDERSNATCH: return table_from_acc_t<Bandersnatch>(ctx, t, d_acc, n);
+    }
+    return VC_E_INVALID;
 }
 
 int fixed_base_precompute(vc_ctx* ctx, Table* t, int c) {

@@ -92,6 +92,7 @@ struct vc_ctx {
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, long>> ktime;
+    vk::Table scratch;  // variable-base points of verifiers (grow-only)
 
     hipEvent_t get_event();
     void timer_begin(const char* name, hipEvent_t* a);
@@ -122,9 +123,11 @@ int acc_sum(int curve, const uint32_t* accs, size_t k, uint32_t* out);
 int point_words(int curve);
 int aff_limbs64(int curve);  // NL of the base field in u64 limbs
 int bases_upload(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, int* id);
+int bases_fill(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf, size_t n);
 int bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id);
 int bases_download(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf);
 int fixed_base_precompute(vc_ctx* ctx, Table* t, int c);
+int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf);
 }  // namespace vk

@@ -218,6 +218,83 @@ VK_HD fe<F> fe_inv(const fe<F>& a) {
     return acc;
 }
 
+// Montgomery inverse by the binary extended Euclidean algorithm (variable time; latency
+// ~50x lower than the Fermat chain above, which matters in latency-bound tails):
+// for aR (Montgomery form of a != 0) returns a^-1 R.
+template <class F>
+VK_HD void fe_shr1(fe<F>& a, uint32_t top) {
+#pragma unroll
+    for (int i = 0; i < F::N - 1; i++) a.v[i] = (a.v[i] >> 1) | (a.v[i + 1] << 31);
+    a.v[F::N - 1] = (a.v[F::N - 1] >> 1) | (top << 31);
+}
+template <class F>
+VK_HD uint32_t fe_add_p_raw(fe<F>& a) {  // a += p, returns carry
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+        uint64_t t = (uint64_t)a.v[i] + F::p(i) + c;
+        a.v[i] = (uint32_t)t;
+        c = (uint32_t)(t >> 32);
+    }
+    return c;
+}
+template <class F>
+VK_HD bool fe_geq_raw(const fe<F>& a, const fe<F>& b) {
+    for (int i = F::N - 1; i >= 0; i--) {
+        if (a.v[i] != b.v[i]) return a.v[i] > b.v[i];
+    }
+    return true;
+}
+template <class F>
+VK_HD void fe_sub_raw(fe<F>& a, const fe<F>& b) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) {
+        uint64_t t = (uint64_t)a.v[i] - b.v[i] - br;
+        a.v[i] = (uint32_t)t;
+        br = (uint32_t)(t >> 63);
+    }
+}
+template <class F>
+VK_HD bool fe_is_one_raw(const fe<F>& a) {
+    uint32_t o = a.v[0] ^ 1u;
+#pragma unroll
+    for (int i = 1; i < F::N; i++) o |= a.v[i];
+    return o == 0;
+}
+template <class F>
+VK_HD fe<F> fe_inv_bin(const fe<F>& a_mont) {
+    fe<F> u = a_mont, v, x1 = fe_zero<F>(), x2 = fe_zero<F>();
+#pragma unroll
+    for (int i = 0; i < F::N; i++) v.v[i] = F::p(i);
+    x1.v[0] = 1;
+    if (fe_is_zero<F>(u)) return fe_zero<F>();
+    while (!fe_is_one_raw<F>(u) && !fe_is_one_raw<F>(v)) {
+        while ((u.v[0] & 1) == 0) {
+            fe_shr1<F>(u, 0);
+            uint32_t c = (x1.v[0] & 1) ? fe_add_p_raw<F>(x1) : 0u;
+            fe_shr1<F>(x1, c);
+        }
+        while ((v.v[0] & 1) == 0) {
+            fe_shr1<F>(v, 0);
+            uint32_t c = (x2.v[0] & 1) ? fe_add_p_raw<F>(x2) : 0u;
+            fe_shr1<F>(x2, c);
+        }
+        if (fe_geq_raw<F>(u, v)) {
+            fe_sub_raw<F>(u, v);
+            x1 = fe_sub<F>(x1, x2);
+        } else {
+            fe_sub_raw<F>(v, u);
+            x2 = fe_sub<F>(x2, x1);
+        }
+    }
+    fe<F> r = fe_is_one_raw<F>(u) ? x1 : x2;  // (aR)^-1
+    fe<F> r2;
+#pragma unroll
+    for (int i = 0; i < F::N; i++) r2.v[i] = F::r2(i);
+    return fe_mul<F>(fe_mul<F>(r, r2), r2);  // (aR)^-1 R^2 = a^-1 R
+}
+
 // small-constant multiple (k <= 8) via additions
 template <class F, int K>
 VK_HD fe<F> fe_mul_small(const fe<F>& a) {

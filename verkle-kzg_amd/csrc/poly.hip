@@ -1,0 +1,323 @@
+// Scalar-field kernels of the protocol layer (gfx950): domain powers, batched inversion,
+// the KZG quotients (reference lagrange_basis.rs:91-142 + precompute.rs:72-90) and the
+// KZG Lagrange SRS (kzg/mod.rs:115-124 via SURVEY Appendix A.7).
+//
+// The reference divides per element (two Fr inversions per i in divide_by_vanishing); here
+// every denominator goes through one chunked Montgomery batch inversion whose per-chunk
+// inverse is the binary extended Euclid (latency ~1/50 of a Fermat chain), and the two
+// sums the formulas need (barycentric y, q_m) are block reductions.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+#include "ec.hpp"
+#include "poly.hpp"
+
+namespace vk {
+
+template <class F>
+__global__ void k_canon_to_mont(const fe<F>* __restrict__ in, size_t n, size_t n_valid, fe<F>* __restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = i < n_valid ? fe_to_mont<F>(in[i]) : fe_zero<F>();
+}
+template <class F>
+__global__ void k_mont_to_canon(const fe<F>* __restrict__ in, size_t n, fe<F>* __restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = fe_from_mont<F>(in[i]);
+}
+
+// out[i] = w^i
+template <class F>
+__global__ void k_powers(fe<F> w, size_t n, fe<F>* __restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<F> r = fe_one<F>(), b = w;
+    size_t e = i;
+    while (e) {
+        if (e & 1) r = fe_mul<F>(r, b);
+        e >>= 1;
+        if (e) b = fe_sqr<F>(b);
+    }
+    out[i] = r;
+}
+
+// out[k] = 1 / in[k] for k < n (zeros map to zero), chunks of CH per thread:
+// prefix products, one binary-Euclid inversion per chunk, backward substitution
+template <class F>
+__global__ void __launch_bounds__(256) k_batch_inv(const fe<F>* __restrict__ in, fe<F>* __restrict__ out, size_t n,
+                                                  int CH) {
+    size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t lo = c * CH;
+    if (lo >= n) return;
+    size_t hi = lo + CH < n ? lo + CH : n;
+    fe<F> acc = fe_one<F>();
+    for (size_t k = lo; k < hi; k++) {
+        fe<F> v = in[k];
+        if (!fe_is_zero<F>(v)) acc = fe_mul<F>(acc, v);
+        out[k] = acc;
+    }
+    fe<F> inv = fe_inv_bin<F>(acc);
+    for (size_t k = hi; k-- > lo;) {
+        fe<F> v = in[k];
+        if (fe_is_zero<F>(v)) {
+            out[k] = fe_zero<F>();
+            continue;
+        }
+        fe<F> prev = k > lo ? out[k - 1] : fe_one<F>();
+        out[k] = fe_mul<F>(inv, prev);
+        inv = fe_mul<F>(inv, v);
+    }
+}
+
+// den[i] = w^i - z   (out of domain)   or   w^i - w^m with den[m] = 1 (in domain)
+template <class F>
+__global__ void k_den(const fe<F>* __restrict__ pw, size_t n, fe<F> z, long long m, fe<F>* __restrict__ den) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    den[i] = ((long long)i == m) ? fe_one<F>() : fe_sub<F>(pw[i], z);
+}
+
+// partial[b] = sum over the block's i of f_i * w^i * inv_i  (f_i = 0 beyond max)
+template <class F>
+__global__ void __launch_bounds__(256) k_bary_partial(const fe<F>* __restrict__ f, size_t max,
+                                                     const fe<F>* __restrict__ pw, const fe<F>* __restrict__ inv,
+                                                     size_t n, fe<F>* __restrict__ partial) {
+    __shared__ fe<F> sh[256];
+    size_t i0 = (size_t)blockIdx.x * 256 * 8 + threadIdx.x;
+    fe<F> acc = fe_zero<F>();
+    for (int k = 0; k < 8; k++) {
+        size_t i = i0 + (size_t)k * 256;
+        if (i < n && i < max) acc = fe_add<F>(acc, fe_mul<F>(fe_mul<F>(f[i], pw[i]), inv[i]));
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) sh[threadIdx.x] = fe_add<F>(sh[threadIdx.x], sh[threadIdx.x + h]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+// q_i = (f_i - y) * inv_i   (outside domain)
+template <class F>
+__global__ void k_q_out(const fe<F>* __restrict__ f, size_t max, const fe<F>* __restrict__ inv, size_t n, fe<F> y,
+                        fe<F>* __restrict__ q) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<F> fi = i < max ? f[i] : fe_zero<F>();
+    q[i] = fe_mul<F>(fe_sub<F>(fi, y), inv[i]);
+}
+
+// in domain at m: q_i = (f_i - f_m) * inv_i (i != m); partial sums of q_i * w^i for q_m
+template <class F>
+__global__ void __launch_bounds__(256) k_q_in(const fe<F>* __restrict__ f, size_t max, const fe<F>* __restrict__ inv,
+                                             const fe<F>* __restrict__ pw, size_t n, size_t m, fe<F> fm,
+                                             fe<F>* __restrict__ q, fe<F>* __restrict__ partial) {
+    __shared__ fe<F> sh[256];
+    size_t i0 = (size_t)blockIdx.x * 256 * 8 + threadIdx.x;
+    fe<F> acc = fe_zero<F>();
+    for (int k = 0; k < 8; k++) {
+        size_t i = i0 + (size_t)k * 256;
+        if (i >= n) break;
+        if (i == m) {
+            q[i] = fe_zero<F>();
+            continue;
+        }
+        fe<F> fi = i < max ? f[i] : fe_zero<F>();
+        fe<F> qi = fe_mul<F>(fe_sub<F>(fi, fm), inv[i]);
+        q[i] = qi;
+        acc = fe_add<F>(acc, fe_mul<F>(qi, pw[i]));
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) sh[threadIdx.x] = fe_add<F>(sh[threadIdx.x], sh[threadIdx.x + h]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+template <class F>
+__global__ void k_set(fe<F>* __restrict__ a, size_t i, fe<F> v) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) a[i] = v;
+}
+
+// ---------------------------------------------------------------- Lagrange SRS (A.7)
+// c_j = n^-1 * ((s w^-j)^m - 1) / (s w^-j - 1); the numerator/denominator pass, then one
+// batch inversion, then the fixed-base scalar multiplications c_j * G.
+template <class F>
+__global__ void k_srs_num_den(const fe<F>* __restrict__ pw_inv, size_t n, fe<F> s, uint64_t m, fe<F> ninv,
+                              fe<F>* __restrict__ num, fe<F>* __restrict__ den) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    fe<F> b = fe_mul<F>(s, pw_inv[j]);
+    fe<F> r = fe_one<F>(), x = b;
+    uint64_t e = m;
+    while (e) {
+        if (e & 1) r = fe_mul<F>(r, x);
+        e >>= 1;
+        if (e) x = fe_sqr<F>(x);
+    }
+    num[j] = fe_mul<F>(fe_sub<F>(r, fe_one<F>()), ninv);
+    den[j] = fe_sub<F>(b, fe_one<F>());
+}
+template <class F>
+__global__ void k_mul_elem(fe<F>* __restrict__ a, const fe<F>* __restrict__ b, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    a[i] = fe_mul<F>(a[i], b[i]);
+}
+
+template <class C, class Fr>
+__global__ void k_fixed_mul_gen(const fe<Fr>* __restrict__ sc_mont, size_t n, typename C::Aff g,
+                                typename C::Acc* __restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<Fr> s = fe_from_mont<Fr>(sc_mont[i]);
+    typename C::Acc acc = C::zero();
+    for (int b = Fr::N * 32 - 1; b >= 0; b--) {
+        acc = C::dbl(acc);
+        if ((s.v[b >> 5] >> (b & 31)) & 1) acc = C::madd(acc, g, false);
+    }
+    out[i] = acc;
+}
+
+// ---------------------------------------------------------------- host drivers
+template <class F>
+static fe<F> host_sum(const std::vector<fe<F>>& v) {
+    fe<F> a = fe_zero<F>();
+    for (auto& x : v) a = fe_add<F>(a, x);
+    return a;
+}
+
+template <class F>
+int domain_powers(vc_ctx* ctx, const fe<F>& w, size_t n, fe<F>* d_out) {
+    VK_LAUNCH(ctx, "powers", (k_powers<F>), (n + 255) / 256, 256, 0, w, n, d_out);
+    return VC_OK;
+}
+
+template <class F>
+int batch_inverse(vc_ctx* ctx, const fe<F>* d_in, fe<F>* d_out, size_t n) {
+    const int CH = 16;
+    size_t chunks = (n + CH - 1) / CH;
+    VK_LAUNCH(ctx, "batch_inv", (k_batch_inv<F>), (chunks + 255) / 256, 256, 0, d_in, d_out, n, CH);
+    return VC_OK;
+}
+
+// q and y for KZG prove_point (device, Montgomery). point given in Montgomery form.
+template <class F>
+int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
+                     fe<F>* d_q, fe<F>* y_out, DevBuf& pw, DevBuf& tmp, DevBuf& part) {
+    hipStream_t st = ctx->stream;
+    VK_TRY(pw.ensure(n * sizeof(fe<F>)));
+    VK_TRY(tmp.ensure(n * sizeof(fe<F>)));
+    fe<F>* den = d_q;  // denominators staged in the output buffer, inverses in tmp
+    size_t nblk = (n + 2047) / 2048;
+    VK_TRY(part.ensure(nblk * sizeof(fe<F>)));
+    VK_TRY(domain_powers<F>(ctx, omega, n, pw.as<fe<F>>()));
+    fe<F>* inv = tmp.as<fe<F>>();
+    std::vector<fe<F>> hp(nblk);
+    // prove_point: `point <= size` -> in-domain branch with index to_usize(point)
+    fe<F> pc = fe_from_mont<F>(point);
+    bool small = true;
+    for (int i = 2; i < F::N; i++) small &= pc.v[i] == 0;
+    uint64_t pv = (uint64_t)pc.v[0] | ((uint64_t)pc.v[1] << 32);
+    if (small && pv <= n) {
+        if (pv == n) return VC_E_DOMAIN;  // reference: vanishing_at(size) out of bounds
+        size_t m = (size_t)pv;
+        // y = evaluate(point): stored value, or 0 inside [max, size]
+        fe<F> fm = fe_zero<F>();
+        if (m < max) VK_CHECK_HIP(hipMemcpyAsync(&fm, d_f + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        fe<F> wm;
+        VK_CHECK_HIP(hipMemcpyAsync(&wm, pw.as<fe<F>>() + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        VK_CHECK_HIP(hipStreamSynchronize(st));
+        VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pw.as<fe<F>>(), n, wm, (long long)m, den);
+        VK_TRY(batch_inverse<F>(ctx, den, inv, n));
+        VK_LAUNCH(ctx, "kzg_q_in", (k_q_in<F>), nblk, 256, 0, d_f, max, inv, pw.as<fe<F>>(), n, m, fm, d_q,
+                  part.as<fe<F>>());
+        VK_CHECK_HIP(hipMemcpyAsync(hp.data(), part.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        VK_CHECK_HIP(hipStreamSynchronize(st));
+        // q_m = -w^-m * sum_{i != m} q_i w^i
+        fe<F> s = host_sum<F>(hp);
+        fe<F> qm = fe_neg<F>(fe_mul<F>(s, fe_inv_bin<F>(wm)));
+        VK_LAUNCH(ctx, "kzg_set", (k_set<F>), 1, 64, 0, d_q, m, qm);
+        *y_out = fm;
+        return VC_OK;
+    }
+    // outside: inv_i = 1/(w^i - z); y = -t * sum f_i w^i inv_i, t = (z^n - 1)/n
+    VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pw.as<fe<F>>(), n, point, (long long)-1, den);
+    VK_TRY(batch_inverse<F>(ctx, den, inv, n));
+    VK_LAUNCH(ctx, "kzg_bary", (k_bary_partial<F>), nblk, 256, 0, d_f, max, pw.as<fe<F>>(), inv, n,
+              part.as<fe<F>>());
+    VK_CHECK_HIP(hipMemcpyAsync(hp.data(), part.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipStreamSynchronize(st));
+    fe<F> zn = fe_one<F>(), b = point;
+    for (uint64_t e = n; e; e >>= 1) {
+        if (e & 1) zn = fe_mul<F>(zn, b);
+        b = fe_sqr<F>(b);
+    }
+    fe<F> nn = fe_zero<F>();
+    nn.v[0] = (uint32_t)n;
+    nn.v[1] = (uint32_t)((uint64_t)n >> 32);
+    fe<F> t = fe_mul<F>(fe_sub<F>(zn, fe_one<F>()), fe_inv_bin<F>(fe_to_mont<F>(nn)));
+    fe<F> y = fe_neg<F>(fe_mul<F>(t, host_sum<F>(hp)));
+    VK_LAUNCH(ctx, "kzg_q_out", (k_q_out<F>), (n + 255) / 256, 256, 0, d_f, max, inv, n, y, d_q);
+    *y_out = y;
+    return VC_OK;
+}
+
+template <class F>
+int canon_to_mont_dev(vc_ctx* ctx, const void* d_in, size_t n, size_t n_valid, fe<F>* d_out) {
+    VK_LAUNCH(ctx, "to_mont", (k_canon_to_mont<F>), (n + 255) / 256, 256, 0, reinterpret_cast<const fe<F>*>(d_in), n,
+              n_valid, d_out);
+    return VC_OK;
+}
+template <class F>
+int mont_to_canon_dev(vc_ctx* ctx, const fe<F>* d_in, size_t n, void* d_out) {
+    VK_LAUNCH(ctx, "to_canon", (k_mont_to_canon<F>), (n + 255) / 256, 256, 0, d_in, n, reinterpret_cast<fe<F>*>(d_out));
+    return VC_OK;
+}
+
+// Lagrange SRS points (projective accumulators) for max_items over a domain of size n
+template <class C, class Fr>
+int kzg_srs_dev(vc_ctx* ctx, size_t max_items, size_t n, const fe<Fr>& s_mont, const fe<Fr>& omega,
+                const typename C::Aff& g, typename C::Acc* d_out) {
+    DevBuf pwi, num, den;
+    VK_TRY(pwi.ensure(n * sizeof(fe<Fr>)));
+    VK_TRY(num.ensure(n * sizeof(fe<Fr>)));
+    VK_TRY(den.ensure(n * sizeof(fe<Fr>)));
+    fe<Fr> winv = fe_inv_bin<Fr>(omega);
+    VK_TRY(domain_powers<Fr>(ctx, winv, n, pwi.as<fe<Fr>>()));
+    fe<Fr> nn = fe_zero<Fr>();
+    nn.v[0] = (uint32_t)n;
+    nn.v[1] = (uint32_t)((uint64_t)n >> 32);
+    fe<Fr> ninv = fe_inv_bin<Fr>(fe_to_mont<Fr>(nn));
+    VK_LAUNCH(ctx, "srs_num_den", (k_srs_num_den<Fr>), (n + 255) / 256, 256, 0, pwi.as<fe<Fr>>(), n, s_mont,
+              (uint64_t)max_items, ninv, num.as<fe<Fr>>(), den.as<fe<Fr>>());
+    VK_TRY(batch_inverse<Fr>(ctx, den.as<fe<Fr>>(), pwi.as<fe<Fr>>(), n));  // pwi no longer needed
+    VK_LAUNCH(ctx, "srs_mul", (k_mul_elem<Fr>), (n + 255) / 256, 256, 0, num.as<fe<Fr>>(), pwi.as<fe<Fr>>(), n);
+    VK_LAUNCH(ctx, "srs_points", (k_fixed_mul_gen<C, Fr>), (n + 127) / 128, 128, 0, num.as<fe<Fr>>(), n, g, d_out);
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+// explicit instantiations
+#define VK_INST_F(F)                                                                                   \
+    template int domain_powers<F>(vc_ctx*, const fe<F>&, size_t, fe<F>*);                             \
+    template int batch_inverse<F>(vc_ctx*, const fe<F>*, fe<F>*, size_t);                                           \
+    template int kzg_quotient_dev<F>(vc_ctx*, size_t, const fe<F>*, size_t, const fe<F>&, const fe<F>&, \
+                                     fe<F>*, fe<F>*, DevBuf&, DevBuf&, DevBuf&);                       \
+    template int canon_to_mont_dev<F>(vc_ctx*, const void*, size_t, size_t, fe<F>*);                  \
+    template int mont_to_canon_dev<F>(vc_ctx*, const fe<F>*, size_t, void*);
+VK_INST_F(BN254Fr)
+VK_INST_F(BLS381Fr)
+template int kzg_srs_dev<BN254G1, BN254Fr>(vc_ctx*, size_t, size_t, const fe<BN254Fr>&, const fe<BN254Fr>&,
+                                           const BN254G1::Aff&, BN254G1::Acc*);
+template int kzg_srs_dev<BLS381G1, BLS381Fr>(vc_ctx*, size_t, size_t, const fe<BLS381Fr>&, const fe<BLS381Fr>&,
+                                             const BLS381G1::Aff&, BLS381G1::Acc*);
+
+}  // namespace vk

@@ -1,0 +1,21 @@
+// Declarations of the scalar-field device routines (poly.hip) used by the protocol layer.
+#pragma once
+#include "ctx.hpp"
+#include "ec.hpp"
+
+namespace vk {
+template <class F>
+int domain_powers(vc_ctx* ctx, const fe<F>& w, size_t n, fe<F>* d_out);
+template <class F>
+int batch_inverse(vc_ctx* ctx, const fe<F>* d_in, fe<F>* d_out, size_t n);
+template <class F>
+int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
+                     fe<F>* d_q, fe<F>* y_out, DevBuf& pw, DevBuf& tmp, DevBuf& part);
+template <class F>
+int canon_to_mont_dev(vc_ctx* ctx, const void* d_in, size_t n, size_t n_valid, fe<F>* d_out);
+template <class F>
+int mont_to_canon_dev(vc_ctx* ctx, const fe<F>* d_in, size_t n, void* d_out);
+template <class C, class Fr>
+int kzg_srs_dev(vc_ctx* ctx, size_t max_items, size_t n, const fe<Fr>& s_mont, const fe<Fr>& omega,
+                const typename C::Aff& g, typename C::Acc* d_out);
+}  // namespace vk

@@ -1,0 +1,792 @@
+// Protocol layer on the GPU engine (reference: vector-commit/src/{ipa,kzg}/mod.rs,
+// multiproof.rs, lagrange_basis.rs, precompute.rs). Serial Fiat-Shamir stays on the host
+// (scheme_host.cpp); every MSM, batch of commitments, quotient and big field pass runs on
+// the device.
+//
+// IPA prover without point folding: the reference folds the generators every round
+// (vec_add_and_distribute on points, utils.rs:31-38 -- m full scalar multiplications per
+// round). Here the folded generator g^(k)_j is kept as scalar coefficients over the ORIGINAL
+// CRS (coeff_i, the prover-side twin of the verifier's points_coeffs), so each round's
+// L and R are two width-(N+1) fixed-base commitments (q is base N) served by the
+// precomputed window tables of commit.hip. Same group elements, no point folding.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+#include "ec.hpp"
+#include "poly.hpp"
+#include "scheme_internal.hpp"
+
+namespace vk {
+
+using F = BN254Fr;
+using C = BN254G1;
+using Acc = C::Acc;
+
+// ---------------------------------------------------------------- host point helpers
+static Acc acc_of(const uint64_t* xy, bool inf) {
+    if (inf) return C::zero();
+    Acc a;
+    a.x = canon_to_mont<BN254Fq>(xy);
+    a.y = canon_to_mont<BN254Fq>(xy + 4);
+    a.zz = fe_one<BN254Fq>();
+    a.zzz = fe_one<BN254Fq>();
+    return a;
+}
+static void aff_of(const Acc& a, uint64_t* xy, uint8_t* inf) {
+    acc_to_affine(VC_CURVE_BN254, reinterpret_cast<const uint32_t*>(&a), xy, inf);
+}
+static Fr fr_of(const uint64_t* w) { return canon_to_mont<F>(w); }
+static void canon_of(const Fr& a, uint64_t* w) { mont_to_canon<F>(a, w); }
+
+static std::vector<Fr> host_batch_inv(const std::vector<Fr>& v) {
+    std::vector<Fr> pre(v.size());
+    Fr acc = fe_one<F>();
+    for (size_t i = 0; i < v.size(); i++) {
+        pre[i] = acc;
+        if (!fe_is_zero<F>(v[i])) acc = fe_mul<F>(acc, v[i]);
+    }
+    Fr inv = fe_inv_bin<F>(acc);
+    std::vector<Fr> out(v.size());
+    for (size_t i = v.size(); i-- > 0;) {
+        if (fe_is_zero<F>(v[i])) {
+            out[i] = fe_zero<F>();
+            continue;
+        }
+        out[i] = fe_mul<F>(inv, pre[i]);
+        inv = fe_mul<F>(inv, v[i]);
+    }
+    return out;
+}
+
+static Fr fr_u64(uint64_t v) { return mont_from_u64<F>(v); }
+
+// PrecomputedLagrange::compute_barycentric_coefficients (precompute.rs:72-90)
+static std::vector<Fr> barycentric(size_t size, const Fr& point, const Fr& omega) {
+    std::vector<Fr> res(size, fe_zero<F>());
+    Fr pc = fe_from_mont<F>(point);
+    bool small = true;
+    for (int i = 2; i < 8; i++) small &= pc.v[i] == 0;
+    uint64_t pv = (uint64_t)pc.v[0] | ((uint64_t)pc.v[1] << 32);
+    if (small && pv < size) {
+        res[pv] = fe_one<F>();
+        return res;
+    }
+    Fr t = fe_mul<F>(fe_sub<F>(fe_pow_u64<F>(point, size), fe_one<F>()), fe_inv_bin<F>(fr_u64(size)));
+    std::vector<Fr> pw(size), den(size);
+    Fr w = fe_one<F>();
+    for (size_t i = 0; i < size; i++) {
+        pw[i] = w;
+        den[i] = fe_sub<F>(point, w);
+        w = fe_mul<F>(w, omega);
+    }
+    std::vector<Fr> inv = host_batch_inv(den);
+    for (size_t i = 0; i < size; i++) res[i] = fe_mul<F>(fe_mul<F>(t, pw[i]), inv[i]);
+    return res;
+}
+
+static Fr inner(const Fr* a, const Fr* b, size_t n) {
+    Fr s = fe_zero<F>();
+    for (size_t i = 0; i < n; i++) s = fe_add<F>(s, fe_mul<F>(a[i], b[i]));
+    return s;
+}
+
+static bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
+
+// width-w fixed-base commitments of Montgomery scalars (host) -> canonical affine (host)
+static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
+                        uint8_t* out_inf) {
+    VK_TRY(ctx->ws[WS_SCALARS].ensure(batch * width * 32));
+    VK_TRY(ctx->ws[WS_MISC].ensure(batch * 65));
+    uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
+    uint8_t* dinf = dxy + batch * 64;
+    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_SCALARS].p, sc, batch * width * 32, hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(msm_batch_run(ctx, t, width, ctx->ws[WS_SCALARS].p, batch, 1, dxy, dinf));
+    VK_CHECK_HIP(hipMemcpyAsync(out_xy, dxy, batch * 64, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipMemcpyAsync(out_inf, dinf, batch, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+// variable-base MSM over host points (ctx scratch table) with Montgomery scalars -> Acc
+static int msm_points(vc_ctx* ctx, const std::vector<uint64_t>& xy, const std::vector<uint8_t>& inf,
+                      const std::vector<Fr>& sc, Acc* out) {
+    size_t n = sc.size();
+    VK_TRY(bases_fill(ctx, &ctx->scratch, xy.data(), inf.data(), n));
+    DevBuf d;
+    VK_TRY(d.ensure(std::max<size_t>(n, 1) * 32));
+    VK_CHECK_HIP(hipMemcpyAsync(d.p, sc.data(), n * 32, hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(msm_run(ctx, &ctx->scratch, 0, d.p, n, 1, reinterpret_cast<uint32_t*>(out)));
+    return VC_OK;
+}
+
+// ---------------------------------------------------------------- IPA prove (a8/a9)
+struct IpaState {
+    std::vector<Fr> a, b, coeff;
+    Fr eval, w;
+    vc_transcript* tr;
+    bool own;
+};
+
+int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vector<Fr>>& data,
+                   const std::vector<Acc>& coms, const std::vector<Fr>& points, vc_transcript** trs,
+                   vc_ipa_proof* proofs) {
+    const size_t B = data.size();
+    if (!is_pow2(N) || t->n < N + 1) return VC_E_INVALID;
+    size_t K = 0;
+    while ((1ull << K) < N) K++;
+    Fr omega = bn254_group_gen(N);
+    std::vector<IpaState> st(B);
+    for (size_t p = 0; p < B; p++) {
+        if (proofs[p].rounds < K || !proofs[p].l_xy || !proofs[p].r_xy || !proofs[p].l_inf || !proofs[p].r_inf)
+            return VC_E_INVALID;
+        IpaState& s = st[p];
+        s.a = data[p];
+        s.b = barycentric(N, points[p], omega);
+        s.eval = inner(s.a.data(), s.b.data(), N);
+        s.own = !(trs && trs[p]);
+        s.tr = s.own ? vc_transcript_new("ipa") : trs[p];
+        uint64_t cxy[8];
+        uint8_t cinf;
+        aff_of(coms[p], cxy, &cinf);
+        transcript_append_point(s.tr, cxy, cinf, "C");
+        transcript_append_fr(s.tr, points[p], "input point");
+        transcript_append_fr(s.tr, s.eval, "output point");
+        s.w = transcript_digest(s.tr, "w");
+        s.coeff.assign(N, fe_one<F>());
+    }
+    const size_t W = N + 1;
+    std::vector<Fr> sc(2 * B * W);
+    std::vector<uint64_t> oxy(2 * B * 8);
+    std::vector<uint8_t> oinf(2 * B);
+    for (size_t r = 0; r < K; r++) {
+        const size_t m = N >> r, half = m / 2;
+        for (size_t p = 0; p < B; p++) {
+            IpaState& s = st[p];
+            Fr* sL = &sc[(2 * p) * W];
+            Fr* sR = &sc[(2 * p + 1) * W];
+            for (size_t i = 0; i < N; i++) {
+                size_t j = i % m;
+                if (j >= half) {
+                    sL[i] = fe_mul<F>(s.a[j - half], s.coeff[i]);
+                    sR[i] = fe_zero<F>();
+                } else {
+                    sR[i] = fe_mul<F>(s.a[j + half], s.coeff[i]);
+                    sL[i] = fe_zero<F>();
+                }
+            }
+            // q' * <a_L, b_R> = q * (w <a_L, b_R>)
+            sL[N] = fe_mul<F>(s.w, inner(&s.a[0], &s.b[half], half));
+            sR[N] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
+        }
+        VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data()));
+        for (size_t p = 0; p < B; p++) {
+            IpaState& s = st[p];
+            const uint64_t* Lxy = &oxy[(2 * p) * 8];
+            const uint64_t* Rxy = &oxy[(2 * p + 1) * 8];
+            memcpy(proofs[p].l_xy + r * 8, Lxy, 64);
+            memcpy(proofs[p].r_xy + r * 8, Rxy, 64);
+            proofs[p].l_inf[r] = oinf[2 * p];
+            proofs[p].r_inf[r] = oinf[2 * p + 1];
+            transcript_append_point(s.tr, Lxy, oinf[2 * p], "L");
+            transcript_append_point(s.tr, Rxy, oinf[2 * p + 1], "R");
+            Fr x = transcript_digest(s.tr, "x");
+            // a <- a_L + x a_R ; b <- b_R + x b_L ; g <- g_R + x g_L (coefficients)
+            for (size_t j = 0; j < half; j++) {
+                s.a[j] = fe_add<F>(s.a[j], fe_mul<F>(x, s.a[j + half]));
+                s.b[j] = fe_add<F>(s.b[j + half], fe_mul<F>(x, s.b[j]));
+            }
+            s.a.resize(half);
+            s.b.resize(half);
+            for (size_t i = 0; i < N; i++)
+                if ((i % m) < half) s.coeff[i] = fe_mul<F>(s.coeff[i], x);
+        }
+    }
+    for (size_t p = 0; p < B; p++) {
+        proofs[p].rounds = K;
+        canon_of(st[p].a[0], proofs[p].tip);
+        canon_of(st[p].eval, proofs[p].y);
+        if (st[p].own) vc_transcript_free(st[p].tr);
+    }
+    return VC_OK;
+}
+
+// ---------------------------------------------------------------- IPA verify (a10)
+int ipa_verify_impl(vc_ctx* ctx, Table* t, size_t N, const Acc& com, const Fr& point, const vc_ipa_proof* pr,
+                    vc_transcript* tr_in, int* result) {
+    if (!is_pow2(N) || t->n < N + 1) return VC_E_INVALID;
+    size_t K = pr->rounds;
+    if ((1ull << K) != N) return VC_E_INVALID;  // gens = g[0..2^rounds], zip with points_coeffs
+    Fr omega = bn254_group_gen(N);
+    std::vector<Fr> b = barycentric(N, point, omega);
+    bool own = tr_in == nullptr;
+    vc_transcript* tr = own ? vc_transcript_new("ipa") : tr_in;
+    uint64_t cxy[8];
+    uint8_t cinf;
+    aff_of(com, cxy, &cinf);
+    Fr y = fr_of(pr->y), tip = fr_of(pr->tip);
+    transcript_append_point(tr, cxy, cinf, "C");
+    transcript_append_fr(tr, point, "input point");
+    transcript_append_fr(tr, y, "output point");
+    Fr w = transcript_digest(tr, "w");
+    std::vector<Fr> xs(K);
+    for (size_t k = 0; k < K; k++) {
+        transcript_append_point(tr, pr->l_xy + 8 * k, pr->l_inf[k], "L");
+        transcript_append_point(tr, pr->r_xy + 8 * k, pr->r_inf[k], "R");
+        xs[k] = transcript_digest(tr, "x");
+    }
+    if (own) vc_transcript_free(tr);
+    // points_coeffs: [1] -> each round c -> [c x, c]
+    std::vector<Fr> s(1, fe_one<F>());
+    for (size_t k = 0; k < K; k++) {
+        std::vector<Fr> ns(2 * s.size());
+        for (size_t i = 0; i < s.size(); i++) {
+            ns[2 * i] = fe_mul<F>(s[i], xs[k]);
+            ns[2 * i + 1] = s[i];
+        }
+        s.swap(ns);
+    }
+    Fr cb = inner(b.data(), s.data(), N);
+    Fr prodx = fe_one<F>();
+    for (auto& x : xs) prodx = fe_mul<F>(prodx, x);
+    // fixed part over (g, q): -tip*s_i, (prodx*w*y - w*tip*<b,s>)
+    std::vector<Fr> fs(N + 1);
+    for (size_t i = 0; i < N; i++) fs[i] = fe_neg<F>(fe_mul<F>(tip, s[i]));
+    fs[N] = fe_sub<F>(fe_mul<F>(fe_mul<F>(prodx, w), y), fe_mul<F>(fe_mul<F>(w, tip), cb));
+    uint64_t axy[8];
+    uint8_t ainf;
+    VK_TRY(commit_batch(ctx, t, N + 1, fs.data(), 1, axy, &ainf));
+    // variable part: prodx*C + sum_k P_k L_k + P_k x_k^2 R_k,  P_k = prod_{j>k} x_j
+    std::vector<uint64_t> vxy(8 * (1 + 2 * K));
+    std::vector<uint8_t> vinf(1 + 2 * K);
+    std::vector<Fr> vs(1 + 2 * K);
+    memcpy(&vxy[0], cxy, 64);
+    vinf[0] = cinf;
+    vs[0] = prodx;
+    Fr P = fe_one<F>();
+    for (size_t k = K; k-- > 0;) {
+        memcpy(&vxy[8 * (1 + 2 * k)], pr->l_xy + 8 * k, 64);
+        memcpy(&vxy[8 * (2 + 2 * k)], pr->r_xy + 8 * k, 64);
+        vinf[1 + 2 * k] = pr->l_inf[k];
+        vinf[2 + 2 * k] = pr->r_inf[k];
+        vs[1 + 2 * k] = P;
+        vs[2 + 2 * k] = fe_mul<F>(P, fe_sqr<F>(xs[k]));
+        P = fe_mul<F>(P, xs[k]);
+    }
+    Acc vb;
+    VK_TRY(msm_points(ctx, vxy, vinf, vs, &vb));
+    Acc tot = C::add(acc_of(axy, ainf), vb);
+    *result = C::is_zero(tot) ? 1 : 0;
+    return VC_OK;
+}
+
+// ---------------------------------------------------------------- KZG (a3/a4/a5/a6/a7)
+template <class Fr_>
+static fe<Fr_> group_gen_t(uint64_t n, uint32_t gen) {
+    fe<Fr_> e;
+    for (int i = 0; i < Fr_::N; i++) e.v[i] = Fr_::p(i);
+    e.v[0] -= 1;
+    int lg = 0;
+    while ((1ull << lg) < n) lg++;
+    for (int s = 0; s < lg; s++) {
+        for (int i = 0; i < Fr_::N - 1; i++) e.v[i] = (e.v[i] >> 1) | (e.v[i + 1] << 31);
+        e.v[Fr_::N - 1] >>= 1;
+    }
+    return fe_pow_fe<Fr_, Fr_>(mont_from_u64<Fr_>(gen), e);
+}
+template <class Fr_>
+static uint32_t fr_generator();
+template <>
+uint32_t fr_generator<BN254Fr>() { return 5; }
+template <>
+uint32_t fr_generator<BLS381Fr>() { return 7; }
+
+template <class C_, class Fr_>
+static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                       uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y_out, uint64_t* q_out) {
+    if (!is_pow2(size) || max > size) return VC_E_INVALID;
+    if (t && t->n < size) return VC_E_RANGE;
+    DevBuf d_f, d_q, pw, tmp, part;
+    VK_TRY(d_f.ensure(size * 32));
+    VK_TRY(d_q.ensure(size * 32));
+    VK_TRY(tmp.ensure(size * 32));
+    if (max > 0) VK_CHECK_HIP(hipMemcpyAsync(tmp.p, evals, max * 32, hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(canon_to_mont_dev<Fr_>(ctx, tmp.p, size, max, d_f.as<fe<Fr_>>()));
+    fe<Fr_> pm = canon_to_mont<Fr_>(point);
+    fe<Fr_> omega = group_gen_t<Fr_>(size, fr_generator<Fr_>());
+    fe<Fr_> y;
+    VK_TRY(kzg_quotient_dev<Fr_>(ctx, size, d_f.as<fe<Fr_>>(), max, pm, omega, d_q.as<fe<Fr_>>(), &y, pw, tmp, part));
+    mont_to_canon<Fr_>(y, y_out);
+    if (q_out) {
+        VK_TRY(mont_to_canon_dev<Fr_>(ctx, d_q.as<fe<Fr_>>(), size, tmp.p));
+        VK_CHECK_HIP(hipMemcpyAsync(q_out, tmp.p, size * 32, hipMemcpyDeviceToHost, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    if (t) {
+        std::vector<uint32_t> acc(point_words(ctx->curve));
+        VK_TRY(msm_run(ctx, t, 0, d_q.p, size, 1, acc.data()));
+        VK_TRY(acc_to_affine(ctx->curve, acc.data(), proof_xy, proof_inf));
+    }
+    return VC_OK;
+}
+
+// ---------------------------------------------------------------- multiproof kernels
+// S[zi][k] = sum over queries i of group zi of r^i * f_i[k]
+__global__ void k_mp_accumulate(const fe<F>* __restrict__ f, const fe<F>* __restrict__ rpow,
+                                const uint32_t* __restrict__ order, const uint32_t* __restrict__ zstart, size_t N,
+                                uint32_t Z, fe<F>* __restrict__ S) {
+    uint32_t zi = blockIdx.y;
+    size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (zi >= Z || k >= N) return;
+    fe<F> acc = fe_zero<F>();
+    for (uint32_t u = zstart[zi]; u < zstart[zi + 1]; u++) {
+        uint32_t i = order[u];
+        acc = fe_add<F>(acc, fe_mul<F>(rpow[i], f[(size_t)i * N + k]));
+    }
+    S[(size_t)zi * N + k] = acc;
+}
+
+// den[zi][k] = w^k - w^z (1 at k == z)
+__global__ void k_mp_den(const fe<F>* __restrict__ pw, const uint32_t* __restrict__ zval, size_t N, uint32_t Z,
+                         fe<F>* __restrict__ den) {
+    size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= N * Z) return;
+    size_t zi = g / N, k = g % N;
+    uint32_t z = zval[zi];
+    den[g] = k == z ? fe_one<F>() : fe_sub<F>(pw[k], pw[z]);
+}
+
+// one block per z group: q_z[k] = (S_z[k] - S_z[z]) * inv[k] (k != z),
+// q_z[z] = -w^-z sum_{k != z} q_z[k] w^k   (divide_by_vanishing, lagrange_basis.rs:91-119)
+__global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, const fe<F>* __restrict__ inv,
+                                                const fe<F>* __restrict__ pw, const fe<F>* __restrict__ pw_inv,
+                                                const uint32_t* __restrict__ zval, size_t N, fe<F>* __restrict__ Q) {
+    __shared__ fe<F> sh[256];
+    uint32_t zi = blockIdx.x;
+    uint32_t z = zval[zi];
+    const fe<F>* Sz = S + (size_t)zi * N;
+    fe<F> fz = Sz[z];
+    fe<F> acc = fe_zero<F>();
+    for (size_t k = threadIdx.x; k < N; k += 256) {
+        fe<F> q = fe_zero<F>();
+        if (k != z) {
+            q = fe_mul<F>(fe_sub<F>(Sz[k], fz), inv[(size_t)zi * N + k]);
+            acc = fe_add<F>(acc, fe_mul<F>(q, pw[k]));
+        }
+        Q[(size_t)zi * N + k] = q;
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) sh[threadIdx.x] = fe_add<F>(sh[threadIdx.x], sh[threadIdx.x + h]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) Q[(size_t)zi * N + z] = fe_neg<F>(fe_mul<F>(sh[0], pw_inv[z]));
+}
+
+// g[k] = sum_z Q[z][k] ; h[k] = sum_z invt[z] S[z][k] ; hmg = h - g
+__global__ void k_mp_combine(const fe<F>* __restrict__ S, const fe<F>* __restrict__ Q, const fe<F>* __restrict__ invt_z,
+                             size_t N, uint32_t Z, fe<F>* __restrict__ g, fe<F>* __restrict__ h) {
+    size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    fe<F> gg = fe_zero<F>(), hh = fe_zero<F>();
+    for (uint32_t zi = 0; zi < Z; zi++) {
+        gg = fe_add<F>(gg, Q[(size_t)zi * N + k]);
+        if (invt_z) hh = fe_add<F>(hh, fe_mul<F>(invt_z[zi], S[(size_t)zi * N + k]));
+    }
+    g[k] = gg;
+    if (invt_z) h[k] = hh;
+}
+
+// ---------------------------------------------------------------- to_data_item (a13)
+__global__ void k_to_data_item(const fe<BN254Fq>* __restrict__ xy, const uint8_t* __restrict__ inf, size_t n,
+                               fe<F>* __restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<F> r = fe_zero<F>();
+    if (!inf[i]) {
+        fe<BN254Fq> x = xy[2 * i], y = xy[2 * i + 1];
+        fe<BN254Fq> ny = fe_sub<BN254Fq>(fe_zero<BN254Fq>(), y);
+        bool neg = false;  // y > p - y (canonical)
+        for (int k = 7; k >= 0; k--) {
+            if (y.v[k] != ny.v[k]) {
+                neg = y.v[k] > ny.v[k];
+                break;
+            }
+        }
+        for (int k = 0; k < 8; k++) r.v[k] = x.v[k];
+        if (neg) r.v[7] |= 0x80000000u;
+        // value < 2^256 < 6r: subtract r while >= r
+        for (int it = 0; it < 6; it++) r = fe_reduce_once<F>(r);
+    }
+    out[i] = r;
+}
+
+}  // namespace vk
+
+using namespace vk;
+
+// ---------------------------------------------------------------- C ABI
+namespace {
+struct Guard {
+    vc_ctx* c;
+    std::lock_guard<std::mutex> lk;
+    explicit Guard(vc_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); }
+    ~Guard() {
+        if (c->timing) c->collect_timers();
+    }
+};
+bool proof_ok(const vc_ipa_proof* p) { return p && p->l_xy && p->r_xy && p->l_inf && p->r_inf; }
+}  // namespace
+
+extern "C" {
+
+int vc_to_data_item_batch(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, uint64_t* out) {
+    if (!ctx || (n && (!xy || !inf || !out))) return VC_E_INVALID;
+    if (ctx->curve != VC_CURVE_BN254) return VC_E_INVALID;
+    Guard g(ctx);
+    if (n == 0) return VC_OK;
+    DevBuf dxy, dinf, dout;
+    VK_TRY(dxy.ensure(n * 64));
+    VK_TRY(dinf.ensure(n));
+    VK_TRY(dout.ensure(n * 32));
+    VK_CHECK_HIP(hipMemcpyAsync(dxy.p, xy, n * 64, hipMemcpyHostToDevice, ctx->stream));
+    VK_CHECK_HIP(hipMemcpyAsync(dinf.p, inf, n, hipMemcpyHostToDevice, ctx->stream));
+    VK_LAUNCH(ctx, "to_data_item", k_to_data_item, (n + 255) / 256, 256, 0, dxy.as<fe<BN254Fq>>(), dinf.as<uint8_t>(),
+              n, dout.as<fe<F>>());
+    VK_CHECK_HIP(hipMemcpyAsync(out, dout.p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+int vc_ipa_commit(vc_ctx* ctx, int table, size_t N, const uint64_t* data, size_t batch, uint64_t* out_xy,
+                  uint8_t* out_inf) {
+    return vc_msm_batch(ctx, table, N, data, batch, 0, out_xy, out_inf);
+}
+
+int vc_ipa_prove(vc_ctx* ctx, int table, size_t N, const uint64_t* data, const uint64_t* com_xy,
+                 const uint8_t* com_inf, const uint64_t* points, size_t batch, vc_transcript** trs,
+                 vc_ipa_proof* proofs) {
+    if (!ctx || !data || !com_xy || !com_inf || !points || !proofs || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    for (size_t p = 0; p < batch; p++)
+        if (!proof_ok(&proofs[p])) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    std::vector<std::vector<Fr>> d(batch, std::vector<Fr>(N));
+    std::vector<Acc> coms(batch);
+    std::vector<Fr> pts(batch);
+    for (size_t p = 0; p < batch; p++) {
+        for (size_t i = 0; i < N; i++) d[p][i] = fr_of(data + (p * N + i) * 4);
+        coms[p] = acc_of(com_xy + 8 * p, com_inf[p]);
+        pts[p] = fr_of(points + 4 * p);
+    }
+    return ipa_prove_impl(ctx, t, N, d, coms, pts, trs, proofs);
+}
+
+int vc_ipa_verify(vc_ctx* ctx, int table, size_t N, const uint64_t* com_xy, uint8_t com_inf, const uint64_t* point,
+                  const vc_ipa_proof* proof, vc_transcript* tr, int* result) {
+    if (!ctx || !point || !proof_ok(proof) || !result || (!com_xy && !com_inf) || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    uint64_t zero[8] = {0};
+    return ipa_verify_impl(ctx, t, N, acc_of(com_inf ? zero : com_xy, com_inf), fr_of(point), proof, tr, result);
+}
+
+int vc_kzg_setup(vc_ctx* ctx, size_t max_items, const uint64_t* secret, int* table_id, size_t* size) {
+    if (!ctx || !secret || !table_id || max_items == 0) return VC_E_INVALID;
+    Guard g(ctx);
+    size_t n = 1;
+    while (n < max_items) n <<= 1;
+    DevBuf acc;
+    Table* t = new Table();
+    int st = VC_OK;
+    if (ctx->curve == VC_CURVE_BN254) {
+        st = acc.ensure(n * sizeof(BN254G1::Acc));
+        BN254G1::Aff gen;
+        uint64_t gxy[8] = {1, 0, 0, 0, 2, 0, 0, 0};
+        gen.x = canon_to_mont<BN254Fq>(gxy);
+        gen.y = canon_to_mont<BN254Fq>(gxy + 4);
+        if (st == VC_OK)
+            st = kzg_srs_dev<BN254G1, BN254Fr>(ctx, max_items, n, canon_to_mont<BN254Fr>(secret),
+                                               group_gen_t<BN254Fr>(n, 5), gen, acc.as<BN254G1::Acc>());
+    } else if (ctx->curve == VC_CURVE_BLS12_381) {
+        st = acc.ensure(n * sizeof(BLS381G1::Acc));
+        BLS381G1::Aff gen;
+        const uint64_t gx[6] = {0xfb3af00adb22c6bbull, 0x6c55e83ff97a1aefull, 0xa14e3a3f171bac58ull,
+                                0xc3688c4f9774b905ull, 0x2695638c4fa9ac0full, 0x17f1d3a73197d794ull};
+        const uint64_t gy[6] = {0x0caa232946c5e7e1ull, 0xd03cc744a2888ae4ull, 0x00db18cb2c04b3edull,
+                                0xfcf5e095d5d00af6ull, 0xa09e30ed741d8ae4ull, 0x08b3f481e3aaa0f1ull};
+        gen.x = canon_to_mont<BLS381Fq>(gx);
+        gen.y = canon_to_mont<BLS381Fq>(gy);
+        if (st == VC_OK)
+            st = kzg_srs_dev<BLS381G1, BLS381Fr>(ctx, max_items, n, canon_to_mont<BLS381Fr>(secret),
+                                                 group_gen_t<BLS381Fr>(n, 7), gen, acc.as<BLS381G1::Acc>());
+    } else {
+        st = VC_E_INVALID;
+    }
+    if (st == VC_OK) st = table_from_acc(ctx, t, acc.p, n);
+    if (st != VC_OK) {
+        delete t;
+        return st;
+    }
+    ctx->tables.push_back(t);
+    *table_id = (int)ctx->tables.size() - 1;
+    if (size) *size = n;
+    return VC_OK;
+}
+
+int vc_kzg_prove(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                 uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y) {
+    if (!ctx || (max && !evals) || !point || !proof_xy || !proof_inf || !y) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    if (ctx->curve == VC_CURVE_BN254)
+        return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, size, evals, max, point, proof_xy, proof_inf, y, nullptr);
+    if (ctx->curve == VC_CURVE_BLS12_381)
+        return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, evals, max, point, proof_xy, proof_inf, y, nullptr);
+    return VC_E_INVALID;
+}
+
+int vc_kzg_quotient(vc_ctx* ctx, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                    uint64_t* q_out, uint64_t* y) {
+    if (!ctx || (max && !evals) || !point || !q_out || !y) return VC_E_INVALID;
+    Guard g(ctx);
+    if (ctx->curve == VC_CURVE_BN254)
+        return kzg_prove_t<BN254G1, BN254Fr>(ctx, nullptr, size, evals, max, point, nullptr, nullptr, y, q_out);
+    if (ctx->curve == VC_CURVE_BLS12_381)
+        return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, nullptr, size, evals, max, point, nullptr, nullptr, y, q_out);
+    return VC_E_INVALID;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- multiproof (a11)
+namespace vk {
+
+struct MpPrep {
+    Fr r, t;
+    std::vector<Fr> rpow;
+};
+
+static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                                    const uint64_t* y) {
+    vc_transcript* tr = vc_transcript_new("multiproof");
+    for (size_t i = 0; i < Q; i++) {
+        vc_transcript_append_point(tr, com_xy + 8 * i, com_inf[i], "C");
+        vc_transcript_append_u64(tr, z[i], "z");
+        vc_transcript_append_fr(tr, y + 4 * i, "y");
+    }
+    return tr;
+}
+
+static std::vector<Fr> invert_domain_at(const Fr& t, size_t N) {  // utils.rs:57-62 (integer i)
+    std::vector<Fr> d(N);
+    for (size_t i = 0; i < N; i++) d[i] = fe_sub<F>(t, fr_u64(i));
+    return host_batch_inv(d);
+}
+
+static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const uint64_t* data, const uint64_t* com_xy,
+                    const uint8_t* com_inf, const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
+                    vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
+    for (size_t i = 0; i < Q; i++)
+        if (z[i] >= N) return VC_E_DOMAIN;
+    vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y);
+    Fr r = transcript_digest(tr, "r");
+    std::vector<Fr> rpow(Q);
+    Fr cur = fe_one<F>();
+    for (size_t i = 0; i < Q; i++) {
+        rpow[i] = cur;
+        cur = fe_mul<F>(cur, r);
+    }
+    // group queries by z (counting sort)
+    std::vector<uint32_t> cnt(N + 1, 0), order(Q);
+    for (size_t i = 0; i < Q; i++) cnt[z[i] + 1]++;
+    for (size_t k = 0; k < N; k++) cnt[k + 1] += cnt[k];
+    {
+        std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
+        for (size_t i = 0; i < Q; i++) order[pos[z[i]]++] = (uint32_t)i;
+    }
+    std::vector<uint32_t> zval, zstart;
+    for (size_t k = 0; k < N; k++)
+        if (cnt[k + 1] > cnt[k]) {
+            zval.push_back((uint32_t)k);
+            zstart.push_back(cnt[k]);
+        }
+    zstart.push_back((uint32_t)Q);
+    const uint32_t Z = (uint32_t)zval.size();
+    hipStream_t st = ctx->stream;
+    DevBuf d_raw, d_f, d_r, d_order, d_zs, d_zv, d_S, d_den, d_inv, d_Q, d_pw, d_pwi, d_g, d_h, d_it;
+    VK_TRY(d_raw.ensure(Q * N * 32));
+    VK_TRY(d_f.ensure(Q * N * 32));
+    VK_TRY(d_r.ensure(Q * 32));
+    VK_TRY(d_order.ensure(Q * 4));
+    VK_TRY(d_zs.ensure((Z + 1) * 4));
+    VK_TRY(d_zv.ensure(Z * 4));
+    VK_TRY(d_S.ensure((size_t)Z * N * 32));
+    VK_TRY(d_den.ensure((size_t)Z * N * 32));
+    VK_TRY(d_inv.ensure((size_t)Z * N * 32));
+    VK_TRY(d_Q.ensure((size_t)Z * N * 32));
+    VK_TRY(d_pw.ensure(N * 32));
+    VK_TRY(d_pwi.ensure(N * 32));
+    VK_TRY(d_g.ensure(N * 32));
+    VK_TRY(d_h.ensure(N * 32));
+    VK_TRY(d_it.ensure(Z * 32));
+    VK_CHECK_HIP(hipMemcpyAsync(d_raw.p, data, Q * N * 32, hipMemcpyHostToDevice, st));
+    VK_TRY(canon_to_mont_dev<F>(ctx, d_raw.p, Q * N, Q * N, d_f.as<fe<F>>()));
+    VK_CHECK_HIP(hipMemcpyAsync(d_r.p, rpow.data(), Q * 32, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(d_order.p, order.data(), Q * 4, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(d_zs.p, zstart.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(d_zv.p, zval.data(), Z * 4, hipMemcpyHostToDevice, st));
+    VK_LAUNCH(ctx, "mp_accumulate", k_mp_accumulate, dim3((N + 255) / 256, Z), 256, 0, d_f.as<fe<F>>(),
+              d_r.as<fe<F>>(), d_order.as<uint32_t>(), d_zs.as<uint32_t>(), N, Z, d_S.as<fe<F>>());
+    Fr omega = bn254_group_gen(N);
+    VK_TRY(domain_powers<F>(ctx, omega, N, d_pw.as<fe<F>>()));
+    VK_TRY(domain_powers<F>(ctx, fe_inv_bin<F>(omega), N, d_pwi.as<fe<F>>()));
+    VK_LAUNCH(ctx, "mp_den", k_mp_den, ((size_t)Z * N + 255) / 256, 256, 0, d_pw.as<fe<F>>(), d_zv.as<uint32_t>(), N,
+              Z, d_den.as<fe<F>>());
+    VK_TRY(batch_inverse<F>(ctx, d_den.as<fe<F>>(), d_inv.as<fe<F>>(), (size_t)Z * N));
+    VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, d_S.as<fe<F>>(), d_inv.as<fe<F>>(), d_pw.as<fe<F>>(),
+              d_pwi.as<fe<F>>(), d_zv.as<uint32_t>(), N, d_Q.as<fe<F>>());
+    VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
+              (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
+    std::vector<Fr> g(N), h(N);
+    VK_CHECK_HIP(hipMemcpyAsync(g.data(), d_g.p, N * 32, hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipStreamSynchronize(st));
+    // D = commit(g)
+    uint64_t dxy[8];
+    uint8_t dinf;
+    VK_TRY(commit_batch(ctx, t, N, g.data(), 1, dxy, &dinf));
+    transcript_append_point(tr, dxy, dinf, "D");
+    Fr tt = transcript_digest(tr, "t");
+    std::vector<Fr> invs = invert_domain_at(tt, N);
+    std::vector<Fr> invz(Z);
+    for (uint32_t k = 0; k < Z; k++) invz[k] = invs[zval[k]];
+    VK_CHECK_HIP(hipMemcpyAsync(d_it.p, invz.data(), Z * 32, hipMemcpyHostToDevice, st));
+    VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
+              d_it.as<fe<F>>(), N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
+    VK_CHECK_HIP(hipMemcpyAsync(h.data(), d_h.p, N * 32, hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipStreamSynchronize(st));
+    uint64_t exy[8];
+    uint8_t einf;
+    VK_TRY(commit_batch(ctx, t, N, h.data(), 1, exy, &einf));
+    transcript_append_point(tr, exy, einf, "E");
+    std::vector<Fr> hmg(N);
+    for (size_t k = 0; k < N; k++) hmg[k] = fe_sub<F>(h[k], g[k]);
+    Acc mc = C::add(acc_of(exy, einf), C::neg(acc_of(dxy, dinf)));
+    memcpy(d_xy, dxy, 64);
+    *d_inf = dinf;
+    int stt;
+    if (scheme == 0) {
+        std::vector<std::vector<Fr>> dd(1, hmg);
+        std::vector<Acc> cs(1, mc);
+        std::vector<Fr> ps(1, tt);
+        vc_transcript* trs[1] = {tr};
+        stt = ipa_prove_impl(ctx, t, N, dd, cs, ps, trs, ipa_proof);
+    } else {
+        std::vector<uint64_t> ev(N * 4);
+        for (size_t k = 0; k < N; k++) canon_of(hmg[k], &ev[4 * k]);
+        uint64_t tc[4];
+        canon_of(tt, tc);
+        stt = kzg_prove_t<BN254G1, BN254Fr>(ctx, t, N, ev.data(), N, tc, kzg_xy, kzg_inf, kzg_y, nullptr);
+    }
+    vc_transcript_free(tr);
+    return stt;
+}
+
+// E - D and t of verify_multiproof (:178-215); tr returned positioned after "E"
+static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                    const uint64_t* y, const uint64_t* d_xy, uint8_t d_inf, Acc* claim, Fr* t_out,
+                    vc_transcript** tr_out) {
+    for (size_t i = 0; i < Q; i++)
+        if (z[i] >= N) return VC_E_DOMAIN;
+    vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y);
+    Fr r = transcript_digest(tr, "r");
+    vc_transcript_append_point(tr, d_xy, d_inf, "D");
+    Fr tt = transcript_digest(tr, "t");
+    std::vector<Fr> invs = invert_domain_at(tt, N);
+    std::vector<Fr> coef(Q);
+    Fr rp = fe_one<F>();
+    for (size_t i = 0; i < Q; i++) {
+        coef[i] = fe_mul<F>(rp, invs[z[i]]);
+        rp = fe_mul<F>(rp, r);
+    }
+    std::vector<uint64_t> xy(com_xy, com_xy + 8 * Q);
+    std::vector<uint8_t> inf(com_inf, com_inf + Q);
+    Acc e;
+    int st = msm_points(ctx, xy, inf, coef, &e);
+    if (st != VC_OK) {
+        vc_transcript_free(tr);
+        return st;
+    }
+    uint64_t exy[8];
+    uint8_t einf;
+    aff_of(e, exy, &einf);
+    vc_transcript_append_point(tr, exy, einf, "E");
+    *claim = C::add(e, C::neg(acc_of(d_xy, d_inf)));
+    *t_out = tt;
+    *tr_out = tr;
+    return VC_OK;
+}
+
+}  // namespace vk
+
+extern "C" {
+
+int vc_multiproof_prove(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* data,
+                        const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                        uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf,
+                        uint64_t* kzg_y) {
+    if (!ctx || !data || !com_xy || !com_inf || !z || !y || !d_xy || !d_inf || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    if (scheme == 0 && !proof_ok(ipa_proof)) return VC_E_INVALID;
+    if (scheme == 1 && (!kzg_xy || !kzg_inf || !kzg_y)) return VC_E_INVALID;
+    if (scheme != 0 && scheme != 1) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    return mp_prove(ctx, scheme, t, N, Q, data, com_xy, com_inf, z, y, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf, kzg_y);
+}
+
+int vc_multiproof_verify_ipa(vc_ctx* ctx, int table, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                             const uint64_t* z, const uint64_t* y, const uint64_t* d_xy, uint8_t d_inf,
+                             const vc_ipa_proof* proof, int* result) {
+    if (!ctx || !com_xy || !com_inf || !z || !y || !d_xy || !proof_ok(proof) || !result || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    Acc claim;
+    Fr tt;
+    vc_transcript* tr = nullptr;
+    VK_TRY(mp_claim(ctx, N, Q, com_xy, com_inf, z, y, d_xy, d_inf, &claim, &tt, &tr));
+    int st = ipa_verify_impl(ctx, t, N, claim, tt, proof, tr, result);
+    vc_transcript_free(tr);
+    return st;
+}
+
+int vc_multiproof_kzg_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                            const uint64_t* z, const uint64_t* y, const uint64_t* d_xy, uint8_t d_inf, uint64_t* c_xy,
+                            uint8_t* c_inf, uint64_t* t_out) {
+    if (!ctx || !com_xy || !com_inf || !z || !y || !d_xy || !c_xy || !c_inf || !t_out || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    Guard g(ctx);
+    Acc claim;
+    Fr tt;
+    vc_transcript* tr = nullptr;
+    VK_TRY(mp_claim(ctx, N, Q, com_xy, com_inf, z, y, d_xy, d_inf, &claim, &tt, &tr));
+    vc_transcript_free(tr);
+    aff_of(claim, c_xy, c_inf);
+    canon_of(tt, t_out);
+    return VC_OK;
+}
+
+}  // extern "C"

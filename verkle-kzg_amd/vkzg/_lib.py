@@ -10,7 +10,7 @@ import re
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
 LIB_PATH = os.environ.get("VKZG_LIB") or os.path.join(ROOT, "lib", "libvkzg.so")
-HEADER = os.path.join(os.path.dirname(ROOT), "include", "vc_msm.h")
+HEADERS = [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("vc_msm.h", "vc_scheme.h")]
 
 c_void_p, c_int, c_size_t, c_uint64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
 c_double, c_long, c_char_p = ctypes.c_double, ctypes.c_long, ctypes.c_char_p
@@ -38,6 +38,29 @@ SIGNATURES = {
     "vc_msm_batch": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
     "vc_msm_batch_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
     "vc_fixed_base_precompute": (c_int, [c_void_p, c_int, c_int]),
+    # vc_scheme.h
+    "vc_transcript_new": (c_void_p, [c_char_p]),
+    "vc_transcript_clone": (c_void_p, [c_void_p]),
+    "vc_transcript_free": (None, [c_void_p]),
+    "vc_transcript_append_bytes": (c_int, [c_void_p, P, c_size_t, c_char_p]),
+    "vc_transcript_append_point": (c_int, [c_void_p, P, ctypes.c_uint8, c_char_p]),
+    "vc_transcript_append_fr": (c_int, [c_void_p, P, c_char_p]),
+    "vc_transcript_append_u64": (c_int, [c_void_p, c_uint64, c_char_p]),
+    "vc_transcript_digest": (c_int, [c_void_p, c_char_p, P]),
+    "vc_hash_to_field": (c_int, [P, c_size_t, P, c_size_t, P]),
+    "vc_point_compress": (c_int, [P, ctypes.c_uint8, P]),
+    "vc_to_data_item_batch": (c_int, [c_void_p, P, P, c_size_t, P]),
+    "vc_ipa_crs": (c_int, [P, c_size_t, c_size_t, c_size_t, P]),
+    "vc_kzg_setup": (c_int, [c_void_p, c_size_t, P, ctypes.POINTER(c_int), ctypes.POINTER(c_size_t)]),
+    "vc_ipa_commit": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P]),
+    "vc_ipa_prove": (c_int, [c_void_p, c_int, c_size_t, P, P, P, P, c_size_t, P, P]),
+    "vc_ipa_verify": (c_int, [c_void_p, c_int, c_size_t, P, ctypes.c_uint8, P, P, c_void_p, ctypes.POINTER(c_int)]),
+    "vc_kzg_prove": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
+    "vc_kzg_quotient": (c_int, [c_void_p, c_size_t, P, c_size_t, P, P, P]),
+    "vc_multiproof_prove": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P, P, P, P, P, P]),
+    "vc_multiproof_verify_ipa": (c_int, [c_void_p, c_int, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P,
+                                         ctypes.POINTER(c_int)]),
+    "vc_multiproof_kzg_claim": (c_int, [c_void_p, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P, P, P]),
 }
 
 _lib = None
@@ -78,7 +101,10 @@ def check(status, where):
 
 
 def header_functions():
-    """Names of every function declared in include/vc_msm.h."""
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(vc_[a-z0-9_]+)\s*\(", src)))
+    """Names of every function declared in include/vc_msm.h and include/vc_scheme.h."""
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(vc_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)

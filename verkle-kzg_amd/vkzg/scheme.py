@@ -1,0 +1,341 @@
+"""Reference-shaped VectorCommitment API over the HIP engine (include/vc_scheme.h).
+
+Mirrors /root/reference/vector-commit/src: `IPA` (ipa/mod.rs), `KZG` (kzg/mod.rs),
+`LagrangeBasis` (lagrange_basis.rs), `TranscriptHasher` (transcript.rs),
+`prove_multiproof` / `verify_multiproof` (multiproof.rs), `to_data_item` (lib.rs:56-67).
+Same names, argument meaning and error behaviour (errors raise `VCError` where the Rust
+returns Err or panics). Curve: BN254 G1 (the reference's only instantiation).
+Points are canonical affine (x, y) tuples, the identity is None; field elements are ints.
+All arithmetic runs in libvkzg.so; this module only marshals.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import VCError, check, lib
+from .engine import Engine, ints_to_limbs, limbs_to_int
+
+R_BN254 = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+_P = ctypes.c_void_p
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _fr(x):
+    return ints_to_limbs([int(x) % R_BN254], 4)[0].copy()
+
+
+def _pt_arrays(pts):
+    xy = np.zeros((len(pts), 8), dtype=np.uint64)
+    inf = np.zeros(len(pts), dtype=np.uint8)
+    for i, P in enumerate(pts):
+        if P is None:
+            inf[i] = 1
+        else:
+            xy[i, :4] = ints_to_limbs([P[0]], 4)[0]
+            xy[i, 4:] = ints_to_limbs([P[1]], 4)[0]
+    return xy, inf
+
+
+def _pt(xy, inf):
+    if inf:
+        return None
+    return (limbs_to_int(xy[:4]), limbs_to_int(xy[4:8]))
+
+
+# ---------------------------------------------------------------- transcript.rs
+class TranscriptHasher:
+    def __init__(self, label, _h=None):
+        self.h = _h if _h is not None else lib().vc_transcript_new(label.encode())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().vc_transcript_free(self.h)
+            self.h = None
+
+    def clone(self):
+        return TranscriptHasher(None, lib().vc_transcript_clone(self.h))
+
+    def append_point(self, P, label):
+        xy, inf = _pt_arrays([P])
+        check(lib().vc_transcript_append_point(self.h, _p(xy), int(inf[0]), label.encode()), "append_point")
+
+    def append_fr(self, x, label):
+        check(lib().vc_transcript_append_fr(self.h, _p(_fr(x)), label.encode()), "append_fr")
+
+    def append_usize(self, z, label):
+        check(lib().vc_transcript_append_u64(self.h, int(z), label.encode()), "append_usize")
+
+    def digest(self, label, clear=True):
+        out = np.zeros(4, dtype=np.uint64)
+        check(lib().vc_transcript_digest(self.h, label.encode(), _p(out)), "digest")
+        return limbs_to_int(out)
+
+
+def hash_to_field(msg, dst):
+    m = np.frombuffer(bytes(msg) or b"\0", dtype=np.uint8).copy()
+    d = np.frombuffer(bytes(dst) or b"\0", dtype=np.uint8).copy()
+    out = np.zeros(4, dtype=np.uint64)
+    check(lib().vc_hash_to_field(_p(m), len(msg), _p(d), len(dst), _p(out)), "hash_to_field")
+    return limbs_to_int(out)
+
+
+def point_compress(P):
+    xy, inf = _pt_arrays([P])
+    out = np.zeros(32, dtype=np.uint8)
+    check(lib().vc_point_compress(_p(xy), int(inf[0]), _p(out)), "point_compress")
+    return out.tobytes()
+
+
+def to_data_item(engine, pts):
+    """VCCommitment::to_data_item for a batch of points (device)."""
+    xy, inf = _pt_arrays(pts)
+    out = np.zeros((len(pts), 4), dtype=np.uint64)
+    check(lib().vc_to_data_item_batch(engine.h, _p(xy), _p(inf), len(pts), _p(out)), "to_data_item")
+    return [limbs_to_int(r) for r in out]
+
+
+def ipa_crs(num, seed=b"eth_verkle_oct_2021", max_=256):
+    """IPAPointGenerator::gen (ipa_point_generator.rs:51-67); VCError(VC_E_RANGE) = OutOfBounds."""
+    s = np.frombuffer(seed, dtype=np.uint8).copy()
+    out = np.zeros((max(num, 1), 8), dtype=np.uint64)
+    check(lib().vc_ipa_crs(_p(s), len(seed), max_, num, _p(out)), "ipa_crs")
+    return [_pt(out[i], 0) for i in range(num)]
+
+
+# ---------------------------------------------------------------- lagrange_basis.rs
+class LagrangeBasis:
+    """Evaluations over a radix-2 domain (possibly shorter than it: `max`)."""
+
+    def __init__(self, evals, domain_size=None):
+        self.evals = [int(e) % R_BN254 for e in evals]
+        ds = 1
+        while ds < len(self.evals):
+            ds <<= 1
+        self.dsize = domain_size if domain_size is not None else ds
+
+    @classmethod
+    def from_vec(cls, data):
+        return cls(data)
+
+    def __getitem__(self, i):
+        return self.evals[i]
+
+    def max(self):
+        return len(self.evals) - 1
+
+    def limbs(self, n=None):
+        arr = ints_to_limbs(self.evals, 4)
+        if n is not None and arr.shape[0] < n:
+            arr = np.vstack([arr, np.zeros((n - arr.shape[0], 4), dtype=np.uint64)])
+        return np.ascontiguousarray(arr)
+
+
+# ---------------------------------------------------------------- proofs
+class _ProofBuf(ctypes.Structure):
+    _fields_ = [("rounds", ctypes.c_size_t), ("l_xy", _P), ("l_inf", _P), ("r_xy", _P), ("r_inf", _P),
+                ("tip", ctypes.c_uint64 * 4), ("y", ctypes.c_uint64 * 4)]
+
+
+class IPAProof:
+    def __init__(self, l, r, tip, y):
+        self.l, self.r, self.tip, self.y = l, r, tip, y
+
+    def as_dict(self):
+        return {"l": self.l, "r": self.r, "tip": self.tip, "y": self.y}
+
+    @staticmethod
+    def _alloc(rounds):
+        arrs = {"lxy": np.zeros((rounds, 8), dtype=np.uint64), "linf": np.zeros(rounds, dtype=np.uint8),
+                "rxy": np.zeros((rounds, 8), dtype=np.uint64), "rinf": np.zeros(rounds, dtype=np.uint8)}
+        b = _ProofBuf(rounds, _p(arrs["lxy"]), _p(arrs["linf"]), _p(arrs["rxy"]), _p(arrs["rinf"]))
+        return b, arrs
+
+    @staticmethod
+    def _from(b, arrs):
+        k = b.rounds
+        return IPAProof([_pt(arrs["lxy"][i], arrs["linf"][i]) for i in range(k)],
+                        [_pt(arrs["rxy"][i], arrs["rinf"][i]) for i in range(k)],
+                        limbs_to_int(list(b.tip)), limbs_to_int(list(b.y)))
+
+    def _to(self):
+        k = len(self.l)
+        b, arrs = IPAProof._alloc(k)
+        xy, inf = _pt_arrays(self.l)
+        arrs["lxy"][:] = xy
+        arrs["linf"][:] = inf
+        xy, inf = _pt_arrays(self.r)
+        arrs["rxy"][:] = xy
+        arrs["rinf"][:] = inf
+        b.tip[:] = [int(v) for v in _fr(self.tip)]
+        b.y[:] = [int(v) for v in _fr(self.y)]
+        return b, arrs
+
+
+def _log2(n):
+    k = 0
+    while (1 << k) < n:
+        k += 1
+    return k
+
+
+# ---------------------------------------------------------------- ipa/mod.rs
+class IPA:
+    """IPA<N, G1(BN254), DefaultFieldHasher<Sha256>, GeneralEvaluationDomain>."""
+
+    def __init__(self, engine, N, points):
+        if engine.curve != "bn254":
+            raise ValueError("the protocol layer is instantiated for BN254")
+        assert len(points) == N + 1
+        self.engine, self.N = engine, N
+        self.g, self.q = points[:N], points[N]
+        self.table = engine.upload_points(points)          # IPAUniversalParams::new_from_vec
+
+    @classmethod
+    def setup(cls, engine, max_items, gen_max=256, seed=b"eth_verkle_oct_2021"):
+        """IPA::setup (:121-128): N + 1 generator points (fails OutOfBounds, Appendix B.1)."""
+        return cls(engine, max_items, ipa_crs(max_items + 1, seed, gen_max))
+
+    def max_size(self):
+        return self.N
+
+    def commit(self, data):
+        return self.commit_batch([data])[0]
+
+    def commit_batch(self, datas):
+        sc = np.concatenate([d.limbs(self.N)[: self.N] for d in datas])
+        xy, inf = self.engine.msm_batch(self.table, sc, self.N)
+        return [_pt(xy[i], inf[i]) for i in range(len(datas))]
+
+    def prove_point(self, commitment, point, data, transcript=None):
+        return self.prove_batch_points([commitment], [point], [data], [transcript])[0]
+
+    def prove_batch_points(self, commitments, points, datas, transcripts=None):
+        B = len(datas)
+        d = np.concatenate([x.limbs(self.N)[: self.N] for x in datas])
+        cxy, cinf = _pt_arrays(commitments)
+        pts = ints_to_limbs([int(p) % R_BN254 for p in points], 4)
+        K = _log2(self.N)
+        bufs = [IPAProof._alloc(K) for _ in range(B)]
+        arr = (_ProofBuf * B)(*[b for b, _ in bufs])
+        trs = None
+        if transcripts is not None and any(t is not None for t in transcripts):
+            trs = (_P * B)(*[(t.h if t is not None else None) for t in transcripts])
+        check(lib().vc_ipa_prove(self.engine.h, self.table, self.N, _p(d), _p(cxy), _p(cinf), _p(pts), B,
+                                 ctypes.cast(trs, _P) if trs is not None else None, ctypes.cast(arr, _P)),
+              "ipa_prove")
+        return [IPAProof._from(arr[i], bufs[i][1]) for i in range(B)]
+
+    def prove(self, commitment, index, data):
+        return self.prove_point(commitment, index, data)
+
+    def verify_point(self, commitment, point, proof, transcript=None):
+        cxy, cinf = _pt_arrays([commitment])
+        b, arrs = proof._to()
+        res = ctypes.c_int()
+        check(lib().vc_ipa_verify(self.engine.h, self.table, self.N, _p(cxy), int(cinf[0]), _p(_fr(point)),
+                                  ctypes.byref(b), transcript.h if transcript is not None else None,
+                                  ctypes.byref(res)), "ipa_verify")
+        return bool(res.value)
+
+    def verify(self, commitment, index, proof):
+        return self.verify_point(commitment, index, proof)
+
+
+# ---------------------------------------------------------------- kzg/mod.rs
+class KZG:
+    """KZG<Bn254, ...> prover side (pairing verification is out of scope: see DESIGN.md)."""
+
+    def __init__(self, engine, max_items, secret=100):
+        self.engine = engine
+        tid = ctypes.c_int()
+        size = ctypes.c_size_t()
+        check(lib().vc_kzg_setup(engine.h, max_items, _p(_fr(secret)), ctypes.byref(tid), ctypes.byref(size)),
+              "kzg_setup")
+        self.table, self.size, self.secret = tid.value, size.value, secret
+
+    def max_size(self):
+        return self.size
+
+    def lagrange_points(self):
+        xy, inf = self.engine.download_bases(self.table)
+        return [_pt(xy[i], inf[i]) for i in range(self.size)]
+
+    def commit(self, data):
+        """:126-134 inner_product(lagrange_commitments, evals) (zip-truncating)."""
+        sc = data.limbs()
+        xy, inf = self.engine.msm(self.table, sc)
+        return _pt(xy, inf)
+
+    def prove_point(self, commitment, point, data, transcript=None):
+        ev = data.limbs()
+        pxy = np.zeros(8, dtype=np.uint64)
+        pinf = np.zeros(1, dtype=np.uint8)
+        y = np.zeros(4, dtype=np.uint64)
+        check(lib().vc_kzg_prove(self.engine.h, self.table, self.size, _p(ev), len(data.evals), _p(_fr(point)),
+                                 _p(pxy), _p(pinf), _p(y)), "kzg_prove")
+        return {"proof": _pt(pxy, pinf[0]), "y": limbs_to_int(y)}
+
+    def prove(self, commitment, index, data):
+        return self.prove_point(commitment, index, data)
+
+    def quotient(self, point, data):
+        ev = data.limbs()
+        q = np.zeros((self.size, 4), dtype=np.uint64)
+        y = np.zeros(4, dtype=np.uint64)
+        check(lib().vc_kzg_quotient(self.engine.h, self.size, _p(ev), len(data.evals), _p(_fr(point)), _p(q),
+                                    _p(y)), "kzg_quotient")
+        return [limbs_to_int(r) for r in q], limbs_to_int(y)
+
+
+# ---------------------------------------------------------------- multiproof.rs
+def _queries(queries, N):
+    Q = len(queries)
+    data = np.concatenate([q[0].limbs(N)[:N] for q in queries])
+    cxy, cinf = _pt_arrays([q[1] for q in queries])
+    z = np.array([int(q[2]) for q in queries], dtype=np.uint64)
+    y = ints_to_limbs([int(q[3]) % R_BN254 for q in queries], 4)
+    return Q, data, cxy, cinf, z, y
+
+
+def prove_multiproof(vc, queries):
+    """queries: list of (LagrangeBasis data, commitment, z, y). Returns {"proof", "d"}."""
+    N = vc.N if isinstance(vc, IPA) else vc.size
+    Q, data, cxy, cinf, z, y = _queries(queries, N)
+    dxy = np.zeros(8, dtype=np.uint64)
+    dinf = np.zeros(1, dtype=np.uint8)
+    if isinstance(vc, IPA):
+        b, arrs = IPAProof._alloc(_log2(N))
+        check(lib().vc_multiproof_prove(vc.engine.h, 0, vc.table, N, Q, _p(data), _p(cxy), _p(cinf), _p(z), _p(y),
+                                        _p(dxy), _p(dinf), ctypes.byref(b), None, None, None), "multiproof_prove")
+        return {"proof": IPAProof._from(b, arrs), "d": _pt(dxy, dinf[0])}
+    kxy = np.zeros(8, dtype=np.uint64)
+    kinf = np.zeros(1, dtype=np.uint8)
+    ky = np.zeros(4, dtype=np.uint64)
+    check(lib().vc_multiproof_prove(vc.engine.h, 1, vc.table, N, Q, _p(data), _p(cxy), _p(cinf), _p(z), _p(y),
+                                    _p(dxy), _p(dinf), None, _p(kxy), _p(kinf), _p(ky)), "multiproof_prove")
+    return {"proof": {"proof": _pt(kxy, kinf[0]), "y": limbs_to_int(ky)}, "d": _pt(dxy, dinf[0])}
+
+
+def verify_multiproof(vc, vqueries, mp):
+    """IPA: full verification. KZG: returns the (E - D, t) claim for an external pairing check."""
+    N = vc.N if isinstance(vc, IPA) else vc.size
+    Q = len(vqueries)
+    cxy, cinf = _pt_arrays([q[0] for q in vqueries])
+    z = np.array([int(q[1]) for q in vqueries], dtype=np.uint64)
+    y = ints_to_limbs([int(q[2]) % R_BN254 for q in vqueries], 4)
+    dxy, dinf = _pt_arrays([mp["d"]])
+    if isinstance(vc, IPA):
+        b, arrs = mp["proof"]._to()
+        res = ctypes.c_int()
+        check(lib().vc_multiproof_verify_ipa(vc.engine.h, vc.table, N, Q, _p(cxy), _p(cinf), _p(z), _p(y), _p(dxy),
+                                             int(dinf[0]), ctypes.byref(b), ctypes.byref(res)), "multiproof_verify")
+        return bool(res.value)
+    oxy = np.zeros(8, dtype=np.uint64)
+    oinf = np.zeros(1, dtype=np.uint8)
+    t = np.zeros(4, dtype=np.uint64)
+    check(lib().vc_multiproof_kzg_claim(vc.engine.h, N, Q, _p(cxy), _p(cinf), _p(z), _p(y), _p(dxy), int(dinf[0]),
+                                        _p(oxy), _p(oinf), _p(t)), "multiproof_kzg_claim")
+    return {"commitment": _pt(oxy, oinf[0]), "t": limbs_to_int(t)}
