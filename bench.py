@@ -27,6 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import vkzg  # noqa: E402
+from vkzg import dist as vdist  # noqa: E402
 
 METRIC = "width-256 commits/sec + 2^20-pt MSM ms at 1/2/4/8 GPU; achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -92,20 +93,12 @@ def main():
     table = eng.random_bases(n, seed=2024)
     rng = np.random.default_rng(1234)
     scalars = vkzg.random_scalars(curve, n, rng)
-    lo, hi = rank * n // world, (rank + 1) * n // world
+    lo, hi = vdist.shard_range(n, rank, world)
     d_sc = torch.from_numpy(scalars[lo:hi].view(np.int64).copy()).to(dev)
-    words = eng.point_words()
-    gathered = torch.zeros((world, words), dtype=torch.int32, device=dev)
 
     def step():
-        part = eng.msm_device_partial(table, d_sc.data_ptr(), hi - lo, offset=lo)
-        if world > 1:
-            t = torch.from_numpy(part.view(np.int32)).to(dev)
-            dist.all_gather_into_tensor(gathered, t)
-            parts = gathered.cpu().numpy().view(np.uint32)
-        else:
-            parts = part[None, :]
-        return eng.partials_sum(parts)
+        # shard partial (HIP) -> RCCL all-gather of projective partials -> host sum
+        return vdist.msm_sharded(eng, table, d_sc.data_ptr(), n, rank, world, dev if world > 1 else None)
 
     for _ in range(a.warmup):
         res = step()

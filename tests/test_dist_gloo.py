@@ -1,0 +1,74 @@
+"""world_size-2 gloo test (CPU) of the multi-GPU MSM exchange: point-range shards, all-gather of
+projective partials, host sum (vkzg.dist) == the whole MSM. Shard partials come from the
+oracle here (no GPU in this container); on the GPU box bench.py runs the same path with the
+HIP partials over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, curve, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd"), os.path.join(ROOT, "oracle")]
+    import random
+    import torch.distributed as dist
+    from pyoracle import cref
+    from pyoracle.curves import CURVES, random_points
+    from vkzg import dist as vdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    C = CURVES[curve]
+    rng = random.Random(17)
+    n = 37
+    pts = random_points(C, n, rng)
+    sc = [rng.randrange(C.r) for _ in range(n)]
+    lo, hi = vdist.shard_range(n, rank, world)
+    part = cref.msm(curve, pts[lo:hi], sc[lo:hi], 1)
+    words = vdist.affine_to_acc_words(curve, part)
+    parts = vdist.all_gather_partials(words, world, None)
+    xy, inf = vdist.partials_sum(curve, parts)
+    full = cref.msm(curve, pts, sc, 1)
+    nl = len(xy) // 2
+    got = None if inf else (sum(int(v) << (64 * j) for j, v in enumerate(xy[:nl])),
+                            sum(int(v) << (64 * j) for j, v in enumerate(xy[nl:])))
+    if curve == "bandersnatch" and inf:
+        got = (0, 1)
+    q.put((rank, got == full, parts.shape))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("curve", ["bn254", "bls12_381", "bandersnatch"])
+def test_sharded_msm_gloo_world2(curve, oracle_c):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, curve, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(shape[0] == 2 for _, _, shape in res)
+
+
+def test_shard_range_covers():
+    from vkzg import dist as vdist
+    for n in (0, 1, 7, 1 << 20):
+        for w in (1, 2, 3, 8):
+            parts = [vdist.shard_range(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))

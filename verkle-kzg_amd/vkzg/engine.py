@@ -70,6 +70,17 @@ def random_scalars(curve, n, rng):
     return s
 
 
+def partials_sum(curve, accs):
+    """vc_partials_sum: add projective accumulators on the host (no device needed)."""
+    accs = np.ascontiguousarray(accs, dtype=np.uint32)
+    nl = NL[curve]
+    out = np.zeros(2 * nl, dtype=np.uint64)
+    oinf = np.zeros(1, dtype=np.uint8)
+    check(lib().vc_partials_sum(CURVE_IDS[curve], _ptr(accs), accs.shape[0], _ptr(out), _ptr(oinf)),
+          "vc_partials_sum")
+    return out, int(oinf[0])
+
+
 class Engine:
     """One vc_ctx: a curve on one device."""
 
@@ -178,12 +189,7 @@ class Engine:
         return acc
 
     def partials_sum(self, accs):
-        accs = np.ascontiguousarray(accs, dtype=np.uint32)
-        out = np.zeros(2 * self.nl, dtype=np.uint64)
-        oinf = np.zeros(1, dtype=np.uint8)
-        check(lib().vc_partials_sum(self.cid, _ptr(accs), accs.shape[0], _ptr(out), _ptr(oinf)),
-              "vc_partials_sum")
-        return out, int(oinf[0])
+        return partials_sum(self.curve, accs)
 
     def msm_batch(self, table, scalars, width, mont=False):
         """scalars: (batch*width, 4) uint64. Returns ((batch, 2*NL) uint64, (batch,) uint8)."""
