@@ -124,8 +124,8 @@ def main():
     # dominant kernel (bucket accumulation) device time, HIP events on the launch stream
     acc_ms, acc_n = eng.kernel_time("msm_accumulate")
     kernels = {}
-    for k in ("msm_digits", "msm_scan", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce",
-              "msm_winsum"):
+    for k in ("msm_digits", "msm_scan", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_segsum",
+              "msm_bitsum", "msm_sumpart"):
         ms, cnt = eng.kernel_time(k)
         if cnt:
             kernels[k] = round(ms / cnt, 4)

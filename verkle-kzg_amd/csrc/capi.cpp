@@ -48,14 +48,14 @@ hipEvent_t vc_ctx::get_event() {
     return e;
 }
 
-void vc_ctx::timer_begin(const char*, hipEvent_t* a) {
+void vc_ctx::timer_begin(const char*, hipEvent_t* a, hipStream_t s) {
     *a = get_event();
-    (void)hipEventRecord(*a, stream);
+    (void)hipEventRecord(*a, s ? s : stream);
 }
 
-void vc_ctx::timer_end(const char* name, hipEvent_t a) {
+void vc_ctx::timer_end(const char* name, hipEvent_t a, hipStream_t s) {
     hipEvent_t b = get_event();
-    (void)hipEventRecord(b, stream);
+    (void)hipEventRecord(b, s ? s : stream);
     pending.push_back({a, b, name});
 }
 
@@ -123,6 +123,13 @@ int vc_ctx_create(int curve, int device, vc_ctx** out) {
         delete c;
         return VC_E_HIP;
     }
+    e = hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        vk::last_hip_error() = e;
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return VC_E_HIP;
+    }
     c->stream = c->own_stream;
     *out = c;
     return VC_OK;
@@ -142,6 +149,10 @@ void vc_ctx_destroy(vc_ctx* ctx) {
             (void)hipEventDestroy(p.b);
         }
         for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+        if (ctx->side_stream) {
+            (void)hipStreamSynchronize(ctx->side_stream);
+            (void)hipStreamDestroy(ctx->side_stream);
+        }
         if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     }
     delete ctx;

@@ -70,6 +70,8 @@ enum WsSlot {
     WS_SCALARS,
     WS_OUT,
     WS_MISC,
+    WS_TREE,
+    WS_TAIL,
     WS_COUNT_
 };
 
@@ -85,6 +87,7 @@ struct vc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
+    hipStream_t side_stream = nullptr;  // second queue for latency-bound tails
     std::mutex mu;
     std::vector<vk::Table*> tables;
     vk::DevBuf ws[vk::WS_COUNT_];
@@ -95,8 +98,8 @@ struct vc_ctx {
     vk::Table scratch;  // variable-base points of verifiers (grow-only)
 
     hipEvent_t get_event();
-    void timer_begin(const char* name, hipEvent_t* a);
-    void timer_end(const char* name, hipEvent_t a);
+    void timer_begin(const char* name, hipEvent_t* a, hipStream_t s = nullptr);
+    void timer_end(const char* name, hipEvent_t a, hipStream_t s = nullptr);
     void collect_timers();  // call after the stream is synchronised
     vk::Table* table(int id) {
         if (id < 0 || id >= (int)tables.size() || !tables[id]) return nullptr;
@@ -111,6 +114,15 @@ struct vc_ctx {
         if ((ctx)->timing) (ctx)->timer_begin(name, &ev_a_);                         \
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), shmem, (ctx)->stream, __VA_ARGS__); \
         if ((ctx)->timing) (ctx)->timer_end(name, ev_a_);                            \
+        VK_CHECK_HIP(hipGetLastError());                                             \
+    } while (0)
+
+#define VK_LAUNCH_ON(ctx, strm, name, kernel, grid, block, shmem, ...)                 \
+    do {                                                                             \
+        hipEvent_t ev_a_ = nullptr;                                                  \
+        if ((ctx)->timing) (ctx)->timer_begin(name, &ev_a_, strm);                   \
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), shmem, strm, __VA_ARGS__); \
+        if ((ctx)->timing) (ctx)->timer_end(name, ev_a_, strm);                      \
         VK_CHECK_HIP(hipGetLastError());                                             \
     } while (0)
 

@@ -13,18 +13,38 @@
 
 namespace vk {
 
+template <class F, bool IL>
+VK_HD fe<F> fsqr(const fe<F>& a) {
+    return fmul<F, IL>(a, a);
+}
+
+template <class F>
+struct SWAff {
+    fe<F> x, y;
+};
+template <class F>
+struct SWAcc {
+    fe<F> x, y, zz, zzz;
+};
+template <class F>
+struct TEAff {
+    fe<F> x, y, kt;  // kt = d*x*y
+};
+template <class F>
+struct TEAcc {
+    fe<F> X, Y, T, Z;
+};
+
 // ================================================================ short Weierstrass, a = 0
-template <class Fq_, int B_>
+// IL = inline field multiplies (latency-bound kernels); same point types either way.
+template <class Fq_, int B_, bool IL = false>
 struct SWCurve {
     using F = Fq_;
     static constexpr bool is_te = false;
     static constexpr int COEFF_B = B_;
-    struct Aff {
-        fe<F> x, y;
-    };
-    struct Acc {
-        fe<F> x, y, zz, zzz;
-    };
+    using Aff = SWAff<F>;
+    using Acc = SWAcc<F>;
+    using Inl = SWCurve<Fq_, B_, true>;
     static constexpr int AFF_WORDS = 2 * F::N;
     static constexpr int ACC_WORDS = 4 * F::N;
 
@@ -49,29 +69,29 @@ struct SWCurve {
     VK_HD static Acc dbl(const Acc& p) {
         if (is_zero(p)) return p;
         fe<F> U = fe_dbl<F>(p.y);
-        fe<F> V = fe_sqr<F>(U);
-        fe<F> W = fe_mul<F>(U, V);
-        fe<F> S = fe_mul<F>(p.x, V);
-        fe<F> X2 = fe_sqr<F>(p.x);
+        fe<F> V = fsqr<F, IL>(U);
+        fe<F> W = fmul<F, IL>(U, V);
+        fe<F> S = fmul<F, IL>(p.x, V);
+        fe<F> X2 = fsqr<F, IL>(p.x);
         fe<F> M = fe_add<F>(fe_dbl<F>(X2), X2);
         Acc r;
-        r.x = fe_sub<F>(fe_sqr<F>(M), fe_dbl<F>(S));
-        r.y = fe_sub<F>(fe_mul<F>(M, fe_sub<F>(S, r.x)), fe_mul<F>(W, p.y));
-        r.zz = fe_mul<F>(V, p.zz);
-        r.zzz = fe_mul<F>(W, p.zzz);
+        r.x = fe_sub<F>(fsqr<F, IL>(M), fe_dbl<F>(S));
+        r.y = fe_sub<F>(fmul<F, IL>(M, fe_sub<F>(S, r.x)), fmul<F, IL>(W, p.y));
+        r.zz = fmul<F, IL>(V, p.zz);
+        r.zzz = fmul<F, IL>(W, p.zzz);
         return r;
     }
     // doubling of an affine point (used in the madd exceptional case)
     VK_HD static Acc dbl_aff(const fe<F>& x, const fe<F>& y) {
         fe<F> U = fe_dbl<F>(y);
-        fe<F> V = fe_sqr<F>(U);
-        fe<F> W = fe_mul<F>(U, V);
-        fe<F> S = fe_mul<F>(x, V);
-        fe<F> X2 = fe_sqr<F>(x);
+        fe<F> V = fsqr<F, IL>(U);
+        fe<F> W = fmul<F, IL>(U, V);
+        fe<F> S = fmul<F, IL>(x, V);
+        fe<F> X2 = fsqr<F, IL>(x);
         fe<F> M = fe_add<F>(fe_dbl<F>(X2), X2);
         Acc r;
-        r.x = fe_sub<F>(fe_sqr<F>(M), fe_dbl<F>(S));
-        r.y = fe_sub<F>(fe_mul<F>(M, fe_sub<F>(S, r.x)), fe_mul<F>(W, y));
+        r.x = fe_sub<F>(fsqr<F, IL>(M), fe_dbl<F>(S));
+        r.y = fe_sub<F>(fmul<F, IL>(M, fe_sub<F>(S, r.x)), fmul<F, IL>(W, y));
         r.zz = V;
         r.zzz = W;
         return r;
@@ -87,46 +107,46 @@ struct SWCurve {
             r.zzz = fe_one<F>();
             return r;
         }
-        fe<F> U2 = fe_mul<F>(q.x, p.zz);
-        fe<F> S2 = fe_mul<F>(y2, p.zzz);
+        fe<F> U2 = fmul<F, IL>(q.x, p.zz);
+        fe<F> S2 = fmul<F, IL>(y2, p.zzz);
         fe<F> P = fe_sub<F>(U2, p.x);
         fe<F> R = fe_sub<F>(S2, p.y);
         if (fe_is_zero<F>(P)) {
             if (fe_is_zero<F>(R)) return dbl_aff(q.x, y2);
             return zero();
         }
-        fe<F> PP = fe_sqr<F>(P);
-        fe<F> PPP = fe_mul<F>(P, PP);
-        fe<F> Q = fe_mul<F>(p.x, PP);
+        fe<F> PP = fsqr<F, IL>(P);
+        fe<F> PPP = fmul<F, IL>(P, PP);
+        fe<F> Q = fmul<F, IL>(p.x, PP);
         Acc r;
-        r.x = fe_sub<F>(fe_sub<F>(fe_sqr<F>(R), PPP), fe_dbl<F>(Q));
-        r.y = fe_sub<F>(fe_mul<F>(R, fe_sub<F>(Q, r.x)), fe_mul<F>(p.y, PPP));
-        r.zz = fe_mul<F>(p.zz, PP);
-        r.zzz = fe_mul<F>(p.zzz, PPP);
+        r.x = fe_sub<F>(fe_sub<F>(fsqr<F, IL>(R), PPP), fe_dbl<F>(Q));
+        r.y = fe_sub<F>(fmul<F, IL>(R, fe_sub<F>(Q, r.x)), fmul<F, IL>(p.y, PPP));
+        r.zz = fmul<F, IL>(p.zz, PP);
+        r.zzz = fmul<F, IL>(p.zzz, PPP);
         return r;
     }
     // add-2008-s
     VK_HD static Acc add(const Acc& p, const Acc& q) {
         if (is_zero(p)) return q;
         if (is_zero(q)) return p;
-        fe<F> U1 = fe_mul<F>(p.x, q.zz);
-        fe<F> U2 = fe_mul<F>(q.x, p.zz);
-        fe<F> S1 = fe_mul<F>(p.y, q.zzz);
-        fe<F> S2 = fe_mul<F>(q.y, p.zzz);
+        fe<F> U1 = fmul<F, IL>(p.x, q.zz);
+        fe<F> U2 = fmul<F, IL>(q.x, p.zz);
+        fe<F> S1 = fmul<F, IL>(p.y, q.zzz);
+        fe<F> S2 = fmul<F, IL>(q.y, p.zzz);
         fe<F> P = fe_sub<F>(U2, U1);
         fe<F> R = fe_sub<F>(S2, S1);
         if (fe_is_zero<F>(P)) {
             if (fe_is_zero<F>(R)) return dbl(p);
             return zero();
         }
-        fe<F> PP = fe_sqr<F>(P);
-        fe<F> PPP = fe_mul<F>(P, PP);
-        fe<F> Q = fe_mul<F>(U1, PP);
+        fe<F> PP = fsqr<F, IL>(P);
+        fe<F> PPP = fmul<F, IL>(P, PP);
+        fe<F> Q = fmul<F, IL>(U1, PP);
         Acc r;
-        r.x = fe_sub<F>(fe_sub<F>(fe_sqr<F>(R), PPP), fe_dbl<F>(Q));
-        r.y = fe_sub<F>(fe_mul<F>(R, fe_sub<F>(Q, r.x)), fe_mul<F>(S1, PPP));
-        r.zz = fe_mul<F>(fe_mul<F>(p.zz, q.zz), PP);
-        r.zzz = fe_mul<F>(fe_mul<F>(p.zzz, q.zzz), PPP);
+        r.x = fe_sub<F>(fe_sub<F>(fsqr<F, IL>(R), PPP), fe_dbl<F>(Q));
+        r.y = fe_sub<F>(fmul<F, IL>(R, fe_sub<F>(Q, r.x)), fmul<F, IL>(S1, PPP));
+        r.zz = fmul<F, IL>(fmul<F, IL>(p.zz, q.zz), PP);
+        r.zzz = fmul<F, IL>(fmul<F, IL>(p.zzz, q.zzz), PPP);
         return r;
     }
     VK_HD static Acc neg(const Acc& p) {
@@ -138,25 +158,22 @@ struct SWCurve {
     VK_HD static bool to_aff(const Acc& p, fe<F>& x, fe<F>& y) {
         if (is_zero(p)) return false;
         fe<F> izzz = fe_inv<F>(p.zzz);
-        fe<F> t = fe_mul<F>(izzz, p.zz);   // 1/ZZ^(1/2)... ZZ*1/ZZZ = 1/Z
-        fe<F> izz = fe_sqr<F>(t);          // 1/ZZ
-        x = fe_mul<F>(p.x, izz);
-        y = fe_mul<F>(p.y, izzz);
+        fe<F> t = fmul<F, IL>(izzz, p.zz);   // 1/ZZ^(1/2)... ZZ*1/ZZZ = 1/Z
+        fe<F> izz = fsqr<F, IL>(t);          // 1/ZZ
+        x = fmul<F, IL>(p.x, izz);
+        y = fmul<F, IL>(p.y, izzz);
         return true;
     }
 };
 
 // ================================================================ twisted Edwards, a = -5
-template <class Fq_, class DParam>
+template <class Fq_, class DParam, bool IL = false>
 struct TECurve {
     using F = Fq_;
     static constexpr bool is_te = true;
-    struct Aff {
-        fe<F> x, y, kt;  // kt = d*x*y
-    };
-    struct Acc {
-        fe<F> X, Y, T, Z;
-    };
+    using Aff = TEAff<F>;
+    using Acc = TEAcc<F>;
+    using Inl = TECurve<Fq_, DParam, true>;
     static constexpr int AFF_WORDS = 3 * F::N;
     static constexpr int ACC_WORDS = 4 * F::N;
 
@@ -182,7 +199,7 @@ struct TECurve {
         Acc r;
         r.X = neg ? fe_neg<F>(p.x) : p.x;
         r.Y = p.y;
-        r.T = fe_mul<F>(r.X, r.Y);
+        r.T = fmul<F, IL>(r.X, r.Y);
         r.Z = fe_one<F>();
         return r;
     }
@@ -190,53 +207,53 @@ struct TECurve {
     VK_HD static Acc madd(const Acc& p, const Aff& q, bool neg) {
         fe<F> x2 = neg ? fe_neg<F>(q.x) : q.x;
         fe<F> kt = neg ? fe_neg<F>(q.kt) : q.kt;
-        fe<F> A = fe_mul<F>(p.X, x2);
-        fe<F> B = fe_mul<F>(p.Y, q.y);
-        fe<F> C = fe_mul<F>(p.T, kt);
-        fe<F> E = fe_sub<F>(fe_sub<F>(fe_mul<F>(fe_add<F>(p.X, p.Y), fe_add<F>(x2, q.y)), A), B);
+        fe<F> A = fmul<F, IL>(p.X, x2);
+        fe<F> B = fmul<F, IL>(p.Y, q.y);
+        fe<F> C = fmul<F, IL>(p.T, kt);
+        fe<F> E = fe_sub<F>(fe_sub<F>(fmul<F, IL>(fe_add<F>(p.X, p.Y), fe_add<F>(x2, q.y)), A), B);
         fe<F> Fv = fe_sub<F>(p.Z, C);
         fe<F> G = fe_add<F>(p.Z, C);
         fe<F> H = fe_add<F>(B, fe_mul_small<F, 5>(A));  // B - a*A, a = -5
         Acc r;
-        r.X = fe_mul<F>(E, Fv);
-        r.Y = fe_mul<F>(G, H);
-        r.T = fe_mul<F>(E, H);
-        r.Z = fe_mul<F>(Fv, G);
+        r.X = fmul<F, IL>(E, Fv);
+        r.Y = fmul<F, IL>(G, H);
+        r.T = fmul<F, IL>(E, H);
+        r.Z = fmul<F, IL>(Fv, G);
         return r;
     }
     // unified add (add-2008-hwcd): 9M + 1 const mul
     VK_HD static Acc add(const Acc& p, const Acc& q) {
-        fe<F> A = fe_mul<F>(p.X, q.X);
-        fe<F> B = fe_mul<F>(p.Y, q.Y);
-        fe<F> C = fe_mul<F>(fe_mul<F>(p.T, q.T), d());
-        fe<F> D = fe_mul<F>(p.Z, q.Z);
-        fe<F> E = fe_sub<F>(fe_sub<F>(fe_mul<F>(fe_add<F>(p.X, p.Y), fe_add<F>(q.X, q.Y)), A), B);
+        fe<F> A = fmul<F, IL>(p.X, q.X);
+        fe<F> B = fmul<F, IL>(p.Y, q.Y);
+        fe<F> C = fmul<F, IL>(fmul<F, IL>(p.T, q.T), d());
+        fe<F> D = fmul<F, IL>(p.Z, q.Z);
+        fe<F> E = fe_sub<F>(fe_sub<F>(fmul<F, IL>(fe_add<F>(p.X, p.Y), fe_add<F>(q.X, q.Y)), A), B);
         fe<F> Fv = fe_sub<F>(D, C);
         fe<F> G = fe_add<F>(D, C);
         fe<F> H = fe_add<F>(B, fe_mul_small<F, 5>(A));
         Acc r;
-        r.X = fe_mul<F>(E, Fv);
-        r.Y = fe_mul<F>(G, H);
-        r.T = fe_mul<F>(E, H);
-        r.Z = fe_mul<F>(Fv, G);
+        r.X = fmul<F, IL>(E, Fv);
+        r.Y = fmul<F, IL>(G, H);
+        r.T = fmul<F, IL>(E, H);
+        r.Z = fmul<F, IL>(Fv, G);
         return r;
     }
     // dbl-2008-hwcd: 4M + 4S
     VK_HD static Acc dbl(const Acc& p) {
-        fe<F> A = fe_sqr<F>(p.X);
-        fe<F> B = fe_sqr<F>(p.Y);
-        fe<F> C = fe_dbl<F>(fe_sqr<F>(p.Z));
+        fe<F> A = fsqr<F, IL>(p.X);
+        fe<F> B = fsqr<F, IL>(p.Y);
+        fe<F> C = fe_dbl<F>(fsqr<F, IL>(p.Z));
         fe<F> D = fe_neg<F>(fe_mul_small<F, 5>(A));  // a*A
         fe<F> xy = fe_add<F>(p.X, p.Y);
-        fe<F> E = fe_sub<F>(fe_sub<F>(fe_sqr<F>(xy), A), B);
+        fe<F> E = fe_sub<F>(fe_sub<F>(fsqr<F, IL>(xy), A), B);
         fe<F> G = fe_add<F>(D, B);
         fe<F> Fv = fe_sub<F>(G, C);
         fe<F> H = fe_sub<F>(D, B);
         Acc r;
-        r.X = fe_mul<F>(E, Fv);
-        r.Y = fe_mul<F>(G, H);
-        r.T = fe_mul<F>(E, H);
-        r.Z = fe_mul<F>(Fv, G);
+        r.X = fmul<F, IL>(E, Fv);
+        r.Y = fmul<F, IL>(G, H);
+        r.T = fmul<F, IL>(E, H);
+        r.Z = fmul<F, IL>(Fv, G);
         return r;
     }
     VK_HD static Acc neg(const Acc& p) {
@@ -247,8 +264,8 @@ struct TECurve {
     }
     VK_HD static bool to_aff(const Acc& p, fe<F>& x, fe<F>& y) {
         fe<F> iz = fe_inv<F>(p.Z);
-        x = fe_mul<F>(p.X, iz);
-        y = fe_mul<F>(p.Y, iz);
+        x = fmul<F, IL>(p.X, iz);
+        y = fmul<F, IL>(p.Y, iz);
         return !(fe_is_zero<F>(x) && fe_eq<F>(y, fe_one<F>()));
     }
 };

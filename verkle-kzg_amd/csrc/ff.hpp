@@ -116,40 +116,63 @@ VK_HD fe<F> fe_neg(const fe<F>& a) {
 // On the device it is an out-of-line call: a fully inlined 12-limb multiply is ~600
 // instructions, and an EC add holds 10-16 of them -- inlining every one blows the
 // instruction cache (and compile time) for no gain.
-#ifdef VK_MUL_ROLLED
-// experiment switch: inline CIOS with the outer row loop rolled (b shifted per row)
+#ifndef __HIP_DEVICE_COMPILE__
+// Host build of the same multiply on 64-bit limbs (unsigned __int128): for even N the
+// Montgomery form is identical (R = 2^(32N) = 2^(64 N/2)), so host and device share bytes.
 template <class F>
-VK_HD fe<F> fe_mul(const fe<F>& a, fe<F> b) {
-    constexpr int N = F::N;
-    uint32_t t[N];
-#pragma unroll
-    for (int j = 0; j < N; j++) t[j] = 0;
-#pragma unroll 1
-    for (int i = 0; i < N; i++) {
-        uint32_t bi = b.v[0];
-#pragma unroll
-        for (int k = 0; k < N - 1; k++) b.v[k] = b.v[k + 1];
-        uint64_t A = (uint64_t)a.v[0] * bi + t[0];
-        t[0] = (uint32_t)A;
-        uint32_t m = t[0] * F::inv;
-        uint64_t C = (uint64_t)m * F::p(0) + t[0];
-#pragma unroll
-        for (int j = 1; j < N; j++) {
-            A = (uint64_t)a.v[j] * bi + t[j] + (A >> 32);
-            C = (uint64_t)m * F::p(j) + (uint32_t)A + (C >> 32);
-            t[j - 1] = (uint32_t)C;
+constexpr uint64_t host_inv64() {
+    uint64_t p0 = (uint64_t)F::p(0) | ((uint64_t)F::p(1) << 32);
+    uint64_t x = 1;
+    for (int i = 0; i < 7; i++) x *= 2 - p0 * x;
+    return (uint64_t)0 - x;
+}
+template <class F>
+inline fe<F> fe_mul_host64(const fe<F>& a, const fe<F>& b) {
+    constexpr int M = F::N / 2;
+    constexpr uint64_t inv = host_inv64<F>();
+    uint64_t pa[M], pb[M], pp[M], t[M + 2] = {0};
+    for (int i = 0; i < M; i++) {
+        pa[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+        pb[i] = (uint64_t)b.v[2 * i] | ((uint64_t)b.v[2 * i + 1] << 32);
+        pp[i] = (uint64_t)F::p(2 * i) | ((uint64_t)F::p(2 * i + 1) << 32);
+    }
+    typedef unsigned __int128 u128;
+    for (int i = 0; i < M; i++) {
+        uint64_t C = 0;
+        for (int j = 0; j < M; j++) {
+            u128 s = (u128)pa[j] * pb[i] + t[j] + C;
+            t[j] = (uint64_t)s;
+            C = (uint64_t)(s >> 64);
         }
-        t[N - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+        u128 s = (u128)t[M] + C;
+        t[M] = (uint64_t)s;
+        t[M + 1] = (uint64_t)(s >> 64);
+        uint64_t m = t[0] * inv;
+        s = (u128)m * pp[0] + t[0];
+        C = (uint64_t)(s >> 64);
+        for (int j = 1; j < M; j++) {
+            s = (u128)m * pp[j] + t[j] + C;
+            t[j - 1] = (uint64_t)s;
+            C = (uint64_t)(s >> 64);
+        }
+        s = (u128)t[M] + C;
+        t[M - 1] = (uint64_t)s;
+        t[M] = t[M + 1] + (uint64_t)(s >> 64);
     }
     fe<F> r;
-#pragma unroll
-    for (int j = 0; j < N; j++) r.v[j] = t[j];
-    return fe_reduce_once<F>(r);
+    for (int i = 0; i < M; i++) {
+        r.v[2 * i] = (uint32_t)t[i];
+        r.v[2 * i + 1] = (uint32_t)(t[i] >> 32);
+    }
+    return fe_reduce_once<F>(r);  // t[M] == 0 here: every modulus leaves spare top bits
 }
-#else
-#define VK_MUL_ATTR __host__ __device__ __noinline__
+#endif
+
 template <class F>
-VK_MUL_ATTR fe<F> fe_mul(const fe<F> a, const fe<F> b) {
+VK_HD fe<F> fe_mul_body(const fe<F>& a, const fe<F>& b) {
+#ifndef __HIP_DEVICE_COMPILE__
+    if constexpr (F::N % 2 == 0) return fe_mul_host64<F>(a, b);
+#endif
     constexpr int N = F::N;
     uint32_t t[N];
 #pragma unroll
@@ -173,7 +196,28 @@ VK_MUL_ATTR fe<F> fe_mul(const fe<F> a, const fe<F> b) {
     for (int j = 0; j < N; j++) r.v[j] = t[j];
     return fe_reduce_once<F>(r);
 }
+}  // namespace vk
+#include "mul_asm.hpp"
+namespace vk {
+
+// Device multiply: the generated inline-asm CIOS (mul_asm.hpp) for 8- and 12-limb fields --
+// 1.5x the throughput of the compiler-built CIOS above, whose carries cost ~620 zero-extension
+// moves per 12-limb multiply (tools/mulvariants.hip). Host: 64-bit limbs.
+template <class F>
+VK_HD fe<F> fe_mul(const fe<F>& a, const fe<F>& b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr (F::N == 12) return fe_mul_asm12<F>(a, b);
+    else if constexpr (F::N == 8) return fe_mul_asm8<F>(a, b);
+    else return fe_mul_body<F>(a, b);
+#else
+    return fe_mul_body<F>(a, b);
 #endif
+}
+// policy switch kept for the curve templates (both policies use the same multiply now)
+template <class F, bool IL>
+VK_HD fe<F> fmul(const fe<F>& a, const fe<F>& b) {
+    return fe_mul<F>(a, b);
+}
 
 template <class F>
 VK_HD fe<F> fe_sqr(const fe<F>& a) {
@@ -193,7 +237,9 @@ template <class F>
 VK_HD fe<F> fe_from_mont(const fe<F>& a) {
     fe<F> one = fe_zero<F>();
     one.v[0] = 1;
-    return fe_mul<F>(a, one);
+    // compiler multiply: with b = 1 it folds to a plain Montgomery reduction and does not pin
+    // the asm multiply's fixed VGPR block (keeps e.g. the digit kernel at high occupancy)
+    return fe_mul_body<F>(a, one);
 }
 
 // a^(p-2) (slow; only for rare normalisations)

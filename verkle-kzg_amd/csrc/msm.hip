@@ -18,11 +18,13 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "ctx.hpp"
 #include "ec.hpp"
+#include "msm_tail.hpp"
 
 namespace vk {
 
@@ -78,12 +80,20 @@ __global__ void __launch_bounds__(256) k_msm_scatter(const int32_t* __restrict__
                                                     uint32_t* __restrict__ sorted) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    for (int w = 0; w < W; w++) {
-        int32_t d = digits[(size_t)w * n + i];
-        if (d == 0) continue;
-        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-        uint32_t pos = atomicAdd(&cursor[(size_t)w * NB + b], 1u);
-        sorted[pos] = i | (d < 0 ? 0x80000000u : 0u);
+    // 4 windows at a time: issue the returning atomics back to back, then the stores
+    for (int w0 = 0; w0 < W; w0 += 4) {
+        int32_t d[4];
+        uint32_t pos[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[k] = (w0 + k < W) ? digits[(size_t)(w0 + k) * n + i] : 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint32_t b = (uint32_t)(d[k] < 0 ? -d[k] : d[k]) - 1;
+            pos[k] = d[k] ? atomicAdd(&cursor[(size_t)(w0 + k) * NB + b], 1u) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (d[k]) sorted[pos[k]] = i | (d[k] < 0 ? 0x80000000u : 0u);
     }
 }
 
@@ -91,14 +101,14 @@ __global__ void __launch_bounds__(256) k_msm_scatter(const int32_t* __restrict__
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_accumulate(
     const typename C::Aff* __restrict__ bases, const uint32_t* __restrict__ sorted,
-    const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t L, uint32_t M,
+    const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t k_begin, uint32_t L, uint32_t M,
     typename C::Acc* __restrict__ buckets, typename C::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename C::Acc* __restrict__ owner_piece,
     uint32_t* __restrict__ owner_bucket) {
     using Acc = typename C::Acc;
     using Aff = typename C::Aff;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t k = t * M;
+    uint32_t k = k_begin + t * M;  // this launch covers sorted entries [k_begin, L)
     if (k >= L) return;
     uint32_t e = min(k + M, L);
     owner_bucket[t] = NONE;
@@ -147,78 +157,6 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(
     }
 }
 
-template <class C>
-__global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__ buckets,
-                                                  const typename C::Acc* __restrict__ carry_in,
-                                                  const uint8_t* __restrict__ through,
-                                                  const typename C::Acc* __restrict__ owner_piece,
-                                                  const uint32_t* __restrict__ owner_bucket,
-                                                  uint32_t T) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    uint32_t b = owner_bucket[t];
-    if (b == NONE) return;
-    typename C::Acc acc = owner_piece[t];
-    uint32_t u = t + 1;
-    while (u < T) {
-        acc = C::add(acc, carry_in[u]);
-        if (!through[u]) break;
-        u++;
-    }
-    buckets[b] = acc;
-}
-
-// ------------------------------------------------------------------ bucket reduction
-template <class C>
-__device__ typename C::Acc mul_small(const typename C::Acc& p, uint32_t k) {
-    typename C::Acc r = C::zero();
-    if (k == 0) return r;
-    int top = 31 - __builtin_clz(k);
-    r = p;
-    for (int i = top - 1; i >= 0; i--) {
-        r = C::dbl(r);
-        if ((k >> i) & 1) r = C::add(r, p);
-    }
-    return r;
-}
-
-template <class C>
-__global__ void __launch_bounds__(256) k_msm_reduce(const typename C::Acc* __restrict__ buckets,
-                                                   const uint32_t* __restrict__ offsets,
-                                                   uint32_t NB, int W, uint32_t Lseg, uint32_t S,
-                                                   typename C::Acc* __restrict__ seg_out) {
-    uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t w = gid / S, s = gid % S;
-    if (w >= (uint32_t)W) return;
-    uint32_t lo = s * Lseg, hi = min(lo + Lseg, NB);
-    typename C::Acc R = C::zero(), acc = C::zero();
-    for (uint32_t j = hi; j-- > lo;) {
-        size_t g = (size_t)w * NB + j;
-        if (offsets[g + 1] > offsets[g]) R = C::add(R, buckets[g]);
-        acc = C::add(acc, R);
-    }
-    // bucket j has digit value j + 1: contribution = acc + lo * R
-    if (lo > 0) acc = C::add(acc, mul_small<C>(R, lo));
-    seg_out[gid] = acc;
-}
-
-template <class C>
-__global__ void __launch_bounds__(256) k_msm_winsum(const typename C::Acc* __restrict__ seg_out,
-                                                   uint32_t S, typename C::Acc* __restrict__ win) {
-    using Acc = typename C::Acc;
-    __shared__ Acc sh[256];
-    uint32_t w = blockIdx.x, tid = threadIdx.x;
-    Acc acc = C::zero();
-    for (uint32_t s = tid; s < S; s += 256) acc = C::add(acc, seg_out[(size_t)w * S + s]);
-    sh[tid] = acc;
-    __syncthreads();
-    for (uint32_t h = 128; h > 0; h >>= 1) {
-        if (tid < h) sh[tid] = C::add(sh[tid], sh[tid + h]);
-        __syncthreads();
-    }
-    if (tid == 0) win[w] = sh[0];
-}
-
 // ------------------------------------------------------------------ host side
 static int choose_window(size_t n) {
     if (n >= (1u << 19)) return 16;
@@ -246,8 +184,10 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     const uint32_t NB = 1u << (c - 1);
     const uint32_t NBtot = NB * W;
     const uint32_t M = 32;                 // sorted entries per accumulate thread
-    const uint32_t Lseg = NB >= 4096 ? 8 : (NB >= 256 ? 4 : 2);
-    const uint32_t S = (NB + Lseg - 1) / Lseg;
+    const uint32_t Lseg = NB >= 256 ? 8 : (NB >= 4 ? 2 : 1);
+    const uint32_t S = NB / Lseg;  // power of two
+    uint32_t J = 0;
+    while ((1u << J) < S) J++;
     const size_t maxL = n * (size_t)W;
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     hipStream_t st = ctx->stream;
@@ -258,12 +198,14 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_TRY(ctx->ws[WS_CURSOR].ensure((size_t)(NBtot + 1) * 4));
     VK_TRY(ctx->ws[WS_SORTED].ensure(maxL * 4));
     VK_TRY(ctx->ws[WS_BUCKETS].ensure((size_t)NBtot * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_CARRY].ensure((size_t)Tmax * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_THROUGH].ensure((size_t)Tmax));
-    VK_TRY(ctx->ws[WS_OWNER].ensure((size_t)Tmax * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_OWNER_B].ensure((size_t)Tmax * 4));
+    VK_TRY(ctx->ws[WS_CARRY].ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_THROUGH].ensure((size_t)(Tmax + 8)));
+    VK_TRY(ctx->ws[WS_OWNER].ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(ctx->ws[WS_SEG].ensure((size_t)S * W * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_TREE].ensure((size_t)S * W * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
 
     int32_t* digits = ctx->ws[WS_DIGITS].as<int32_t>();
     uint32_t* counts = ctx->ws[WS_COUNTS].as<uint32_t>();
@@ -276,7 +218,9 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     Acc* owner = ctx->ws[WS_OWNER].as<Acc>();
     uint32_t* owner_b = ctx->ws[WS_OWNER_B].as<uint32_t>();
     Acc* seg = ctx->ws[WS_SEG].as<Acc>();
-    Acc* win = ctx->ws[WS_WIN].as<Acc>();
+    Acc* rs = ctx->ws[WS_TREE].as<Acc>();
+    Acc* part = ctx->ws[WS_WIN].as<Acc>();
+    Acc* tail = ctx->ws[WS_TAIL].as<Acc>();
 
     const Aff* bases = t->bases.as<Aff>() + offset;
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
@@ -304,21 +248,27 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_CHECK_HIP(hipStreamSynchronize(st));
     if (L > 0) {
         const uint32_t T = (L + M - 1) / M;
-        VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (T + 255) / 256, 256, 0, bases,
-                  sorted, offsets, NBtot, L, M, buckets, carry, through, owner, owner_b);
-        VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<C>), (T + 255) / 256, 256, 0, buckets, carry,
-                  through, owner, owner_b, T);
+        VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (T + 255) / 256, 256, 0, bases, sorted, offsets,
+                  NBtot, 0u, L, M, buckets, carry, through, owner, owner_b);
+        VK_TRY(msm_tail_fixup<C>(ctx, T, buckets, carry, through, owner, owner_b));
     }
-    VK_LAUNCH(ctx, "msm_reduce", (k_msm_reduce<C>), (S * W + 255) / 256, 256, 0, buckets, offsets,
-              NB, W, Lseg, S, seg);
-    VK_LAUNCH(ctx, "msm_winsum", (k_msm_winsum<C>), W, 256, 0, seg, S, win);
-    std::vector<Acc> hwin(W);
-    VK_CHECK_HIP(hipMemcpyAsync(hwin.data(), win, (size_t)W * sizeof(Acc), hipMemcpyDeviceToHost, st));
+    VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, part, tail));
+    std::vector<Acc> ht((size_t)W * (J + 1));
+    VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));
-    Acc res = hwin[W - 1];
-    for (int w = W - 2; w >= 0; w--) {
-        for (int k = 0; k < c; k++) res = C::dbl(res);
-        res = C::add(res, hwin[w]);
+    // MSM = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host, 64-bit limbs)
+    int lg_seg = 0;
+    while ((1u << lg_seg) < Lseg) lg_seg++;
+    const int maxpos = c * (W - 1) + lg_seg + (int)J;
+    std::vector<std::vector<int>> at(maxpos + 1);
+    for (int w = 0; w < W; w++) {
+        at[c * w].push_back(w * (int)(J + 1) + (int)J);
+        for (uint32_t j = 0; j < J; j++) at[c * w + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
+    }
+    Acc res = C::zero();
+    for (int pos = maxpos; pos >= 0; pos--) {
+        if (!C::is_zero(res)) res = C::dbl(res);
+        for (int idx : at[pos]) res = C::add(res, ht[idx]);
     }
     memcpy(out_acc, &res, sizeof(Acc));
     return VC_OK;

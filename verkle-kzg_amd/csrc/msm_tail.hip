@@ -1,0 +1,161 @@
+// Latency-bound tail of the Pippenger MSM (split from msm.hip so the inlined field
+// multiplies these kernels use -- the compiler can then interleave independent multiplies,
+// which halves the latency of a serial EC chain -- do not slow every rebuild of msm.hip).
+#include <hip/hip_runtime.h>
+
+#include "ctx.hpp"
+#include "ec.hpp"
+#include "msm_tail.hpp"
+
+namespace vk {
+
+constexpr uint32_t NONE_T = 0xffffffffu;
+
+template <class C>
+__global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__ buckets,
+                                                  const typename C::Acc* __restrict__ carry_in,
+                                                  const uint8_t* __restrict__ through,
+                                                  const typename C::Acc* __restrict__ owner_piece,
+                                                  const uint32_t* __restrict__ owner_bucket,
+                                                  uint32_t T) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    uint32_t b = owner_bucket[t];
+    if (b == NONE_T) return;
+    typename C::Acc acc = owner_piece[t];
+    uint32_t u = t + 1;
+    while (u < T) {
+        acc = C::add(acc, carry_in[u]);
+        if (!through[u]) break;
+        u++;
+    }
+    buckets[b] = acc;
+}
+
+// ------------------------------------------------------------------ bucket reduction
+// Window sum  V_w = sum_b (b + 1) B_b  over NB buckets, in two shallow GPU stages and a host pass:
+//  (1) k_msm_segsum: segment s of Lseg buckets -> acc_s = sum (b - lo + 1) B_b, R_s = sum B_b
+//      (2 Lseg serial adds);  V_w = sum_s acc_s + Lseg * sum_s s R_s
+//  (2) k_msm_bitsum: sum_s s R_s = sum_j 2^j T_j with T_j = sum_{s: bit j of s} R_s, and
+//      A = sum_s acc_s: J + 1 plain sums per window (8 serial adds per lane + wave butterflies)
+//  (3) host: MSM = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj) -- every term is a point at a
+//      bit position, so one Horner pass over positions (msm.hip).
+// Serial GPU depth 2 Lseg + 13 EC adds instead of 2 Lseg + ~22 (lo * R by double-and-add)
+// + 24 (per-window reduction) before.
+template <class C>
+__global__ void __launch_bounds__(256) k_msm_segsum(const typename C::Acc* __restrict__ buckets,
+                                                   const uint32_t* __restrict__ offsets, uint32_t NB, int W,
+                                                   uint32_t Lseg, uint32_t S, typename C::Acc* __restrict__ accs,
+                                                   typename C::Acc* __restrict__ Rs) {
+    uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t w = gid / S, s = gid % S;
+    if (w >= (uint32_t)W) return;
+    uint32_t lo = s * Lseg, hi = min(lo + Lseg, NB);
+    typename C::Acc R = C::zero(), acc = C::zero();
+    for (uint32_t j = hi; j-- > lo;) {
+        size_t g = (size_t)w * NB + j;
+        if (offsets[g + 1] > offsets[g]) R = C::add(R, buckets[g]);
+        acc = C::add(acc, R);
+    }
+    accs[gid] = acc;
+    Rs[gid] = R;
+}
+
+// wave-level sum of one point per lane: xor-shuffle butterfly (no LDS, no barriers); lane 0 gets
+// the sum of lanes [0, span)
+template <class C>
+__device__ __forceinline__ typename C::Acc wave_sum(typename C::Acc v, uint32_t span = 64) {
+    for (uint32_t m = 1; m < span; m <<= 1) {
+        typename C::Acc o;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+        for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
+        v = C::add(v, o);
+    }
+    return v;
+}
+
+// stage 1: lane sums BITSUM_K selected items of one (w, q) sum serially, then the wave folds
+// its 64 lane sums (butterfly):  q < J: R_s over s with bit q set (S/2 items);  q == J: acc_s
+// (S items).  partial[(w * (J + 1) + q) * PW + wave_in_sum], PW = ceil(S / (64 K)).
+// Cost model: a wave-level EC add is ~17 us of one SIMD's issue (CDNA4, BLS12-381), so the
+// stage is priced in SIMD rounds: (K + 6) adds on ~W(J+2)S/(128K) waves.
+constexpr uint32_t BITSUM_K = 8;
+template <class C>
+__global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __restrict__ accs,
+                                                   const typename C::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
+                                                   uint32_t PW, uint32_t n_waves,
+                                                   typename C::Acc* __restrict__ partial) {
+    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
+    if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
+    const uint32_t sum = gw / PW, wv = gw % PW;
+    const uint32_t w = sum / (J + 1), q = sum % (J + 1);
+    const uint32_t n_items = q < J ? S / 2 : S;
+    const uint32_t base = wv * 64 * BITSUM_K;
+    if (base >= n_items) {  // whole wave idle (uniform branch)
+        if (lane == 0) partial[gw] = C::zero();
+        return;
+    }
+    typename C::Acc v = C::zero();
+    for (uint32_t k = 0; k < BITSUM_K; k++) {
+        uint32_t m = base + k * 64 + lane;  // lane-interleaved: coalesced-ish rows
+        if (m >= n_items) break;
+        if (q < J) {
+            uint32_t s = ((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1));
+            v = C::add(v, Rs[(size_t)w * S + s]);
+        } else {
+            v = C::add(v, accs[(size_t)w * S + m]);
+        }
+    }
+    v = wave_sum<C>(v);
+    if (lane == 0) partial[gw] = v;
+}
+
+// stage 2: one wave per sum folds its PW partials (PW / 64 per lane, then the butterfly)
+template <class C>
+__global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __restrict__ partial, uint32_t PW,
+                                                   typename C::Acc* __restrict__ out) {
+    const uint32_t sum = blockIdx.x, lane = threadIdx.x;
+    typename C::Acc v = C::zero();
+    for (uint32_t k = lane; k < PW; k += 64) v = C::add(v, partial[(size_t)sum * PW + k]);
+    uint32_t span = 1;
+    while (span < PW && span < 64) span <<= 1;
+    v = wave_sum<C>(v, span);
+    if (lane == 0) out[sum] = v;
+}
+
+template <class C>
+int msm_tail_fixup(vc_ctx* ctx, uint32_t T, typename C::Acc* buckets, const typename C::Acc* carry,
+                   const uint8_t* through, const typename C::Acc* owner, const uint32_t* owner_b) {
+    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<typename C::Inl>), (T + 255) / 256, 256, 0, buckets, carry, through,
+              owner, owner_b, T);
+    return VC_OK;
+}
+
+// outputs W x (J + 1) points: [w][q] = T_wq (q < J), A_w (q == J)
+template <class C>
+int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t* offsets, uint32_t NB, int W,
+                    uint32_t Lseg, uint32_t S, uint32_t J, typename C::Acc* accs, typename C::Acc* Rs,
+                    typename C::Acc* partial, typename C::Acc* out) {
+    using CI = typename C::Inl;
+    VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<CI>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB, W,
+              Lseg, S, accs, Rs);
+    const uint32_t sums = (uint32_t)W * (J + 1);
+    const uint32_t PW = msm_bitsum_pw(S);
+    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (sums * PW * 64 + 255) / 256, 256, 0, accs, Rs, S, J, PW,
+              sums * PW, partial);
+    VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<CI>), sums, 64, 0, partial, PW, out);
+    return VC_OK;
+}
+
+#define VK_INST_TAIL(C)                                                                                        \
+    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, C::Acc*, const C::Acc*, const uint8_t*, const C::Acc*,  \
+                                   const uint32_t*);                                                           \
+    template int msm_tail_reduce<C>(vc_ctx*, const C::Acc*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
+                                    uint32_t, C::Acc*, C::Acc*, C::Acc*, C::Acc*);
+VK_INST_TAIL(BN254G1)
+VK_INST_TAIL(BLS381G1)
+VK_INST_TAIL(Bandersnatch)
+
+}  // namespace vk

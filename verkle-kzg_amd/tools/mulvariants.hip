@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "../csrc/ec.hpp"
+#include "../csrc/mul_asm.hpp"
 using namespace vk;
 using F = BLS381Fq;
 
@@ -106,6 +107,51 @@ __device__ __forceinline__ fe<F> mul_v6(const fe<F>& a, fe<F> b) {
 }
 struct MulV6 { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return mul_v6<G>(a, b); } };
 
+
+// V8: row-parallel CIOS: all N products of a row are independent mads onto {t_j, 0} pairs,
+// followed by one add-with-carry chain (VCC) per half-row; no 64-bit carry arithmetic.
+template <class F>
+__device__ __forceinline__ fe<F> mul_v8(const fe<F>& a, const fe<F>& b) {
+    constexpr int N = F::N;
+    uint64_t X[N + 1];
+#pragma unroll
+    for (int j = 0; j <= N; j++) X[j] = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        uint64_t P[N];
+#pragma unroll
+        for (int j = 0; j < N; j++) P[j] = (uint64_t)a.v[j] * b.v[i] + X[j];
+        // t_j = lo(P_j) + hi(P_{j-1}) + carry ; top word t_N = X[N] + hi(P_{N-1}) + carry
+        uint32_t c = 0;
+        uint32_t t[N + 1];
+        t[0] = (uint32_t)P[0];
+#pragma unroll
+        for (int j = 1; j < N; j++) t[j] = __builtin_addc((uint32_t)P[j], (uint32_t)(P[j - 1] >> 32), c, &c);
+        t[N] = __builtin_addc((uint32_t)X[N], (uint32_t)(P[N - 1] >> 32), c, &c);
+        uint32_t m = t[0] * F::inv;
+#pragma unroll
+        for (int j = 0; j < N; j++) P[j] = (uint64_t)m * F::p(j) + t[j];
+        // shift down one limb: X_{j-1} = lo(P_j) + hi(P_{j-1}) + carry
+        c = 0;
+#pragma unroll
+        for (int j = 1; j < N; j++) X[j - 1] = __builtin_addc((uint32_t)P[j], (uint32_t)(P[j - 1] >> 32), c, &c);
+        X[N - 1] = __builtin_addc(t[N], (uint32_t)(P[N - 1] >> 32), c, &c);
+        X[N] = 0;  // no-carry bound: t < 2p < 2^(32N)
+    }
+    fe<F> r;
+#pragma unroll
+    for (int j = 0; j < N; j++) r.v[j] = (uint32_t)X[j];
+    return fe_reduce_once<F>(r);
+}
+struct MulV8 { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return mul_v8<G>(a, b); } };
+template <class G>
+__device__ __noinline__ fe<G> mul_v8_noinline(const fe<G> a, const fe<G> b) { return mul_v8<G>(a, b); }
+struct MulV8N { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return mul_v8_noinline<G>(a, b); } };
+
+struct MulAsm { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return fe_mul_asm12<G>(a, b); } };
+template <class G>
+__device__ __noinline__ fe<G> mul_asm_noinline(const fe<G> a, const fe<G> b) { return fe_mul_asm12<G>(a, b); }
+struct MulAsmN { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return mul_asm_noinline<G>(a, b); } };
 struct MulNoinline { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return fe_mul<G>(a, b); } };
 struct MulRolled { template <class G> __device__ static fe<G> mul(const fe<G>& a, const fe<G>& b) { return mul_rolled<G>(a, b); } };
 
@@ -141,7 +187,9 @@ __global__ void k_check(uint32_t* bad, uint32_t seed) {
     for (int i = 0; i < F::N; i++) { x = x * 1664525u + 1013904223u; a.v[i] = x; x = x * 1664525u + 1013904223u; b.v[i] = x; }
     a.v[F::N - 1] &= 0x0fffffff; b.v[F::N - 1] &= 0x0fffffff;
     for (int it = 0; it < 8; it++) {
-        fe<F> r1 = fe_mul<F>(a, b), r2 = mul_ps<F>(a, b), r3 = mul_v6<F>(a, b);
+        fe<F> r1 = fe_mul<F>(a, b), r2 = mul_ps<F>(a, b), r3 = mul_v6<F>(a, b), r4 = mul_v8<F>(a, b), r5 = fe_mul_asm12<F>(a, b);
+        if (!fe_eq<F>(r1, r5)) atomicAdd(bad + 1, 1u);
+        if (!fe_eq<F>(r1, r4)) atomicAdd(bad, 1u);
         if (!fe_eq<F>(r1, r3)) atomicAdd(bad, 1u);
         if (!fe_eq<F>(r1, r2)) atomicAdd(bad, 1u);
         a = r1; b = fe_add<F>(b, r1);
@@ -180,15 +228,15 @@ int main() {
     hipMalloc(&b, (1u << 20) * sizeof(BLS381G1::Aff));
     hipMemset(b, 0x11, (1u << 20) * sizeof(BLS381G1::Aff));
     hipMalloc(&o, 256 * 8 * 256 * sizeof(BLS381G1::Acc));
-    uint32_t* bad; hipMalloc(&bad, 4); hipMemset(bad, 0, 4);
+    uint32_t* bad; hipMalloc(&bad, 8); hipMemset(bad, 0, 8);
     for (int s = 0; s < 16; s++) hipLaunchKernelGGL(k_check, dim3(1024), dim3(256), 0, 0, bad, (uint32_t)s * 7919u);
-    uint32_t hb = 0; hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
-    printf("{\"check_mul_ps_mismatches\":%u}\n", hb);
+    uint32_t hb[2] = {0, 0}; hipMemcpy(hb, bad, 8, hipMemcpyDeviceToHost);
+    printf("{\"check_mismatches_ps_v6_v8\":%u, \"check_mismatches_asm\":%u}\n", hb[0], hb[1]);
     for (int rep = 0; rep < 2; rep++) {
     run<Inl<MulNoinline>>("noinline_mul", b, o);
-    run<Inl<MulRolled>>("rolled_inline_mul", b, o);
-    run<Called<MulRolled>>("rolled_mul_called_madd", b, o);
-    run<Inl<MulV6>>("v6_addc_rolled", b, o);
+
+    run<Inl<MulAsm>>("asm_inline", b, o);
+    run<Inl<MulAsmN>>("asm_noinline", b, o);
     }
     return 0;
 }
