@@ -124,7 +124,7 @@ def main():
     # dominant kernel (bucket accumulation) device time, HIP events on the launch stream
     acc_ms, acc_n = eng.kernel_time("msm_accumulate")
     kernels = {}
-    for k in ("msm_digits", "msm_scan", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_segsum",
+    for k in ("msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate", "msm_fixup", "msm_segsum",
               "msm_bitsum", "msm_sumpart"):
         ms, cnt = eng.kernel_time(k)
         if cnt:

@@ -2,16 +2,15 @@
 // (/root/reference/vector-commit/src/utils.rs:16-19) at large n (configs 2 and 4).
 //
 // Pipeline (all on the ctx stream, one host sync at the end):
-//   k_msm_digits     scalar -> W signed c-bit digits (|d| <= 2^(c-1)), bucket histogram
-//   hipcub scan      bucket counts -> bucket offsets (all windows concatenated)
-//   k_msm_scatter    (w, i) -> sorted[offset[w,|d|] + k] = i | sign<<31  (counting sort)
+//   k_sort_*         scalar -> W signed c-bit digits (|d| <= 2^(c-1)); two-pass LDS counting
+//                    sort of the (window, bucket) keys: sorted[] = i | sign<<31 grouped by
+//                    bucket, offsets[] = bucket starts (all windows concatenated)
 //   k_msm_accumulate every thread sums exactly M consecutive sorted entries (mixed adds
 //                    of affine bases gathered from HBM), writing complete buckets directly
 //                    and bucket pieces that straddle a thread boundary to side slots
 //   k_msm_fixup      owner thread of a straddling bucket folds the pieces
-//   k_msm_reduce     per window, segments of Lseg buckets: running sums -> sum_b b*B_b
-//   k_msm_winsum     per window, LDS tree over segments
-//   host             Horner over windows (c doublings per window) -> projective result
+//   msm_tail.hip     segment sums, bit sums (window sum = sum_b b B_b without a serial
+//                    running sum over all buckets), then host Horner over bit positions
 // Load balance does not depend on the scalar distribution: the accumulate work per
 // thread is fixed (M entries) even when every scalar hits one bucket.
 #include <hip/hip_runtime.h>
@@ -40,23 +39,15 @@ __device__ __forceinline__ fe<Fr> load_scalar(const uint32_t* __restrict__ sc, s
     return s;
 }
 
-// ------------------------------------------------------------------ digits + histogram
-template <class Fr>
-__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ sc,
-                                                   const uint8_t* __restrict__ inf, uint32_t n,
-                                                   int c, int W, int mont,
-                                                   int32_t* __restrict__ digits,
-                                                   uint32_t* __restrict__ counts, uint32_t NB) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fe<Fr> s = load_scalar<Fr>(sc, i);
-    if (mont) s = fe_from_mont<Fr>(s);
-    bool skip = inf != nullptr && inf[i];
+// ------------------------------------------------------------------ bucket sort
+// Signed c-bit digits of one scalar, least significant window first: d_w in (-2^(c-1), 2^(c-1)],
+// carry into the next window; W windows have one spare bit, so the last carry is absorbed.
+template <class Fr, class Fn>
+__device__ __forceinline__ void for_each_digit(fe<Fr> s, int c, int W, Fn&& f) {
     const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
     uint32_t carry = 0;
     for (int w = 0; w < W; w++) {
         uint32_t raw = (s.v[0] & mask) + carry;
-        // s >>= c (c < 32)
 #pragma unroll
         for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
         s.v[7] >>= c;
@@ -68,32 +59,100 @@ __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__
             d = (int32_t)raw;
             carry = 0;
         }
-        if (skip) d = 0;
-        digits[(size_t)w * n + i] = d;
-        if (d != 0) atomicAdd(&counts[(size_t)w * NB + (uint32_t)(d < 0 ? -d : d) - 1], 1u);
+        f(w, d);
     }
 }
 
-__global__ void __launch_bounds__(256) k_msm_scatter(const int32_t* __restrict__ digits, uint32_t n,
-                                                    int W, uint32_t NB,
-                                                    uint32_t* __restrict__ cursor,
-                                                    uint32_t* __restrict__ sorted) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    // 4 windows at a time: issue the returning atomics back to back, then the stores
-    for (int w0 = 0; w0 < W; w0 += 4) {
-        int32_t d[4];
-        uint32_t pos[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) d[k] = (w0 + k < W) ? digits[(size_t)(w0 + k) * n + i] : 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            uint32_t b = (uint32_t)(d[k] < 0 ? -d[k] : d[k]) - 1;
-            pos[k] = d[k] ? atomicAdd(&cursor[(size_t)(w0 + k) * NB + b], 1u) : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (d[k]) sorted[pos[k]] = i | (d[k] < 0 ? 0x80000000u : 0u);
+// Two-pass MSD counting sort of the n*W (window, bucket) keys, all in LDS -- no global atomics
+// (global atomics execute memory-side on CDNA4, ~26 G/s for scattered words, which made the
+// one-pass global-histogram sort cost 2.2 ms at 2^20 x 16 windows).
+//   coarse bin g = w * NBC + (b >> FB)          (NBC = NB >> FB coarse bins per window)
+//   k_sort_hist     block = CHUNK scalars: LDS histogram of coarse bins -> counts[g][block]
+//   hipcub scan     counts -> base[g][block] (global position of the block's run in bin g)
+//   k_sort_coarse   same digits again, LDS cursors from base: tmp[pos] = fine<<32 | i | sign<<31
+//   k_sort_fine     block = coarse bin: LDS histogram of the 2^FB fine buckets -> bucket
+//                   offsets (written directly), then scatter into sorted[]
+// Order inside a bucket is arbitrary (EC addition is commutative and exact).
+constexpr uint32_t SORT_CHUNK = 1024;
+
+template <class Fr>
+__global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
+                                                  uint32_t n, int c, int W, int mont, uint32_t FB, uint32_t NBC,
+                                                  uint32_t nblk, uint32_t* __restrict__ counts) {
+    extern __shared__ uint32_t hist[];
+    const uint32_t bins = (uint32_t)W * NBC;
+    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        if (inf != nullptr && inf[i]) continue;
+        fe<Fr> s = load_scalar<Fr>(sc, i);
+        if (mont) s = fe_from_mont<Fr>(s);
+        for_each_digit<Fr>(s, c, W, [&](int w, int32_t d) {
+            if (d != 0) atomicAdd(&hist[(uint32_t)w * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
+        });
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(size_t)k * nblk + blockIdx.x] = hist[k];
+}
+
+template <class Fr>
+__global__ void __launch_bounds__(256) k_sort_coarse(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
+                                                    uint32_t n, int c, int W, int mont, uint32_t FB, uint32_t NBC,
+                                                    uint32_t nblk, const uint32_t* __restrict__ base,
+                                                    uint64_t* __restrict__ tmp) {
+    extern __shared__ uint32_t cur[];
+    const uint32_t bins = (uint32_t)W * NBC;
+    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + blockIdx.x];
+    __syncthreads();
+    const uint32_t fmask = (1u << FB) - 1;
+    const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        if (inf != nullptr && inf[i]) continue;
+        fe<Fr> s = load_scalar<Fr>(sc, i);
+        if (mont) s = fe_from_mont<Fr>(s);
+        for_each_digit<Fr>(s, c, W, [&](int w, int32_t d) {
+            if (d != 0) {
+                uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+                uint32_t pos = atomicAdd(&cur[(uint32_t)w * NBC + (b >> FB)], 1u);
+                tmp[pos] = ((uint64_t)(b & fmask) << 32) | i | (d < 0 ? 0x80000000u : 0u);
+            }
+        });
+    }
+}
+
+// one block per coarse bin; offsets[g * 2^FB + f] = start of fine bucket f of bin g
+__global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ tmp, const uint32_t* __restrict__ base,
+                                                  uint32_t nblk, uint32_t bins, uint32_t FB,
+                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
+    __shared__ uint32_t h[256], x[256];
+    const uint32_t g = blockIdx.x, F = 1u << FB, t = threadIdx.x;
+    const uint32_t start = base[(size_t)g * nblk];
+    const uint32_t end = base[(size_t)(g + 1) * nblk];  // base has bins*nblk + 1 entries
+    h[t] = 0;
+    __syncthreads();
+    for (uint32_t p = start + t; p < end; p += blockDim.x) atomicAdd(&h[(uint32_t)(tmp[p] >> 32)], 1u);
+    __syncthreads();
+    // inclusive Hillis-Steele scan over 256 counters
+    uint32_t v = h[t];
+    x[t] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+        uint32_t a = t >= o ? x[t - o] : 0u;
+        __syncthreads();
+        x[t] += a;
+        __syncthreads();
+    }
+    const uint32_t excl = x[t] - v;
+    if (t < F) offsets[(size_t)g * F + t] = start + excl;
+    if (g == bins - 1 && t == 0) offsets[(size_t)bins * F] = end;
+    __syncthreads();
+    h[t] = excl;  // cursors
+    __syncthreads();
+    for (uint32_t p = start + t; p < end; p += blockDim.x) {
+        uint64_t e = tmp[p];
+        uint32_t pos = start + atomicAdd(&h[(uint32_t)(e >> 32)], 1u);
+        sorted[pos] = (uint32_t)e;
     }
 }
 
@@ -192,10 +251,17 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     hipStream_t st = ctx->stream;
 
-    VK_TRY(ctx->ws[WS_DIGITS].ensure(maxL * 4));
-    VK_TRY(ctx->ws[WS_COUNTS].ensure((size_t)(NBtot + 1) * 4));
+    // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
+    uint32_t lgNB = (uint32_t)c - 1;
+    const uint32_t FB = lgNB < 8 ? lgNB : 8;
+    const uint32_t NBC = NB >> FB, bins = (uint32_t)W * NBC;
+    const uint32_t nblk = (uint32_t)((n + SORT_CHUNK - 1) / SORT_CHUNK);
+    const size_t ncnt = (size_t)bins * nblk + 1;
+
+    VK_TRY(ctx->ws[WS_DIGITS].ensure(maxL * 8));
+    VK_TRY(ctx->ws[WS_COUNTS].ensure(ncnt * 4));
+    VK_TRY(ctx->ws[WS_CURSOR].ensure(ncnt * 4));
     VK_TRY(ctx->ws[WS_OFFSETS].ensure((size_t)(NBtot + 1) * 4));
-    VK_TRY(ctx->ws[WS_CURSOR].ensure((size_t)(NBtot + 1) * 4));
     VK_TRY(ctx->ws[WS_SORTED].ensure(maxL * 4));
     VK_TRY(ctx->ws[WS_BUCKETS].ensure((size_t)NBtot * sizeof(Acc)));
     VK_TRY(ctx->ws[WS_CARRY].ensure((size_t)(Tmax + 8) * sizeof(Acc)));
@@ -207,10 +273,10 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S) * sizeof(Acc)));
     VK_TRY(ctx->ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
 
-    int32_t* digits = ctx->ws[WS_DIGITS].as<int32_t>();
+    uint64_t* tmp = ctx->ws[WS_DIGITS].as<uint64_t>();
     uint32_t* counts = ctx->ws[WS_COUNTS].as<uint32_t>();
+    uint32_t* base = ctx->ws[WS_CURSOR].as<uint32_t>();
     uint32_t* offsets = ctx->ws[WS_OFFSETS].as<uint32_t>();
-    uint32_t* cursor = ctx->ws[WS_CURSOR].as<uint32_t>();
     uint32_t* sorted = ctx->ws[WS_SORTED].as<uint32_t>();
     Acc* buckets = ctx->ws[WS_BUCKETS].as<Acc>();
     Acc* carry = ctx->ws[WS_CARRY].as<Acc>();
@@ -225,23 +291,23 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     const Aff* bases = t->bases.as<Aff>() + offset;
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
 
-    VK_CHECK_HIP(hipMemsetAsync(counts, 0, (size_t)(NBtot + 1) * 4, st));
-    const uint32_t nb = (uint32_t)((n + 255) / 256);
-    VK_LAUNCH(ctx, "msm_digits", (k_msm_digits<Fr>), nb, 256, 0, d_sc, inf, (uint32_t)n, c, W, mont,
-              digits, counts, NB);
+    const size_t lds = (size_t)bins * 4;
+    if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
+    VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
+    VK_LAUNCH(ctx, "msm_sort_hist", (k_sort_hist<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, W, mont, FB, NBC,
+              nblk, counts);
     size_t tmp_bytes = 0;
-    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, offsets, NBtot + 1, st));
+    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
     VK_TRY(ctx->ws[WS_SCAN_TMP].ensure(tmp_bytes));
     {
         hipEvent_t ev = nullptr;
         if (ctx->timing) ctx->timer_begin("msm_scan", &ev);
-        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->ws[WS_SCAN_TMP].p, tmp_bytes, counts,
-                                                      offsets, NBtot + 1, st));
+        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
         if (ctx->timing) ctx->timer_end("msm_scan", ev);
     }
-    VK_CHECK_HIP(hipMemcpyAsync(cursor, offsets, (size_t)(NBtot + 1) * 4, hipMemcpyDeviceToDevice, st));
-    VK_LAUNCH(ctx, "msm_scatter", k_msm_scatter, nb, 256, 0, digits, (uint32_t)n, W, NB, cursor,
-              sorted);
+    VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, W, mont, FB,
+              NBC, nblk, base, tmp);
+    VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
     // total entries L = offsets[NBtot]
     uint32_t L = 0;
     VK_CHECK_HIP(hipMemcpyAsync(&L, offsets + NBtot, 4, hipMemcpyDeviceToHost, st));

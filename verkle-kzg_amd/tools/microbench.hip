@@ -14,6 +14,36 @@ __global__ void k_mad(uint32_t* out, uint32_t seed, int iters) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
 }
 
+__global__ void k_fma64(uint32_t* out, uint32_t seed, int iters) {
+    double x = 1.0 + threadIdx.x * 1e-9, y = 1e-3 * seed;
+    double a0 = x, a1 = y, a2 = x * y, a3 = x + y, a4 = 5, a5 = 7, a6 = 9, a7 = 11;
+    for (int i = 0; i < iters; i++) {
+#define F(a) a = __builtin_fma(a, x, y);
+        F(a0) F(a1) F(a2) F(a3) F(a4) F(a5) F(a6) F(a7)
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7);
+}
+
+__global__ void k_mul24(uint32_t* out, uint32_t seed, int iters) {
+    uint32_t x = (seed + threadIdx.x) & 0xffffff, y = seed * 3 + blockIdx.x;
+    uint32_t a0 = x, a1 = y, a2 = x ^ y, a3 = x + y, a4 = 5, a5 = 7, a6 = 9, a7 = 11;
+    for (int i = 0; i < iters; i++) {
+#define U(a) a = __umul24(a, x) + y;
+        U(a0) U(a1) U(a2) U(a3) U(a4) U(a5) U(a6) U(a7)
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
+__global__ void k_mullo(uint32_t* out, uint32_t seed, int iters) {
+    uint32_t x = seed + threadIdx.x, y = seed * 3 + blockIdx.x;
+    uint32_t a0 = x, a1 = y, a2 = x ^ y, a3 = x + y, a4 = 5, a5 = 7, a6 = 9, a7 = 11;
+    for (int i = 0; i < iters; i++) {
+#define L(a) a = a * x + y;
+        L(a0) L(a1) L(a2) L(a3) L(a4) L(a5) L(a6) L(a7)
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 template <class F>
 __global__ void k_fmul(uint32_t* out, uint32_t seed, int iters) {
     fe<F> a, b, c, d;
@@ -58,6 +88,12 @@ int main() {
     double ms = timeit(k_mad, blocks, 4096, out);
     double mads = (double)blocks * 256 * 4096 * 8;
     printf("{\"bench\":\"v_mad_u64_u32\",\"ms\":%.3f,\"Gop_per_s\":%.1f}\n", ms, mads / ms / 1e6);
+    ms = timeit(k_fma64, blocks, 4096, out);
+    printf("{\"bench\":\"v_fma_f64\",\"ms\":%.3f,\"Gop_per_s\":%.1f}\n", ms, mads / ms / 1e6);
+    ms = timeit(k_mul24, blocks, 4096, out);
+    printf("{\"bench\":\"v_mad_u32_u24\",\"ms\":%.3f,\"Gop_per_s\":%.1f}\n", ms, mads / ms / 1e6);
+    ms = timeit(k_mullo, blocks, 4096, out);
+    printf("{\"bench\":\"v_mad_u32 (mul_lo+add)\",\"ms\":%.3f,\"Gop_per_s\":%.1f}\n", ms, mads / ms / 1e6);
     ms = timeit(k_fmul<BLS381Fq>, blocks, 256, out);
     double muls = (double)blocks * 256 * 256 * 4;
     printf("{\"bench\":\"fe_mul_bls381_fq_12limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
