@@ -160,14 +160,15 @@ __global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ 
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_accumulate(
     const typename C::Aff* __restrict__ bases, const uint32_t* __restrict__ sorted,
-    const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t k_begin, uint32_t L, uint32_t M,
+    const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename C::Acc* __restrict__ buckets, typename C::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename C::Acc* __restrict__ owner_piece,
     uint32_t* __restrict__ owner_bucket) {
     using Acc = typename C::Acc;
     using Aff = typename C::Aff;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t k = k_begin + t * M;  // this launch covers sorted entries [k_begin, L)
+    const uint32_t L = offsets[NBtot];  // entry count, read on the device: no host round trip
+    uint32_t k = t * M;                 // grid sized for the n*W upper bound
     if (k >= L) return;
     uint32_t e = min(k + M, L);
     owner_bucket[t] = NONE;
@@ -242,7 +243,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     const int W = (Fr::BITS + 1 + c - 1) / c;  // one spare bit absorbs the final carry
     const uint32_t NB = 1u << (c - 1);
     const uint32_t NBtot = NB * W;
-    const uint32_t M = 32;                 // sorted entries per accumulate thread
+    const uint32_t M = 64;  // sorted entries per accumulate thread (64: 2 rounds of 2048 waves at 2^20 x 16)
     const uint32_t Lseg = NB >= 256 ? 8 : (NB >= 4 ? 2 : 1);
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
@@ -308,16 +309,10 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, W, mont, FB,
               NBC, nblk, base, tmp);
     VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
-    // total entries L = offsets[NBtot]
-    uint32_t L = 0;
-    VK_CHECK_HIP(hipMemcpyAsync(&L, offsets + NBtot, 4, hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipStreamSynchronize(st));
-    if (L > 0) {
-        const uint32_t T = (L + M - 1) / M;
-        VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (T + 255) / 256, 256, 0, bases, sorted, offsets,
-                  NBtot, 0u, L, M, buckets, carry, through, owner, owner_b);
-        VK_TRY(msm_tail_fixup<C>(ctx, T, buckets, carry, through, owner, owner_b));
-    }
+    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= n*W
+    VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, sorted, offsets,
+              NBtot, M, buckets, carry, through, owner, owner_b);
+    VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b));
     VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, part, tail));
     std::vector<Acc> ht((size_t)W * (J + 1));
     VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));

@@ -17,9 +17,10 @@ __global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__
                                                   const uint8_t* __restrict__ through,
                                                   const typename C::Acc* __restrict__ owner_piece,
                                                   const uint32_t* __restrict__ owner_bucket,
-                                                  uint32_t T) {
+                                                  uint32_t Tmax, const uint32_t* __restrict__ Lp, uint32_t M) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
+    const uint32_t T = (*Lp + M - 1) / M;  // accumulate threads that ran
+    if (t >= T || t >= Tmax) return;
     uint32_t b = owner_bucket[t];
     if (b == NONE_T) return;
     typename C::Acc acc = owner_piece[t];
@@ -126,10 +127,10 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __res
 }
 
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, typename C::Acc* buckets, const typename C::Acc* carry,
+int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets, const typename C::Acc* carry,
                    const uint8_t* through, const typename C::Acc* owner, const uint32_t* owner_b) {
     VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<typename C::Inl>), (T + 255) / 256, 256, 0, buckets, carry, through,
-              owner, owner_b, T);
+              owner, owner_b, T, Lp, M);
     return VC_OK;
 }
 
@@ -150,7 +151,7 @@ int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t*
 }
 
 #define VK_INST_TAIL(C)                                                                                        \
-    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, C::Acc*, const C::Acc*, const uint8_t*, const C::Acc*,  \
+    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, const C::Acc*, const uint8_t*, const C::Acc*,  \
                                    const uint32_t*);                                                           \
     template int msm_tail_reduce<C>(vc_ctx*, const C::Acc*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
                                     uint32_t, C::Acc*, C::Acc*, C::Acc*, C::Acc*);
