@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--curve", default="bls12_381")
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--commit-batch", type=int, default=10000)
-    ap.add_argument("--commit-window", type=int, default=8)
+    ap.add_argument("--commit-window", type=int, default=16)
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 14, help="terms of the CPU naive MSM sample")

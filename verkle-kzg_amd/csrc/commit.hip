@@ -21,6 +21,24 @@
 
 namespace vk {
 
+// Table entry (kept as a type so the layout can change in one place).
+template <class C>
+struct FbEntryNoPad {
+    typename C::Aff a;
+};
+template <class C>
+using FbE = FbEntryNoPad<C>;  // padding 96 -> 128 B measured slower (4.54 -> 4.93 ms at c = 16)
+
+// copy one window's normalised multiples into the table: tab[(i*W + w)*NBk + k] = aff[i*NBk + k]
+template <class C>
+__global__ void k_fb_place(const typename C::Aff* __restrict__ aff, uint32_t n, uint32_t NBk, int W, int w,
+                           FbE<C>* __restrict__ tab) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= (size_t)n * NBk) return;
+    size_t i = j / NBk, k = j - i * NBk;
+    tab[(i * W + w) * NBk + k].a = aff[j];
+}
+
 template <class Fr>
 __device__ __forceinline__ fe<Fr> load_scalar_fb(const uint32_t* __restrict__ sc, size_t i) {
     const uint4* p = reinterpret_cast<const uint4*>(sc + 8 * i);
@@ -153,49 +171,89 @@ __global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __rest
 }
 
 // ------------------------------------------------------------------ the batched commit
+// Persistent item ranges: the batch x width (commit, base) items are cut into nlanes equal
+// runs of K consecutive items (K <= width, so a run touches at most two commits), one run
+// per lane, with nlanes = what the chip holds in ONE round (occupancy x CUs). A run keeps
+// one accumulator per commit it touches and stores them as two pieces; k_fb_combine adds
+// the ~width/K pieces of each commit. (A thread-group-per-commit mapping left the last
+// round 20 % full at 10k commits: 61 % of the chip.)
 template <class C, class Fr>
-__global__ void __launch_bounds__(256) k_fb_commit(const typename C::Aff* __restrict__ tab,
+__global__ void __launch_bounds__(256) k_fb_commit(const FbE<C>* __restrict__ tab,
                                                   const uint8_t* __restrict__ inf, uint32_t width,
                                                   int c, int W, const uint32_t* __restrict__ sc,
-                                                  uint32_t batch, int mont, int tpc,
-                                                  typename C::Acc* __restrict__ out) {
+                                                  uint32_t batch, int mont, uint32_t K, uint32_t nlanes,
+                                                  typename C::Acc* __restrict__ piece) {
     using Acc = typename C::Acc;
-    const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t g = gtid / tpc, sub = gtid % tpc;
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nlanes) return;
     const uint32_t NBk = 1u << (c - 1);
     const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
+    const size_t items = (size_t)batch * width;
+    const size_t it0 = (size_t)l * K, it1 = min(it0 + K, items);
+    uint32_t g_cur = (uint32_t)(it0 / width);
+    int slot = 0;
     Acc acc = C::zero();
-    if (g < batch) {
-        for (uint32_t i = sub; i < width; i += tpc) {
-            if (inf[i]) continue;
-            fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
-            if (mont) s = fe_from_mont<Fr>(s);
-            const typename C::Aff* ti = tab + (size_t)i * W * NBk;
-            uint32_t carry = 0;
-            for (int w = 0; w < W; w++) {
-                uint32_t raw = (s.v[0] & mask) + carry;
+    for (size_t it = it0; it < it1; it++) {
+        const uint32_t g = (uint32_t)(it / width), i = (uint32_t)(it - (size_t)g * width);
+        if (g != g_cur) {  // run crosses into the next commit (at most once: K <= width)
+            piece[2 * (size_t)l] = acc;
+            acc = C::zero();
+            slot = 1;
+            g_cur = g;
+        }
+        if (inf[i]) continue;
+        fe<Fr> s = load_scalar_fb<Fr>(sc, it);
+        if (mont) s = fe_from_mont<Fr>(s);
+        const FbE<C>* ti = tab + (size_t)i * W * NBk;
+        uint32_t carry = 0;
+        // digit of the next window computed one step ahead so its table entry is in flight
+        // while the current mixed add runs (random 96 B reads from a 0.1-13 GB table)
+        auto next_digit = [&]() -> int32_t {
+            uint32_t raw = (s.v[0] & mask) + carry;
 #pragma unroll
-                for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
-                s.v[7] >>= c;
-                carry = raw > half ? 1u : 0u;
-                int32_t d = carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
-                if (d != 0) {
-                    uint32_t a = (uint32_t)(d < 0 ? -d : d) - 1;
-                    acc = C::madd(acc, ti[(size_t)w * NBk + a], d < 0);
-                }
+            for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
+            s.v[7] >>= c;
+            carry = raw > half ? 1u : 0u;
+            return carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
+        };
+        int32_t dn = next_digit();
+        typename C::Aff Pn = ti[dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0].a;
+        for (int w = 0; w < W; w++) {
+            const int32_t d = dn;
+            const typename C::Aff P = Pn;
+            if (w + 1 < W) {
+                dn = next_digit();
+                Pn = ti[(size_t)(w + 1) * NBk + (dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0)].a;
             }
+            if (d != 0) acc = C::madd(acc, P, d < 0);
         }
     }
-    // fold the tpc partial sums of one commit (tpc is a power of two <= 64)
-    for (int m = tpc >> 1; m > 0; m >>= 1) {
-        Acc o;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&acc);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
-#pragma unroll
-        for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
-        acc = C::add(acc, o);
+    piece[2 * (size_t)l + slot] = acc;
+}
+
+// commit g = sum of its pieces: lanes l0..l1 cover items [g*width, (g+1)*width)
+template <class C>
+__global__ void __launch_bounds__(256) k_fb_combine(const typename C::Acc* __restrict__ piece, uint32_t width,
+                                                   uint32_t batch, uint32_t K, typename C::Acc* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= batch) return;
+    const size_t l0 = (size_t)g * width / K, l1 = ((size_t)(g + 1) * width - 1) / K;
+    typename C::Acc acc = C::zero();
+    for (size_t l = l0; l <= l1; l++) {
+        const uint32_t gl = (uint32_t)(l * K / width);  // first commit of lane l's run
+        acc = C::add(acc, piece[2 * l + (gl == g ? 0 : 1)]);
     }
-    if (sub == 0 && g < batch) out[g] = acc;
+    out[g] = acc;
+}
+
+// lanes resident in one round for a kernel (occupancy x CUs x block)
+template <class Kern>
+static uint32_t resident_lanes(Kern k, int block) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, block, 0) != hipSuccess) return 0;
+    return (uint32_t)(cus * per_cu * block);
 }
 
 // ------------------------------------------------------------------ host drivers
@@ -212,7 +270,7 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c) {
     const uint32_t NBk = 1u << (c - 1);
     if (t->fb_c == c && t->fb.p) return VC_OK;
     t->fb.release();
-    VK_TRY(t->fb.ensure(std::max<size_t>((size_t)n * W * NBk, 1) * sizeof(Aff)));
+    VK_TRY(t->fb.ensure(std::max<size_t>((size_t)n * W * NBk, 1) * sizeof(FbE<C>)));
     DevBuf Q, tmp, aff_w;
     VK_TRY(Q.ensure(std::max<uint32_t>(n, 1) * sizeof(Acc)));
     VK_TRY(tmp.ensure(std::max<size_t>((size_t)n * NBk, 1) * sizeof(Acc)));
@@ -227,10 +285,9 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c) {
         size_t cnt = (size_t)n * NBk;
         VK_LAUNCH(ctx, "fb_normalize", (k_normalize<C>), (cnt + 255) / 256, 256, 0, tmp.as<Acc>(), cnt,
                   aff_w.as<Aff>(), (uint32_t*)nullptr, (uint8_t*)nullptr);
-        // scatter window w into T[i][w][k]
-        VK_CHECK_HIP(hipMemcpy2DAsync(t->fb.as<Aff>() + (size_t)w * NBk, (size_t)W * NBk * sizeof(Aff),
-                                      aff_w.p, (size_t)NBk * sizeof(Aff), (size_t)NBk * sizeof(Aff), n,
-                                      hipMemcpyDeviceToDevice, ctx->stream));
+        // place window w into T[i][w][k]
+        VK_LAUNCH(ctx, "fb_place", (k_fb_place<C>), (cnt + 255) / 256, 256, 0, aff_w.as<Aff>(), n, NBk, W, w,
+                  t->fb.as<FbE<C>>());
     }
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     t->fb_c = c;
@@ -246,13 +303,21 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
     if (batch == 0) return VC_OK;
     VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
-    int tpc = 16;
-    while (tpc > 1 && (size_t)tpc > width) tpc >>= 1;
-    size_t threads = batch * (size_t)tpc;
-    VK_LAUNCH(ctx, "fb_commit", (k_fb_commit<C, Fr>), (threads + 255) / 256, 256, 0,
-              t->fb.as<typename C::Aff>(), t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, t->fb_W,
-              reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, tpc,
-              ctx->ws[WS_OUT].as<Acc>());
+    static uint32_t lanes_cache = 0;
+    if (!lanes_cache) lanes_cache = resident_lanes(k_fb_commit<C, Fr>, 256);
+    const size_t items = batch * width;
+    const size_t lanes = lanes_cache ? lanes_cache : 131072;
+    size_t K = (items + lanes - 1) / lanes;
+    K = std::max<size_t>(1, std::min<size_t>(K, width));
+    const size_t nlanes = (items + K - 1) / K;
+    if (nlanes >= (1ull << 31)) return VC_E_RANGE;
+    VK_TRY(ctx->ws[WS_PIECE].ensure(2 * nlanes * sizeof(Acc)));
+    VK_LAUNCH(ctx, "fb_commit", (k_fb_commit<C, Fr>), (nlanes + 255) / 256, 256, 0,
+              t->fb.as<FbE<C>>(), t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, t->fb_W,
+              reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, (uint32_t)K, (uint32_t)nlanes,
+              ctx->ws[WS_PIECE].as<Acc>());
+    VK_LAUNCH(ctx, "fb_combine", (k_fb_combine<C>), (batch + 255) / 256, 256, 0, ctx->ws[WS_PIECE].as<Acc>(),
+              (uint32_t)width, (uint32_t)batch, (uint32_t)K, ctx->ws[WS_OUT].as<Acc>());
     VK_LAUNCH(ctx, "fb_normalize_out", (k_normalize<C>), (batch + 255) / 256, 256, 0,
               ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
               reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);

@@ -72,6 +72,7 @@ enum WsSlot {
     WS_MISC,
     WS_TREE,
     WS_TAIL,
+    WS_PIECE,
     WS_COUNT_
 };
 

@@ -1,7 +1,7 @@
 // Field-multiply and v_mad_u64_u32 throughput microbenchmark (gfx950). Prints JSON lines.
 #include <hip/hip_runtime.h>
 #include <cstdio>
-#include "../csrc/ff.hpp"
+#include "../csrc/ec.hpp"
 using namespace vk;
 
 __global__ void k_mad(uint32_t* out, uint32_t seed, int iters) {
@@ -65,6 +65,24 @@ __global__ void k_fmul(uint32_t* out, uint32_t seed, int iters) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+// EC mixed-add chain with the operand in registers (no memory): compute ceiling of the
+// accumulate / fixed-base commit inner loops
+template <class C>
+__global__ void k_madd(uint32_t* out, uint32_t seed, int iters) {
+    typename C::Aff P;
+    uint32_t* pw = reinterpret_cast<uint32_t*>(&P);
+    for (int k = 0; k < (int)(sizeof(P) / 4); k++) pw[k] = (seed * 2654435761u + k * 77 + threadIdx.x) & 0x0fffffff;
+    typename C::Acc acc = C::from_aff(P, false);
+    for (int i = 0; i < iters; i++) {
+        acc = C::madd(acc, P, (i & 1) != 0);
+        pw[0] ^= i;
+    }
+    const uint32_t* aw = reinterpret_cast<const uint32_t*>(&acc);
+    uint32_t r = 0;
+    for (int k = 0; k < C::ACC_WORDS; k++) r ^= aw[k];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
 template <class K>
 static double timeit(K kern, int blocks, int iters, uint32_t* out) {
     hipEvent_t a, b;
@@ -101,5 +119,12 @@ int main() {
     printf("{\"bench\":\"fe_mul_bls381_fr_8limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
     ms = timeit(k_fmul<BN254Fq>, blocks, 256, out);
     printf("{\"bench\":\"fe_mul_bn254_fq_8limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
+    ms = timeit(k_madd<BLS381G1>, blocks, 64, out);
+    double madds = (double)blocks * 256 * 64;
+    printf("{\"bench\":\"madd_bls381_xyzz_chain\",\"ms\":%.3f,\"Gmadd_per_s\":%.2f}\n", ms, madds / ms / 1e6);
+    ms = timeit(k_madd<Bandersnatch>, blocks, 64, out);
+    printf("{\"bench\":\"madd_bandersnatch_ext_chain\",\"ms\":%.3f,\"Gmadd_per_s\":%.2f}\n", ms, madds / ms / 1e6);
+    ms = timeit(k_madd<BN254G1>, blocks, 64, out);
+    printf("{\"bench\":\"madd_bn254_xyzz_chain\",\"ms\":%.3f,\"Gmadd_per_s\":%.2f}\n", ms, madds / ms / 1e6);
     return 0;
 }
