@@ -2,14 +2,15 @@
 """Benchmark: single 2^20-point BLS12-381 G1 MSM (BASELINE.json configs[1]) on N MI355X.
 
 A step = one 2^20-point MSM over synthetic inputs already resident in HBM (bases uploaded
-once, scalars on the device). With N ranks the MSM is split by point range (each rank
-streams only its n/N bases and scalars), the per-rank projective partial sums are
-all-gathered over RCCL and added on the host: one exchange step, so
-scaling is "strong" (total work fixed).
+once, scalars on the device). With N ranks the MSM is split by Pippenger windows (rank k
+computes windows [kW/N, (k+1)W/N) of all n terms; vkzg.dist), the per-rank projective
+partial sums are all-gathered over RCCL and added on the host: one exchange step
+(SURVEY.md 8(e)), so scaling is "strong" (total work fixed).
 
-Secondary line items (same JSON object): 10k batched width-256 Bandersnatch commits/s on
-this rank (config 3), and the CPU baseline: the reference's naive MSM restated in C
-(oracle/c/ref_curve.c) timed on a bounded sample on this host.
+Secondary line items (same JSON object): 10k batched width-256 Bandersnatch commits/s
+(config 3; the batch split across the N ranks, results all-gathered), and the CPU baseline:
+the reference's naive MSM restated in C (oracle/c/ref_curve.c) timed on a bounded sample on
+this host.
 
     python bench.py [--gpus N --steps K --warmup W]
 """
@@ -34,6 +35,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # algorithmic bytes per 2^20 BLS12-381 MSM: n*(96 B affine + 32 B scalar) + 96 B out
 BYTES_PER_POINT = {"bls12_381": 96 + 32, "bn254": 64 + 32, "bandersnatch": 64 + 32}
 OUT_BYTES = {"bls12_381": 96, "bn254": 64, "bandersnatch": 64}
+# VALU roofline: field multiplies per mixed add in the accumulate kernel
+# (XYZZ 8M+2S; extended Edwards 8M) x 2 N^2 v_mad_u64_u32 per N-limb Montgomery multiply
+MULS_PER_MADD = {"bls12_381": 10, "bn254": 10, "bandersnatch": 8}
+LIMBS32 = {"bls12_381": 12, "bn254": 8, "bandersnatch": 8}
+SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
+# HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
+# (tools_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
 
 
 def parse():
@@ -47,7 +56,7 @@ def parse():
     ap.add_argument("--commit-window", type=int, default=16)
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 14, help="terms of the CPU naive MSM sample")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
     return ap.parse_args()
 
 
@@ -93,12 +102,12 @@ def main():
     table = eng.random_bases(n, seed=2024)
     rng = np.random.default_rng(1234)
     scalars = vkzg.random_scalars(curve, n, rng)
-    lo, hi = vdist.shard_range(n, rank, world)
-    d_sc = torch.from_numpy(scalars[lo:hi].view(np.int64).copy()).to(dev)
+    d_sc = torch.from_numpy(scalars.view(np.int64).copy()).to(dev)
 
     def step():
-        # shard partial (HIP) -> RCCL all-gather of projective partials -> host sum
-        return vdist.msm_sharded(eng, table, d_sc.data_ptr(), n, rank, world, dev if world > 1 else None)
+        # window-slice partial (HIP) -> RCCL all-gather of projective partials -> host sum
+        return vdist.msm_sharded(eng, table, d_sc.data_ptr(), n, rank, world, dev if world > 1 else None,
+                                 split="windows")
 
     for _ in range(a.warmup):
         res = step()
@@ -124,13 +133,32 @@ def main():
     # dominant kernel (bucket accumulation) device time, HIP events on the launch stream
     acc_ms, acc_n = eng.kernel_time("msm_accumulate")
     kernels = {}
-    for k in ("msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate", "msm_fixup", "msm_segsum",
-              "msm_bitsum", "msm_sumpart"):
+    for k in ("msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate", "msm_fixup",
+              "msm_segsum", "msm_bitsum", "msm_sumpart"):
         ms, cnt = eng.kernel_time(k)
         if cnt:
             kernels[k] = round(ms / cnt, 4)
-    shard_bytes = (hi - lo) * BYTES_PER_POINT[curve] + OUT_BYTES[curve]
-    achieved = shard_bytes / (acc_ms / acc_n * 1e-3) / 1e9 if acc_n else None
+    acc_s = acc_ms / acc_n * 1e-3 if acc_n else None
+    # algorithmic bytes of this rank's share of the MSM (n*(96+32) + 96 per MSM)
+    shard_bytes = (n * BYTES_PER_POINT[curve] + OUT_BYTES[curve]) / world
+    achieved = shard_bytes / acc_s / 1e9 if acc_s else None
+    # VALU roofline: mixed adds of this rank's window slice (one per nonzero digit ~ n per window)
+    from vkzg.dist import window_count
+    c_bits, w_total = window_count(curve, n)
+    w_rank = (rank + 1) * w_total // world - rank * w_total // world
+    mads = n * w_rank * MULS_PER_MADD[curve] * 2 * LIMBS32[curve] ** 2
+    mad_peak = eng.device_mad_rate()
+    valu = {"achieved": mads / acc_s / 1e12 if acc_s else None, "peak": mad_peak, "unit": "T v_mad_u64_u32/s",
+            "frac": (mads / acc_s / 1e12 / mad_peak) if acc_s else None,
+            "work": f"{n}x{w_rank} mixed adds x {MULS_PER_MADD[curve]} Fq mults x {2 * LIMBS32[curve] ** 2} mads",
+            "peak_source": "vc_device_mad_rate, measured live on this GPU"}
+    traffic, traffic_src = None, None
+    if world == 1 and os.path.exists(PMC_SUMMARY):
+        pmc = json.load(open(PMC_SUMMARY))
+        key = [k for k in pmc.get("kernels", {}) if "k_msm_accumulate<vk::SWCurve<vk::BLS381Fq" in k]
+        if key and pmc.get("config", {}).get("log_n") == a.log_n and curve == "bls12_381":
+            traffic = pmc["kernels"][key[0]].get("hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
 
     out = {
         "metric": METRIC,
@@ -146,45 +174,68 @@ def main():
         "dtype": "u32",
         "data": "synthetic (random subgroup bases s_i*G generated on device, uniform scalars < r)",
         "config": {"workload": f"single 2^{a.log_n}-point {curve} G1 Pippenger MSM (configs[1])",
-                   "n_points": n, "curve": curve, "parallelism": f"point-range shards x{world}",
-                   "window_bits": 16 if n >= (1 << 19) else None},
+                   "n_points": n, "curve": curve, "parallelism": f"Pippenger-window slices x{world}",
+                   "window_bits": c_bits, "windows": w_total},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "msm_accumulate",
                      "kernel_ms": (acc_ms / acc_n) if acc_n else None,
                      "algorithmic_bytes_per_launch": shard_bytes,
-                     "note": "EC MSM is VALU integer-multiply bound, not HBM bound (SURVEY 8(d))"},
+                     "valu": valu,
+                     "note": "EC MSM is VALU integer-multiply bound, not HBM bound (SURVEY 8(d)); "
+                             "the valu object is the binding roofline"},
         "kernel_ms": kernels,
         "result_inf": int(res[1]),
     }
 
-    if rank == 0 and not a.no_secondary:
-        # config 3: batched width-256 commits (fixed-base tables), this rank only
+    if not a.no_secondary:
+        # config 3: batched width-256 commits (fixed-base tables), batch split across ranks
         ceng = vkzg.Engine("bandersnatch", local)
         ceng.set_stream(stream.cuda_stream)
         ctab = ceng.random_bases(256, seed=3)
         ceng.fixed_base_precompute(ctab, a.commit_window)
         B = a.commit_batch
-        csc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(5))
-        dcs = torch.from_numpy(csc.view(np.int64)).to(dev)
-        dxy = torch.zeros((B, 8), dtype=torch.int64, device=dev)
-        dinf = torch.zeros(B, dtype=torch.uint8, device=dev)
+        blo, bhi = vdist.shard_range(B, rank, world)
+        Bl = bhi - blo
+        csc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(5))[blo * 256:bhi * 256]
+        dcs = torch.from_numpy(np.ascontiguousarray(csc).view(np.int64)).to(dev)
+        dxy = torch.zeros((max(Bl, 1), 8), dtype=torch.int64, device=dev)
+        dinf = torch.zeros(max(Bl, 1), dtype=torch.uint8, device=dev)
+
+        def cstep():
+            ceng.msm_batch_device(ctab, 256, dcs.data_ptr(), Bl, dxy.data_ptr(), dinf.data_ptr())
+            if world > 1:  # every rank ends with all B commitments (RCCL all-gather)
+                return vdist.all_gather_commitments(dxy[:Bl], dinf[:Bl], B, world)
+            return dxy, dinf
+
         for _ in range(2):
-            ceng.msm_batch_device(ctab, 256, dcs.data_ptr(), B, dxy.data_ptr(), dinf.data_ptr())
+            cstep()
         torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         ceng.enable_timing(True)
         t0 = time.perf_counter()
         reps = 5
         for _ in range(reps):
-            ceng.msm_batch_device(ctab, 256, dcs.data_ptr(), B, dxy.data_ptr(), dinf.data_ptr())
+            cstep()
         torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         cdt = (time.perf_counter() - t0) / reps
+        if world > 1:
+            tt = torch.tensor([cdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            cdt = float(tt.item())
         fb_ms, fb_n = ceng.kernel_time("fb_commit")
         out["secondary"] = {
-            "workload": f"{B} batched width-256 Bandersnatch commits (configs[2]), fixed-base c={a.commit_window}",
+            "workload": f"{B} batched width-256 Bandersnatch commits (configs[2]), fixed-base c={a.commit_window}, "
+                        f"batch split over {world} rank(s)",
             "commits_per_s": B / cdt, "ms_per_batch": cdt * 1e3,
             "fb_commit_kernel_ms": fb_ms / fb_n if fb_n else None,
-            "achieved_GBps": (B * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
+            "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
+            "table_bytes": 256 * ((253 + 1 + a.commit_window - 1) // a.commit_window)
+                           * (1 << (a.commit_window - 1)) * 96,
         }
         ceng.close()
 

@@ -50,6 +50,9 @@ typedef struct vc_ctx vc_ctx;
 
 const char* vc_strerror(int status);
 int vc_version(void);
+/* Diagnostics (not part of the reference boundary): measured v_mad_u64_u32 throughput of the
+ * ctx's device in tera-ops/s -- the peak of the VALU roofline bench.py reports. */
+int vc_device_mad_rate(vc_ctx* ctx, double* tera_per_s);
 
 /* Context: one device, one stream. device = HIP ordinal. */
 int vc_ctx_create(int curve, int device, vc_ctx** out);
@@ -87,6 +90,14 @@ int vc_msm_device(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalar
 int vc_point_words(int curve);
 int vc_msm_device_partial(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars,
                           size_t n, int mont, uint32_t* out_acc);
+/* Window-sliced partial MSM (the other way to shard one MSM across GPUs): part k of `parts`
+ * covers Pippenger windows [k*W/parts, (k+1)*W/parts) of ALL n terms, including their 2^(c*w)
+ * weights, so the parts' accumulators sum (vc_partials_sum) to the whole MSM. Each part
+ * streams every base but builds and reduces only its windows' buckets: the bucket reduction,
+ * which does not shrink with n, is divided by `parts` (a point split leaves it whole). */
+int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows);  /* c and W chosen for n */
+int vc_msm_device_window_part(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars, size_t n,
+                              int mont, int part, int parts, uint32_t* out_acc);
 /* Sum k partial accumulators (host) and normalise to canonical affine. */
 int vc_partials_sum(int curve, const uint32_t* accs, size_t k, uint64_t* out_xy, uint8_t* out_inf);
 

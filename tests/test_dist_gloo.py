@@ -1,7 +1,8 @@
-"""world_size-2 gloo test (CPU) of the multi-GPU MSM exchange: point-range shards, all-gather of
-projective partials, host sum (vkzg.dist) == the whole MSM. Shard partials come from the
-oracle here (no GPU in this container); on the GPU box bench.py runs the same path with the
-HIP partials over RCCL."""
+"""world_size-2 gloo test (CPU) of the multi-GPU MSM exchange: point-range shards or window
+slices, all-gather of projective partials, host sum (vkzg.dist) == the whole MSM. Shard
+partials come from the oracle here (no GPU in this container); on the GPU box bench.py runs
+the same path with the HIP partials over RCCL (tests/test_gpu_msm.py checks the HIP window
+parts against the same oracle)."""
 import os
 import socket
 
@@ -20,12 +21,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, curve, q):
+def _worker(rank, world, port, curve, q, split="points"):
     import sys
     sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd"), os.path.join(ROOT, "oracle")]
     import random
     import torch.distributed as dist
     from pyoracle import cref
+    from pyoracle import pippenger
     from pyoracle.curves import CURVES, random_points
     from vkzg import dist as vdist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -35,8 +37,11 @@ def _worker(rank, world, port, curve, q):
     n = 37
     pts = random_points(C, n, rng)
     sc = [rng.randrange(C.r) for _ in range(n)]
-    lo, hi = vdist.shard_range(n, rank, world)
-    part = cref.msm(curve, pts[lo:hi], sc[lo:hi], 1)
+    if split == "points":
+        lo, hi = vdist.shard_range(n, rank, world)
+        part = cref.msm(curve, pts[lo:hi], sc[lo:hi], 1)
+    else:  # window slice `rank` of `world` over all n terms
+        part = cref.msm(curve, pts, pippenger.part_scalars(curve, sc, rank, world, C.r), 1)
     words = vdist.affine_to_acc_words(curve, part)
     parts = vdist.all_gather_partials(words, world, None)
     xy, inf = vdist.partials_sum(curve, parts)
@@ -50,12 +55,13 @@ def _worker(rank, world, port, curve, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("split", ["points", "windows"])
 @pytest.mark.parametrize("curve", ["bn254", "bls12_381", "bandersnatch"])
-def test_sharded_msm_gloo_world2(curve, oracle_c):
+def test_sharded_msm_gloo_world2(curve, split, oracle_c):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, curve, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, curve, q, split)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]
@@ -72,3 +78,37 @@ def test_shard_range_covers():
             parts = [vdist.shard_range(n, r, w) for r in range(w)]
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+def _commit_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd")]
+    import torch
+    import torch.distributed as dist
+    from vkzg import dist as vdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B = 7
+    lo, hi = vdist.shard_range(B, rank, world)
+    # stand-in commitments: row j = (j, j^2, ...) so the gathered order is checkable
+    xy = torch.tensor([[j * 10 + k for k in range(8)] for j in range(lo, hi)], dtype=torch.int64)
+    inf = torch.tensor([j % 2 for j in range(lo, hi)], dtype=torch.uint8)
+    gxy, ginf = vdist.all_gather_commitments(xy, inf, B, world)
+    ok = (gxy.shape == (B, 8) and all(int(gxy[j, k]) == j * 10 + k for j in range(B) for k in range(8))
+          and [int(v) for v in ginf] == [j % 2 for j in range(B)])
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_batched_commit_gather_gloo_world2():
+    """the batch-sliced commit path's all-gather (bench.py secondary)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_commit_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(ok for _, ok in res), res

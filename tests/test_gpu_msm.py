@@ -116,6 +116,34 @@ def test_msm_offset_and_partials(engines, oracle_c, curve):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("n,parts", [(7, 2), (300, 3), (5000, 4), (70000, 2)])
+def test_msm_window_parts(engines, oracle_c, curve, n, parts):
+    """window-sliced partials (the default multi-GPU split): each part equals the oracle's
+    window-part MSM, and the parts add up to the whole MSM."""
+    import torch
+    import vkzg
+    from pyoracle import pippenger
+    from pyoracle.curves import CURVES as OC
+    e = engines[curve]
+    rng = np.random.default_rng(21 + n)
+    tid = e.random_bases(n, seed=22)
+    xy, inf = e.download_bases(tid)
+    sc = vkzg.random_scalars(curve, n, rng)
+    whole = e.msm(tid, sc)
+    dsc = torch.from_numpy(sc.view(np.int64)).cuda()
+    accs = [e.msm_device_window_part(tid, dsc.data_ptr(), n, k, parts) for k in range(parts)]
+    summed = e.partials_sum(np.stack(accs))
+    assert np.array_equal(summed[0], whole[0]) and summed[1] == whole[1]
+    if n <= 5000:
+        ints = [vkzg.limbs_to_int(row) for row in sc]
+        k = parts - 1
+        want = _oracle(oracle_c, curve, xy, inf,
+                       vkzg.ints_to_limbs(pippenger.part_scalars(curve, ints, k, parts, OC[curve].r)))
+        got = e.partials_sum(accs[k][None, :])
+        assert got[1] == want[1] and np.array_equal(got[0], want[0])
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_batch_commit(engines, oracle_c, curve):
     """vc_msm_batch (fixed-base tables) vs per-commit oracle MSM; width 256 and ragged width."""
     import vkzg

@@ -338,4 +338,38 @@ int point_words(int curve) {
 }
 int aff_limbs64(int curve) { return curve == VC_CURVE_BLS12_381 ? 6 : 4; }
 
+// ------------------------------------------------------------------ VALU peak probe
+// v_mad_u64_u32 throughput (8 independent chains per lane, 16 waves per SIMD): the peak the
+// MSM kernels' VALU roofline is priced against.
+__global__ void __launch_bounds__(256) k_mad_probe(uint32_t* out, uint32_t seed, int iters) {
+    uint32_t x = seed + threadIdx.x, y = seed * 3 + blockIdx.x;
+    uint64_t a0 = x, a1 = y, a2 = x ^ y, a3 = x + y, a4 = 5, a5 = 7, a6 = 9, a7 = 11;
+    for (int i = 0; i < iters; i++) {
+#define VK_MAD_(a) a = (uint64_t)(uint32_t)a * x + (a >> 32);
+        VK_MAD_(a0) VK_MAD_(a1) VK_MAD_(a2) VK_MAD_(a3) VK_MAD_(a4) VK_MAD_(a5) VK_MAD_(a6) VK_MAD_(a7)
+#undef VK_MAD_
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
+}
+
+int device_mad_rate(vc_ctx* ctx, double* tera_per_s) {
+    const int blocks = 4096, iters = 4096;
+    DevBuf out;
+    VK_TRY(out.ensure((size_t)blocks * 256 * 4));
+    hipEvent_t a, b;
+    VK_CHECK_HIP(hipEventCreate(&a));
+    VK_CHECK_HIP(hipEventCreate(&b));
+    hipLaunchKernelGGL(k_mad_probe, dim3(blocks), dim3(256), 0, ctx->stream, out.as<uint32_t>(), 1u, iters);
+    VK_CHECK_HIP(hipEventRecord(a, ctx->stream));
+    hipLaunchKernelGGL(k_mad_probe, dim3(blocks), dim3(256), 0, ctx->stream, out.as<uint32_t>(), 2u, iters);
+    VK_CHECK_HIP(hipEventRecord(b, ctx->stream));
+    VK_CHECK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    VK_CHECK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *tera_per_s = (double)blocks * 256 * iters * 8 / (ms * 1e-3) / 1e12;
+    return VC_OK;
+}
+
 }  // namespace vk

@@ -107,6 +107,12 @@ const char* vc_strerror(int s) {
 
 int vc_version(void) { return 1; }
 
+int vc_device_mad_rate(vc_ctx* ctx, double* tera_per_s) {
+    if (!ctx || !tera_per_s) return VC_E_INVALID;
+    Guard g(ctx);
+    return vk::device_mad_rate(ctx, tera_per_s);
+}
+
 int vc_ctx_create(int curve, int device, vc_ctx** out) {
     if (!out || !valid_curve(curve)) return VC_E_INVALID;
     *out = nullptr;
@@ -222,12 +228,24 @@ int vc_bases_download(vc_ctx* ctx, int id, uint64_t* xy, uint8_t* inf) {
 int vc_point_words(int curve) { return valid_curve(curve) ? vk::point_words(curve) : VC_E_INVALID; }
 
 static int msm_device_acc(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont,
-                          uint32_t* acc) {
+                          uint32_t* acc, int part = 0, int parts = 1) {
     vk::Table* t = ctx->table(id);
     if (!t) return VC_E_TABLE;
     if (offset > t->n || n > t->n - offset) return VC_E_RANGE;
     if (n > 0 && !d_sc) return VC_E_INVALID;
-    return vk::msm_run(ctx, t, offset, d_sc, n, mont, acc);
+    return vk::msm_run(ctx, t, offset, d_sc, n, mont, acc, part, parts);
+}
+
+int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows) {
+    if (!valid_curve(curve) || !window_bits || !windows) return VC_E_INVALID;
+    return vk::msm_windows(curve, n, window_bits, windows);
+}
+
+int vc_msm_device_window_part(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont, int part,
+                              int parts, uint32_t* out_acc) {
+    if (!ctx || !out_acc || parts < 1 || part < 0 || part >= parts) return VC_E_INVALID;
+    Guard g(ctx);
+    return msm_device_acc(ctx, id, offset, d_sc, n, mont, out_acc, part, parts);
 }
 
 int vc_msm_device_partial(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont,

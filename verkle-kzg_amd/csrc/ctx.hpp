@@ -129,8 +129,10 @@ struct vc_ctx {
 
 namespace vk {
 // implemented per translation unit with explicit instantiations
+int device_mad_rate(vc_ctx* ctx, double* tera_per_s);
+int msm_windows(int curve, size_t n, int* c, int* W);
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
-            uint32_t* out_acc_words /*host, projective, vc_point_words*/);
+            uint32_t* out_acc, int part = 0, int parts = 1);
 int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out_inf);
 int acc_sum(int curve, const uint32_t* accs, size_t k, uint32_t* out);
 int point_words(int curve);

@@ -77,10 +77,10 @@ constexpr uint32_t SORT_CHUNK = 1024;
 
 template <class Fr>
 __global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
-                                                  uint32_t n, int c, int W, int mont, uint32_t FB, uint32_t NBC,
-                                                  uint32_t nblk, uint32_t* __restrict__ counts) {
+                                                  uint32_t n, int c, int wb, int we, int mont, uint32_t FB,
+                                                  uint32_t NBC, uint32_t nblk, uint32_t* __restrict__ counts) {
     extern __shared__ uint32_t hist[];
-    const uint32_t bins = (uint32_t)W * NBC;
+    const uint32_t bins = (uint32_t)(we - wb) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
@@ -88,8 +88,9 @@ __global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ 
         if (inf != nullptr && inf[i]) continue;
         fe<Fr> s = load_scalar<Fr>(sc, i);
         if (mont) s = fe_from_mont<Fr>(s);
-        for_each_digit<Fr>(s, c, W, [&](int w, int32_t d) {
-            if (d != 0) atomicAdd(&hist[(uint32_t)w * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
+        for_each_digit<Fr>(s, c, we, [&](int w, int32_t d) {
+            if (d != 0 && w >= wb)
+                atomicAdd(&hist[(uint32_t)(w - wb) * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
         });
     }
     __syncthreads();
@@ -98,11 +99,11 @@ __global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ 
 
 template <class Fr>
 __global__ void __launch_bounds__(256) k_sort_coarse(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
-                                                    uint32_t n, int c, int W, int mont, uint32_t FB, uint32_t NBC,
-                                                    uint32_t nblk, const uint32_t* __restrict__ base,
+                                                    uint32_t n, int c, int wb, int we, int mont, uint32_t FB,
+                                                    uint32_t NBC, uint32_t nblk, const uint32_t* __restrict__ base,
                                                     uint64_t* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
-    const uint32_t bins = (uint32_t)W * NBC;
+    const uint32_t bins = (uint32_t)(we - wb) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + blockIdx.x];
     __syncthreads();
     const uint32_t fmask = (1u << FB) - 1;
@@ -111,10 +112,10 @@ __global__ void __launch_bounds__(256) k_sort_coarse(const uint32_t* __restrict_
         if (inf != nullptr && inf[i]) continue;
         fe<Fr> s = load_scalar<Fr>(sc, i);
         if (mont) s = fe_from_mont<Fr>(s);
-        for_each_digit<Fr>(s, c, W, [&](int w, int32_t d) {
-            if (d != 0) {
+        for_each_digit<Fr>(s, c, we, [&](int w, int32_t d) {
+            if (d != 0 && w >= wb) {
                 uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-                uint32_t pos = atomicAdd(&cur[(uint32_t)w * NBC + (b >> FB)], 1u);
+                uint32_t pos = atomicAdd(&cur[(uint32_t)(w - wb) * NBC + (b >> FB)], 1u);
                 tmp[pos] = ((uint64_t)(b & fmask) << 32) | i | (d < 0 ? 0x80000000u : 0u);
             }
         });
@@ -230,7 +231,7 @@ static int choose_window(size_t n) {
 
 template <class C, class Fr>
 static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc, size_t n,
-                     int mont, uint32_t* out_acc) {
+                     int mont, int part, int parts, uint32_t* out_acc) {
     using Acc = typename C::Acc;
     using Aff = typename C::Aff;
     if (n == 0) {
@@ -239,8 +240,18 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         return VC_OK;
     }
     if (n >= 0x7fffffffu) return VC_E_INVALID;
+    if (parts < 1 || part < 0 || part >= parts) return VC_E_INVALID;
     const int c = choose_window(n);
-    const int W = (Fr::BITS + 1 + c - 1) / c;  // one spare bit absorbs the final carry
+    const int Wfull = (Fr::BITS + 1 + c - 1) / c;  // one spare bit absorbs the final carry
+    // window slice [wb, we) of this call (parts > 1: the MSM split by windows across GPUs;
+    // the slices' results add up to the whole MSM)
+    const int wb = part * Wfull / parts, we = (part + 1) * Wfull / parts;
+    const int W = we - wb;
+    if (W == 0) {
+        Acc z = C::zero();
+        memcpy(out_acc, &z, sizeof(Acc));
+        return VC_OK;
+    }
     const uint32_t NB = 1u << (c - 1);
     const uint32_t NBtot = NB * W;
     const uint32_t M = 64;  // sorted entries per accumulate thread (64: 2 rounds of 2048 waves at 2^20 x 16)
@@ -286,7 +297,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     uint32_t* owner_b = ctx->ws[WS_OWNER_B].as<uint32_t>();
     Acc* seg = ctx->ws[WS_SEG].as<Acc>();
     Acc* rs = ctx->ws[WS_TREE].as<Acc>();
-    Acc* part = ctx->ws[WS_WIN].as<Acc>();
+    Acc* bsum_part = ctx->ws[WS_WIN].as<Acc>();
     Acc* tail = ctx->ws[WS_TAIL].as<Acc>();
 
     const Aff* bases = t->bases.as<Aff>() + offset;
@@ -295,8 +306,8 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     const size_t lds = (size_t)bins * 4;
     if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
     VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
-    VK_LAUNCH(ctx, "msm_sort_hist", (k_sort_hist<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, W, mont, FB, NBC,
-              nblk, counts);
+    VK_LAUNCH(ctx, "msm_sort_hist", (k_sort_hist<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, wb, we, mont, FB,
+              NBC, nblk, counts);
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
     VK_TRY(ctx->ws[WS_SCAN_TMP].ensure(tmp_bytes));
@@ -306,25 +317,26 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
         if (ctx->timing) ctx->timer_end("msm_scan", ev);
     }
-    VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, W, mont, FB,
-              NBC, nblk, base, tmp);
+    VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, wb, we, mont,
+              FB, NBC, nblk, base, tmp);
     VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= n*W
     VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, sorted, offsets,
               NBtot, M, buckets, carry, through, owner, owner_b);
     VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b));
-    VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, part, tail));
+    VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
     std::vector<Acc> ht((size_t)W * (J + 1));
     VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));
     // MSM = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host, 64-bit limbs)
     int lg_seg = 0;
     while ((1u << lg_seg) < Lseg) lg_seg++;
-    const int maxpos = c * (W - 1) + lg_seg + (int)J;
+    const int maxpos = c * (we - 1) + lg_seg + (int)J;
     std::vector<std::vector<int>> at(maxpos + 1);
     for (int w = 0; w < W; w++) {
-        at[c * w].push_back(w * (int)(J + 1) + (int)J);
-        for (uint32_t j = 0; j < J; j++) at[c * w + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
+        const int p0 = c * (wb + w);  // absolute bit position of window wb + w
+        at[p0].push_back(w * (int)(J + 1) + (int)J);
+        for (uint32_t j = 0; j < J; j++) at[p0 + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
     }
     Acc res = C::zero();
     for (int pos = maxpos; pos >= 0; pos--) {
@@ -335,13 +347,22 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     return VC_OK;
 }
 
+int msm_windows(int curve, size_t n, int* c, int* W) {
+    int bits = curve == VC_CURVE_BN254 ? BN254Fr::BITS : curve == VC_CURVE_BLS12_381 ? BLS381Fr::BITS : BandFr::BITS;
+    *c = choose_window(n);
+    *W = (bits + 1 + *c - 1) / *c;
+    return VC_OK;
+}
+
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
-            uint32_t* out_acc) {
+            uint32_t* out_acc, int part, int parts) {
     const uint32_t* sc = reinterpret_cast<const uint32_t*>(d_scalars);
     switch (t->curve) {
-        case VC_CURVE_BN254: return msm_run_t<BN254G1, BN254Fr>(ctx, t, offset, sc, n, mont, out_acc);
-        case VC_CURVE_BLS12_381: return msm_run_t<BLS381G1, BLS381Fr>(ctx, t, offset, sc, n, mont, out_acc);
-        case VC_CURVE_BANDERSNATCH: return msm_run_t<Bandersnatch, BandFr>(ctx, t, offset, sc, n, mont, out_acc);
+        case VC_CURVE_BN254: return msm_run_t<BN254G1, BN254Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
+        case VC_CURVE_BLS12_381:
+            return msm_run_t<BLS381G1, BLS381Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
+        case VC_CURVE_BANDERSNATCH:
+            return msm_run_t<Bandersnatch, BandFr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
     }
     return VC_E_INVALID;
 }

@@ -1,0 +1,61 @@
+"""Summarise a tools_profile.sh run: kernel durations (trace pass) + HBM bytes per launch
+from the FETCH_SIZE / WRITE_SIZE PMC passes, with the gfx950 correction of
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts 64 B per 128-B read request, so it is
+doubled; WRITE_SIZE is taken as is.  usage: prof_summary.py <prof dir> <out json>"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    name = re.sub(r"\(.*$", "", name)          # drop the argument list
+    name = name.replace("void ", "")
+    return name
+
+
+def main(d, out):
+    stats = {}
+    with open(f"{d}/trace/run_kernel_stats.csv") as f:
+        for r in csv.DictReader(f):
+            stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                      "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+    pmc = defaultdict(lambda: defaultdict(list))
+    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        try:
+            with open(f"{d}/{sub}/run_counter_collection.csv") as f:
+                for r in csv.DictReader(f):
+                    if r["Counter_Name"] == ctr:
+                        pmc[short(r["Kernel_Name"])][ctr].append(float(r["Counter_Value"]))
+        except FileNotFoundError:
+            pass
+    res = {}
+    for k, v in stats.items():
+        e = dict(v)
+        p = pmc.get(k, {})
+        if p.get("FETCH_SIZE"):
+            e["FETCH_SIZE_KB_per_launch_raw"] = sum(p["FETCH_SIZE"]) / len(p["FETCH_SIZE"])
+        if p.get("WRITE_SIZE"):
+            e["WRITE_SIZE_KB_per_launch"] = sum(p["WRITE_SIZE"]) / len(p["WRITE_SIZE"])
+        if "FETCH_SIZE_KB_per_launch_raw" in e and "WRITE_SIZE_KB_per_launch" in e:
+            e["hbm_bytes_per_launch"] = 1024.0 * (2.0 * e["FETCH_SIZE_KB_per_launch_raw"]
+                                                  + e["WRITE_SIZE_KB_per_launch"])
+        res[k] = e
+    res = dict(sorted(res.items(), key=lambda kv: -kv[1]["total_ns"]))
+    bench, config = None, {}
+    try:
+        lines = [ln for ln in open(f"{d}/bench_trace.json") if ln.startswith("{")]
+        bench = json.loads(lines[-1])
+        npts = bench["config"]["n_points"]
+        config = {"log_n": npts.bit_length() - 1, "curve": bench["config"]["curve"], "n_gpus": bench["n_gpus"]}
+    except (OSError, IndexError, KeyError, ValueError):
+        pass
+    with open(out, "w") as f:
+        json.dump({"config": config, "bench_under_rocprof": bench, "note": "avg_ns from the kernel-trace pass; FETCH/WRITE from separate --pmc passes of the "
+                           "same command; hbm_bytes_per_launch = 1024*(2*FETCH_KB + WRITE_KB) (gfx950 FETCH "
+                           "correction, MI355X_MICROARCH.md HBM section)", "kernels": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

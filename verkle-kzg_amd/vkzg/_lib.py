@@ -34,6 +34,9 @@ SIGNATURES = {
     "vc_msm_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
     "vc_point_words": (c_int, [c_int]),
     "vc_msm_device_partial": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P]),
+    "vc_device_mad_rate": (c_int, [c_void_p, P]),
+    "vc_msm_windows": (c_int, [c_int, c_size_t, P, P]),
+    "vc_msm_device_window_part": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, c_int, c_int, P]),
     "vc_partials_sum": (c_int, [c_int, P, c_size_t, P, P]),
     "vc_msm_batch": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
     "vc_msm_batch_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),

@@ -1,12 +1,17 @@
-"""Multi-GPU sharding of one MSM: one process per GPU, point-range shards,
-one exchange step.
+"""Multi-GPU sharding of one MSM: one process per GPU, one exchange step.
 
-Each rank runs the Pippenger engine on its contiguous slice [lo, hi) of the bases and
-scalars (it streams only n/world of them from its own HBM), producing an un-normalised
-projective partial sum (vc_msm_device_partial). The partials are all-gathered
-(torch.distributed: RCCL over xGMI with the "nccl" backend, gloo on CPU in tests) and
-added on the host (vc_partials_sum). The message is world x 128-192 bytes: latency-bound,
-nowhere near the xGMI link rate, so a single all-gather is the right collective.
+Two splits, both ending in one all-gather of un-normalised projective partials
+(torch.distributed: RCCL over xGMI with the "nccl" backend, gloo on CPU in tests) that are
+added on the host (vc_partials_sum); the message is world x 128-192 bytes, latency-bound,
+so a single all-gather is the right collective:
+
+  split="windows" (default): rank k computes Pippenger windows [kW/G, (k+1)W/G) of ALL n
+      terms (vc_msm_device_window_part). Accumulation work is n*W/G per rank as with a point
+      split, but the bucket reduction -- W * 2^(c-1) buckets, independent of n -- is divided
+      by G too. Every rank streams all n bases (resident on each GPU; 100 MB at 2^20); the
+      MSM is VALU-bound, not HBM-bound, so re-reading them is free.
+  split="points": rank k takes the contiguous slice [kn/G, (k+1)n/G) of bases and scalars
+      (vc_msm_device_partial) and runs a full Pippenger on it.
 """
 import numpy as np
 
@@ -57,11 +62,51 @@ def all_gather_partials(part_words, world, device=None):
     return torch.stack(outs).cpu().numpy().view(np.uint32)
 
 
-def msm_sharded(engine, table, d_scalars_ptr, n, rank, world, device):
-    """Whole-MSM result on every rank: local shard partial -> all-gather -> host sum.
-    d_scalars_ptr points at this rank's shard scalars (4 u64 each) in device memory."""
-    lo, hi = shard_range(n, rank, world)
-    part = engine.msm_device_partial(table, d_scalars_ptr, hi - lo, offset=lo)
+def window_count(curve, n):
+    """(window bits c, window count W) the engine picks for an n-term MSM (vc_msm_windows)."""
+    import ctypes
+    from ._lib import check, lib
+    from .engine import CURVE_IDS
+    c, w = ctypes.c_int(0), ctypes.c_int(0)
+    check(lib().vc_msm_windows(CURVE_IDS[curve], n, ctypes.byref(c), ctypes.byref(w)), "vc_msm_windows")
+    return c.value, w.value
+
+
+def all_gather_commitments(xy, inf, total, world):
+    """Batched commits sharded by contiguous batch slices (shard_range): all-gather every
+    rank's (xy, inf) slice so each rank holds all `total` commitments in batch order.
+    xy: (b_k, 2*NL) int64 tensor, inf: (b_k,) uint8 tensor on this rank's device (or CPU
+    with gloo). Slices differ in length by at most one, so they are padded to the largest."""
+    import torch
+    import torch.distributed as dist
+    bmax = (total + world - 1) // world
+    pad_xy = torch.zeros((bmax, xy.shape[1]), dtype=xy.dtype, device=xy.device)
+    pad_inf = torch.zeros((bmax,), dtype=inf.dtype, device=inf.device)
+    pad_xy[:xy.shape[0]] = xy
+    pad_inf[:inf.shape[0]] = inf
+    outs_xy = [torch.zeros_like(pad_xy) for _ in range(world)]
+    outs_inf = [torch.zeros_like(pad_inf) for _ in range(world)]
+    dist.all_gather(outs_xy, pad_xy)
+    dist.all_gather(outs_inf, pad_inf)
+    parts_xy, parts_inf = [], []
+    for r in range(world):
+        lo, hi = shard_range(total, r, world)
+        parts_xy.append(outs_xy[r][:hi - lo])
+        parts_inf.append(outs_inf[r][:hi - lo])
+    return torch.cat(parts_xy), torch.cat(parts_inf)
+
+
+def msm_sharded(engine, table, d_scalars_ptr, n, rank, world, device, split="windows"):
+    """Whole-MSM result on every rank: local partial -> all-gather -> host sum.
+    split="windows": d_scalars_ptr points at ALL n scalars (4 u64 each) in device memory;
+    split="points": at this rank's shard [lo, hi) only."""
+    if split == "windows":
+        part = engine.msm_device_window_part(table, d_scalars_ptr, n, rank, world)
+    elif split == "points":
+        lo, hi = shard_range(n, rank, world)
+        part = engine.msm_device_partial(table, d_scalars_ptr, hi - lo, offset=lo)
+    else:
+        raise ValueError(f"unknown split {split!r}")
     parts = all_gather_partials(part, world, device) if world > 1 else part[None, :]
     return partials_sum(engine.curve, parts)
 

@@ -179,6 +179,12 @@ class Engine:
                                   1 if mont else 0, _ptr(out), _ptr(oinf)), "vc_msm_device")
         return out, int(oinf[0])
 
+    def device_mad_rate(self):
+        """Measured v_mad_u64_u32 throughput of this device (tera-ops/s)."""
+        v = ctypes.c_double(0)
+        check(lib().vc_device_mad_rate(self.h, ctypes.byref(v)), "vc_device_mad_rate")
+        return v.value
+
     def point_words(self):
         return lib().vc_point_words(self.cid)
 
@@ -186,6 +192,14 @@ class Engine:
         acc = np.zeros(self.point_words(), dtype=np.uint32)
         check(lib().vc_msm_device_partial(self.h, table, offset, ctypes.c_void_p(d_scalars_ptr), n,
                                           1 if mont else 0, _ptr(acc)), "vc_msm_device_partial")
+        return acc
+
+    def msm_device_window_part(self, table, d_scalars_ptr, n, part, parts, offset=0, mont=False):
+        """Accumulator of Pippenger windows [part*W/parts, (part+1)*W/parts) of the whole MSM."""
+        acc = np.zeros(self.point_words(), dtype=np.uint32)
+        check(lib().vc_msm_device_window_part(self.h, table, offset, ctypes.c_void_p(d_scalars_ptr), n,
+                                              1 if mont else 0, part, parts, _ptr(acc)),
+              "vc_msm_device_window_part")
         return acc
 
     def partials_sum(self, accs):
