@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--commit-window", type=int, default=16)
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kzg", action="store_true", help="skip the KZG commit+open line (configs[3])")
+    ap.add_argument("--kzg-log-d", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
     return ap.parse_args()
 
@@ -82,6 +84,68 @@ def cpu_baseline(curve, n_full, sample):
             "sample": f"{sample} of {n_full} terms of the naive {curve} MSM (reference utils.rs:16-19 "
                       f"restated in C, oracle/c/ref_curve.c), 1 thread, {dt:.2f} s, extrapolated linearly",
             "ms_per_msm": per_msm_s * 1e3, "host_cpus": os.cpu_count()}
+
+
+def kzg_line(a, rank, world, local, dev, stream):
+    """configs[3]: KZG commit + open at d = 2^kzg_log_d on BLS12-381 (the north_star's KZG
+    curve): commit = MSM over the Lagrange SRS, open = quotient + MSM (kzg/mod.rs:126-154),
+    at an in-domain index m = d/3 and at an out-of-domain point; both MSMs window-split
+    across ranks. The SRS (L_j = l_j(100) G, Appendix A.7) is built on the GPU once, untimed."""
+    import ctypes
+    from vkzg._lib import check, lib
+    d = 1 << a.kzg_log_d
+    keng = vkzg.Engine("bls12_381", local)
+    keng.set_stream(stream.cuda_stream)
+    secret = vkzg.ints_to_limbs([100])[0].copy()
+    tid, size = ctypes.c_int(), ctypes.c_size_t()
+    t0 = time.perf_counter()
+    check(lib().vc_kzg_setup(keng.h, d, ctypes.c_void_p(secret.ctypes.data), ctypes.byref(tid), ctypes.byref(size)),
+          "vc_kzg_setup")
+    setup_s = time.perf_counter() - t0
+    tid = tid.value
+    ev = vkzg.random_scalars("bls12_381", d, np.random.default_rng(44))
+    d_ev = torch.from_numpy(ev.view(np.int64).copy()).to(dev)
+    g = dev if world > 1 else None
+    pts = {"in_domain": d // 3, "outside": d + 987654321}
+
+    def step(point):
+        com = vdist.msm_sharded(keng, tid, d_ev.data_ptr(), d, rank, world, g, split="windows")
+        prf = vdist.kzg_open_sharded(keng, tid, d, d_ev.data_ptr(), d, point, rank, world, g)
+        return com, prf
+
+    res = {}
+    for name, point in pts.items():
+        step(point)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        keng.enable_timing(True)
+        keng.reset_timing()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step(point)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        dt = (time.perf_counter() - t0) / reps
+        if world > 1:
+            tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        keng.enable_timing(False)
+        qk = {}
+        for k in ("kzg_den", "batch_inv", "kzg_q_in", "kzg_q_out", "kzg_bary", "powers", "to_mont"):
+            ms, cnt = keng.kernel_time(k)
+            if cnt:
+                qk[k] = round(ms / cnt, 4)
+        res[name] = {"ms_per_commit_open": dt * 1e3, "quotient_kernels_ms": qk}
+    keng.close()
+    fused_bytes = d * (96 + 32) + 2 * 96  # SURVEY 8(d) C4 fused minimum
+    return {"workload": f"KZG commit + open, d = 2^{a.kzg_log_d}, BLS12-381 (configs[3]), MSMs window-split "
+                        f"over {world} rank(s)", "srs_setup_s": setup_s, **res,
+            "algorithmic_bytes_per_unit": fused_bytes,
+            "achieved_GBps_in_domain": fused_bytes / (res["in_domain"]["ms_per_commit_open"] * 1e-3) / 1e9}
 
 
 def main():
@@ -238,6 +302,9 @@ def main():
                            * (1 << (a.commit_window - 1)) * 96,
         }
         ceng.close()
+
+    if not a.no_kzg:
+        out["kzg"] = kzg_line(a, rank, world, local, dev, stream)
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(curve, n, a.cpu_sample)

@@ -85,6 +85,14 @@ int vc_ipa_verify(vc_ctx* ctx, int table, size_t N, const uint64_t* com_xy, uint
  * reference panics there, Appendix B.4). */
 int vc_kzg_prove(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t max,
                  const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y);
+/* same with the evaluations already in device memory (canonical, 4 u64 each) */
+int vc_kzg_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
+                        const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y);
+/* multi-GPU open: the quotient (every part computes it; it is elementwise and ~10 % of the
+ * MSM) and window slice `part` of `parts` of the proof MSM as an un-normalised accumulator;
+ * the parts' accumulators sum (vc_partials_sum) to the proof */
+int vc_kzg_prove_device_part(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
+                             const uint64_t* point, int part, int parts, uint32_t* out_acc, uint64_t* y);
 /* the quotient alone (a5/a6), for parity tests: q (size x 4 u64) and y */
 int vc_kzg_quotient(vc_ctx* ctx, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
                     uint64_t* q_out, uint64_t* y);

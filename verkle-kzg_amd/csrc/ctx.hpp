@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -97,6 +98,8 @@ struct vc_ctx {
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, long>> ktime;
     vk::Table scratch;  // variable-base points of verifiers (grow-only)
+    // per-domain constant tables (domain powers, 1/(w^k - 1)), keyed by field and size
+    std::map<std::string, std::unique_ptr<vk::DevBuf>> dcache;
 
     hipEvent_t get_event();
     void timer_begin(const char* name, hipEvent_t* a, hipStream_t s = nullptr);

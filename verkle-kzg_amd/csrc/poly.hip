@@ -208,17 +208,64 @@ int batch_inverse(vc_ctx* ctx, const fe<F>* d_in, fe<F>* d_out, size_t n) {
     return VC_OK;
 }
 
+// inv[i] = w^-m / (w^((i - m) mod n) - 1) = 1 / (w^i - w^m)  (i != m), from the per-domain
+// table inv1[k] = 1/(w^k - 1): the in-domain quotient needs no inversion per open
+template <class F>
+__global__ void k_inv_shift(const fe<F>* __restrict__ inv1, size_t n, size_t m, fe<F> wminv, fe<F>* __restrict__ inv) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    inv[i] = i == m ? fe_zero<F>() : fe_mul<F>(wminv, inv1[(i + n - m) & (n - 1)]);
+}
+
+template <class F>
+static std::string dkey(const char* tag, size_t n) {
+    return std::string(tag) + ":" + std::to_string(F::BITS) + ":" + std::to_string(F::N) + ":" + std::to_string(n);
+}
+
+// domain powers w^i, i < n (cached per ctx: PrecomputedLagrange keeps them too, precompute.rs:25-58)
+template <class F>
+static int cached_powers(vc_ctx* ctx, const fe<F>& omega, size_t n, fe<F>** out) {
+    auto& slot = ctx->dcache[dkey<F>("pw", n)];
+    if (!slot) {
+        auto b = std::make_unique<DevBuf>();
+        VK_TRY(b->ensure(n * sizeof(fe<F>)));
+        VK_TRY(domain_powers<F>(ctx, omega, n, b->as<fe<F>>()));
+        slot = std::move(b);
+    }
+    *out = reinterpret_cast<fe<F>*>(slot->p);
+    return VC_OK;
+}
+
+// inv1[k] = 1/(w^k - 1) for 0 < k < n (inv1[0] unused), cached per ctx
+template <class F>
+static int cached_inv1(vc_ctx* ctx, const fe<F>* pw, size_t n, fe<F>** out) {
+    auto& slot = ctx->dcache[dkey<F>("inv1", n)];
+    if (!slot) {
+        auto b = std::make_unique<DevBuf>();
+        DevBuf den;
+        VK_TRY(b->ensure(n * sizeof(fe<F>)));
+        VK_TRY(den.ensure(n * sizeof(fe<F>)));
+        VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pw, n, fe_one<F>(), 0LL, den.as<fe<F>>());
+        VK_TRY(batch_inverse<F>(ctx, den.as<fe<F>>(), b->as<fe<F>>(), n));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // den is freed on return
+        slot = std::move(b);
+    }
+    *out = reinterpret_cast<fe<F>*>(slot->p);
+    return VC_OK;
+}
+
 // q and y for KZG prove_point (device, Montgomery). point given in Montgomery form.
 template <class F>
 int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
                      fe<F>* d_q, fe<F>* y_out, DevBuf& pw, DevBuf& tmp, DevBuf& part) {
     hipStream_t st = ctx->stream;
-    VK_TRY(pw.ensure(n * sizeof(fe<F>)));
+    (void)pw;
     VK_TRY(tmp.ensure(n * sizeof(fe<F>)));
     fe<F>* den = d_q;  // denominators staged in the output buffer, inverses in tmp
     size_t nblk = (n + 2047) / 2048;
     VK_TRY(part.ensure(nblk * sizeof(fe<F>)));
-    VK_TRY(domain_powers<F>(ctx, omega, n, pw.as<fe<F>>()));
+    fe<F>* pwp = nullptr;
+    VK_TRY(cached_powers<F>(ctx, omega, n, &pwp));
     fe<F>* inv = tmp.as<fe<F>>();
     std::vector<fe<F>> hp(nblk);
     // prove_point: `point <= size` -> in-domain branch with index to_usize(point)
@@ -232,12 +279,14 @@ int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const 
         // y = evaluate(point): stored value, or 0 inside [max, size]
         fe<F> fm = fe_zero<F>();
         if (m < max) VK_CHECK_HIP(hipMemcpyAsync(&fm, d_f + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
-        fe<F> wm;
-        VK_CHECK_HIP(hipMemcpyAsync(&wm, pw.as<fe<F>>() + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        fe<F> wm, wminv;
+        VK_CHECK_HIP(hipMemcpyAsync(&wm, pwp + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        VK_CHECK_HIP(hipMemcpyAsync(&wminv, pwp + ((n - m) & (n - 1)), sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        fe<F>* inv1 = nullptr;
+        VK_TRY(cached_inv1<F>(ctx, pwp, n, &inv1));
         VK_CHECK_HIP(hipStreamSynchronize(st));
-        VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pw.as<fe<F>>(), n, wm, (long long)m, den);
-        VK_TRY(batch_inverse<F>(ctx, den, inv, n));
-        VK_LAUNCH(ctx, "kzg_q_in", (k_q_in<F>), nblk, 256, 0, d_f, max, inv, pw.as<fe<F>>(), n, m, fm, d_q,
+        VK_LAUNCH(ctx, "kzg_inv_shift", (k_inv_shift<F>), (n + 255) / 256, 256, 0, inv1, n, m, wminv, inv);
+        VK_LAUNCH(ctx, "kzg_q_in", (k_q_in<F>), nblk, 256, 0, d_f, max, inv, pwp, n, m, fm, d_q,
                   part.as<fe<F>>());
         VK_CHECK_HIP(hipMemcpyAsync(hp.data(), part.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, st));
         VK_CHECK_HIP(hipStreamSynchronize(st));
@@ -249,10 +298,9 @@ int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const 
         return VC_OK;
     }
     // outside: inv_i = 1/(w^i - z); y = -t * sum f_i w^i inv_i, t = (z^n - 1)/n
-    VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pw.as<fe<F>>(), n, point, (long long)-1, den);
+    VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pwp, n, point, (long long)-1, den);
     VK_TRY(batch_inverse<F>(ctx, den, inv, n));
-    VK_LAUNCH(ctx, "kzg_bary", (k_bary_partial<F>), nblk, 256, 0, d_f, max, pw.as<fe<F>>(), inv, n,
-              part.as<fe<F>>());
+    VK_LAUNCH(ctx, "kzg_bary", (k_bary_partial<F>), nblk, 256, 0, d_f, max, pwp, inv, n, part.as<fe<F>>());
     VK_CHECK_HIP(hipMemcpyAsync(hp.data(), part.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));
     fe<F> zn = fe_one<F>(), b = point;

@@ -304,28 +304,37 @@ uint32_t fr_generator<BN254Fr>() { return 5; }
 template <>
 uint32_t fr_generator<BLS381Fr>() { return 7; }
 
+// evals: host (d_evals == false) or device canonical scalars; out_acc != nullptr returns the
+// un-normalised proof accumulator of window slice `part` of `parts` (multi-GPU) instead of
+// the affine proof
 template <class C_, class Fr_>
 static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
-                       uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y_out, uint64_t* q_out) {
+                       uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y_out, uint64_t* q_out, bool d_evals = false,
+                       int part = 0, int parts = 1, uint32_t* out_acc = nullptr) {
     if (!is_pow2(size) || max > size) return VC_E_INVALID;
     if (t && t->n < size) return VC_E_RANGE;
-    DevBuf d_f, d_q, pw, tmp, part;
+    DevBuf d_f, d_q, pw, tmp, part_buf;
     VK_TRY(d_f.ensure(size * 32));
     VK_TRY(d_q.ensure(size * 32));
     VK_TRY(tmp.ensure(size * 32));
-    if (max > 0) VK_CHECK_HIP(hipMemcpyAsync(tmp.p, evals, max * 32, hipMemcpyHostToDevice, ctx->stream));
-    VK_TRY(canon_to_mont_dev<Fr_>(ctx, tmp.p, size, max, d_f.as<fe<Fr_>>()));
+    const void* ev_dev = tmp.p;
+    if (d_evals) ev_dev = evals;
+    else if (max > 0) VK_CHECK_HIP(hipMemcpyAsync(tmp.p, evals, max * 32, hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(canon_to_mont_dev<Fr_>(ctx, ev_dev, size, max, d_f.as<fe<Fr_>>()));
     fe<Fr_> pm = canon_to_mont<Fr_>(point);
     fe<Fr_> omega = group_gen_t<Fr_>(size, fr_generator<Fr_>());
     fe<Fr_> y;
-    VK_TRY(kzg_quotient_dev<Fr_>(ctx, size, d_f.as<fe<Fr_>>(), max, pm, omega, d_q.as<fe<Fr_>>(), &y, pw, tmp, part));
+    VK_TRY(kzg_quotient_dev<Fr_>(ctx, size, d_f.as<fe<Fr_>>(), max, pm, omega, d_q.as<fe<Fr_>>(), &y, pw, tmp,
+                                 part_buf));
     mont_to_canon<Fr_>(y, y_out);
     if (q_out) {
         VK_TRY(mont_to_canon_dev<Fr_>(ctx, d_q.as<fe<Fr_>>(), size, tmp.p));
         VK_CHECK_HIP(hipMemcpyAsync(q_out, tmp.p, size * 32, hipMemcpyDeviceToHost, ctx->stream));
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     }
-    if (t) {
+    if (t && out_acc) {
+        VK_TRY(msm_run(ctx, t, 0, d_q.p, size, 1, out_acc, part, parts));
+    } else if (t) {
         std::vector<uint32_t> acc(point_words(ctx->curve));
         VK_TRY(msm_run(ctx, t, 0, d_q.p, size, 1, acc.data()));
         VK_TRY(acc_to_affine(ctx->curve, acc.data(), proof_xy, proof_inf));
@@ -552,6 +561,37 @@ int vc_kzg_prove(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, siz
         return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, size, evals, max, point, proof_xy, proof_inf, y, nullptr);
     if (ctx->curve == VC_CURVE_BLS12_381)
         return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, evals, max, point, proof_xy, proof_inf, y, nullptr);
+    return VC_E_INVALID;
+}
+
+int vc_kzg_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
+                        const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y) {
+    if (!ctx || (max && !d_evals) || !point || !proof_xy || !proof_inf || !y) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    const uint64_t* ev = reinterpret_cast<const uint64_t*>(d_evals);
+    if (ctx->curve == VC_CURVE_BN254)
+        return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, size, ev, max, point, proof_xy, proof_inf, y, nullptr, true);
+    if (ctx->curve == VC_CURVE_BLS12_381)
+        return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, ev, max, point, proof_xy, proof_inf, y, nullptr, true);
+    return VC_E_INVALID;
+}
+
+int vc_kzg_prove_device_part(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
+                             const uint64_t* point, int part, int parts, uint32_t* out_acc, uint64_t* y) {
+    if (!ctx || (max && !d_evals) || !point || !out_acc || !y || parts < 1 || part < 0 || part >= parts)
+        return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    const uint64_t* ev = reinterpret_cast<const uint64_t*>(d_evals);
+    if (ctx->curve == VC_CURVE_BN254)
+        return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, size, ev, max, point, nullptr, nullptr, y, nullptr, true, part,
+                                             parts, out_acc);
+    if (ctx->curve == VC_CURVE_BLS12_381)
+        return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, ev, max, point, nullptr, nullptr, y, nullptr, true,
+                                               part, parts, out_acc);
     return VC_E_INVALID;
 }
 

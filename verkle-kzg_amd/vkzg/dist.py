@@ -115,3 +115,22 @@ def partials_sum(curve, parts):
     """Host-side sum of projective partials -> ((2*NL,) uint64 canonical affine, inf)."""
     from .engine import partials_sum as _ps
     return _ps(curve, parts)
+
+
+def kzg_open_sharded(engine, table, size, d_evals_ptr, max_items, point, rank, world, device):
+    """KZG open (kzg/mod.rs:136-154) across ranks: every rank computes the
+    quotient (elementwise, ~10 % of the open) and window slice `rank` of the proof MSM
+    (vc_kzg_prove_device_part); one all-gather of partials, host sum.
+    Returns ((2*NL,) uint64 canonical affine proof, inf, y limbs)."""
+    import ctypes
+    from ._lib import check, lib
+    pt = np.array([(int(point) >> (64 * j)) & 0xFFFFFFFFFFFFFFFF for j in range(4)], dtype=np.uint64)
+    acc = np.zeros(engine.point_words(), dtype=np.uint32)
+    y = np.zeros(4, dtype=np.uint64)
+    check(lib().vc_kzg_prove_device_part(engine.h, table, size, ctypes.c_void_p(d_evals_ptr), max_items,
+                                         ctypes.c_void_p(pt.ctypes.data), rank, world,
+                                         ctypes.c_void_p(acc.ctypes.data), ctypes.c_void_p(y.ctypes.data)),
+          "vc_kzg_prove_device_part")
+    parts = all_gather_partials(acc, world, device) if world > 1 else acc[None, :]
+    xy, inf = partials_sum(engine.curve, parts)
+    return xy, inf, y
