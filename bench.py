@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kzg", action="store_true", help="skip the KZG commit+open line (configs[3])")
     ap.add_argument("--kzg-log-d", type=int, default=20)
+    ap.add_argument("--no-mp", action="store_true", help="skip the IPA multiproof line (configs[4])")
+    ap.add_argument("--mp-log-q", type=int, default=16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
     return ap.parse_args()
 
@@ -146,6 +148,77 @@ def kzg_line(a, rank, world, local, dev, stream):
                         f"over {world} rank(s)", "srs_setup_s": setup_s, **res,
             "algorithmic_bytes_per_unit": fused_bytes,
             "achieved_GBps_in_domain": fused_bytes / (res["in_domain"]["ms_per_commit_open"] * 1e-3) / 1e9}
+
+
+def mp_line(a, rank, world, local, dev, stream):
+    """configs[4]: IPA multiproof (multiproof.rs:99-176) over Q = 2^mp_log_q width-256 queries
+    on BN254 (the reference's curve), the query set sharded over the ranks (vkzg.dist
+    .multiproof_prove_sharded: host transcript on every rank, per-point sums of the local
+    slice on the GPU, one all-gather of the 256 x 256 sums, finish on every rank). Inputs:
+    random evaluations (< 2^252), their commitments (batched fixed-base commits, untimed),
+    uniform points z in [0, 256), y = f(z)."""
+    from vkzg import scheme
+    N, Q = 256, 1 << a.mp_log_q
+    meng = vkzg.Engine("bn254", local)
+    meng.set_stream(stream.cuda_stream)
+    crs = scheme.ipa_crs(N + 1, max_=512)
+    ipa = scheme.IPA(meng, N, crs)
+    rng = np.random.default_rng(77)
+    lo, hi = vdist.shard_range(Q, rank, world)
+    data = rng.integers(0, 1 << 63, size=(Q * N, 4), dtype=np.uint64)
+    data[:, 3] &= np.uint64((1 << 60) - 1)          # < 2^252 < r
+    z = rng.integers(0, N, size=Q, dtype=np.uint64)
+    y = data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)].copy()
+    # commitments of all queries (every rank needs all of them for the transcript), untimed
+    d_all = torch.from_numpy(data.view(np.int64)).to(dev)
+    cxy_d = torch.zeros((Q, 8), dtype=torch.int64, device=dev)
+    cinf_d = torch.zeros(Q, dtype=torch.uint8, device=dev)
+    meng.msm_batch_device(ipa.table, N, d_all.data_ptr(), Q, cxy_d.data_ptr(), cinf_d.data_ptr())
+    torch.cuda.synchronize(dev)
+    cxy = cxy_d.cpu().numpy().view(np.uint64).copy()
+    cinf = cinf_d.cpu().numpy().copy()
+    d_slice = d_all[lo * N:hi * N]
+    g = dev if world > 1 else None
+
+    def step():
+        return vdist.multiproof_prove_sharded(ipa, cxy, cinf, z, y, d_slice.data_ptr(), rank, world, g)
+
+    step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    meng.enable_timing(True)
+    meng.reset_timing()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        mp = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / reps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kms = {}
+    for k in ("mp_rpow", "mp_chunk", "mp_chunk_reduce", "mp_sum_parts", "mp_quot", "fb_commit"):
+        ms, cnt = meng.kernel_time(k)
+        if cnt:
+            kms[k] = round(ms / cnt, 4)
+    meng.enable_timing(False)
+    # host transcript alone (the serial part every rank repeats)
+    t0 = time.perf_counter()
+    tr, _, _ = scheme.multiproof_begin(N, cxy, cinf, z, y)
+    t_begin = time.perf_counter() - t0
+    from vkzg._lib import lib
+    lib().vc_transcript_free(tr)
+    meng.close()
+    alg = Q * N * 32 + Q * 64 + Q * 40  # SURVEY 8(d) C5
+    return {"workload": f"IPA multiproof, Q = 2^{a.mp_log_q} width-256 queries, BN254 (configs[4]), query set "
+                        f"split over {world} rank(s)", "ms_per_multiproof": dt * 1e3,
+            "host_transcript_ms": t_begin * 1e3, "kernel_ms": kms, "algorithmic_bytes_per_unit": alg,
+            "achieved_GBps": alg / dt / 1e9, "d_inf": mp["d"] is None}
 
 
 def main():
@@ -305,6 +378,9 @@ def main():
 
     if not a.no_kzg:
         out["kzg"] = kzg_line(a, rank, world, local, dev, stream)
+
+    if not a.no_mp:
+        out["multiproof"] = mp_line(a, rank, world, local, dev, stream)
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(curve, n, a.cpu_sample)

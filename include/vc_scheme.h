@@ -105,6 +105,22 @@ int vc_multiproof_prove(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, 
                         const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                         const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proof,
                         uint64_t* kzg_proof_xy, uint8_t* kzg_proof_inf, uint64_t* kzg_y);
+/* The same prover in three phases, so the Q x N field phase shards over GPUs with one
+ * exchange. vc_multiproof_prove == begin + accumulate(all Q) + finish(G=1).
+ * phase 1 (host, every rank): transcript over all (C, z, y) (:106-114), challenge r
+ *   (canonical), and the number of distinct query points `rows` (the rows of S). */
+int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                        const uint64_t* y, vc_transcript** transcript, uint64_t* r, size_t* rows);
+/* phase 2 (device, per shard): S[row][k] = sum r^i f_i[k] over queries i in [first, first + Qs)
+ *   grouped by point; d_data = that slice's Qs x N evaluations (canonical, device); d_S =
+ *   rows x N x 4 u64 (canonical, device). z = ALL Q points (it fixes the rows). */
+int vc_multiproof_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* z, size_t first, size_t Qs,
+                             const void* d_data, const uint64_t* r, void* d_S);
+/* phase 3: G shards' S matrices (device, contiguous, e.g. an all-gather) are summed; then
+ *   quotients, g, D, t, h, E and the inner proof (:129-175). Advances `transcript`. */
+int vc_multiproof_finish(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* z,
+                         const void* d_S_parts, int G, vc_transcript* transcript, uint64_t* d_xy, uint8_t* d_inf,
+                         vc_ipa_proof* ipa_proof, uint64_t* kzg_proof_xy, uint8_t* kzg_proof_inf, uint64_t* kzg_y);
 /* IPA-scheme verification (verify_multiproof :178-215 + low_level_verify_ipa) */
 int vc_multiproof_verify_ipa(vc_ctx* ctx, int table, size_t N, size_t Q, const uint64_t* com_xy,
                              const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,

@@ -112,3 +112,58 @@ def test_batched_commit_gather_gloo_world2():
     for p in procs:
         p.join(60)
     assert all(ok for _, ok in res), res
+
+
+def _mp_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd")]
+    import random
+    import torch
+    import torch.distributed as dist
+    from vkzg import dist as vdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    rng = random.Random(3)
+    N, Q = 8, 13
+    f = [[rng.randrange(R) for _ in range(N)] for _ in range(Q)]
+    z = [rng.randrange(N) for _ in range(Q)]
+    r = rng.randrange(R)
+    rows = sorted(set(z))
+
+    def sums(lo, hi):  # restatement of k_mp_chunk + k_mp_chunk_reduce: S[row][k] = sum r^i f_i[k]
+        S = [[0] * N for _ in rows]
+        for i in range(lo, hi):
+            for k in range(N):
+                S[rows.index(z[i])][k] = (S[rows.index(z[i])][k] + pow(r, i, R) * f[i][k]) % R
+        return S
+
+    lo, hi = vdist.shard_range(Q, rank, world)
+    mine = sums(lo, hi)
+    t = torch.tensor([[[(v >> (64 * j)) & 0xFFFFFFFFFFFFFFFF for j in range(4)] for v in row] for row in mine],
+                     dtype=torch.uint64).view(torch.int64)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    got = [[0] * N for _ in rows]
+    for o in outs:
+        u = o.numpy().view("uint64")
+        for a in range(len(rows)):
+            for k in range(N):
+                got[a][k] = (got[a][k] + sum(int(u[a, k, j]) << (64 * j) for j in range(4))) % R
+    q.put((rank, got == sums(0, Q)))
+    dist.destroy_process_group()
+
+
+def test_multiproof_sums_exchange_gloo_world2():
+    """the sharded multiproof's one exchange: per-rank per-point sums over query slices,
+    all-gathered and added mod r, equal the whole query set's sums."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert all(ok for _, ok in res), res

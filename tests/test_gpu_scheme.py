@@ -168,3 +168,36 @@ def test_multiproof_golden(eng, crs, name):
         claim = scheme.verify_multiproof(vc, vq, mp)
         ok = protocol.KZG(32)
         assert ok.verify_point(claim["commitment"], claim["t"], mp["proof"])
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_multiproof_sharded_phases_golden(eng, crs, G):
+    """the three-phase prover (vc_multiproof_begin / accumulate / finish) with the query set cut
+    into G shards accumulated separately (as G ranks would) == the golden multiproof."""
+    import numpy as np
+    import torch
+    from vkzg import dist as vdist
+    from vkzg import scheme
+    g = load("multiproof_32.json")["ipa"]
+    vc = scheme.IPA(eng, 32, crs[:33])
+    queries = []
+    for q in g["queries"]:
+        d = scheme.LagrangeBasis([H(x) for x in q["data"]])
+        queries.append((d, vc.commit(d), q["z"], H(q["y"])))
+    Q, data, cxy, cinf, z, y = scheme._queries(queries, 32)
+    d_data = torch.from_numpy(data.view(np.int64).copy()).cuda()
+    if G == 1:
+        mp = vdist.multiproof_prove_sharded(vc, cxy, cinf, z, y, d_data.data_ptr(), 0, 1)
+    else:
+        tr, r, rows = scheme.multiproof_begin(32, cxy, cinf, z, y)
+        parts = torch.zeros((G, rows, 32, 4), dtype=torch.int64, device="cuda")
+        for k in range(G):
+            lo, hi = vdist.shard_range(Q, k, G)
+            scheme.multiproof_accumulate(eng, 32, z, lo, hi - lo, d_data[lo * 32:].data_ptr(), r,
+                                         parts[k].data_ptr())
+        mp = scheme.multiproof_finish_ipa(vc, z, parts.data_ptr(), G, tr)
+    assert mp["d"] == P(g["d"])
+    want = g["proof"]
+    pr = mp["proof"]
+    assert pr.l == [P(x) for x in want["l"]] and pr.r == [P(x) for x in want["r"]]
+    assert pr.tip == H(want["tip"]) and pr.y == H(want["y"])

@@ -343,21 +343,6 @@ static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals
 }
 
 // ---------------------------------------------------------------- multiproof kernels
-// S[zi][k] = sum over queries i of group zi of r^i * f_i[k]
-__global__ void k_mp_accumulate(const fe<F>* __restrict__ f, const fe<F>* __restrict__ rpow,
-                                const uint32_t* __restrict__ order, const uint32_t* __restrict__ zstart, size_t N,
-                                uint32_t Z, fe<F>* __restrict__ S) {
-    uint32_t zi = blockIdx.y;
-    size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (zi >= Z || k >= N) return;
-    fe<F> acc = fe_zero<F>();
-    for (uint32_t u = zstart[zi]; u < zstart[zi + 1]; u++) {
-        uint32_t i = order[u];
-        acc = fe_add<F>(acc, fe_mul<F>(rpow[i], f[(size_t)i * N + k]));
-    }
-    S[(size_t)zi * N + k] = acc;
-}
-
 // den[zi][k] = w^k - w^z (1 at k == z)
 __global__ void k_mp_den(const fe<F>* __restrict__ pw, const uint32_t* __restrict__ zval, size_t N, uint32_t Z,
                          fe<F>* __restrict__ den) {
@@ -633,43 +618,149 @@ static std::vector<Fr> invert_domain_at(const Fr& t, size_t N) {  // utils.rs:57
     return host_batch_inv(d);
 }
 
-static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const uint64_t* data, const uint64_t* com_xy,
-                    const uint8_t* com_inf, const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
-                    vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+// ---- multiproof prover in three phases (multiproof.rs:99-176), so the Q x N field phase can
+// be sharded over GPUs with one exchange:
+//   mp_begin       host: transcript over all (C, z, y) and the challenge r        (:106-114)
+//   mp_accumulate  device, per query shard [first, first + Qs): dense per-z sums
+//                  S[z][k] = sum_{i: z_i = z} r^i f_i[k]  (canonical, N x N)      (:116-127)
+//   mp_finish      device + host: sum of the shards' S, quotients, g, D, t, h, E and the
+//                  inner proof                                                     (:129-175)
+// Grouping queries by z and summing per group first is the same field arithmetic as the
+// reference's per-group LagrangeBasis sums; rows of z with no query are zero and add nothing.
+static int mp_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                    const uint64_t* y, vc_transcript** tr_out, Fr* r_out) {
     if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
     vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y);
-    Fr r = transcript_digest(tr, "r");
-    std::vector<Fr> rpow(Q);
-    Fr cur = fe_one<F>();
-    for (size_t i = 0; i < Q; i++) {
-        rpow[i] = cur;
-        cur = fe_mul<F>(cur, r);
+    *r_out = transcript_digest(tr, "r");
+    *tr_out = tr;
+    return VC_OK;
+}
+
+// distinct query points, sorted (the rows of S)
+static std::vector<uint32_t> mp_points(size_t Q, const uint64_t* z) {
+    std::vector<uint32_t> v(Q);
+    for (size_t i = 0; i < Q; i++) v[i] = (uint32_t)z[i];
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    return v;
+}
+
+// rp[i] = r^(first + i) (Montgomery)
+__global__ void k_mp_rpow(Fr r, size_t first, size_t n, Fr* __restrict__ rp) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fr acc = fe_one<F>(), b = r;
+    size_t e = first + i;
+    while (e) {
+        if (e & 1) acc = fe_mul<F>(acc, b);
+        e >>= 1;
+        if (e) b = fe_sqr<F>(b);
     }
-    // group queries by z (counting sort)
-    std::vector<uint32_t> cnt(N + 1, 0), order(Q);
-    for (size_t i = 0; i < Q; i++) cnt[z[i] + 1]++;
-    for (size_t k = 0; k < N; k++) cnt[k + 1] += cnt[k];
+    rp[i] = acc;
+}
+
+// one block per (k block, chunk c of <= MP_CHUNK queries of one z): partial[c][k] =
+// sum over sorted positions [be[2c], be[2c+1]) of r^i f_i[k] (f canonical, r^i Montgomery ->
+// canonical products)
+constexpr uint32_t MP_CHUNK = 16;
+__global__ void __launch_bounds__(256) k_mp_chunk(const Fr* __restrict__ f, const Fr* __restrict__ rp,
+                                                 const uint32_t* __restrict__ order, const uint32_t* __restrict__ be,
+                                                 size_t N, uint32_t kblk, Fr* __restrict__ partial) {
+    const uint32_t c = blockIdx.x / kblk;  // 1-D grid: chunks can outnumber gridDim.y's 65535
+    const size_t k = (size_t)(blockIdx.x % kblk) * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    Fr acc = fe_zero<F>();
+    for (uint32_t u = be[2 * c]; u < be[2 * c + 1]; u++) {
+        const uint32_t i = order[u];
+        acc = fe_add<F>(acc, fe_mul<F>(rp[i], f[(size_t)i * N + k]));
+    }
+    partial[(size_t)c * N + k] = acc;
+}
+
+// S[row][k] = sum of the partials of the row's chunks [zc[row], zc[row+1])
+__global__ void k_mp_chunk_reduce(const Fr* __restrict__ partial, const uint32_t* __restrict__ zc, size_t N,
+                                  uint32_t kblk, Fr* __restrict__ S) {
+    const uint32_t zz = blockIdx.x / kblk;
+    const size_t k = (size_t)(blockIdx.x % kblk) * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    Fr acc = fe_zero<F>();
+    for (uint32_t c = zc[zz]; c < zc[zz + 1]; c++) acc = fe_add<F>(acc, partial[(size_t)c * N + k]);
+    S[(size_t)zz * N + k] = acc;
+}
+
+// rows of S are the distinct query points zval (sorted, over ALL queries -- every shard
+// uses the same rows so the shards' S add up); Z = zval.size()
+static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, const uint64_t* z, const Fr& r,
+                         size_t first, const std::vector<uint32_t>& zval, void* d_S) {
+    hipStream_t st = ctx->stream;
+    const size_t Z = zval.size();
+    if (Qs == 0) {
+        VK_CHECK_HIP(hipMemsetAsync(d_S, 0, Z * N * 32, st));
+        return VC_OK;
+    }
+    // row of each query: binary search in zval
+    std::vector<uint32_t> row(Qs);
+    for (size_t i = 0; i < Qs; i++) {
+        auto it = std::lower_bound(zval.begin(), zval.end(), (uint32_t)std::min<uint64_t>(z[i], 0xffffffffu));
+        if (z[i] >= N || it == zval.end() || *it != z[i]) return VC_E_DOMAIN;
+        row[i] = (uint32_t)(it - zval.begin());
+    }
+    // counting sort of the shard's queries by row, then chunks of <= MP_CHUNK queries
+    std::vector<uint32_t> cnt(Z + 1, 0), order(Qs);
+    for (size_t i = 0; i < Qs; i++) cnt[row[i] + 1]++;
+    for (size_t k = 0; k < Z; k++) cnt[k + 1] += cnt[k];
     {
         std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
-        for (size_t i = 0; i < Q; i++) order[pos[z[i]]++] = (uint32_t)i;
+        for (size_t i = 0; i < Qs; i++) order[pos[row[i]]++] = (uint32_t)i;
     }
-    std::vector<uint32_t> zval, zstart;
-    for (size_t k = 0; k < N; k++)
-        if (cnt[k + 1] > cnt[k]) {
-            zval.push_back((uint32_t)k);
-            zstart.push_back(cnt[k]);
+    // chunks of <= MP_CHUNK queries inside one row; zc[row] = first chunk of the row
+    std::vector<uint32_t> be, zc(Z + 1, 0);
+    for (size_t k = 0; k < Z; k++) {
+        zc[k] = (uint32_t)(be.size() / 2);
+        for (uint32_t u = cnt[k]; u < cnt[k + 1]; u += MP_CHUNK) {
+            be.push_back(u);
+            be.push_back(std::min<uint32_t>(u + MP_CHUNK, cnt[k + 1]));
         }
-    zstart.push_back((uint32_t)Q);
-    const uint32_t Z = (uint32_t)zval.size();
+    }
+    const uint32_t nch = (uint32_t)(be.size() / 2);
+    zc[Z] = nch;
+    DevBuf d_rp, d_order, d_be, d_zc, d_part;
+    VK_TRY(d_rp.ensure(Qs * 32));
+    VK_TRY(d_order.ensure(Qs * 4));
+    VK_TRY(d_be.ensure(be.size() * 4));
+    VK_TRY(d_zc.ensure((Z + 1) * 4));
+    VK_TRY(d_part.ensure(std::max<size_t>(nch, 1) * N * 32));
+    VK_LAUNCH(ctx, "mp_rpow", k_mp_rpow, (Qs + 255) / 256, 256, 0, r, first, Qs, d_rp.as<Fr>());
+    VK_CHECK_HIP(hipMemcpyAsync(d_order.p, order.data(), Qs * 4, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(d_be.p, be.data(), be.size() * 4, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
+    const uint32_t kblk = (uint32_t)((N + 255) / 256);
+    VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk, (size_t)nch * kblk, 256, 0, reinterpret_cast<const Fr*>(d_data),
+              d_rp.as<Fr>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
+    VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,
+              kblk, reinterpret_cast<Fr*>(d_S));
+    VK_CHECK_HIP(hipStreamSynchronize(st));  // host vectors above die on return
+    return VC_OK;
+}
+
+// S = sum over G shards (canonical) -> Montgomery
+__global__ void k_mp_sum_parts(const Fr* __restrict__ parts, int G, size_t NN, Fr* __restrict__ S) {
+    size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= NN) return;
+    Fr acc = parts[g];
+    for (int k = 1; k < G; k++) acc = fe_add<F>(acc, parts[(size_t)k * NN + g]);
+    S[g] = fe_to_mont<F>(acc);
+}
+
+static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vector<uint32_t>& zval,
+                     const void* d_S_parts, int G, vc_transcript* tr, uint64_t* d_xy, uint8_t* d_inf,
+                     vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!is_pow2(N) || G < 1 || zval.empty()) return VC_E_INVALID;
     hipStream_t st = ctx->stream;
-    DevBuf d_raw, d_f, d_r, d_order, d_zs, d_zv, d_S, d_den, d_inv, d_Q, d_pw, d_pwi, d_g, d_h, d_it;
-    VK_TRY(d_raw.ensure(Q * N * 32));
-    VK_TRY(d_f.ensure(Q * N * 32));
-    VK_TRY(d_r.ensure(Q * 32));
-    VK_TRY(d_order.ensure(Q * 4));
-    VK_TRY(d_zs.ensure((Z + 1) * 4));
+    const uint32_t Z = (uint32_t)zval.size();
+    DevBuf d_zv, d_S, d_den, d_inv, d_Q, d_pw, d_pwi, d_g, d_h, d_it;
     VK_TRY(d_zv.ensure(Z * 4));
     VK_TRY(d_S.ensure((size_t)Z * N * 32));
     VK_TRY(d_den.ensure((size_t)Z * N * 32));
@@ -680,14 +771,9 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     VK_TRY(d_g.ensure(N * 32));
     VK_TRY(d_h.ensure(N * 32));
     VK_TRY(d_it.ensure(Z * 32));
-    VK_CHECK_HIP(hipMemcpyAsync(d_raw.p, data, Q * N * 32, hipMemcpyHostToDevice, st));
-    VK_TRY(canon_to_mont_dev<F>(ctx, d_raw.p, Q * N, Q * N, d_f.as<fe<F>>()));
-    VK_CHECK_HIP(hipMemcpyAsync(d_r.p, rpow.data(), Q * 32, hipMemcpyHostToDevice, st));
-    VK_CHECK_HIP(hipMemcpyAsync(d_order.p, order.data(), Q * 4, hipMemcpyHostToDevice, st));
-    VK_CHECK_HIP(hipMemcpyAsync(d_zs.p, zstart.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_zv.p, zval.data(), Z * 4, hipMemcpyHostToDevice, st));
-    VK_LAUNCH(ctx, "mp_accumulate", k_mp_accumulate, dim3((N + 255) / 256, Z), 256, 0, d_f.as<fe<F>>(),
-              d_r.as<fe<F>>(), d_order.as<uint32_t>(), d_zs.as<uint32_t>(), N, Z, d_S.as<fe<F>>());
+    VK_LAUNCH(ctx, "mp_sum_parts", k_mp_sum_parts, ((size_t)Z * N + 255) / 256, 256, 0,
+              reinterpret_cast<const Fr*>(d_S_parts), G, (size_t)Z * N, d_S.as<Fr>());
     Fr omega = bn254_group_gen(N);
     VK_TRY(domain_powers<F>(ctx, omega, N, d_pw.as<fe<F>>()));
     VK_TRY(domain_powers<F>(ctx, fe_inv_bin<F>(omega), N, d_pwi.as<fe<F>>()));
@@ -707,7 +793,7 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     VK_TRY(commit_batch(ctx, t, N, g.data(), 1, dxy, &dinf));
     transcript_append_point(tr, dxy, dinf, "D");
     Fr tt = transcript_digest(tr, "t");
-    std::vector<Fr> invs = invert_domain_at(tt, N);
+    std::vector<Fr> invs = invert_domain_at(tt, N);  // 1/(t - z), z an integer (utils.rs:57-62)
     std::vector<Fr> invz(Z);
     for (uint32_t k = 0; k < Z; k++) invz[k] = invs[zval[k]];
     VK_CHECK_HIP(hipMemcpyAsync(d_it.p, invz.data(), Z * 32, hipMemcpyHostToDevice, st));
@@ -724,22 +810,37 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     Acc mc = C::add(acc_of(exy, einf), C::neg(acc_of(dxy, dinf)));
     memcpy(d_xy, dxy, 64);
     *d_inf = dinf;
-    int stt;
     if (scheme == 0) {
         std::vector<std::vector<Fr>> dd(1, hmg);
         std::vector<Acc> cs(1, mc);
         std::vector<Fr> ps(1, tt);
         vc_transcript* trs[1] = {tr};
-        stt = ipa_prove_impl(ctx, t, N, dd, cs, ps, trs, ipa_proof);
-    } else {
-        std::vector<uint64_t> ev(N * 4);
-        for (size_t k = 0; k < N; k++) canon_of(hmg[k], &ev[4 * k]);
-        uint64_t tc[4];
-        canon_of(tt, tc);
-        stt = kzg_prove_t<BN254G1, BN254Fr>(ctx, t, N, ev.data(), N, tc, kzg_xy, kzg_inf, kzg_y, nullptr);
+        return ipa_prove_impl(ctx, t, N, dd, cs, ps, trs, ipa_proof);
     }
+    std::vector<uint64_t> ev(N * 4);
+    for (size_t k = 0; k < N; k++) canon_of(hmg[k], &ev[4 * k]);
+    uint64_t tc[4];
+    canon_of(tt, tc);
+    return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, N, ev.data(), N, tc, kzg_xy, kzg_inf, kzg_y, nullptr);
+}
+
+static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const uint64_t* data, const uint64_t* com_xy,
+                    const uint8_t* com_inf, const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
+                    vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+    vc_transcript* tr = nullptr;
+    Fr r;
+    VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
+    std::vector<uint32_t> zval = mp_points(Q, z);
+    DevBuf d_data, d_S;
+    int st = d_data.ensure(Q * N * 32);
+    if (st == VC_OK) st = d_S.ensure(zval.size() * N * 32);
+    if (st == VC_OK && hipMemcpyAsync(d_data.p, data, Q * N * 32, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        st = VC_E_HIP;
+    if (st == VC_OK) st = mp_accumulate(ctx, N, Q, d_data.p, z, r, 0, zval, d_S.p);
+    if (st == VC_OK)
+        st = mp_finish(ctx, scheme, t, N, zval, d_S.p, 1, tr, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf, kzg_y);
     vc_transcript_free(tr);
-    return stt;
+    return st;
 }
 
 // E - D and t of verify_multiproof (:178-215); tr returned positioned after "E"
@@ -794,6 +895,42 @@ int vc_multiproof_prove(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, 
     Table* t = ctx->table(table);
     if (!t) return VC_E_TABLE;
     return mp_prove(ctx, scheme, t, N, Q, data, com_xy, com_inf, z, y, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf, kzg_y);
+}
+
+int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                        const uint64_t* y, vc_transcript** tr_out, uint64_t* r_out, size_t* rows) {
+    if (!com_xy || !com_inf || !z || !y || !tr_out || !r_out || !rows) return VC_E_INVALID;
+    vc_transcript* tr = nullptr;
+    Fr r;
+    VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
+    canon_of(r, r_out);
+    *rows = mp_points(Q, z).size();
+    *tr_out = tr;
+    return VC_OK;
+}
+
+int vc_multiproof_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* z, size_t first, size_t Qs,
+                             const void* d_data, const uint64_t* r, void* d_S) {
+    if (!ctx || !z || !r || !d_S || (Qs && !d_data) || first > Q || Qs > Q - first || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
+    Guard g(ctx);
+    return mp_accumulate(ctx, N, Qs, d_data, z + first, fr_of(r), first, mp_points(Q, z), d_S);
+}
+
+int vc_multiproof_finish(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* z,
+                         const void* d_S_parts, int G, vc_transcript* tr, uint64_t* d_xy, uint8_t* d_inf,
+                         vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!ctx || !z || !d_S_parts || G < 1 || !tr || !d_xy || !d_inf || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    if (scheme == 0 && !proof_ok(ipa_proof)) return VC_E_INVALID;
+    if (scheme == 1 && (!kzg_xy || !kzg_inf || !kzg_y)) return VC_E_INVALID;
+    if (scheme != 0 && scheme != 1) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    return mp_finish(ctx, scheme, t, N, mp_points(Q, z), d_S_parts, G, tr, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf,
+                     kzg_y);
 }
 
 int vc_multiproof_verify_ipa(vc_ctx* ctx, int table, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,

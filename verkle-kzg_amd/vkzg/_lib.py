@@ -63,6 +63,10 @@ SIGNATURES = {
     "vc_kzg_prove_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
     "vc_kzg_prove_device_part": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, c_int, c_int, P, P]),
     "vc_multiproof_prove": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P, P, P, P, P, P]),
+    "vc_multiproof_begin": (c_int, [c_size_t, c_size_t, P, P, P, P, P, P, P]),
+    "vc_multiproof_accumulate": (c_int, [c_void_p, c_size_t, c_size_t, P, c_size_t, c_size_t, P, P, P]),
+    "vc_multiproof_finish": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, c_int, c_void_p, P, P, P, P,
+                                     P, P]),
     "vc_multiproof_verify_ipa": (c_int, [c_void_p, c_int, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P,
                                          ctypes.POINTER(c_int)]),
     "vc_multiproof_kzg_claim": (c_int, [c_void_p, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P, P, P]),

@@ -339,3 +339,36 @@ def verify_multiproof(vc, vqueries, mp):
     check(lib().vc_multiproof_kzg_claim(vc.engine.h, N, Q, _p(cxy), _p(cinf), _p(z), _p(y), _p(dxy), int(dinf[0]),
                                         _p(oxy), _p(oinf), _p(t)), "multiproof_kzg_claim")
     return {"commitment": _pt(oxy, oinf[0]), "t": limbs_to_int(t)}
+
+
+# ---------------------------------------------------------------- sharded multiproof
+def multiproof_begin(N, cxy, cinf, z, y):
+    """Phase 1 (host, every rank): transcript over all queries -> (transcript handle, r limbs, rows)."""
+    Q = len(z)
+    tr = ctypes.c_void_p()
+    r = np.zeros(4, dtype=np.uint64)
+    rows = ctypes.c_size_t()
+    check(lib().vc_multiproof_begin(N, Q, _p(cxy), _p(cinf), _p(z), _p(y), ctypes.byref(tr), _p(r),
+                                    ctypes.byref(rows)), "multiproof_begin")
+    return tr, r, rows.value
+
+
+def multiproof_accumulate(engine, N, z, first, count, d_data_ptr, r, d_S_ptr):
+    """Phase 2 (device): this shard's rows x N per-point sums into d_S (canonical u64 x 4)."""
+    check(lib().vc_multiproof_accumulate(engine.h, N, len(z), _p(z), first, count, ctypes.c_void_p(d_data_ptr),
+                                         _p(r), ctypes.c_void_p(d_S_ptr)), "multiproof_accumulate")
+
+
+def multiproof_finish_ipa(ipa, z, d_S_parts_ptr, G, tr):
+    """Phase 3: sum the G shards' S, then D, t, E and the inner IPA proof. Frees `tr`."""
+    N = ipa.N
+    dxy = np.zeros(8, dtype=np.uint64)
+    dinf = np.zeros(1, dtype=np.uint8)
+    b, arrs = IPAProof._alloc(_log2(N))
+    try:
+        check(lib().vc_multiproof_finish(ipa.engine.h, 0, ipa.table, N, len(z), _p(z), ctypes.c_void_p(d_S_parts_ptr),
+                                         G, tr, _p(dxy), _p(dinf), ctypes.byref(b), None, None, None),
+              "multiproof_finish")
+    finally:
+        lib().vc_transcript_free(tr)
+    return {"proof": IPAProof._from(b, arrs), "d": _pt(dxy, dinf[0])}
