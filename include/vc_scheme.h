@@ -31,6 +31,7 @@ typedef struct vc_transcript vc_transcript;
 vc_transcript* vc_transcript_new(const char* label);
 vc_transcript* vc_transcript_clone(const vc_transcript* t);
 void vc_transcript_free(vc_transcript* t);
+void vc_transcript_reserve(vc_transcript* t, size_t bytes); /* capacity hint for long transcripts */
 int vc_transcript_append_bytes(vc_transcript* t, const uint8_t* bytes, size_t n, const char* label);
 int vc_transcript_append_point(vc_transcript* t, const uint64_t* xy, uint8_t inf, const char* label);
 int vc_transcript_append_fr(vc_transcript* t, const uint64_t* fr, const char* label);

@@ -144,6 +144,27 @@ def test_msm_window_parts(engines, oracle_c, curve, n, parts):
 
 
 @pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("width,batch,c", [(256, 700, 8), (64, 3000, 12), (255, 520, 16)])
+def test_batch_commit_persistent(engines, oracle_c, curve, width, batch, c):
+    """large batches take the persistent equal-run path (runs straddling two commits, piece
+    combine); sampled commits vs the oracle, for three table window sizes"""
+    import vkzg
+    e = engines[curve]
+    rng = np.random.default_rng(31 + c)
+    tid = e.random_bases(width, seed=width + c)
+    xy, inf = e.download_bases(tid)
+    e.fixed_base_precompute(tid, c)
+    sc = vkzg.random_scalars(curve, width * batch, rng)
+    sc[3 * width:4 * width] = 0      # an all-zero commit in the middle
+    got_xy, got_inf = e.msm_batch(tid, sc, width)
+    for j in sorted({0, 1, 3, batch // 2, batch - 2, batch - 1} | set(rng.integers(0, batch, 10).tolist())):
+        want = _oracle(oracle_c, curve, xy, inf, sc[j * width:(j + 1) * width])
+        assert got_inf[j] == want[1], j
+        if not want[1]:
+            assert np.array_equal(got_xy[j], want[0]), j
+
+
+@pytest.mark.parametrize("curve", CURVES)
 def test_batch_commit(engines, oracle_c, curve):
     """vc_msm_batch (fixed-base tables) vs per-commit oracle MSM; width 256 and ragged width."""
     import vkzg

@@ -246,6 +246,76 @@ __global__ void __launch_bounds__(256) k_fb_combine(const typename C::Acc* __res
     out[g] = acc;
 }
 
+// ---- latency path for small batches (the IPA prover's L/R, multiproof D/E): every thread
+// adds the table points of WPT windows of one base, then a wave butterfly and an LDS step
+// fold the block to one partial; k_fb_combine_small adds a commit's few block partials.
+// Serial depth WPT + 8 + blocks-per-commit adds instead of W + width (persistent path at K = 1).
+constexpr int FB_WPT = 4;
+
+template <class C>
+__device__ __forceinline__ typename C::Acc fb_wave_sum(typename C::Acc v) {
+    for (int m = 1; m < 64; m <<= 1) {
+        typename C::Acc o;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+        for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
+        v = C::add(v, o);
+    }
+    return v;
+}
+
+template <class C, class Fr>
+__global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
+                                                        const uint8_t* __restrict__ inf, uint32_t width, int c,
+                                                        int W, const uint32_t* __restrict__ sc, int mont,
+                                                        uint32_t bpc, typename C::Acc* __restrict__ part) {
+    using Acc = typename C::Acc;
+    __shared__ Acc wsum[4];
+    const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
+    const uint32_t WG = (uint32_t)(W + FB_WPT - 1) / FB_WPT;
+    const uint32_t j = blk * 256 + threadIdx.x;
+    const uint32_t i = j / WG, wg = j % WG;
+    const uint32_t NBk = 1u << (c - 1);
+    const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
+    Acc acc = C::zero();
+    if (i < width && !inf[i]) {
+        fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
+        if (mont) s = fe_from_mont<Fr>(s);
+        const FbE<C>* ti = tab + (size_t)i * W * NBk;
+        const int wb = (int)wg * FB_WPT, we = min(W, wb + FB_WPT);
+        uint32_t carry = 0;
+        for (int w = 0; w < we; w++) {
+            uint32_t raw = (s.v[0] & mask) + carry;
+#pragma unroll
+            for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
+            s.v[7] >>= c;
+            carry = raw > half ? 1u : 0u;
+            const int32_t d = carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
+            if (w >= wb && d != 0)
+                acc = C::madd(acc, ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].a, d < 0);
+        }
+    }
+    acc = fb_wave_sum<C>(acc);
+    const int wave = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0) wsum[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Acc t = C::add(C::add(wsum[0], wsum[1]), C::add(wsum[2], wsum[3]));
+        part[blockIdx.x] = t;
+    }
+}
+
+template <class C>
+__global__ void k_fb_combine_small(const typename C::Acc* __restrict__ part, uint32_t bpc, uint32_t batch,
+                                   typename C::Acc* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= batch) return;
+    typename C::Acc acc = part[(size_t)g * bpc];
+    for (uint32_t b = 1; b < bpc; b++) acc = C::add(acc, part[(size_t)g * bpc + b]);
+    out[g] = acc;
+}
+
 // lanes resident in one round for a kernel (occupancy x CUs x block)
 template <class Kern>
 static uint32_t resident_lanes(Kern k, int block) {
@@ -307,6 +377,21 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (!lanes_cache) lanes_cache = resident_lanes(k_fb_commit<C, Fr>, 256);
     const size_t items = batch * width;
     const size_t lanes = lanes_cache ? lanes_cache : 131072;
+    const int W = t->fb_W;
+    const size_t WG = (size_t)(W + FB_WPT - 1) / FB_WPT;
+    if (items * WG <= lanes) {  // small batch: latency path
+        const uint32_t bpc = (uint32_t)((width * WG + 255) / 256);
+        VK_TRY(ctx->ws[WS_PIECE].ensure((size_t)batch * bpc * sizeof(Acc)));
+        VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
+                  t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, W, reinterpret_cast<const uint32_t*>(d_sc), mont,
+                  bpc, ctx->ws[WS_PIECE].as<Acc>());
+        VK_LAUNCH(ctx, "fb_combine_small", (k_fb_combine_small<C>), (batch + 63) / 64, 64, 0,
+                  ctx->ws[WS_PIECE].as<Acc>(), bpc, (uint32_t)batch, ctx->ws[WS_OUT].as<Acc>());
+        VK_LAUNCH(ctx, "fb_normalize_out", (k_normalize<C>), (batch + 255) / 256, 256, 0,
+                  ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
+                  reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);
+        return VC_OK;
+    }
     size_t K = (items + lanes - 1) / lanes;
     K = std::max<size_t>(1, std::min<size_t>(K, width));
     const size_t nlanes = (items + K - 1) / K;

@@ -2,11 +2,69 @@
 // (reference transcript.rs:28-62 via DefaultFieldHasher<Sha256>) and the IPA CRS
 // generator (ipa_point_generator.rs:96-108).
 #pragma once
+#include <immintrin.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
 
 namespace vk {
+
+static const uint32_t kSha256K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+// x86 SHA extensions (SHA-NI): 4 rounds per sha256rnds2 pair, message schedule by
+// sha256msg1/msg2. Used when the host CPU has them (the multiproof transcript hashes ~5 MB at
+// Q = 2^16 -- 4x faster than the portable rounds); same digest, checked in tests/test_abi.py.
+__attribute__((target("sha,sse4.1"))) static inline void sha256_blocks_shani(uint32_t st[8], const uint8_t* data,
+                                                                             size_t nblocks) {
+    const __m128i MASK = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i TMP = _mm_loadu_si128(reinterpret_cast<const __m128i*>(&st[0]));
+    __m128i S1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(&st[4]));
+    TMP = _mm_shuffle_epi32(TMP, 0xB1);
+    S1 = _mm_shuffle_epi32(S1, 0x1B);
+    __m128i S0 = _mm_alignr_epi8(TMP, S1, 8);
+    S1 = _mm_blend_epi16(S1, TMP, 0xF0);
+    while (nblocks--) {
+        const __m128i A0 = S0, C0 = S1;
+        __m128i M[4];
+        for (int k = 0; k < 4; k++)
+            M[k] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(data + 16 * k)), MASK);
+        for (int g = 0; g < 16; g++) {
+            const __m128i cur = M[g & 3];
+            __m128i MSG = _mm_add_epi32(cur, _mm_loadu_si128(reinterpret_cast<const __m128i*>(&kSha256K[4 * g])));
+            S1 = _mm_sha256rnds2_epu32(S1, S0, MSG);
+            if (g >= 3 && g <= 14) {
+                __m128i& nx = M[(g + 1) & 3];
+                nx = _mm_add_epi32(nx, _mm_alignr_epi8(cur, M[(g + 3) & 3], 4));
+                nx = _mm_sha256msg2_epu32(nx, cur);
+            }
+            MSG = _mm_shuffle_epi32(MSG, 0x0E);
+            S0 = _mm_sha256rnds2_epu32(S0, S1, MSG);
+            if (g >= 1 && g <= 12) M[(g + 3) & 3] = _mm_sha256msg1_epu32(M[(g + 3) & 3], cur);
+        }
+        S0 = _mm_add_epi32(S0, A0);
+        S1 = _mm_add_epi32(S1, C0);
+        data += 64;
+    }
+    TMP = _mm_shuffle_epi32(S0, 0x1B);
+    S1 = _mm_shuffle_epi32(S1, 0xB1);
+    S0 = _mm_blend_epi16(TMP, S1, 0xF0);
+    S1 = _mm_alignr_epi8(S1, TMP, 8);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(&st[0]), S0);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(&st[4]), S1);
+}
+
+inline bool sha256_have_shani() {
+    static const int have = __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1") ? 1 : 0;
+    return have != 0;
+}
 
 class Sha256 {
    public:
@@ -22,6 +80,13 @@ class Sha256 {
         const uint8_t* p = static_cast<const uint8_t*>(data);
         len_ += n;
         while (n > 0) {
+            if (nbuf_ == 0 && n >= 64) {  // whole blocks straight from the input
+                size_t nb = n / 64;
+                blocks(p, nb);
+                p += nb * 64;
+                n -= nb * 64;
+                continue;
+            }
             size_t take = 64 - nbuf_;
             if (take > n) take = n;
             memcpy(buf_ + nbuf_, p, take);
@@ -29,7 +94,7 @@ class Sha256 {
             p += take;
             n -= take;
             if (nbuf_ == 64) {
-                block(buf_);
+                blocks(buf_, 1);
                 nbuf_ = 0;
             }
         }
@@ -52,18 +117,20 @@ class Sha256 {
         reset();
     }
 
+    // force the portable rounds (tests compare both paths)
+    bool portable = false;
+
    private:
+    void blocks(const uint8_t* b, size_t nb) {
+        if (!portable && sha256_have_shani()) {
+            sha256_blocks_shani(h_, b, nb);
+            return;
+        }
+        for (size_t i = 0; i < nb; i++) block(b + 64 * i);
+    }
     static uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
     void block(const uint8_t* b) {
-        static const uint32_t K[64] = {
-            0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
-            0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
-            0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
-            0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
-            0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
-            0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
-            0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
-            0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+        const uint32_t* K = kSha256K;
         uint32_t w[64];
         for (int i = 0; i < 16; i++)
             w[i] = ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) | ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];

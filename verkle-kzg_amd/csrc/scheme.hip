@@ -604,6 +604,7 @@ struct MpPrep {
 static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                                     const uint64_t* y) {
     vc_transcript* tr = vc_transcript_new("multiproof");
+    vc_transcript_reserve(tr, Q * 75 + 64);
     for (size_t i = 0; i < Q; i++) {
         vc_transcript_append_point(tr, com_xy + 8 * i, com_inf[i], "C");
         vc_transcript_append_u64(tr, z[i], "z");
@@ -640,10 +641,13 @@ static int mp_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* c
 
 // distinct query points, sorted (the rows of S)
 static std::vector<uint32_t> mp_points(size_t Q, const uint64_t* z) {
-    std::vector<uint32_t> v(Q);
-    for (size_t i = 0; i < Q; i++) v[i] = (uint32_t)z[i];
-    std::sort(v.begin(), v.end());
-    v.erase(std::unique(v.begin(), v.end()), v.end());
+    uint64_t zmax = 0;
+    for (size_t i = 0; i < Q; i++) zmax = std::max(zmax, z[i]);
+    std::vector<uint8_t> seen(zmax + 1, 0);  // z < N (checked by the callers)
+    for (size_t i = 0; i < Q; i++) seen[z[i]] = 1;
+    std::vector<uint32_t> v;
+    for (uint64_t k = 0; k <= zmax; k++)
+        if (seen[k]) v.push_back((uint32_t)k);
     return v;
 }
 

@@ -144,6 +144,9 @@ vc_transcript* vc_transcript_new(const char* label) {
 }
 vc_transcript* vc_transcript_clone(const vc_transcript* t) { return t ? new vc_transcript(*t) : nullptr; }
 void vc_transcript_free(vc_transcript* t) { delete t; }
+void vc_transcript_reserve(vc_transcript* t, size_t bytes) {
+    if (t) t->state.reserve(bytes);
+}
 
 int vc_transcript_append_bytes(vc_transcript* t, const uint8_t* b, size_t n, const char* label) {
     if (!t || (n && !b)) return VC_E_INVALID;
