@@ -6,13 +6,14 @@
 //     T[i][w][k] = (k+1) * 2^(c*w) * G_i     (affine, Montgomery; k < 2^(c-1))
 // held in HBM (width 256, c = 8: 67 MB BN254 / 100 MB Bandersnatch -- L3-resident; c = 16:
 // 8.6-13 GB, which only a 288 GB part can afford). A commit is then sum over (i, w) of
-// +-T[i][w][|d_iw|-1]: W mixed adds per base, no doublings, no buckets, no cross-block
-// reduction. TPC lanes share one commit (strided over bases, so scalar loads coalesce)
-// and fold their partial sums with cross-lane shuffles; results are normalised with one
-// workgroup-level batch inversion per 256 commits.
+// +-T[i][w][|d_iw|-1]: W mixed adds per base, no doublings, no buckets. Two schedules:
+// throughput (large batches: persistent equal runs of (commit, base) items, one resident
+// round, piece combine, workgroup batch inversion) and latency (small batches such as the
+// IPA prover's L/R: per-window threads, wave/LDS fold, host combine + normalisation).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -250,7 +251,12 @@ __global__ void __launch_bounds__(256) k_fb_combine(const typename C::Acc* __res
 // adds the table points of WPT windows of one base, then a wave butterfly and an LDS step
 // fold the block to one partial; k_fb_combine_small adds a commit's few block partials.
 // Serial depth WPT + 8 + blocks-per-commit adds instead of W + width (persistent path at K = 1).
-constexpr int FB_WPT = 4;
+// windows per thread of the latency path. 1 is best by far (IPA prover L/R, width 257, c = 8:
+// 111 us per launch vs 469 / 658 us at 2 / 4): a lone wave executing a mixed add's ~25 KB of
+// straight-line code once runs on cold instruction-cache misses, so any serial madd beyond the
+// first costs ~0.35 ms; one (base, window) point per thread leaves only the looped butterfly.
+constexpr int FB_WPT = 1;
+static int fb_wpt() { return FB_WPT; }
 
 template <class C>
 __device__ __forceinline__ typename C::Acc fb_wave_sum(typename C::Acc v) {
@@ -269,11 +275,11 @@ template <class C, class Fr>
 __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
                                                         const uint8_t* __restrict__ inf, uint32_t width, int c,
                                                         int W, const uint32_t* __restrict__ sc, int mont,
-                                                        uint32_t bpc, typename C::Acc* __restrict__ part) {
+                                                        uint32_t bpc, int wpt, typename C::Acc* __restrict__ part) {
     using Acc = typename C::Acc;
     __shared__ Acc wsum[4];
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
-    const uint32_t WG = (uint32_t)(W + FB_WPT - 1) / FB_WPT;
+    const uint32_t WG = (uint32_t)(W + wpt - 1) / wpt;
     const uint32_t j = blk * 256 + threadIdx.x;
     const uint32_t i = j / WG, wg = j % WG;
     const uint32_t NBk = 1u << (c - 1);
@@ -283,7 +289,7 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
         fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
         if (mont) s = fe_from_mont<Fr>(s);
         const FbE<C>* ti = tab + (size_t)i * W * NBk;
-        const int wb = (int)wg * FB_WPT, we = min(W, wb + FB_WPT);
+        const int wb = (int)wg * wpt, we = min(W, wb + wpt);
         uint32_t carry = 0;
         for (int w = 0; w < we; w++) {
             uint32_t raw = (s.v[0] & mask) + carry;
@@ -378,18 +384,31 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     const size_t items = batch * width;
     const size_t lanes = lanes_cache ? lanes_cache : 131072;
     const int W = t->fb_W;
-    const size_t WG = (size_t)(W + FB_WPT - 1) / FB_WPT;
-    if (items * WG <= lanes) {  // small batch: latency path
+    const int wpt = fb_wpt();
+    const size_t WG = (size_t)(W + wpt - 1) / wpt;
+    if (items * WG <= lanes && batch <= 64) {  // small batch: latency path
         const uint32_t bpc = (uint32_t)((width * WG + 255) / 256);
         VK_TRY(ctx->ws[WS_PIECE].ensure((size_t)batch * bpc * sizeof(Acc)));
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
                   t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, W, reinterpret_cast<const uint32_t*>(d_sc), mont,
-                  bpc, ctx->ws[WS_PIECE].as<Acc>());
-        VK_LAUNCH(ctx, "fb_combine_small", (k_fb_combine_small<C>), (batch + 63) / 64, 64, 0,
-                  ctx->ws[WS_PIECE].as<Acc>(), bpc, (uint32_t)batch, ctx->ws[WS_OUT].as<Acc>());
-        VK_LAUNCH(ctx, "fb_normalize_out", (k_normalize<C>), (batch + 255) / 256, 256, 0,
-                  ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
-                  reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);
+                  bpc, wpt, ctx->ws[WS_PIECE].as<Acc>());
+        // the few block partials are added and normalised on the host: a lone GPU lane pays
+        // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
+        std::vector<Acc> parts((size_t)batch * bpc);
+        VK_CHECK_HIP(hipMemcpyAsync(parts.data(), ctx->ws[WS_PIECE].p, parts.size() * sizeof(Acc),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        const int nl = (int)(C::F::N / 2);
+        std::vector<uint64_t> oxy((size_t)batch * 2 * nl);
+        std::vector<uint8_t> oinf(batch);
+        for (size_t g = 0; g < batch; g++) {
+            Acc a = parts[g * bpc];
+            for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
+            VK_TRY(acc_to_affine(ctx->curve, reinterpret_cast<const uint32_t*>(&a), &oxy[g * 2 * nl], &oinf[g]));
+        }
+        VK_CHECK_HIP(hipMemcpyAsync(d_out_xy, oxy.data(), oxy.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+        VK_CHECK_HIP(hipMemcpyAsync(d_out_inf, oinf.data(), batch, hipMemcpyHostToDevice, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // host staging vectors die on return
         return VC_OK;
     }
     size_t K = (items + lanes - 1) / lanes;

@@ -47,3 +47,10 @@ for it in range(3):
     t0 = time.perf_counter()
     ipa.prove_point(c, 1000, d)
     print(f"ipa prove_point {1e3 * (time.perf_counter() - t0):.2f} ms", flush=True)
+e.enable_timing(True)
+e.reset_timing()
+ipa.prove_point(c, 1000, d)
+for k in ("fb_commit_small", "fb_combine_small", "fb_normalize_out", "fb_commit", "fb_combine"):
+    ms, n = e.kernel_time(k)
+    if n:
+        print(f"  {k}: {n} launches, {ms / n * 1e3:.1f} us avg", flush=True)
