@@ -1,0 +1,100 @@
+"""Verkle tree (include/vc_verkle.h, C++ in libvkzg.so) against the oracle restatement of
+/root/reference/verkle-tree/src (oracle/pyoracle/verkle.py): insert / get / path_to_stem
+semantics on CPU (host code, no GPU), including the reference's own tests restated
+(lib.rs:261-350) and its panic case; the level-batched commitments on the GPU
+(tests/test_gpu_verkle.py)."""
+import random
+
+import pytest
+
+
+def _key(rng, N, arity=255, prefix=()):
+    return tuple(prefix) + tuple(rng.randrange(arity) for _ in range(N - len(prefix)))
+
+
+def _val(rng):
+    return bytes(rng.randrange(256) for _ in range(32))
+
+
+def test_reference_insert_get_leaves():
+    """lib.rs:261-297 test_insert_get_leaves (50 leaves, 1/4 sharing a stem), two insertion orders"""
+    from vkzg.verkle import VerkleTree
+    rng = random.Random(1)
+    N = 3
+    stem = _key(rng, N)
+    kvs = {}
+    for _ in range(50 // 4):
+        kvs[_key(rng, N, prefix=stem)] = _val(rng)
+    while len(kvs) < 50:
+        kvs[_key(rng, N)] = _val(rng)
+    keys = list(kvs)
+    keys2 = keys[:]
+    rng.shuffle(keys2)
+    t1, t2 = VerkleTree(N), VerkleTree(N)
+    for k1, k2 in zip(keys, keys2):
+        t1.insert_single(k1, kvs[k1])
+        t2.insert_single(k2, kvs[k2])
+    for k in kvs:
+        assert t1.get_single(k) == t2.get_single(k) == kvs[k]
+
+
+def test_reference_overwrite():
+    """lib.rs:299-311 test_overwrite"""
+    from vkzg.verkle import VerkleTree
+    rng = random.Random(2)
+    t = VerkleTree(3)
+    k = _key(rng, 3)
+    v1, v2 = _val(rng), _val(rng)
+    t.insert_single(k, v1)
+    t.insert_single(k, v2)
+    assert t.get_single(k) == v2
+
+
+def test_reference_path_to_stem():
+    """lib.rs:327-349 test_path_to_stem"""
+    from vkzg.verkle import VerkleTree
+    rng = random.Random(3)
+    t = VerkleTree(3)
+    k = _key(rng, 3)
+    t.insert_single(k, _val(rng))
+    t.insert_single(_key(rng, 3, prefix=(k[0],)), _val(rng))
+    for i, p in enumerate(t.path_to_stem(k)):
+        assert p[0] == tuple(k[:i + 1]) and p[1] == k[i]
+
+
+@pytest.mark.parametrize("N,arity,n", [(3, 255, 300), (3, 4, 40), (4, 3, 60), (5, 2, 30)])
+def test_tree_semantics_match_oracle(N, arity, n):
+    """random trees with heavy prefix sharing (small arity): every insert (or its rejection,
+    where the reference panics), get and path agree with the oracle restatement"""
+    from pyoracle import verkle as ov
+    from vkzg._lib import VCError
+    from vkzg.verkle import VerkleTree
+    rng = random.Random(N * 100 + arity)
+    t, o = VerkleTree(N), ov.VerkleTree(N)
+    keys, rejected = [], 0
+    for _ in range(n):
+        k = _key(rng, N, arity)
+        v = _val(rng)
+        try:
+            o.insert_single(k, v)
+            ok = True
+        except ov.VerklePanic:
+            ok = False
+        if ok:
+            t.insert_single(k, v)
+            keys.append(k)
+        else:
+            rejected += 1
+            with pytest.raises(VCError):
+                t.insert_single(k, v)
+    for k in keys + [_key(rng, N, arity) for _ in range(20)]:
+        assert t.get_single(k) == o.get_single(k), k
+        try:
+            want = o.path_to_stem(k)
+        except KeyError:
+            with pytest.raises(VCError):
+                t.path_to_stem(k)
+            continue
+        assert t.path_to_stem(k) == want
+    if arity <= 4:
+        assert rejected > 0   # the panic path is exercised

@@ -1,0 +1,289 @@
+// Verkle tree (reference verkle-tree/src/{lib,node}.rs) with level-batched commitments on the
+// GPU engine. Host data structure + orchestration; all commitments go through vc_msm_batch
+// (fixed-base batched commits) and vc_to_data_item_batch. See include/vc_verkle.h.
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "../../include/vc_scheme.h"
+#include "../../include/vc_verkle.h"
+#include "ctx.hpp"
+#include "host/fr.hpp"
+
+namespace {
+
+using vk::Fr;
+
+struct VNode {
+    bool ext = false;
+    std::vector<uint8_t> stem;                               // extension: the full key (node.rs:45)
+    std::map<uint8_t, std::array<uint8_t, 32>> leaves;      // extension: unit -> value
+    std::map<uint8_t, int> children;                         // internal: unit -> node
+    bool has_commit = false;
+    uint64_t cxy[8] = {0};
+    uint8_t cinf = 1;
+    uint64_t item[4] = {0};  // to_data_item of the commitment (canonical Fr)
+};
+
+// LE bytes -> canonical Fr words (from_le_bytes_mod_order)
+static void item_of_bytes(const uint8_t* b, size_t len, uint64_t out[4]) {
+    vk::mont_to_canon<vk::BN254Fr>(vk::fe_from_le_bytes_mod<vk::BN254Fr>(b, len), out);
+}
+
+}  // namespace
+
+struct vc_verkle {
+    int N = 3;
+    std::vector<VNode> nodes;  // nodes[0] = root (internal)
+};
+
+namespace {
+
+int new_ext(vc_verkle* t, const uint8_t* stem, uint8_t unit, const uint8_t* value) {
+    VNode n;
+    n.ext = true;
+    n.stem.assign(stem, stem + t->N);
+    std::array<uint8_t, 32> v;
+    memcpy(v.data(), value, 32);
+    n.leaves[unit] = v;
+    t->nodes.push_back(std::move(n));
+    return (int)t->nodes.size() - 1;
+}
+
+// first d > cur with a[d] != b[d] (or N) -- KeyMethods::next_diff_depth (lib.rs:49-58)
+int next_diff_depth(const std::vector<uint8_t>& a, const uint8_t* b, int cur, int N) {
+    int d = cur + 1;
+    while (d < N && a[d] == b[d]) d++;
+    return d;
+}
+
+// get_stem (node.rs:74-95)
+int find_stem(const vc_verkle* t, const uint8_t* stem) {
+    int cur = 0, depth = 0;
+    while (true) {
+        const VNode& n = t->nodes[cur];
+        if (n.ext) return memcmp(n.stem.data(), stem, t->N) == 0 ? cur : -1;
+        if (depth >= t->N) return -1;
+        auto it = n.children.find(stem[depth]);
+        if (it == n.children.end()) return -1;
+        cur = it->second;
+        depth++;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+vc_verkle* vc_verkle_new(int key_len) {
+    if (key_len < 2 || key_len > 32) return nullptr;
+    vc_verkle* t = new vc_verkle();
+    t->N = key_len;
+    t->nodes.emplace_back();  // root: Node::new_internal(vec![])
+    return t;
+}
+
+void vc_verkle_free(vc_verkle* t) { delete t; }
+
+// Node::insert (node.rs:133-204), iteratively. The walk is checked before anything changes,
+// so the reference's panic case leaves the tree untouched.
+int vc_verkle_insert(vc_verkle* t, const uint8_t* key, const uint8_t* value) {
+    if (!t || !key || !value) return VC_E_INVALID;
+    const int N = t->N;
+    const uint8_t* stem = key;       // split(): the stem keeps every unit (lib.rs:61-67)
+    const uint8_t unit = key[N - 1];
+    // dry run: find where the walk ends and reject the panic case first
+    std::vector<int> path;
+    int cur = 0, depth = 0;
+    enum { INTO_EXT, NEW_EXT, SPLIT } action;
+    int parent_k = -1;
+    while (true) {
+        path.push_back(cur);
+        VNode& n = t->nodes[cur];
+        if (n.ext) {
+            if (memcmp(n.stem.data(), stem, N) != 0) return VC_E_INVALID;  // reference panics here
+            action = INTO_EXT;
+            break;
+        }
+        if (depth >= N) return VC_E_INVALID;
+        const uint8_t k = stem[depth];
+        auto it = n.children.find(k);
+        if (it == n.children.end()) {
+            action = NEW_EXT;
+            parent_k = k;
+            break;
+        }
+        VNode& c = t->nodes[it->second];
+        if (c.ext && !(memcmp(c.stem.data(), stem, N) == 0 || depth == N - 2)) {
+            // the reference indexes stem[d] out of bounds (panics) when no unit after `depth`
+            // differs -- reachable only through its level-skipping splits
+            if (next_diff_depth(c.stem, stem, depth, N) >= N) return VC_E_INVALID;
+            action = SPLIT;
+            parent_k = k;
+            break;
+        }
+        cur = it->second;
+        depth++;
+    }
+    for (int p : path) t->nodes[p].has_commit = false;  // clear the commitments on the path
+    VNode* n = &t->nodes[cur];
+    if (action == INTO_EXT) {
+        std::array<uint8_t, 32> v;
+        memcpy(v.data(), value, 32);
+        n->leaves[unit] = v;
+        return VC_OK;
+    }
+    if (action == NEW_EXT) {
+        int e = new_ext(t, stem, unit, value);
+        t->nodes[cur].children[(uint8_t)parent_k] = e;
+        return VC_OK;
+    }
+    // SPLIT: new internal keyed by the first differing unit d (which may skip levels, as in
+    // the reference: node.rs:176-185)
+    const int old = t->nodes[cur].children[(uint8_t)parent_k];
+    const std::vector<uint8_t> old_stem = t->nodes[old].stem;
+    const int d = next_diff_depth(old_stem, stem, depth, N);
+    int e = new_ext(t, stem, unit, value);
+    VNode in;
+    in.children[stem[d]] = e;
+    in.children[old_stem[d]] = old;
+    t->nodes.push_back(std::move(in));
+    t->nodes[cur].children[(uint8_t)parent_k] = (int)t->nodes.size() - 1;
+    return VC_OK;
+}
+
+int vc_verkle_get(const vc_verkle* t, const uint8_t* key, uint8_t* value, int* found) {
+    if (!t || !key || !value || !found) return VC_E_INVALID;
+    *found = 0;
+    int e = find_stem(t, key);
+    if (e < 0) return VC_OK;
+    auto it = t->nodes[e].leaves.find(key[t->N - 1]);
+    if (it == t->nodes[e].leaves.end()) return VC_OK;
+    memcpy(value, it->second.data(), 32);
+    *found = 1;
+    return VC_OK;
+}
+
+// path_to_stem (node.rs:97-120): (prefix, unit) for every internal node down to the
+// extension; the prefix is key[0..=depth], so only the units are returned.
+int vc_verkle_path(const vc_verkle* t, const uint8_t* key, size_t max_len, uint8_t* units, size_t* len) {
+    if (!t || !key || !len) return VC_E_INVALID;
+    size_t n = 0;
+    int cur = 0;
+    while (!t->nodes[cur].ext) {
+        if ((int)n >= t->N) return VC_E_INVALID;
+        auto it = t->nodes[cur].children.find(key[n]);
+        if (it == t->nodes[cur].children.end()) return VC_E_INVALID;  // VerkleError::InvalidPath
+        if (units && n < max_len) units[n] = key[n];
+        n++;
+        cur = it->second;
+    }
+    *len = n;
+    return VC_OK;
+}
+
+int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, size_t* dirty) {
+    if (!t) return VC_E_INVALID;
+    size_t a = 0, b = 0, c = 0;
+    for (const VNode& n : t->nodes) {
+        (n.ext ? b : a)++;
+        if (!n.has_commit) c++;
+    }
+    if (internal) *internal = a;
+    if (extension) *extension = b;
+    if (dirty) *dirty = c;
+    return VC_OK;
+}
+
+// gen_commitment (node.rs:205-277), level-batched.
+int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf) {
+    if (!ctx || !t || !out_xy || !out_inf) return VC_E_INVALID;
+    const int N = t->N;
+    // dirty nodes reachable from the root, with depth (clean subtrees are skipped: an insert
+    // clears every commitment on its path, so a clean node has clean descendants)
+    std::vector<int> exts;
+    std::vector<std::vector<int>> internals;  // by depth
+    std::vector<std::pair<int, int>> stack{{0, 0}};
+    while (!stack.empty()) {
+        auto [id, depth] = stack.back();
+        stack.pop_back();
+        const VNode& n = t->nodes[id];
+        if (n.has_commit) continue;
+        if (n.ext) {
+            exts.push_back(id);
+            continue;
+        }
+        if ((int)internals.size() <= depth) internals.resize(depth + 1);
+        internals[depth].push_back(id);
+        for (auto& kv : n.children) stack.push_back({kv.second, depth + 1});
+    }
+    auto commit_items = [&](size_t width, const std::vector<uint64_t>& sc, size_t batch, std::vector<uint64_t>& xy,
+                            std::vector<uint8_t>& inf, std::vector<uint64_t>& items) -> int {
+        xy.assign(batch * 8, 0);
+        inf.assign(batch, 0);
+        items.assign(batch * 4, 0);
+        if (batch == 0) return VC_OK;
+        VK_TRY(vc_msm_batch(ctx, table, width, sc.data(), batch, 0, xy.data(), inf.data()));
+        return vc_to_data_item_batch(ctx, xy.data(), inf.data(), batch, items.data());
+    };
+    std::vector<uint64_t> xy, items, xy2, items2;
+    std::vector<uint8_t> inf, inf2;
+    // extension nodes: c1, c2 (width N), then [1, stem, c1, c2] (width 4)
+    if (!exts.empty()) {
+        const size_t E = exts.size();
+        std::vector<uint64_t> sc(2 * E * N * 4, 0);
+        for (size_t e = 0; e < E; e++) {
+            const VNode& n = t->nodes[exts[e]];
+            for (auto& kv : n.leaves) {
+                const size_t index = kv.first;
+                uint64_t lo[4], hi[4];
+                item_of_bytes(kv.second.data(), 16, lo);
+                item_of_bytes(kv.second.data() + 16, 16, hi);
+                const size_t il = (2 * index) % N, ih = (2 * index + 1) % N;
+                uint64_t* base = &sc[(2 * e + (index < (size_t)(N / 2) ? 0 : 1)) * N * 4];
+                memcpy(base + 4 * il, lo, 32);
+                memcpy(base + 4 * ih, hi, 32);
+            }
+        }
+        VK_TRY(commit_items(N, sc, 2 * E, xy, inf, items));
+        std::vector<uint64_t> ed(E * 4 * 4, 0);
+        for (size_t e = 0; e < E; e++) {
+            const VNode& n = t->nodes[exts[e]];
+            ed[e * 16 + 0] = 1;
+            item_of_bytes(n.stem.data(), N, &ed[e * 16 + 4]);  // bytes_to_item(stem.to_bytes())
+            memcpy(&ed[e * 16 + 8], &items[(2 * e) * 4], 32);
+            memcpy(&ed[e * 16 + 12], &items[(2 * e + 1) * 4], 32);
+        }
+        VK_TRY(commit_items(4, ed, E, xy2, inf2, items2));
+        for (size_t e = 0; e < E; e++) {
+            VNode& n = t->nodes[exts[e]];
+            memcpy(n.cxy, &xy2[e * 8], 64);
+            n.cinf = inf2[e];
+            memcpy(n.item, &items2[e * 4], 32);
+            n.has_commit = true;
+        }
+    }
+    // internal nodes, deepest level first (HACK in the reference: width hard-coded 256)
+    for (int depth = (int)internals.size() - 1; depth >= 0; depth--) {
+        const std::vector<int>& lv = internals[depth];
+        const size_t B = lv.size();
+        std::vector<uint64_t> sc(B * 256 * 4, 0);
+        for (size_t b = 0; b < B; b++)
+            for (auto& kv : t->nodes[lv[b]].children) memcpy(&sc[(b * 256 + kv.first) * 4], t->nodes[kv.second].item, 32);
+        VK_TRY(commit_items(256, sc, B, xy, inf, items));
+        for (size_t b = 0; b < B; b++) {
+            VNode& n = t->nodes[lv[b]];
+            memcpy(n.cxy, &xy[b * 8], 64);
+            n.cinf = inf[b];
+            memcpy(n.item, &items[b * 4], 32);
+            n.has_commit = true;
+        }
+    }
+    memcpy(out_xy, t->nodes[0].cxy, 64);
+    *out_inf = t->nodes[0].cinf;
+    return VC_OK;
+}
+
+}  // extern "C"

@@ -10,7 +10,7 @@ import re
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
 LIB_PATH = os.environ.get("VKZG_LIB") or os.path.join(ROOT, "lib", "libvkzg.so")
-HEADERS = [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("vc_msm.h", "vc_scheme.h")]
+HEADERS = [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("vc_msm.h", "vc_scheme.h", "vc_verkle.h")]
 
 c_void_p, c_int, c_size_t, c_uint64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
 c_double, c_long, c_char_p = ctypes.c_double, ctypes.c_long, ctypes.c_char_p
@@ -35,6 +35,22 @@ SIGNATURES = {
     "vc_point_words": (c_int, [c_int]),
     "vc_msm_device_partial": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P]),
     "vc_device_mad_rate": (c_int, [c_void_p, P]),
+    "vc_verkle_new": (c_void_p, [c_int]),
+    "vc_verkle_free": (None, [c_void_p]),
+    "vc_verkle_insert": (c_int, [c_void_p, P, P]),
+    "vc_verkle_get": (c_int, [c_void_p, P, P, P]),
+    "vc_verkle_path": (c_int, [c_void_p, P, c_size_t, P, P]),
+    "vc_verkle_commitment": (c_int, [c_void_p, c_int, c_void_p, P, P]),
+    "vc_verkle_stats": (c_int, [c_void_p, P, P, P]),
+    "vc_transcript_reserve": (None, [c_void_p, c_size_t]),
+    "vc_verkle_new": (c_void_p, [c_int]),
+    "vc_verkle_free": (None, [c_void_p]),
+    "vc_verkle_insert": (c_int, [c_void_p, P, P]),
+    "vc_verkle_get": (c_int, [c_void_p, P, P, P]),
+    "vc_verkle_path": (c_int, [c_void_p, P, c_size_t, P, P]),
+    "vc_verkle_commitment": (c_int, [c_void_p, c_int, c_void_p, P, P]),
+    "vc_verkle_stats": (c_int, [c_void_p, P, P, P]),
+    "vc_transcript_reserve": (None, [c_void_p, c_size_t]),
     "vc_msm_windows": (c_int, [c_int, c_size_t, P, P]),
     "vc_msm_device_window_part": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, c_int, c_int, P]),
     "vc_partials_sum": (c_int, [c_int, P, c_size_t, P, P]),
@@ -110,7 +126,7 @@ def check(status, where):
 
 
 def header_functions():
-    """Names of every function declared in include/vc_msm.h and include/vc_scheme.h."""
+    """Names of every function declared in the include/vc_*.h headers."""
     names = set()
     for h in HEADERS:
         src = open(h).read()
