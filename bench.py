@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--kzg-log-d", type=int, default=20)
     ap.add_argument("--no-mp", action="store_true", help="skip the IPA multiproof line (configs[4])")
     ap.add_argument("--mp-log-q", type=int, default=16)
+    ap.add_argument("--no-verkle", action="store_true", help="skip the verkle-tree commitment line (8(f) rank 1)")
+    ap.add_argument("--verkle-keys", type=int, default=1 << 16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
     return ap.parse_args()
 
@@ -219,6 +221,52 @@ def mp_line(a, rank, world, local, dev, stream):
                         f"split over {world} rank(s)", "ms_per_multiproof": dt * 1e3,
             "host_transcript_ms": t_begin * 1e3, "kernel_ms": kms, "algorithmic_bytes_per_unit": alg,
             "achieved_GBps": alg / dt / 1e9, "d_inf": mp["d"] is None}
+
+
+def verkle_line(a, local, stream):
+    """verkle-tree commitment (lib.rs:127-129 / node.rs:205-277) over a
+    KZG(256) Lagrange SRS on BN254, 32-unit keys (Ethereum-style 31-byte stem + suffix), random
+    32-byte values: the full commitment of a fresh tree, then after 1% of the keys are updated
+    (only the dirty nodes of each level are recommitted, one batched launch per level)."""
+    from vkzg import scheme
+    from vkzg.verkle import VerkleTree
+    veng = vkzg.Engine("bn254", local)
+    veng.set_stream(stream.cuda_stream)
+    kzg = scheme.KZG(veng, 256)
+    rng = np.random.default_rng(91)
+    nk = a.verkle_keys
+    keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    t = VerkleTree(32)
+    t0 = time.perf_counter()
+    for i in range(nk):
+        t.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    t_ins = time.perf_counter() - t0
+    kzg.commit(scheme.LagrangeBasis([1]))  # builds the SRS fixed-base tables, untimed
+    st = t.stats()
+    veng.enable_timing(True)
+    veng.reset_timing()
+    t0 = time.perf_counter()
+    t.commitment(veng, kzg.table)
+    t_full = time.perf_counter() - t0
+    kms = {}
+    for k in ("fb_commit", "fb_combine", "fb_normalize_out", "fb_commit_small", "to_data_item"):
+        ms, cnt = veng.kernel_time(k)
+        if cnt:
+            kms[k] = round(ms, 3)
+    veng.enable_timing(False)
+    upd = max(1, nk // 100)
+    for i in rng.integers(0, nk, size=upd):
+        t.insert_single(keys[i].tobytes(), rng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
+    dirty = t.stats()["dirty"]
+    t0 = time.perf_counter()
+    t.commitment(veng, kzg.table)
+    t_upd = time.perf_counter() - t0
+    veng.close()
+    return {"workload": f"verkle tree, {nk} random 32-unit keys, KZG(256) BN254 (8(f) rank 1)",
+            "nodes": st, "insert_s": t_ins, "full_commitment_ms": t_full * 1e3,
+            "nodes_per_s_full": st["dirty"] / t_full, "full_kernel_ms_total": kms, "updated_keys": upd, "dirty_nodes": dirty,
+            "update_commitment_ms": t_upd * 1e3}
 
 
 def main():
@@ -381,6 +429,9 @@ def main():
 
     if not a.no_mp:
         out["multiproof"] = mp_line(a, rank, world, local, dev, stream)
+
+    if rank == 0 and not a.no_verkle:
+        out["verkle"] = verkle_line(a, local, stream)
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(curve, n, a.cpu_sample)

@@ -27,8 +27,14 @@ struct VNode {
     uint64_t item[4] = {0};  // to_data_item of the commitment (canonical Fr)
 };
 
-// LE bytes -> canonical Fr words (from_le_bytes_mod_order)
+// LE bytes -> canonical Fr words (from_le_bytes_mod_order); < 31 bytes is already < r
 static void item_of_bytes(const uint8_t* b, size_t len, uint64_t out[4]) {
+    if (len <= 31) {
+        uint8_t w[32] = {0};
+        memcpy(w, b, len);
+        memcpy(out, w, 32);
+        return;
+    }
     vk::mont_to_canon<vk::BN254Fr>(vk::fe_from_le_bytes_mod<vk::BN254Fr>(b, len), out);
 }
 
