@@ -10,6 +10,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #define VK_HD __host__ __device__ __forceinline__
 
@@ -127,44 +128,61 @@ constexpr uint64_t host_inv64() {
     return (uint64_t)0 - x;
 }
 template <class F>
+struct HostP64 {
+    uint64_t v[F::N / 2];
+    constexpr HostP64() : v() {
+        for (int i = 0; i < F::N / 2; i++) v[i] = (uint64_t)F::p(2 * i) | ((uint64_t)F::p(2 * i + 1) << 32);
+    }
+};
+// no-carry CIOS on 64-bit limbs (every modulus leaves spare top bits), fully unrolled, with a
+// branchless final subtraction; the 32-bit limb array is read as 64-bit limbs (little-endian
+// host). 26 ns for BLS12-381 Fq on the GPU box's EPYC vs 38 ns for the looped version
+// (tools/hostmul.cpp): it carries the MSM's host Horner pass.
+template <class F>
 inline fe<F> fe_mul_host64(const fe<F>& a, const fe<F>& b) {
     constexpr int M = F::N / 2;
     constexpr uint64_t inv = host_inv64<F>();
-    uint64_t pa[M], pb[M], pp[M], t[M + 2] = {0};
-    for (int i = 0; i < M; i++) {
-        pa[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
-        pb[i] = (uint64_t)b.v[2 * i] | ((uint64_t)b.v[2 * i + 1] << 32);
-        pp[i] = (uint64_t)F::p(2 * i) | ((uint64_t)F::p(2 * i + 1) << 32);
-    }
+    static constexpr HostP64<F> P{};
     typedef unsigned __int128 u128;
+    uint64_t pa[M], pb[M], t[M + 1] = {0};
+    memcpy(pa, a.v, sizeof pa);
+    memcpy(pb, b.v, sizeof pb);
+#pragma unroll
     for (int i = 0; i < M; i++) {
         uint64_t C = 0;
+#pragma unroll
         for (int j = 0; j < M; j++) {
             u128 s = (u128)pa[j] * pb[i] + t[j] + C;
             t[j] = (uint64_t)s;
             C = (uint64_t)(s >> 64);
         }
-        u128 s = (u128)t[M] + C;
-        t[M] = (uint64_t)s;
-        t[M + 1] = (uint64_t)(s >> 64);
-        uint64_t m = t[0] * inv;
-        s = (u128)m * pp[0] + t[0];
+        t[M] += C;
+        const uint64_t m = t[0] * inv;
+        u128 s = (u128)m * P.v[0] + t[0];
         C = (uint64_t)(s >> 64);
+#pragma unroll
         for (int j = 1; j < M; j++) {
-            s = (u128)m * pp[j] + t[j] + C;
+            s = (u128)m * P.v[j] + t[j] + C;
             t[j - 1] = (uint64_t)s;
             C = (uint64_t)(s >> 64);
         }
-        s = (u128)t[M] + C;
-        t[M - 1] = (uint64_t)s;
-        t[M] = t[M + 1] + (uint64_t)(s >> 64);
+        t[M - 1] = t[M] + C;
+        t[M] = 0;
     }
+    uint64_t d[M], o[M];
+    uint64_t br = 0;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        u128 s = (u128)t[j] - P.v[j] - br;
+        d[j] = (uint64_t)s;
+        br = (uint64_t)(s >> 64) & 1;
+    }
+    const uint64_t mask = (uint64_t)0 - br;  // borrow: t < p, keep t
+#pragma unroll
+    for (int j = 0; j < M; j++) o[j] = (t[j] & mask) | (d[j] & ~mask);
     fe<F> r;
-    for (int i = 0; i < M; i++) {
-        r.v[2 * i] = (uint32_t)t[i];
-        r.v[2 * i + 1] = (uint32_t)(t[i] >> 32);
-    }
-    return fe_reduce_once<F>(r);  // t[M] == 0 here: every modulus leaves spare top bits
+    memcpy(r.v, o, sizeof o);
+    return r;
 }
 #endif
 
