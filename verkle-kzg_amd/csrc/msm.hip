@@ -254,12 +254,19 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     }
     const uint32_t NB = 1u << (c - 1);
     const uint32_t NBtot = NB * W;
-    const uint32_t M = 64;  // sorted entries per accumulate thread (64: 2 rounds of 2048 waves at 2^20 x 16)
-    const uint32_t Lseg = NB >= 256 ? 8 : (NB >= 4 ? 2 : 1);
+    const size_t maxL = n * (size_t)W;
+    // sorted entries per accumulate thread: 64 at 2^20 x 16 windows (2 rounds of 2048 waves),
+    // fewer for window slices / small MSMs so the grid still fills the chip
+    // (not below 16: a bucket then straddles more threads and the fix-up's serial merge chain
+    // costs more than the emptier accumulate rounds -- measured at 2 windows of 2^20)
+    const uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 8, or
+    // 4 when the segments (one lane each) would not give every SIMD a wave
+    uint32_t Lseg = NB >= 64 ? 8 : (NB >= 4 ? 2 : 1);
+    if (Lseg == 8 && (size_t)(NB / Lseg) * W < 65536) Lseg = 4;
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
     while ((1u << J) < S) J++;
-    const size_t maxL = n * (size_t)W;
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     hipStream_t st = ctx->stream;
 
@@ -282,7 +289,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_TRY(ctx->ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(ctx->ws[WS_SEG].ensure((size_t)S * W * sizeof(Acc)));
     VK_TRY(ctx->ws[WS_TREE].ensure((size_t)S * W * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)W, J)) * sizeof(Acc)));
     VK_TRY(ctx->ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
 
     uint64_t* tmp = ctx->ws[WS_DIGITS].as<uint64_t>();

@@ -43,86 +43,109 @@ __global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__
 //      bit position, so one Horner pass over positions (msm.hip).
 // Serial GPU depth 2 Lseg + 13 EC adds instead of 2 Lseg + ~22 (lo * R by double-and-add)
 // + 24 (per-window reduction) before.
+// I-cache note: an inlined BLS12-381 EC add is ~34 KB of straight-line code (14 asm multiplies),
+// so a kernel with two add call sites in its loop streams ~70 KB per iteration through a 64 KB
+// instruction cache. Every kernel below has ONE add call site: operands are selected first.
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_segsum(const typename C::Acc* __restrict__ buckets,
                                                    const uint32_t* __restrict__ offsets, uint32_t NB, int W,
                                                    uint32_t Lseg, uint32_t S, typename C::Acc* __restrict__ accs,
                                                    typename C::Acc* __restrict__ Rs) {
+    using Acc = typename C::Acc;
     uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t w = gid / S, s = gid % S;
     if (w >= (uint32_t)W) return;
     uint32_t lo = s * Lseg, hi = min(lo + Lseg, NB);
-    typename C::Acc R = C::zero(), acc = C::zero();
-    for (uint32_t j = hi; j-- > lo;) {
-        size_t g = (size_t)w * NB + j;
-        if (offsets[g + 1] > offsets[g]) R = C::add(R, buckets[g]);
-        acc = C::add(acc, R);
+    Acc R = C::zero(), acc = C::zero();
+    // buckets from the top: R += B_j, then acc += R (2 (hi - lo) adds through one call site)
+    for (uint32_t it = 0; it < 2 * (hi - lo); it++) {
+        const bool second = (it & 1) != 0;
+        Acc y;
+        if (second) {
+            y = R;
+        } else {
+            const size_t g = (size_t)w * NB + (hi - 1 - it / 2);
+            y = offsets[g + 1] > offsets[g] ? buckets[g] : C::zero();
+        }
+        const Acc r = C::add(second ? acc : R, y);
+        if (second) acc = r;
+        else R = r;
     }
     accs[gid] = acc;
     Rs[gid] = R;
 }
 
-// wave-level sum of one point per lane: xor-shuffle butterfly (no LDS, no barriers); lane 0 gets
-// the sum of lanes [0, span)
 template <class C>
-__device__ __forceinline__ typename C::Acc wave_sum(typename C::Acc v, uint32_t span = 64) {
-    for (uint32_t m = 1; m < span; m <<= 1) {
-        typename C::Acc o;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+__device__ __forceinline__ typename C::Acc shfl_acc(const typename C::Acc& v, uint32_t m) {
+    typename C::Acc o;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
-        for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
-        v = C::add(v, o);
-    }
-    return v;
+    for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
+    return o;
 }
 
-// stage 1: lane sums BITSUM_K selected items of one (w, q) sum serially, then the wave folds
-// its 64 lane sums (butterfly):  q < J: R_s over s with bit q set (S/2 items);  q == J: acc_s
-// (S items).  partial[(w * (J + 1) + q) * PW + wave_in_sum], PW = ceil(S / (64 K)).
-// Cost model: a wave-level EC add is ~17 us of one SIMD's issue (CDNA4, BLS12-381), so the
-// stage is priced in SIMD rounds: (K + 6) adds on ~W(J+2)S/(128K) waves.
-constexpr uint32_t BITSUM_K = 8;
+// stage 1: lane sums K (msm_bitsum_k) selected items of one (w, q) sum serially, then the wave
+// folds its 64 lane sums (xor butterfly) -- K + 6 iterations of one add:
+//   q < J: R_s over s with bit q set (S/2 items);  q == J: acc_s (S items).
+// partial[(w * (J + 1) + q) * PW + wave_in_sum], PW = ceil(S / (64 K)).
+// Cost model: a wave-level BLS12-381 EC add is ~18 us of one SIMD's issue (a lone wave
+// saturates the SIMD: tools/microbench), priced in SIMD rounds.
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __restrict__ accs,
                                                    const typename C::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
-                                                   uint32_t PW, uint32_t n_waves,
+                                                   uint32_t K, uint32_t PW, uint32_t n_waves,
                                                    typename C::Acc* __restrict__ partial) {
+    using Acc = typename C::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
     const uint32_t sum = gw / PW, wv = gw % PW;
     const uint32_t w = sum / (J + 1), q = sum % (J + 1);
     const uint32_t n_items = q < J ? S / 2 : S;
-    const uint32_t base = wv * 64 * BITSUM_K;
+    const uint32_t base = wv * 64 * K;
     if (base >= n_items) {  // whole wave idle (uniform branch)
         if (lane == 0) partial[gw] = C::zero();
         return;
     }
-    typename C::Acc v = C::zero();
-    for (uint32_t k = 0; k < BITSUM_K; k++) {
-        uint32_t m = base + k * 64 + lane;  // lane-interleaved: coalesced-ish rows
-        if (m >= n_items) break;
-        if (q < J) {
-            uint32_t s = ((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1));
-            v = C::add(v, Rs[(size_t)w * S + s]);
+    const Acc* src = (q < J ? Rs : accs) + (size_t)w * S;
+    Acc v = C::zero();
+    for (uint32_t it = 0; it < K + 6; it++) {
+        Acc o;
+        if (it < K) {
+            const uint32_t m = base + it * 64 + lane;  // lane-interleaved rows
+            const uint32_t idx = q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m;
+            o = m < n_items ? src[idx] : C::zero();
         } else {
-            v = C::add(v, accs[(size_t)w * S + m]);
+            o = shfl_acc<C>(v, 1u << (it - K));
         }
+        v = C::add(v, o);
     }
-    v = wave_sum<C>(v);
     if (lane == 0) partial[gw] = v;
 }
 
-// stage 2: one wave per sum folds its PW partials (PW / 64 per lane, then the butterfly)
+// stage 2: one wave per sum folds its PW partials (ceil(PW/64) per lane, then the butterfly)
 template <class C>
 __global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __restrict__ partial, uint32_t PW,
                                                    typename C::Acc* __restrict__ out) {
+    using Acc = typename C::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
-    typename C::Acc v = C::zero();
-    for (uint32_t k = lane; k < PW; k += 64) v = C::add(v, partial[(size_t)sum * PW + k]);
-    uint32_t span = 1;
-    while (span < PW && span < 64) span <<= 1;
-    v = wave_sum<C>(v, span);
+    uint32_t span = 1, lg = 0;
+    while (span < PW && span < 64) {
+        span <<= 1;
+        lg++;
+    }
+    const uint32_t nk = (PW + 63) / 64;
+    Acc v = C::zero();
+    for (uint32_t it = 0; it < nk + lg; it++) {
+        Acc o;
+        if (it < nk) {
+            const uint32_t k = lane + it * 64;
+            o = k < PW ? partial[(size_t)sum * PW + k] : C::zero();
+        } else {
+            o = shfl_acc<C>(v, 1u << (it - nk));
+        }
+        v = C::add(v, o);
+    }
     if (lane == 0) out[sum] = v;
 }
 
@@ -143,8 +166,9 @@ int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t*
     VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<CI>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB, W,
               Lseg, S, accs, Rs);
     const uint32_t sums = (uint32_t)W * (J + 1);
-    const uint32_t PW = msm_bitsum_pw(S);
-    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (sums * PW * 64 + 255) / 256, 256, 0, accs, Rs, S, J, PW,
+    const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);
+    const uint32_t PW = msm_bitsum_pw(S, K);
+    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (sums * PW * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, PW,
               sums * PW, partial);
     VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<CI>), sums, 64, 0, partial, PW, out);
     return VC_OK;

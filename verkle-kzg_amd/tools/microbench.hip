@@ -119,6 +119,13 @@ int main() {
     printf("{\"bench\":\"fe_mul_bls381_fr_8limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
     ms = timeit(k_fmul<BN254Fq>, blocks, 256, out);
     printf("{\"bench\":\"fe_mul_bn254_fq_8limb\",\"ms\":%.3f,\"Gmul_per_s\":%.2f}\n", ms, muls / ms / 1e6);
+    // occupancy sweep of the 12-limb multiply: 1 / 2 waves per SIMD (256 / 512 blocks of 256)
+    for (int bl : {256, 512, 1024}) {
+        double t = timeit(k_fmul<BLS381Fq>, bl, 1024, out);
+        double m = (double)bl * 256 * 1024 * 4;
+        printf("{\"bench\":\"fe_mul_bls381_fq_blocks_%d\",\"ms\":%.3f,\"Gmul_per_s\":%.2f,\"us_per_mul_per_wave\":%.3f}\n",
+               bl, t, m / t / 1e6, t * 1e3 / (1024.0 * 4));
+    }
     ms = timeit(k_madd<BLS381G1>, blocks, 64, out);
     double madds = (double)blocks * 256 * 64;
     printf("{\"bench\":\"madd_bls381_xyzz_chain\",\"ms\":%.3f,\"Gmadd_per_s\":%.2f}\n", ms, madds / ms / 1e6);
