@@ -90,6 +90,29 @@ def cpu_baseline(curve, n_full, sample):
             "ms_per_msm": per_msm_s * 1e3, "host_cpus": os.cpu_count()}
 
 
+def cpu_commit_baselines(reps=8):
+    """The reference's commit (IPA/KZG::commit = naive inner_product, utils.rs:16-19) restated in
+    C, 1 thread: one width-256 commit on BN254 (configs[0], the reference's own curve) and on
+    Bandersnatch (configs[2]); `reps` commits each."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import cref  # CPU baseline leg only
+    out = {}
+    for name, curve in (("C1_width256_commit_bn254", "bn254"), ("C3_width256_commit_bandersnatch", "bandersnatch")):
+        e = vkzg.Engine(curve, 0)
+        tid = e.random_bases(256, seed=3)
+        xy, inf = e.download_bases(tid)
+        e.close()
+        sc = vkzg.random_scalars(curve, 256 * reps, np.random.default_rng(9))
+        t0 = time.perf_counter()
+        for r in range(reps):
+            cref.msm_arrays(curve, xy, inf, sc[r * 256:(r + 1) * 256], 1)
+        dt = (time.perf_counter() - t0) / reps
+        out[name] = {"value": 1.0 / dt, "unit": "commits/s", "cores": 1, "kind": "port",
+                     "sample": f"{reps} naive width-256 {curve} commits (utils.rs:16-19 in C), 1 thread",
+                     "ms_per_commit": dt * 1e3}
+    return out
+
+
 def kzg_line(a, rank, world, local, dev, stream):
     """configs[3]: KZG commit + open at d = 2^kzg_log_d on BLS12-381 (the north_star's KZG
     curve): commit = MSM over the Lagrange SRS, open = quotient + MSM (kzg/mod.rs:126-154),
@@ -242,7 +265,7 @@ def verkle_line(a, local, stream):
     for i in range(nk):
         t.insert_single(keys[i].tobytes(), vals[i].tobytes())
     t_ins = time.perf_counter() - t0
-    kzg.commit(scheme.LagrangeBasis([1]))  # builds the SRS fixed-base tables, untimed
+    veng.fixed_base_precompute(kzg.table, 8)  # the SRS fixed-base tables, untimed (setup)
     st = t.stats()
     veng.enable_timing(True)
     veng.reset_timing()
@@ -435,6 +458,12 @@ def main():
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(curve, n, a.cpu_sample)
+        out["cpu_baselines_other"] = cpu_commit_baselines()
+        if "kzg" in out:  # configs[3] on the CPU: its two 2^20 MSMs alone (quotient not counted)
+            out["cpu_baselines_other"]["C4_kzg_commit_open_lower_bound"] = {
+                "value": 2 * out["cpu_baseline"]["ms_per_msm"], "unit": "ms", "cores": 1, "kind": "port",
+                "sample": "2 x the naive 2^20 BLS12-381 MSM above (commit + proof MSM); the reference's "
+                          "per-element inversions of the quotient are not counted, so this is a lower bound"}
 
     eng.close()
     if rank == 0:

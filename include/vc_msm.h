@@ -107,6 +107,12 @@ int vc_msm_batch(vc_ctx* ctx, int table_id, size_t width, const uint64_t* scalar
                  int mont, uint64_t* out_xy, uint8_t* out_inf);
 int vc_msm_batch_device(vc_ctx* ctx, int table_id, size_t width, const void* d_scalars,
                         size_t batch, int mont, void* d_out_xy, uint8_t* d_out_inf);
+/* Sparse batched commits (CSR): out[g] = sum_{j in [row_ptr[g], row_ptr[g+1])} s_j * bases[cols[j]].
+ * row_ptr: batch + 1 offsets; cols: column (base index) per non-zero; scalars: 4 u64 per
+ * non-zero. Same fixed-base tables as vc_msm_batch; the work is proportional to the non-zeros
+ * (verkle internal nodes commit ~5 non-zero children of 256, node.rs:262-271). */
+int vc_msm_batch_sparse(vc_ctx* ctx, int table_id, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                        const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
 /* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 16]. */
 int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
 

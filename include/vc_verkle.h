@@ -11,8 +11,10 @@
  * into one batched width-N commit (c1, c2), one batched to_data_item and one batched
  * width-4 commit; then every dirty internal node of one depth goes into one batched
  * width-256 commit, deepest level first -- instead of the reference's one recursive commit
- * per node. The commitment scheme is whatever `table` holds: the KZG Lagrange SRS
- * (vc_kzg_setup) or an IPA CRS (vc_bases_upload), BN254 G1.
+ * per node. Rows are sparse (vc_msm_batch_sparse): an internal node has a few non-zero
+ * children of 256, so only non-zeros are expanded into table points. The commitment scheme
+ * is whatever `table` holds: the KZG Lagrange SRS (vc_kzg_setup) or an IPA CRS
+ * (vc_bases_upload), BN254 G1.
  *
  * Reference quirks kept: the extension commit width is the key length
  * N, not 256; the stem keeps the key's last unit; internal nodes commit at width 256;

@@ -183,3 +183,40 @@ def test_batch_commit(engines, oracle_c, curve):
             assert got_inf[j] == want[1], j
             if not want[1]:
                 assert np.array_equal(got_xy[j], want[0]), j
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_batch_commit_sparse(engines, oracle_c, curve):
+    """vc_msm_batch_sparse (CSR rows) vs the oracle: empty rows, single non-zeros, long rows
+    straddling accumulate threads, repeated columns, a zero scalar, Montgomery input"""
+    import vkzg
+    from pyoracle.curves import CURVES as OC
+    e = engines[curve]
+    C = OC[curve]
+    rng = np.random.default_rng(5)
+    width = 256
+    tid = e.random_bases(width, seed=17)
+    xy, inf = e.download_bases(tid)
+    pts = vkzg.arrays_to_points(curve, xy, inf)
+    lens = [0, 1, 2, 5, 0, 256, 300, 3, 1, 0, 40] + list(rng.integers(0, 12, 60))
+    ptr = [0]
+    cols, vals = [], []
+    for L in lens:
+        for _ in range(int(L)):
+            cols.append(int(rng.integers(0, width)))
+            vals.append(int.from_bytes(rng.bytes(32), "little") % C.r)
+        ptr.append(len(cols))
+    vals[3] = 0
+    got_xy, got_inf = e.msm_batch_sparse(tid, ptr, cols, vkzg.ints_to_limbs(vals))
+    for g in range(len(lens)):
+        lo, hi = ptr[g], ptr[g + 1]
+        want = oracle_c.msm(curve, [pts[c] for c in cols[lo:hi]], vals[lo:hi], 4) if hi > lo else None
+        if curve == "bandersnatch" and want == (0, 1):
+            want = None
+        got = None if got_inf[g] else vkzg.arrays_to_points(curve, got_xy[g:g + 1], got_inf[g:g + 1])[0]
+        assert got == want, g
+    # Montgomery scalars give the same rows
+    R = 1 << (256 if curve != "bls12_381" else 256)
+    mont = [v * R % C.r for v in vals]
+    m_xy, m_inf = e.msm_batch_sparse(tid, ptr, cols, vkzg.ints_to_limbs(mont), mont=True)
+    assert np.array_equal(m_xy, got_xy) and np.array_equal(m_inf, got_inf)

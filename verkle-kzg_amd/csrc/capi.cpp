@@ -304,6 +304,16 @@ int vc_msm_batch_device(vc_ctx* ctx, int id, size_t width, const void* d_sc, siz
     return VC_OK;
 }
 
+int vc_msm_batch_sparse(vc_ctx* ctx, int id, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                        const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf) {
+    if (!ctx || (batch > 0 && (!row_ptr || !out_xy || !out_inf))) return VC_E_INVALID;
+    if (batch > 0 && row_ptr[batch] > 0 && (!cols || !scalars)) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    return vk::msm_batch_sparse(ctx, t, batch, row_ptr, cols, scalars, mont, out_xy, out_inf);
+}
+
 int vc_msm_batch(vc_ctx* ctx, int id, size_t width, const uint64_t* scalars, size_t batch, int mont,
                  uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || (batch > 0 && (!scalars || !out_xy || !out_inf)) || width == 0) return VC_E_INVALID;

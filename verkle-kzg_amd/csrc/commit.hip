@@ -452,6 +452,22 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) {
     return VC_E_INVALID;
 }
 
+// normalise n device accumulators to canonical affine (device outputs)
+int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void* d_out_xy, uint8_t* d_out_inf) {
+    if (n == 0) return VC_OK;
+#define VK_NORM_(C)                                                                                              \
+    VK_LAUNCH(ctx, "normalize_out", (k_normalize<C>), (n + 255) / 256, 256, 0,                                   \
+              reinterpret_cast<const C::Acc*>(d_acc), n, (C::Aff*)nullptr, reinterpret_cast<uint32_t*>(d_out_xy), \
+              d_out_inf)
+    switch (curve) {
+        case VC_CURVE_BN254: VK_NORM_(BN254G1); return VC_OK;
+        case VC_CURVE_BLS12_381: VK_NORM_(BLS381G1); return VC_OK;
+        case VC_CURVE_BANDERSNATCH: VK_NORM_(Bandersnatch); return VC_OK;
+    }
+#undef VK_NORM_
+    return VC_E_INVALID;
+}
+
 int fixed_base_precompute(vc_ctx* ctx, Table* t, int c) {
     switch (t->curve) {
         case VC_CURVE_BN254: return fb_precompute_t<BN254G1>(ctx, t, c);

@@ -74,6 +74,17 @@ enum WsSlot {
     WS_TREE,
     WS_TAIL,
     WS_PIECE,
+    WS_SP_RP,
+    WS_SP_COLS,
+    WS_SP_SC,
+    WS_SP_CNT,
+    WS_SP_EOFF,
+    WS_SP_OFF,
+    WS_SP_ROWS,
+    WS_SP_XY,
+    WS_SP_INF,
+    WS_SP_RC,
+    WS_SP_CHUNKS,
     WS_COUNT_
 };
 
@@ -145,6 +156,9 @@ int bases_fill(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf, si
 int bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id);
 int bases_download(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf);
 int fixed_base_precompute(vc_ctx* ctx, Table* t, int c);
+int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void* d_out_xy, uint8_t* d_out_inf);
+int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                     const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
 int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf);

@@ -354,6 +354,210 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     return VC_OK;
 }
 
+// ------------------------------------------------------------------ sparse batched commits
+// Rows of a CSR matrix (row g = commit g: non-zero (column i, scalar s) pairs) against the
+// fixed-base window tables of a table: every non-zero expands to its non-zero signed window
+// digits, each a table point T[i][w][|d|-1] -- so the entries of a row are contiguous and the
+// rows play the buckets of the Pippenger accumulate: the same balanced k_msm_accumulate (M
+// entries per thread, rows straddling threads merged by the fix-up) sums them. For verkle
+// nodes (~5 non-zeros of 256 per internal node, 2 of N per extension row) this replaces
+// dense width-256 rows.
+template <class Fr>
+__global__ void k_sparse_count(const uint32_t* __restrict__ sc, size_t nnz, int mont, int c, int W,
+                               uint32_t* __restrict__ cnt) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    fe<Fr> s = load_scalar<Fr>(sc, j);
+    if (mont) s = fe_from_mont<Fr>(s);
+    uint32_t k = 0;
+    for_each_digit<Fr>(s, c, W, [&](int, int32_t d) { k += d != 0; });
+    cnt[j] = k;
+}
+
+template <class Fr>
+__global__ void k_sparse_expand(const uint32_t* __restrict__ sc, const uint32_t* __restrict__ cols, size_t nnz,
+                                int mont, int c, int W, const uint32_t* __restrict__ eoff,
+                                uint32_t* __restrict__ entries) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nnz) return;
+    fe<Fr> s = load_scalar<Fr>(sc, j);
+    if (mont) s = fe_from_mont<Fr>(s);
+    const uint32_t NBk = 1u << (c - 1), i = cols[j];
+    uint32_t pos = eoff[j];
+    for_each_digit<Fr>(s, c, W, [&](int w, int32_t d) {
+        if (d != 0)
+            entries[pos++] = (((uint32_t)i * (uint32_t)W + (uint32_t)w) * NBk + (uint32_t)(d < 0 ? -d : d) - 1) |
+                             (d < 0 ? 0x80000000u : 0u);
+    });
+}
+
+// row offsets in entry space; empty rows get the identity (the accumulate never writes them)
+template <class C>
+__global__ void k_sparse_rows(const uint64_t* __restrict__ row_ptr, const uint32_t* __restrict__ eoff, size_t batch,
+                              uint32_t* __restrict__ offsets, typename C::Acc* __restrict__ rows) {
+    size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g > batch) return;
+    offsets[g] = eoff[row_ptr[g]];
+    if (g < batch && eoff[row_ptr[g + 1]] == eoff[row_ptr[g]]) rows[g] = C::zero();
+}
+
+// row g = sum of its chunks [rc[g], rc[g+1]) -- one wave per row: lanes load chunk sums (a
+// strided loop when a row has more than 64), then an xor butterfly over the used lanes
+template <class C>
+__global__ void __launch_bounds__(64) k_sparse_combine(const typename C::Acc* __restrict__ chunks,
+                                                      const uint32_t* __restrict__ rc, typename C::Acc* __restrict__ rows) {
+    using Acc = typename C::Acc;
+    const uint32_t g = blockIdx.x, lane = threadIdx.x;
+    const uint32_t b = rc[g], n = rc[g + 1] - b;
+    if (n == 1) {  // uniform per wave
+        if (lane == 0) rows[g] = chunks[b];
+        return;
+    }
+    uint32_t span = 1, lg = 0;
+    while (span < n && span < 64) {
+        span <<= 1;
+        lg++;
+    }
+    const uint32_t nk = (n + 63) / 64;
+    Acc v = C::zero();
+    for (uint32_t it = 0; it < nk + lg; it++) {  // one add call site (see msm_tail.hip)
+        Acc o;
+        if (it < nk) {
+            const uint32_t k = lane + it * 64;
+            o = k < n ? chunks[b + k] : C::zero();
+        } else {
+            const uint32_t m = 1u << (it - nk);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+            for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
+        }
+        v = C::add(v, o);
+    }
+    if (lane == 0) rows[g] = v;
+}
+
+template <class C, class Fr>
+static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                              const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf) {
+    using Acc = typename C::Acc;
+    using Aff = typename C::Aff;
+    if (batch == 0) return VC_OK;
+    const size_t nnz = row_ptr[batch];
+    for (size_t g = 0; g < batch; g++)
+        if (row_ptr[g + 1] < row_ptr[g]) return VC_E_INVALID;
+    for (size_t j = 0; j < nnz; j++)
+        if (cols[j] >= t->n) return VC_E_RANGE;
+    if (t->fb_c == 0) VK_TRY(fixed_base_precompute(ctx, t, 8));
+    const int c = t->fb_c, W = t->fb_W;
+    // rows are cut into chunks of <= CHNZ non-zeros (the accumulate's buckets), so a long row
+    // (e.g. a verkle root: 256 children x W windows) does not become one bucket straddling
+    // hundreds of threads -- whose pieces the fix-up would add serially; chunk sums are folded
+    // per row by k_sparse_combine
+    const size_t CHNZ = 4;
+    std::vector<uint64_t> cptr{0};
+    std::vector<uint32_t> rc(batch + 1);
+    for (size_t g = 0; g < batch; g++) {
+        rc[g] = (uint32_t)(cptr.size() - 1);
+        if (row_ptr[g + 1] == row_ptr[g]) cptr.push_back(row_ptr[g]);  // empty row -> one empty chunk
+        for (uint64_t j = row_ptr[g]; j < row_ptr[g + 1]; j += CHNZ) cptr.push_back(std::min<uint64_t>(j + CHNZ, row_ptr[g + 1]));
+    }
+    rc[batch] = (uint32_t)(cptr.size() - 1);
+    const size_t nch = cptr.size() - 1;
+    if ((uint64_t)t->n * W << (c - 1) >= (1ull << 31)) return VC_E_RANGE;  // entry index + sign bit
+    const size_t maxL = nnz * (size_t)W;
+    if (maxL >= 0xffffffffull) return VC_E_RANGE;
+    hipStream_t st = ctx->stream;
+    // grow-only ctx workspaces (the MSM's own slots for entries / carries / scan scratch: the
+    // two paths never run concurrently on one ctx)
+    DevBuf& d_rp = ctx->ws[WS_SP_RP];
+    DevBuf& d_cols = ctx->ws[WS_SP_COLS];
+    DevBuf& d_sc = ctx->ws[WS_SP_SC];
+    DevBuf& d_cnt = ctx->ws[WS_SP_CNT];
+    DevBuf& d_eoff = ctx->ws[WS_SP_EOFF];
+    DevBuf& d_ent = ctx->ws[WS_SORTED];
+    DevBuf& d_off = ctx->ws[WS_SP_OFF];
+    DevBuf& d_rows = ctx->ws[WS_SP_ROWS];
+    DevBuf& d_carry = ctx->ws[WS_CARRY];
+    DevBuf& d_thr = ctx->ws[WS_THROUGH];
+    DevBuf& d_own = ctx->ws[WS_OWNER];
+    DevBuf& d_ownb = ctx->ws[WS_OWNER_B];
+    DevBuf& d_tmp = ctx->ws[WS_SCAN_TMP];
+    DevBuf& d_xy = ctx->ws[WS_SP_XY];
+    DevBuf& d_inf = ctx->ws[WS_SP_INF];
+    const uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
+    DevBuf& d_rc = ctx->ws[WS_SP_RC];
+    DevBuf& d_chunks = ctx->ws[WS_SP_CHUNKS];
+    VK_TRY(d_rp.ensure((nch + 1) * 8));
+    VK_TRY(d_rc.ensure((batch + 1) * 4));
+    VK_TRY(d_chunks.ensure(nch * sizeof(Acc)));
+    VK_TRY(d_cols.ensure(std::max<size_t>(nnz, 1) * 4));
+    VK_TRY(d_sc.ensure(std::max<size_t>(nnz, 1) * 32));
+    VK_TRY(d_cnt.ensure((nnz + 1) * 4));
+    VK_TRY(d_eoff.ensure((nnz + 1) * 4));
+    VK_TRY(d_ent.ensure(std::max<size_t>(maxL, 1) * 4));
+    VK_TRY(d_off.ensure((nch + 1) * 4));
+    VK_TRY(d_rows.ensure(batch * sizeof(Acc)));
+    VK_TRY(d_carry.ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(d_thr.ensure((size_t)(Tmax + 8)));
+    VK_TRY(d_own.ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(d_ownb.ensure((size_t)(Tmax + 8) * 4));
+    VK_TRY(d_xy.ensure(batch * 2 * C::F::N * 4));
+    VK_TRY(d_inf.ensure(batch));
+    VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, cptr.data(), (nch + 1) * 8, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, rc.data(), (batch + 1) * 4, hipMemcpyHostToDevice, st));
+    if (nnz) {
+        VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, cols, nnz * 4, hipMemcpyHostToDevice, st));
+        VK_CHECK_HIP(hipMemcpyAsync(d_sc.p, scalars, nnz * 32, hipMemcpyHostToDevice, st));
+    }
+    VK_CHECK_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + nnz, 0, 4, st));
+    if (nnz)
+        VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(), nnz, mont,
+                  c, W, d_cnt.as<uint32_t>());
+    size_t tmp_bytes = 0;
+    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
+                                                  nnz + 1, st));
+    VK_TRY(d_tmp.ensure(std::max<size_t>(tmp_bytes, 1)));
+    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp.p, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
+                                                  nnz + 1, st));
+    if (nnz)
+        VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(),
+                  d_cols.as<uint32_t>(), nnz, mont, c, W, d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
+    VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, d_rp.as<uint64_t>(),
+              d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
+    const Aff* tab = t->fb.as<Aff>();
+    if (Tmax > 0) {  // all-zero rows only: k_sparse_rows already set every chunk to the identity
+        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab,
+                  d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(),
+                  d_carry.as<Acc>(), d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>());
+        VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
+                                 d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>()));
+    }
+    VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
+              d_rc.as<uint32_t>(), d_rows.as<Acc>());
+    VK_TRY(normalize_to_canon(ctx, ctx->curve, d_rows.p, batch, d_xy.p, d_inf.as<uint8_t>()));
+    VK_CHECK_HIP(hipMemcpyAsync(out_xy, d_xy.p, batch * 2 * C::F::N * 4, hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipMemcpyAsync(out_inf, d_inf.p, batch, hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipStreamSynchronize(st));  // host staging vectors die on return
+    return VC_OK;
+}
+
+int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                     const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf) {
+    switch (t->curve) {
+        case VC_CURVE_BN254:
+            return msm_batch_sparse_t<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, cols, scalars, mont, out_xy, out_inf);
+        case VC_CURVE_BLS12_381:
+            return msm_batch_sparse_t<BLS381G1, BLS381Fr>(ctx, t, batch, row_ptr, cols, scalars, mont, out_xy,
+                                                           out_inf);
+        case VC_CURVE_BANDERSNATCH:
+            return msm_batch_sparse_t<Bandersnatch, BandFr>(ctx, t, batch, row_ptr, cols, scalars, mont, out_xy,
+                                                             out_inf);
+    }
+    return VC_E_INVALID;
+}
+
 int msm_windows(int curve, size_t n, int* c, int* W) {
     int bits = curve == VC_CURVE_BN254 ? BN254Fr::BITS : curve == VC_CURVE_BLS12_381 ? BLS381Fr::BITS : BandFr::BITS;
     *c = choose_window(n);

@@ -1,7 +1,11 @@
 // Verkle tree (reference verkle-tree/src/{lib,node}.rs) with level-batched commitments on the
-// GPU engine. Host data structure + orchestration; all commitments go through vc_msm_batch
-// (fixed-base batched commits) and vc_to_data_item_batch. See include/vc_verkle.h.
+// GPU engine. Host data structure + orchestration; all commitments go through
+// vc_msm_batch_sparse (CSR rows of non-zeros against the fixed-base tables) and
+// vc_to_data_item_batch. See include/vc_verkle.h.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <array>
 #include <cstring>
 #include <map>
@@ -27,12 +31,32 @@ struct VNode {
     uint64_t item[4] = {0};  // to_data_item of the commitment (canonical Fr)
 };
 
-// LE bytes -> canonical Fr words (from_le_bytes_mod_order); < 31 bytes is already < r
+// LE bytes -> canonical Fr words (from_le_bytes_mod_order): < 31 bytes is already < r; 32
+// bytes (< 2^256 < 6r) by at most five subtractions of r; longer inputs by the generic path
 static void item_of_bytes(const uint8_t* b, size_t len, uint64_t out[4]) {
-    if (len <= 31) {
+    if (len <= 32) {
         uint8_t w[32] = {0};
         memcpy(w, b, len);
         memcpy(out, w, 32);
+        static const uint64_t R[4] = {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
+                                      0x30644e72e131a029ULL};  // BN254 r
+        for (int k = 0; k < 6; k++) {
+            bool ge = false;
+            for (int i = 3; i >= 0; i--)
+                if (out[i] != R[i]) {
+                    ge = out[i] > R[i];
+                    break;
+                } else if (i == 0) {
+                    ge = true;
+                }
+            if (!ge) break;
+            unsigned __int128 br = 0;
+            for (int i = 0; i < 4; i++) {
+                unsigned __int128 d = (unsigned __int128)out[i] - R[i] - (uint64_t)br;
+                out[i] = (uint64_t)d;
+                br = (d >> 64) & 1;
+            }
+        }
         return;
     }
     vk::mont_to_canon<vk::BN254Fr>(vk::fe_from_le_bytes_mod<vk::BN254Fr>(b, len), out);
@@ -207,6 +231,14 @@ int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, siz
 int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || !t || !out_xy || !out_inf) return VC_E_INVALID;
     const int N = t->N;
+    static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
+    auto tic = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!verbose) return;
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[verkle] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tic).count());
+        tic = now;
+    };
     // dirty nodes reachable from the root, with depth (clean subtrees are skipped: an insert
     // clears every commitment on its path, so a clean node has clean descendants)
     std::vector<int> exts;
@@ -225,44 +257,84 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
         internals[depth].push_back(id);
         for (auto& kv : n.children) stack.push_back({kv.second, depth + 1});
     }
-    auto commit_items = [&](size_t width, const std::vector<uint64_t>& sc, size_t batch, std::vector<uint64_t>& xy,
-                            std::vector<uint8_t>& inf, std::vector<uint64_t>& items) -> int {
-        xy.assign(batch * 8, 0);
-        inf.assign(batch, 0);
-        items.assign(batch * 4, 0);
-        if (batch == 0) return VC_OK;
-        VK_TRY(vc_msm_batch(ctx, table, width, sc.data(), batch, 0, xy.data(), inf.data()));
-        return vc_to_data_item_batch(ctx, xy.data(), inf.data(), batch, items.data());
+    // batched sparse commits (vc_msm_batch_sparse): rows of (column, value) non-zeros
+    struct Rows {
+        std::vector<uint64_t> ptr{0};
+        std::vector<uint32_t> cols;
+        std::vector<uint64_t> vals;
+        void add(uint32_t col, const uint64_t* v) {
+            if (!(v[0] | v[1] | v[2] | v[3])) return;  // zero scalars contribute nothing
+            cols.push_back(col);
+            vals.insert(vals.end(), v, v + 4);
+        }
+        void end_row() { ptr.push_back(cols.size()); }
+        size_t n() const { return ptr.size() - 1; }
+    };
+    lap("collect dirty");
+    auto commit_rows = [&](const Rows& r, std::vector<uint64_t>& xy, std::vector<uint8_t>& inf,
+                           std::vector<uint64_t>& items) -> int {
+        const size_t B = r.n();
+        xy.assign(B * 8, 0);
+        inf.assign(B, 0);
+        items.assign(B * 4, 0);
+        if (B == 0) return VC_OK;
+        lap("build rows");
+        VK_TRY(vc_msm_batch_sparse(ctx, table, B, r.ptr.data(), r.cols.data(), r.vals.data(), 0, xy.data(), inf.data()));
+        lap("sparse commit");
+        int st = vc_to_data_item_batch(ctx, xy.data(), inf.data(), B, items.data());
+        lap("to_data_item");
+        return st;
     };
     std::vector<uint64_t> xy, items, xy2, items2;
     std::vector<uint8_t> inf, inf2;
     // extension nodes: c1, c2 (width N), then [1, stem, c1, c2] (width 4)
     if (!exts.empty()) {
         const size_t E = exts.size();
-        std::vector<uint64_t> sc(2 * E * N * 4, 0);
+        Rows r12;
+        // (position, value) writes of c1 / c2 in leaf order; a later write to the same
+        // position overwrites, as c1_values[index] = ... does (node.rs:226-239)
+        std::vector<std::pair<uint32_t, std::array<uint64_t, 4>>> half[2];
+        auto put = [&](int h, uint32_t pos, const uint64_t* v) {
+            for (auto& pv : half[h])
+                if (pv.first == pos) {
+                    memcpy(pv.second.data(), v, 32);
+                    return;
+                }
+            std::array<uint64_t, 4> a;
+            memcpy(a.data(), v, 32);
+            half[h].push_back({pos, a});
+        };
         for (size_t e = 0; e < E; e++) {
             const VNode& n = t->nodes[exts[e]];
+            half[0].clear();
+            half[1].clear();
             for (auto& kv : n.leaves) {
                 const size_t index = kv.first;
                 uint64_t lo[4], hi[4];
                 item_of_bytes(kv.second.data(), 16, lo);
                 item_of_bytes(kv.second.data() + 16, 16, hi);
-                const size_t il = (2 * index) % N, ih = (2 * index + 1) % N;
-                uint64_t* base = &sc[(2 * e + (index < (size_t)(N / 2) ? 0 : 1)) * N * 4];
-                memcpy(base + 4 * il, lo, 32);
-                memcpy(base + 4 * ih, hi, 32);
+                const int h = index < (size_t)(N / 2) ? 0 : 1;
+                put(h, (uint32_t)((2 * index) % N), lo);
+                put(h, (uint32_t)((2 * index + 1) % N), hi);
+            }
+            for (int h = 0; h < 2; h++) {
+                for (auto& pv : half[h]) r12.add(pv.first, pv.second.data());
+                r12.end_row();
             }
         }
-        VK_TRY(commit_items(N, sc, 2 * E, xy, inf, items));
-        std::vector<uint64_t> ed(E * 4 * 4, 0);
+        VK_TRY(commit_rows(r12, xy, inf, items));
+        Rows rx;
         for (size_t e = 0; e < E; e++) {
             const VNode& n = t->nodes[exts[e]];
-            ed[e * 16 + 0] = 1;
-            item_of_bytes(n.stem.data(), N, &ed[e * 16 + 4]);  // bytes_to_item(stem.to_bytes())
-            memcpy(&ed[e * 16 + 8], &items[(2 * e) * 4], 32);
-            memcpy(&ed[e * 16 + 12], &items[(2 * e + 1) * 4], 32);
+            uint64_t one[4] = {1, 0, 0, 0}, stem_item[4];
+            item_of_bytes(n.stem.data(), N, stem_item);  // bytes_to_item(stem.to_bytes())
+            rx.add(0, one);
+            rx.add(1, stem_item);
+            rx.add(2, &items[(2 * e) * 4]);
+            rx.add(3, &items[(2 * e + 1) * 4]);
+            rx.end_row();
         }
-        VK_TRY(commit_items(4, ed, E, xy2, inf2, items2));
+        VK_TRY(commit_rows(rx, xy2, inf2, items2));
         for (size_t e = 0; e < E; e++) {
             VNode& n = t->nodes[exts[e]];
             memcpy(n.cxy, &xy2[e * 8], 64);
@@ -274,12 +346,13 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
     // internal nodes, deepest level first (HACK in the reference: width hard-coded 256)
     for (int depth = (int)internals.size() - 1; depth >= 0; depth--) {
         const std::vector<int>& lv = internals[depth];
-        const size_t B = lv.size();
-        std::vector<uint64_t> sc(B * 256 * 4, 0);
-        for (size_t b = 0; b < B; b++)
-            for (auto& kv : t->nodes[lv[b]].children) memcpy(&sc[(b * 256 + kv.first) * 4], t->nodes[kv.second].item, 32);
-        VK_TRY(commit_items(256, sc, B, xy, inf, items));
-        for (size_t b = 0; b < B; b++) {
+        Rows ri;
+        for (int id : lv) {
+            for (auto& kv : t->nodes[id].children) ri.add(kv.first, t->nodes[kv.second].item);
+            ri.end_row();
+        }
+        VK_TRY(commit_rows(ri, xy, inf, items));
+        for (size_t b = 0; b < lv.size(); b++) {
             VNode& n = t->nodes[lv[b]];
             memcpy(n.cxy, &xy[b * 8], 64);
             n.cinf = inf[b];

@@ -35,6 +35,7 @@ SIGNATURES = {
     "vc_point_words": (c_int, [c_int]),
     "vc_msm_device_partial": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P]),
     "vc_device_mad_rate": (c_int, [c_void_p, P]),
+    "vc_msm_batch_sparse": (c_int, [c_void_p, c_int, c_size_t, P, P, P, c_int, P, P]),
     "vc_verkle_new": (c_void_p, [c_int]),
     "vc_verkle_free": (None, [c_void_p]),
     "vc_verkle_insert": (c_int, [c_void_p, P, P]),
@@ -43,6 +44,7 @@ SIGNATURES = {
     "vc_verkle_commitment": (c_int, [c_void_p, c_int, c_void_p, P, P]),
     "vc_verkle_stats": (c_int, [c_void_p, P, P, P]),
     "vc_transcript_reserve": (None, [c_void_p, c_size_t]),
+    "vc_msm_batch_sparse": (c_int, [c_void_p, c_int, c_size_t, P, P, P, c_int, P, P]),
     "vc_verkle_new": (c_void_p, [c_int]),
     "vc_verkle_free": (None, [c_void_p]),
     "vc_verkle_insert": (c_int, [c_void_p, P, P]),

@@ -216,6 +216,19 @@ class Engine:
                                  _ptr(oinf)), "vc_msm_batch")
         return out, oinf
 
+    def msm_batch_sparse(self, table, row_ptr, cols, scalars, mont=False):
+        """CSR batched commits: row g = sum over j in [row_ptr[g], row_ptr[g+1]) of
+        scalars[j] * bases[cols[j]]. Returns ((batch, 2*NL) uint64, (batch,) uint8)."""
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.uint64)
+        cols = np.ascontiguousarray(cols, dtype=np.uint32)
+        scalars = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+        batch = len(row_ptr) - 1
+        xy = np.zeros((max(batch, 1), 2 * NL[self.curve]), dtype=np.uint64)
+        inf = np.zeros(max(batch, 1), dtype=np.uint8)
+        check(lib().vc_msm_batch_sparse(self.h, table, batch, _ptr(row_ptr), _ptr(cols), _ptr(scalars),
+                                        1 if mont else 0, _ptr(xy), _ptr(inf)), "vc_msm_batch_sparse")
+        return xy[:batch], inf[:batch]
+
     def msm_batch_device(self, table, width, d_scalars_ptr, batch, d_out_xy_ptr, d_out_inf_ptr, mont=False):
         check(lib().vc_msm_batch_device(self.h, table, width, ctypes.c_void_p(d_scalars_ptr), batch,
                                         1 if mont else 0, ctypes.c_void_p(d_out_xy_ptr),
