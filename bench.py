@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-mp", action="store_true", help="skip the IPA multiproof line (configs[4])")
     ap.add_argument("--mp-log-q", type=int, default=16)
     ap.add_argument("--no-verkle", action="store_true", help="skip the verkle-tree commitment line (8(f) rank 1)")
+    ap.add_argument("--no-ipa", action="store_true", help="skip the single IPA prove/verify line (benches/ipa.rs)")
     ap.add_argument("--verkle-keys", type=int, default=1 << 16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
     return ap.parse_args()
@@ -244,6 +245,39 @@ def mp_line(a, rank, world, local, dev, stream):
                         f"split over {world} rank(s)", "ms_per_multiproof": dt * 1e3,
             "host_transcript_ms": t_begin * 1e3, "kernel_ms": kms, "algorithmic_bytes_per_unit": alg,
             "achieved_GBps": alg / dt / 1e9, "d_inf": mp["d"] is None}
+
+
+def ipa_line(local, stream, batch=256):
+    """The reference's IPA bench shapes (vector-commit/benches/ipa.rs:79-109, N = 256, BN254,
+    data r + i): single commit, prove in / out of domain, verify in domain -- latency of one
+    call each -- and a batch of independent proofs in one vc_ipa_prove call (proofs/s)."""
+    from vkzg import scheme
+    ieng = vkzg.Engine("bn254", local)
+    ieng.set_stream(stream.cuda_stream)
+    N = 256
+    ipa = scheme.IPA(ieng, N, scheme.ipa_crs(N + 1, max_=512))
+    r0 = 0x1234567890ABCDEF1234567890ABCDEF
+    datas = [scheme.LagrangeBasis([(r0 * (k + 1) + i) % scheme.R_BN254 for i in range(N)]) for k in range(batch)]
+    coms = ipa.commit_batch(datas)
+
+    def timed(f, reps=5):
+        f()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = f()
+        return (time.perf_counter() - t0) / reps * 1e3, r
+
+    out = {"workload": "IPA N = 256 on BN254 (benches/ipa.rs shapes, data r + i)"}
+    out["commit_ms"], _ = timed(lambda: ipa.commit(datas[0]))
+    out["prove_in_domain_ms"], prf = timed(lambda: ipa.prove_point(coms[0], 77, datas[0]))
+    out["prove_out_domain_ms"], _ = timed(lambda: ipa.prove_point(coms[0], N * 7 + 3, datas[0]))
+    out["verify_in_domain_ms"], ok = timed(lambda: ipa.verify_point(coms[0], 77, prf))
+    assert ok
+    pts = [(31 * k) % N for k in range(batch)]
+    ms, _ = timed(lambda: ipa.prove_batch_points(coms, pts, datas), reps=2)
+    out["batch_prove"] = {"proofs": batch, "ms": ms, "proofs_per_s": batch / ms * 1e3}
+    ieng.close()
+    return out
 
 
 def verkle_line(a, local, stream):
@@ -452,6 +486,9 @@ def main():
 
     if not a.no_mp:
         out["multiproof"] = mp_line(a, rank, world, local, dev, stream)
+
+    if rank == 0 and not a.no_ipa:
+        out["ipa"] = ipa_line(local, stream)
 
     if rank == 0 and not a.no_verkle:
         out["verkle"] = verkle_line(a, local, stream)
