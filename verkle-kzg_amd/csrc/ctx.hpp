@@ -85,6 +85,10 @@ enum WsSlot {
     WS_SP_INF,
     WS_SP_RC,
     WS_SP_CHUNKS,
+    WS_CARRY2,
+    WS_NXT,
+    WS_NXT2,
+    WS_CHAIN,
     WS_COUNT_
 };
 

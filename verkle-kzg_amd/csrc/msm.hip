@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(
     const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename C::Acc* __restrict__ buckets, typename C::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename C::Acc* __restrict__ owner_piece,
-    uint32_t* __restrict__ owner_bucket) {
+    uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max) {
     using Acc = typename C::Acc;
     using Aff = typename C::Aff;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -202,7 +202,11 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(
                 buckets[b] = acc;
             } else if (left_open) {
                 carry_in[t] = acc;
-                through[t] = right_open ? 1 : 0;
+                through[t] = right_open ? 2 : 1;  // 1: carry piece ending here, 2: bucket continues
+                if (!right_open) {  // chain end: chain length = carry threads of this bucket
+                    const uint32_t L = t - offsets[b] / M;
+                    if (L >= 2) atomicMax(chain_max, L);
+                }
             } else {
                 owner_piece[t] = acc;
                 owner_bucket[t] = b;
@@ -328,9 +332,12 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
               FB, NBC, nblk, base, tmp);
     VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= n*W
+    VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
+    uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
+    VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
     VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, sorted, offsets,
-              NBtot, M, buckets, carry, through, owner, owner_b);
-    VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b));
+              NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
+    VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max));
     VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
     std::vector<Acc> ht((size_t)W * (J + 1));
     VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
@@ -528,11 +535,14 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
               d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
     const Aff* tab = t->fb.as<Aff>();
     if (Tmax > 0) {  // all-zero rows only: k_sparse_rows already set every chunk to the identity
+        VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
+        uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
+        VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
         VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab,
                   d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(),
-                  d_carry.as<Acc>(), d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>());
+                  d_carry.as<Acc>(), d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max);
         VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
-                                 d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>()));
+                                 d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max));
     }
     VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
               d_rc.as<uint32_t>(), d_rows.as<Acc>());

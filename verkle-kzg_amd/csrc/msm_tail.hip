@@ -3,6 +3,8 @@
 // which halves the latency of a serial EC chain -- do not slow every rebuild of msm.hip).
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "ctx.hpp"
 #include "ec.hpp"
 #include "msm_tail.hpp"
@@ -11,26 +13,56 @@ namespace vk {
 
 constexpr uint32_t NONE_T = 0xffffffffu;
 
+// ---- fix-up of buckets that straddle accumulate threads. Thread u's carry piece (through[u]
+// = 1: the bucket ends in u; 2: it continues into u + 1) belongs to the bucket whose owner
+// thread t0 < u holds the first piece. The carry pieces of one bucket form a chain u0 = t0+1
+// .. u1; its sum is built by pointer jumping -- round r adds the piece 2^r threads ahead --
+// so a bucket spanning L threads costs ceil(log2 L) parallel rounds, not L serial adds (an
+// all-equal-scalar 2^20 MSM has one 2^20-entry bucket per window: L = 16k threads). The
+// accumulate reports the longest chain (chain_max, only when >= 2), read back once.
+template <class C>
+__global__ void __launch_bounds__(256) k_fixup_init(const uint8_t* __restrict__ through, uint32_t Tmax,
+                                                   const uint32_t* __restrict__ Lp, uint32_t M,
+                                                   uint32_t* __restrict__ nxt) {
+    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = (*Lp + M - 1) / M;  // accumulate threads that ran
+    if (u >= T || u >= Tmax) return;
+    nxt[u] = through[u] == 2 && u + 1 < T ? u + 1 : NONE_T;
+}
+
+template <class C>
+__global__ void __launch_bounds__(256) k_fixup_jump(const typename C::Acc* __restrict__ val_in,
+                                                   const uint32_t* __restrict__ nxt_in,
+                                                   const uint8_t* __restrict__ through, uint32_t Tmax,
+                                                   const uint32_t* __restrict__ Lp, uint32_t M,
+                                                   typename C::Acc* __restrict__ val_out,
+                                                   uint32_t* __restrict__ nxt_out) {
+    uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = (*Lp + M - 1) / M;
+    if (u >= T || u >= Tmax || through[u] == 0) return;  // no carry piece in thread u
+    const uint32_t n = nxt_in[u];
+    if (n == NONE_T) {
+        val_out[u] = val_in[u];
+        nxt_out[u] = NONE_T;
+        return;
+    }
+    val_out[u] = C::add(val_in[u], val_in[n]);
+    nxt_out[u] = nxt_in[n];
+}
+
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__ buckets,
-                                                  const typename C::Acc* __restrict__ carry_in,
-                                                  const uint8_t* __restrict__ through,
+                                                  const typename C::Acc* __restrict__ chain_sum,
                                                   const typename C::Acc* __restrict__ owner_piece,
                                                   const uint32_t* __restrict__ owner_bucket,
                                                   uint32_t Tmax, const uint32_t* __restrict__ Lp, uint32_t M) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t T = (*Lp + M - 1) / M;  // accumulate threads that ran
+    const uint32_t T = (*Lp + M - 1) / M;
     if (t >= T || t >= Tmax) return;
     uint32_t b = owner_bucket[t];
     if (b == NONE_T) return;
-    typename C::Acc acc = owner_piece[t];
-    uint32_t u = t + 1;
-    while (u < T) {
-        acc = C::add(acc, carry_in[u]);
-        if (!through[u]) break;
-        u++;
-    }
-    buckets[b] = acc;
+    // an owner piece exists only when the bucket continues into t + 1 (< T by construction)
+    buckets[b] = C::add(owner_piece[t], chain_sum[t + 1]);
 }
 
 // ------------------------------------------------------------------ bucket reduction
@@ -150,10 +182,33 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __res
 }
 
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets, const typename C::Acc* carry,
-                   const uint8_t* through, const typename C::Acc* owner, const uint32_t* owner_b) {
-    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<typename C::Inl>), (T + 255) / 256, 256, 0, buckets, carry, through,
-              owner, owner_b, T, Lp, M);
+int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
+                   typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
+                   const uint32_t* owner_b, const uint32_t* d_chain_max) {
+    using CI = typename C::Inl;
+    using Acc = typename C::Acc;
+    uint32_t Lmax = 0;
+    VK_CHECK_HIP(hipMemcpyAsync(&Lmax, d_chain_max, 4, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    const Acc* sum = carry;
+    if (Lmax >= 2) {
+        VK_TRY(ctx->ws[WS_CARRY2].ensure((size_t)(T + 8) * sizeof(Acc)));
+        VK_TRY(ctx->ws[WS_NXT].ensure((size_t)(T + 8) * 4));
+        VK_TRY(ctx->ws[WS_NXT2].ensure((size_t)(T + 8) * 4));
+        Acc* va = carry;
+        Acc* vb = ctx->ws[WS_CARRY2].as<Acc>();
+        uint32_t* na = ctx->ws[WS_NXT].as<uint32_t>();
+        uint32_t* nb = ctx->ws[WS_NXT2].as<uint32_t>();
+        VK_LAUNCH(ctx, "msm_fixup_init", (k_fixup_init<CI>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
+        for (uint32_t span = 1; span < Lmax; span <<= 1) {
+            VK_LAUNCH(ctx, "msm_fixup_jump", (k_fixup_jump<CI>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
+                      nb);
+            std::swap(va, vb);
+            std::swap(na, nb);
+        }
+        sum = va;
+    }
+    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<CI>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
     return VC_OK;
 }
 
@@ -175,8 +230,8 @@ int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t*
 }
 
 #define VK_INST_TAIL(C)                                                                                        \
-    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, const C::Acc*, const uint8_t*, const C::Acc*,  \
-                                   const uint32_t*);                                                           \
+    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, C::Acc*, const uint8_t*,  \
+                                   const C::Acc*, const uint32_t*, const uint32_t*);                           \
     template int msm_tail_reduce<C>(vc_ctx*, const C::Acc*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
                                     uint32_t, C::Acc*, C::Acc*, C::Acc*, C::Acc*);
 VK_INST_TAIL(BN254G1)

@@ -15,8 +15,9 @@ inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J) {
 // partial slots per (window, bit) sum of the bit-sum stage (K items per lane, 64 lanes)
 inline uint32_t msm_bitsum_pw(uint32_t S, uint32_t K) { return (S + 64 * K - 1) / (64 * K); }
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets, const typename C::Acc* carry,
-                   const uint8_t* through, const typename C::Acc* owner, const uint32_t* owner_b);
+int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
+                   typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
+                   const uint32_t* owner_b, const uint32_t* d_chain_max);
 template <class C>
 int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, typename C::Acc* accs, typename C::Acc* Rs,
