@@ -78,6 +78,15 @@ int vc_ipa_prove(vc_ctx* ctx, int table, size_t N, const uint64_t* data, const u
 int vc_ipa_verify(vc_ctx* ctx, int table, size_t N, const uint64_t* com_xy, uint8_t com_inf,
                   const uint64_t* point, const vc_ipa_proof* proof, vc_transcript* transcript,
                   int* result);
+/* prove_commitment (:199-234): proof of knowledge of the first n = data.max() + 1 values
+ * behind a commitment (L, R per round, tip; y is set to 0). n must be a power of two: the
+ * reference's assert in vec_add_and_distribute (utils.rs:37) panics on any odd split above 1
+ * -> VC_E_INVALID here. Fresh "ipa" transcript, `batch` proofs of the same n at once. */
+int vc_ipa_prove_commitment(vc_ctx* ctx, int table, size_t n, const uint64_t* data, const uint64_t* com_xy,
+                            const uint8_t* com_inf, size_t batch, vc_ipa_proof* proofs);
+/* verify_commitment_proof (:237-265) over g[0..2^rounds]; result 1 = valid, 0 = invalid */
+int vc_ipa_verify_commitment_proof(vc_ctx* ctx, int table, const uint64_t* com_xy, uint8_t com_inf,
+                                   const vc_ipa_proof* proof, int* result);
 
 /* ---------------------------------------------------------------- KZG (kzg/mod.rs)
  * prove_point (:136-154): y = evaluate(point), q = divide_by_vanishing(index) when

@@ -93,11 +93,14 @@ def main():
     com = ipa.commit(data)
     pin = ipa.prove(com, 77, data)
     pout = ipa.prove(com, 1000, data)
+    pcom = ipa.prove_commitment(com, data)                              # ipa/mod.rs:199-234
+    assert ipa.verify_commitment_proof(com, pcom)
     ser = lambda p: {"l": [pt(x) for x in p["l"]], "r": [pt(x) for x in p["r"]], "tip": hexs(p["tip"]),
                      "y": hexs(p["y"])}
     dump("ipa_256.json", {"N": N, "data": [hexs(x) for x in data.evals], "commitment": pt(com),
                           "proof_in_domain": {"point": 77, **ser(pin)},
-                          "proof_out_domain": {"point": 1000, **ser(pout)}})
+                          "proof_out_domain": {"point": 1000, **ser(pout)},
+                          "commitment_proof": ser({**pcom, "y": 0})})
 
     # KZG d=256 (s = 100): Lagrange SRS scalars, commit, openings in/boundary/out of domain
     kz = protocol.KZG(256)

@@ -96,6 +96,66 @@ def test_reference_ipa_eval_test(eng, crs):
     assert not ipa.verify(com, 64, bad)
 
 
+def test_ipa_commitment_proof_golden(eng, crs):
+    """prove_commitment (ipa/mod.rs:199-234) at N = 256 == the oracle's proof bytes."""
+    from vkzg import scheme
+    g = load("ipa_256.json")
+    ipa = scheme.IPA(eng, 256, crs)
+    data = scheme.LagrangeBasis([H(x) for x in g["data"]])
+    com = P(g["commitment"])
+    want = g["commitment_proof"]
+    pr = ipa.prove_commitment(com, data)
+    assert pr.tip == H(want["tip"]) and pr.y == 0
+    assert pr.l == [P(x) for x in want["l"]] and pr.r == [P(x) for x in want["r"]]
+    assert ipa.verify_commitment_proof(com, pr)
+
+
+def test_reference_commit_evaluations(eng, crs):
+    """ipa/mod.rs:382-402 (test_commit_evaluations) at N = 32: the commitment proof of 0..31
+    verifies, and fails against C + G; plus a tampered tip / swapped L, R; the oracle accepts
+    the engine's proof."""
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    from vkzg import scheme
+    ipa = scheme.IPA(eng, 32, crs[:33])
+    data = scheme.LagrangeBasis(list(range(32)))
+    com = ipa.commit(data)
+    pr = ipa.prove_commitment(com, data)
+    assert ipa.verify_commitment_proof(com, pr)
+    assert not ipa.verify_commitment_proof(BN254.add(com, BN254.g), pr)
+    bad = scheme.IPAProof(pr.l, pr.r, (pr.tip + 1) % scheme.R_BN254, 0)
+    assert not ipa.verify_commitment_proof(com, bad)
+    assert not ipa.verify_commitment_proof(com, scheme.IPAProof(pr.r, pr.l, pr.tip, 0))
+    oracle = protocol.IPA(32, points=crs[:33])
+    assert oracle.verify_commitment_proof(com, {"l": pr.l, "r": pr.r, "tip": pr.tip})
+
+
+def test_ipa_commitment_proof_batch_and_edges(eng, crs):
+    """batched commitment proofs == single ones; short data (max + 1 = 8 of N = 32, the
+    reference proves over g[0..max+1]); one value (0 rounds: C == tip * g0); the reference's
+    assert on a non-power-of-two length -> error."""
+    from pyoracle import protocol
+    from vkzg import scheme
+    ipa = scheme.IPA(eng, 32, crs[:33])
+    oracle = protocol.IPA(32, points=crs[:33])
+    rng = random.Random(9)
+    datas = [scheme.LagrangeBasis([rng.randrange(scheme.R_BN254) for _ in range(8)]) for _ in range(4)]
+    coms = [oracle.commit(protocol.LagrangeBasis.from_vec(d.evals)) for d in datas]
+    batch = ipa.prove_commitment_batch(coms, datas)
+    for i in range(4):
+        single = ipa.prove_commitment(coms[i], datas[i])
+        assert batch[i].as_dict() == single.as_dict()
+        want = oracle.prove_commitment(coms[i], protocol.LagrangeBasis.from_vec(datas[i].evals))
+        assert (batch[i].l, batch[i].r, batch[i].tip) == (want["l"], want["r"], want["tip"])
+        assert ipa.verify_commitment_proof(coms[i], batch[i])
+    one = scheme.LagrangeBasis([12345])
+    c1 = oracle.commit(protocol.LagrangeBasis.from_vec([12345]))
+    p1 = ipa.prove_commitment(c1, one)
+    assert p1.l == [] and p1.tip == 12345 and ipa.verify_commitment_proof(c1, p1)
+    with pytest.raises(Exception):
+        ipa.prove_commitment(coms[0], scheme.LagrangeBasis(list(range(6))))
+
+
 def test_kzg_256_golden(eng):
     from pyoracle.curves import BN254
     from vkzg import scheme, VCError

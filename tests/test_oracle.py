@@ -136,6 +136,9 @@ def test_golden_ipa_256_proof_verifies():
         proof = {"l": [P(x) for x in pr["l"]], "r": [P(x) for x in pr["r"]], "tip": int(pr["tip"], 16),
                  "y": int(pr["y"], 16)}
         assert ipa.verify(com, pr["point"], proof)
+    cp = g["commitment_proof"]
+    proof = {"l": [P(x) for x in cp["l"]], "r": [P(x) for x in cp["r"]], "tip": int(cp["tip"], 16)}
+    assert ipa.verify_commitment_proof(com, proof)          # ipa/mod.rs:237-265
 
 
 def test_golden_multiproof_verifies_and_tamper():

@@ -493,6 +493,144 @@ int vc_ipa_verify(vc_ctx* ctx, int table, size_t N, const uint64_t* com_xy, uint
     return ipa_verify_impl(ctx, t, N, acc_of(com_inf ? zero : com_xy, com_inf), fr_of(point), proof, tr, result);
 }
 
+// ---------------------------------------------------------------- IPA commitment proof
+// prove_commitment (ipa/mod.rs:199-234): the IPA rounds with neither the evaluation vector b
+// nor q. Same representation as ipa_prove_impl -- the folded generators are coefficients over
+// the first n CRS points -- so each round is one batch of 2B width-n fixed-base commits.
+int vc_ipa_prove_commitment(vc_ctx* ctx, int table, size_t n, const uint64_t* data, const uint64_t* com_xy,
+                            const uint8_t* com_inf, size_t batch, vc_ipa_proof* proofs) {
+    if (!ctx || !data || !com_xy || !com_inf || !proofs || ctx->curve != VC_CURVE_BN254) return VC_E_INVALID;
+    // n = data.max() + 1; the assert in vec_add_and_distribute (utils.rs:37) fires on any
+    // odd split above 1, i.e. unless n is a power of two
+    if (!is_pow2(n)) return VC_E_INVALID;
+    size_t K = 0;
+    while ((1ull << K) < n) K++;
+    for (size_t p = 0; p < batch; p++)
+        if (!proof_ok(&proofs[p]) || proofs[p].rounds < K) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    if (t->n < n) return VC_E_INVALID;  // key.g[0..max + 1] out of bounds
+    std::vector<std::vector<Fr>> a(batch, std::vector<Fr>(n));
+    std::vector<std::vector<Fr>> coeff(batch, std::vector<Fr>(n, fe_one<F>()));
+    std::vector<vc_transcript*> trs(batch);
+    for (size_t p = 0; p < batch; p++) {
+        for (size_t i = 0; i < n; i++) a[p][i] = fr_of(data + (p * n + i) * 4);
+        trs[p] = vc_transcript_new("ipa");
+        transcript_append_point(trs[p], com_xy + 8 * p, com_inf[p], "C");
+        (void)transcript_digest(trs[p], "x");
+    }
+    std::vector<Fr> sc(2 * batch * n);
+    std::vector<uint64_t> oxy(2 * batch * 8);
+    std::vector<uint8_t> oinf(2 * batch);
+    int st = VC_OK;
+    for (size_t r = 0; r < K && st == VC_OK; r++) {
+        const size_t m = n >> r, half = m / 2;
+        for (size_t p = 0; p < batch; p++) {
+            Fr* sL = &sc[(2 * p) * n];
+            Fr* sR = &sc[(2 * p + 1) * n];
+            for (size_t i = 0; i < n; i++) {
+                size_t j = i % m;
+                // L = <gens_R, data_L>, R = <gens_L, data_R>
+                sL[i] = j >= half ? fe_mul<F>(a[p][j - half], coeff[p][i]) : fe_zero<F>();
+                sR[i] = j < half ? fe_mul<F>(a[p][j + half], coeff[p][i]) : fe_zero<F>();
+            }
+        }
+        st = commit_batch(ctx, t, n, sc.data(), 2 * batch, oxy.data(), oinf.data());
+        if (st != VC_OK) break;
+        for (size_t p = 0; p < batch; p++) {
+            const uint64_t* Lxy = &oxy[(2 * p) * 8];
+            const uint64_t* Rxy = &oxy[(2 * p + 1) * 8];
+            memcpy(proofs[p].l_xy + r * 8, Lxy, 64);
+            memcpy(proofs[p].r_xy + r * 8, Rxy, 64);
+            proofs[p].l_inf[r] = oinf[2 * p];
+            proofs[p].r_inf[r] = oinf[2 * p + 1];
+            transcript_append_point(trs[p], Lxy, oinf[2 * p], "L");
+            transcript_append_point(trs[p], Rxy, oinf[2 * p + 1], "R");
+            Fr x = transcript_digest(trs[p], "x");
+            // data <- data_L + x data_R ; gens <- gens_R + x gens_L (coefficients)
+            for (size_t j = 0; j < half; j++) a[p][j] = fe_add<F>(a[p][j], fe_mul<F>(x, a[p][j + half]));
+            a[p].resize(half);
+            for (size_t i = 0; i < n; i++)
+                if ((i % m) < half) coeff[p][i] = fe_mul<F>(coeff[p][i], x);
+        }
+    }
+    for (size_t p = 0; p < batch; p++) {
+        if (st == VC_OK) {
+            proofs[p].rounds = K;
+            canon_of(a[p][0], proofs[p].tip);
+            memset(proofs[p].y, 0, sizeof(proofs[p].y));
+        }
+        vc_transcript_free(trs[p]);
+    }
+    return st;
+}
+
+// verify_commitment_proof (ipa/mod.rs:237-265): c_K = L_K + x_K c_{K-1} + x_K^2 R_K unrolled to
+// (prod x) C + sum_k P_k (L_k + x_k^2 R_k), P_k = prod_{j>k} x_j (one small variable-base MSM),
+// checked against tip * <g[0..2^K], points_coeffs> (one fixed-base commit): their difference
+// must be the identity.
+int vc_ipa_verify_commitment_proof(vc_ctx* ctx, int table, const uint64_t* com_xy, uint8_t com_inf,
+                                   const vc_ipa_proof* pr, int* result) {
+    if (!ctx || !proof_ok(pr) || !result || (!com_xy && !com_inf) || ctx->curve != VC_CURVE_BN254)
+        return VC_E_INVALID;
+    const size_t K = pr->rounds;
+    if (K >= 40) return VC_E_INVALID;
+    const size_t n = 1ull << K;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    if (t->n < n) return VC_E_INVALID;  // key.g[0..2^rounds] out of bounds
+    uint64_t zero[8] = {0};
+    const uint64_t* cxy = com_inf ? zero : com_xy;
+    vc_transcript* tr = vc_transcript_new("ipa");
+    transcript_append_point(tr, cxy, com_inf, "C");
+    (void)transcript_digest(tr, "x");
+    std::vector<Fr> xs(K);
+    for (size_t k = 0; k < K; k++) {
+        transcript_append_point(tr, pr->l_xy + 8 * k, pr->l_inf[k], "L");
+        transcript_append_point(tr, pr->r_xy + 8 * k, pr->r_inf[k], "R");
+        xs[k] = transcript_digest(tr, "x");
+    }
+    vc_transcript_free(tr);
+    std::vector<Fr> s(1, fe_one<F>());
+    for (size_t k = 0; k < K; k++) {
+        std::vector<Fr> ns(2 * s.size());
+        for (size_t i = 0; i < s.size(); i++) {
+            ns[2 * i] = fe_mul<F>(s[i], xs[k]);
+            ns[2 * i + 1] = s[i];
+        }
+        s.swap(ns);
+    }
+    Fr tip = fr_of(pr->tip);
+    std::vector<Fr> fs(n);
+    for (size_t i = 0; i < n; i++) fs[i] = fe_neg<F>(fe_mul<F>(tip, s[i]));
+    uint64_t axy[8];
+    uint8_t ainf;
+    VK_TRY(commit_batch(ctx, t, n, fs.data(), 1, axy, &ainf));
+    std::vector<uint64_t> vxy(8 * (1 + 2 * K));
+    std::vector<uint8_t> vinf(1 + 2 * K);
+    std::vector<Fr> vs(1 + 2 * K);
+    memcpy(&vxy[0], cxy, 64);
+    vinf[0] = com_inf;
+    Fr P = fe_one<F>();
+    for (size_t k = K; k-- > 0;) {
+        memcpy(&vxy[8 * (1 + 2 * k)], pr->l_xy + 8 * k, 64);
+        memcpy(&vxy[8 * (2 + 2 * k)], pr->r_xy + 8 * k, 64);
+        vinf[1 + 2 * k] = pr->l_inf[k];
+        vinf[2 + 2 * k] = pr->r_inf[k];
+        vs[1 + 2 * k] = P;
+        vs[2 + 2 * k] = fe_mul<F>(P, fe_sqr<F>(xs[k]));
+        P = fe_mul<F>(P, xs[k]);
+    }
+    vs[0] = P;
+    Acc vb;
+    VK_TRY(msm_points(ctx, vxy, vinf, vs, &vb));
+    Acc tot = C::add(acc_of(axy, ainf), vb);
+    *result = C::is_zero(tot) ? 1 : 0;
+    return VC_OK;
+}
+
 int vc_kzg_setup(vc_ctx* ctx, size_t max_items, const uint64_t* secret, int* table_id, size_t* size) {
     if (!ctx || !secret || !table_id || max_items == 0) return VC_E_INVALID;
     Guard g(ctx);

@@ -76,6 +76,8 @@ SIGNATURES = {
     "vc_ipa_commit": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P]),
     "vc_ipa_prove": (c_int, [c_void_p, c_int, c_size_t, P, P, P, P, c_size_t, P, P]),
     "vc_ipa_verify": (c_int, [c_void_p, c_int, c_size_t, P, ctypes.c_uint8, P, P, c_void_p, ctypes.POINTER(c_int)]),
+    "vc_ipa_prove_commitment": (c_int, [c_void_p, c_int, c_size_t, P, P, P, c_size_t, P]),
+    "vc_ipa_verify_commitment_proof": (c_int, [c_void_p, c_int, P, ctypes.c_uint8, P, ctypes.POINTER(c_int)]),
     "vc_kzg_prove": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
     "vc_kzg_quotient": (c_int, [c_void_p, c_size_t, P, c_size_t, P, P, P]),
     "vc_kzg_prove_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),

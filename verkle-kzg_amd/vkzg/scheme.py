@@ -243,6 +243,33 @@ class IPA:
     def verify(self, commitment, index, proof):
         return self.verify_point(commitment, index, proof)
 
+    def prove_commitment(self, commitment, data):
+        """:199-234 -> IPAProof with l, r, tip (y = 0)."""
+        return self.prove_commitment_batch([commitment], [data])[0]
+
+    def prove_commitment_batch(self, commitments, datas):
+        n = datas[0].max() + 1
+        if any(d.max() + 1 != n for d in datas):
+            raise ValueError("one batch proves data of one length")
+        B = len(datas)
+        d = np.concatenate([x.limbs(n)[:n] for x in datas])
+        cxy, cinf = _pt_arrays(commitments)
+        K = _log2(n)
+        bufs = [IPAProof._alloc(K) for _ in range(B)]
+        arr = (_ProofBuf * B)(*[b for b, _ in bufs])
+        check(lib().vc_ipa_prove_commitment(self.engine.h, self.table, n, _p(d), _p(cxy), _p(cinf), B,
+                                            ctypes.cast(arr, _P)), "ipa_prove_commitment")
+        return [IPAProof._from(arr[i], bufs[i][1]) for i in range(B)]
+
+    def verify_commitment_proof(self, commitment, proof):
+        """:237-265."""
+        cxy, cinf = _pt_arrays([commitment])
+        b, arrs = proof._to()
+        res = ctypes.c_int()
+        check(lib().vc_ipa_verify_commitment_proof(self.engine.h, self.table, _p(cxy), int(cinf[0]), ctypes.byref(b),
+                                                   ctypes.byref(res)), "ipa_verify_commitment_proof")
+        return bool(res.value)
+
 
 # ---------------------------------------------------------------- kzg/mod.rs
 class KZG:
