@@ -375,7 +375,7 @@ def main():
     # dominant kernel (bucket accumulation) device time, HIP events on the launch stream
     acc_ms, acc_n = eng.kernel_time("msm_accumulate")
     kernels = {}
-    for k in ("msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate", "msm_fixup",
+    for k in ("glv_split", "glv_phi", "msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate", "msm_fixup",
               "msm_segsum", "msm_bitsum", "msm_sumpart"):
         ms, cnt = eng.kernel_time(k)
         if cnt:
@@ -386,13 +386,13 @@ def main():
     achieved = shard_bytes / acc_s / 1e9 if acc_s else None
     # VALU roofline: mixed adds of this rank's window slice (one per nonzero digit ~ n per window)
     from vkzg.dist import window_count
-    c_bits, w_total = window_count(curve, n)
+    c_bits, w_total, terms = window_count(curve, n, with_terms=True)
     w_rank = (rank + 1) * w_total // world - rank * w_total // world
-    mads = n * w_rank * MULS_PER_MADD[curve] * 2 * LIMBS32[curve] ** 2
+    mads = terms * n * w_rank * MULS_PER_MADD[curve] * 2 * LIMBS32[curve] ** 2
     mad_peak = eng.device_mad_rate()
     valu = {"achieved": mads / acc_s / 1e12 if acc_s else None, "peak": mad_peak, "unit": "T v_mad_u64_u32/s",
             "frac": (mads / acc_s / 1e12 / mad_peak) if acc_s else None,
-            "work": f"{n}x{w_rank} mixed adds x {MULS_PER_MADD[curve]} Fq mults x {2 * LIMBS32[curve] ** 2} mads",
+            "work": f"{terms * n}x{w_rank} mixed adds x {MULS_PER_MADD[curve]} Fq mults x {2 * LIMBS32[curve] ** 2} mads",
             "peak_source": "vc_device_mad_rate, measured live on this GPU"}
     traffic, traffic_src = None, None
     if world == 1 and os.path.exists(PMC_SUMMARY):

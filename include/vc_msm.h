@@ -95,7 +95,10 @@ int vc_msm_device_partial(vc_ctx* ctx, int table_id, size_t offset, const void* 
  * weights, so the parts' accumulators sum (vc_partials_sum) to the whole MSM. Each part
  * streams every base but builds and reduces only its windows' buckets: the bucket reduction,
  * which does not shrink with n, is divided by `parts` (a point split leaves it whole). */
-int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows);  /* c and W chosen for n */
+/* c and W chosen for an n-term MSM; terms_per_point (may be NULL) = 2 when the scalars are
+ * split by the GLV endomorphism (BLS12-381, n >= 4096, tables of subgroup points: 2n terms of
+ * 127-bit scalars over P_i and phi(P_i), W windows of those), else 1 */
+int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows, int* terms_per_point);
 int vc_msm_device_window_part(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars, size_t n,
                               int mont, int part, int parts, uint32_t* out_acc);
 /* Sum k partial accumulators (host) and normalise to canonical affine. */

@@ -1,13 +1,36 @@
 """TEST INFRASTRUCTURE ONLY (never shipped, never measured).
 
 Restatement of the engine's signed-window scalar decomposition
-(verkle-kzg_amd/csrc/msm.hip: choose_window, for_each_digit, msm_run_t's window slices), used
-to check the window-sliced multi-GPU split (vc_msm_device_window_part): the part-k MSM equals
-sum_i s_i^(k) P_i with s_i^(k) = sum_{w in [kW/G, (k+1)W/G)} d_iw 2^(c w), and the parts add
-up to the reference inner_product (vector-commit/src/utils.rs:16-19).
+(verkle-kzg_amd/csrc/msm.hip: choose_window, for_each_digit, k_glv_split, msm_run_t's window
+slices), used to check the window-sliced multi-GPU split (vc_msm_device_window_part): the
+part-k MSM equals sum_i s_i^(k) P_i with s_i^(k) = sum_{w in [kW/G, (k+1)W/G)} d_iw 2^(c w)
+(with the GLV split on BLS12-381: the digits of both halves, the k2 half weighted by lambda),
+and the parts add up to the reference inner_product (vector-commit/src/utils.rs:16-19).
 """
 
 SCALAR_BITS = {"bn254": 254, "bls12_381": 255, "bandersnatch": 253}
+# BLS12-381: lambda = z^2 - 1 with r = lambda^2 + lambda + 1 (phi(x, y) = (beta x, y) = [lambda])
+GLV_LAMBDA = 0xac45a4010001a40200000000ffffffff
+GLV_MIN_N = 4096
+GLV_BITS = 128
+
+
+def glv_active(curve, n):
+    return curve == "bls12_381" and GLV_MIN_N <= n < (1 << 30)
+
+
+def glv_split(k, r):
+    """k_glv_split: k mod r = k1 + lambda k2 with |k1|, |k2| <= lambda/2 + 1; returns the
+    signed halves (k1, k2)."""
+    lam = GLV_LAMBDA
+    k %= r
+    q, rem = divmod(k, lam)
+    half = lam >> 1
+    if q > half:                      # (rem - 1) + lambda (q - lambda - 1) = k - r
+        q, rem = q - lam - 1, rem - 1
+    if rem > half:                    # (rem - lambda) + lambda (q + 1)
+        rem, q = rem - lam, q + 1
+    return rem, q
 
 
 def choose_window(n):
@@ -32,17 +55,38 @@ def signed_digits(s, c, W):
     return out
 
 
+def glv_window(nv):
+    return 16 if nv >= 1 << 19 else (13 if nv >= 1 << 15 else 10)
+
+
 def window_slice(curve, n, part, parts):
-    c = choose_window(n)
-    W = (SCALAR_BITS[curve] + 1 + c - 1) // c
+    if glv_active(curve, n):
+        c = glv_window(2 * n)
+        W = (GLV_BITS + c - 1) // c
+    else:
+        c = choose_window(n)
+        W = (SCALAR_BITS[curve] + 1 + c - 1) // c
     return c, W, part * W // parts, (part + 1) * W // parts
+
+
+def _part(v, c, W, wb, we):
+    """digits of |v| in windows [wb, we), with v's sign"""
+    d = signed_digits(abs(v), c, W)
+    t = sum(d[w] << (c * w) for w in range(wb, we))
+    return -t if v < 0 else t
 
 
 def part_scalars(curve, scalars, part, parts, r):
     """Per-term scalars (mod r) of window slice `part` of `parts`."""
     c, W, wb, we = window_slice(curve, len(scalars), part, parts)
+    glv = glv_active(curve, len(scalars))
     out = []
     for s in scalars:
-        d = signed_digits(s, c, W)
-        out.append(sum(d[w] << (c * w) for w in range(wb, we)) % r)
+        if glv:
+            k1, k2 = glv_split(s, r)
+            assert abs(k1) < 1 << 127 and abs(k2) < 1 << 127
+            out.append((_part(k1, c, W, wb, we) + GLV_LAMBDA * _part(k2, c, W, wb, we)) % r)
+        else:
+            d = signed_digits(s, c, W)
+            out.append(sum(d[w] << (c * w) for w in range(wb, we)) % r)
     return out

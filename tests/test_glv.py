@@ -1,0 +1,83 @@
+"""CPU checks of the GLV split the engine applies to BLS12-381 MSMs (verkle-kzg_amd/csrc/msm.hip:
+k_glv_split, k_glv_phi, k_glv_check), through its oracle restatement (oracle/pyoracle/pippenger.py):
+the halves recombine to k mod r, stay below 2^127 at every edge of the balancing, the window
+slices of the split add up to the whole scalar, and the curve constants do what msm.hip assumes
+(phi = [lambda] on the subgroup; the subgroup test rejects points outside it)."""
+import random
+
+BETA = 0x1a0111ea397fe699ec02408663d4de85aa0d857d89759ad4897d29650fb85f9b409427eb4f49fffd8bfd00000000aaac
+Z2 = 0xd201000000010000 ** 2
+
+
+def _edge_scalars(r, lam):
+    half = lam >> 1
+    out = [0, 1, 2, lam - 1, lam, lam + 1, half, half + 1, half + 2, lam + half, lam + half + 1,
+           lam * half, lam * (half + 1), lam * (half + 1) + half + 1, lam * lam, lam * lam + half,
+           r - 1, r - 2, r - half, r - lam, r, r + 5, (1 << 256) - 1, (1 << 255)]
+    rng = random.Random(3)
+    out += [rng.randrange(1 << 256) for _ in range(300)]
+    return out
+
+
+def test_glv_split_recombines_and_is_short():
+    from pyoracle import pippenger
+    from pyoracle.curves import BLS12_381 as C
+    lam, r = pippenger.GLV_LAMBDA, C.r
+    assert lam * lam + lam + 1 == r
+    for k in _edge_scalars(r, lam):
+        k1, k2 = pippenger.glv_split(k, r)
+        assert (k1 + lam * k2 - k) % r == 0
+        assert abs(k1) <= (lam >> 1) + 1 and abs(k2) <= (lam >> 1) + 1
+        assert abs(k1) < 1 << 127 and abs(k2) < 1 << 127
+
+
+def test_glv_window_parts_sum_to_scalar():
+    from pyoracle import pippenger
+    from pyoracle.curves import BLS12_381 as C
+    n = 5000                                            # GLV active
+    c, W, _, _ = pippenger.window_slice("bls12_381", n, 0, 1)
+    assert (c, W) == (10, 13)
+    sc = _edge_scalars(C.r, pippenger.GLV_LAMBDA)
+    sc = (sc * (n // len(sc) + 1))[:n]
+    for parts in (1, 3, 8):
+        tot = [0] * n
+        for k in range(parts):
+            for i, v in enumerate(pippenger.part_scalars("bls12_381", sc, k, parts, C.r)):
+                tot[i] += v
+        assert all((t - s) % C.r == 0 for t, s in zip(tot, sc))
+    assert pippenger.window_slice("bls12_381", 1 << 20, 0, 1)[:2] == (16, 8)
+    assert pippenger.window_slice("bls12_381", 4095, 0, 1)[:2] == (9, 29)      # below GLV_MIN_N
+
+
+def _mulraw(C, P, k):
+    R, Q = None, P
+    while k:
+        if k & 1:
+            R = C.add(R, Q)
+        Q = C.add(Q, Q)
+        k >>= 1
+    return R
+
+
+def test_glv_curve_constants():
+    """phi(P) = (beta x, y) = [lambda] P on the subgroup; the check phi^2(P) + [z^2] P == 0
+    (k_glv_check) holds on the subgroup and fails on curve points outside it."""
+    from pyoracle import pippenger
+    from pyoracle.curves import BLS12_381 as C
+    p = C.p
+    rng = random.Random(5)
+    for _ in range(3):
+        P = C.mul(C.g, rng.randrange(1, C.r))
+        assert (BETA * P[0] % p, P[1]) == C.mul(P, pippenger.GLV_LAMBDA)
+        assert C.add((BETA * BETA * P[0] % p, P[1]), _mulraw(C, P, Z2)) is None
+    outside = 0
+    while outside < 3:
+        x = rng.randrange(p)
+        a = (x ** 3 + 4) % p
+        y = pow(a, (p + 1) // 4, p)
+        if y * y % p != a:
+            continue
+        P = (x, y)
+        assert _mulraw(C, P, C.r) is not None           # not in the r-torsion
+        assert C.add((BETA * BETA * x % p, y), _mulraw(C, P, Z2)) is not None
+        outside += 1

@@ -95,6 +95,77 @@ def test_msm_montgomery_scalars(engines, oracle_c, curve):
     assert np.array_equal(got[0], want[0])
 
 
+def _glv_edge_scalars(r, n, rng):
+    from pyoracle import pippenger
+    lam = pippenger.GLV_LAMBDA
+    half = lam >> 1
+    edge = [0, 1, lam - 1, lam, lam + 1, half, half + 1, lam + half + 1, lam * (half + 1),
+            lam * (half + 1) + half + 1, lam * lam, lam * lam + half, r - 1, r - 2, r - lam]
+    return (edge + [rng.randrange(r) for _ in range(n)])[:n]
+
+
+def test_msm_glv_edges(engines, oracle_c):
+    """BLS12-381 at n >= 4096 takes the GLV split (k = k1 + lambda k2 over P and phi(P)): the
+    balancing edges of the split, repeated / negated / identity bases, Montgomery scalars and
+    all-equal scalars, bit-exact against the naive oracle."""
+    import vkzg
+    from pyoracle import pippenger
+    from pyoracle.curves import BLS12_381 as C
+    e = engines["bls12_381"]
+    n = 4500
+    assert pippenger.glv_active("bls12_381", n)
+    rng = random.Random(17)
+    tid = e.random_bases(n, seed=31)
+    xy, inf = e.download_bases(tid)
+    pts = vkzg.arrays_to_points("bls12_381", xy, inf)
+    pts[20] = pts[21]
+    pts[22] = C.neg(pts[21])
+    pts[23] = None
+    sc = _glv_edge_scalars(C.r, n, rng)
+    sc[21] = sc[22] = sc[20]
+    tid2 = e.upload_points(pts)
+    xy2, inf2 = vkzg.points_to_arrays("bls12_381", pts)
+    want = _oracle(oracle_c, "bls12_381", xy2, inf2, vkzg.ints_to_limbs(sc))
+    got = e.msm(tid2, vkzg.ints_to_limbs(sc))
+    assert got[1] == want[1] and np.array_equal(got[0], want[0])
+    mont = [(s << 256) % C.r for s in sc]
+    got = e.msm(tid2, vkzg.ints_to_limbs(mont), mont=True)
+    assert got[1] == want[1] and np.array_equal(got[0], want[0])
+    for v in (pippenger.GLV_LAMBDA, C.r - 1, (pippenger.GLV_LAMBDA >> 1) + 1):
+        same = [v] * n
+        got = e.msm(tid2, vkzg.ints_to_limbs(same))
+        want = _oracle(oracle_c, "bls12_381", xy2, inf2, vkzg.ints_to_limbs(same))
+        assert got[1] == want[1] and np.array_equal(got[0], want[0])
+
+
+def test_msm_glv_rejects_non_subgroup_table(engines, oracle_c):
+    """A BLS12-381 table with one curve point outside the prime-order subgroup: phi is not
+    [lambda] there, so the engine must see it (k_glv_check) and run the plain MSM -- the result
+    is still the reference's sum of k_i P_i."""
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    e = engines["bls12_381"]
+    n = 4096
+    tid = e.random_bases(n, seed=41)
+    xy, inf = e.download_bases(tid)
+    pts = vkzg.arrays_to_points("bls12_381", xy, inf)
+    rng = random.Random(43)
+    p = C.p
+    while True:
+        x = rng.randrange(p)
+        a = (x ** 3 + 4) % p
+        y = pow(a, (p + 1) // 4, p)
+        if y * y % p == a:
+            break
+    pts[1000] = (x, y)
+    sc = [rng.randrange(C.r) for _ in range(n)]
+    tid2 = e.upload_points(pts)
+    xy2, inf2 = vkzg.points_to_arrays("bls12_381", pts)
+    want = _oracle(oracle_c, "bls12_381", xy2, inf2, vkzg.ints_to_limbs(sc))
+    got = e.msm(tid2, vkzg.ints_to_limbs(sc))
+    assert got[1] == want[1] and np.array_equal(got[0], want[0])
+
+
 @pytest.mark.parametrize("curve", CURVES)
 def test_msm_offset_and_partials(engines, oracle_c, curve):
     """offset slices + partial accumulators summed = whole MSM (the multi-GPU shard path)."""

@@ -172,6 +172,7 @@ static int fill_t(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf,
     t->curve = ctx->curve;
     t->n = n;
     t->fb_c = t->fb_W = 0;  // any fixed-base tables are stale now
+    t->subgroup = -1;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
     if (n == 0) return VC_OK;
@@ -220,6 +221,7 @@ static int random_t(vc_ctx* ctx, uint64_t seed, size_t n, int* id) {
     Table* t = new Table();
     t->curve = ctx->curve;
     t->n = n;
+    t->subgroup = 1;  // multiples of the generator
     int st = t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff));
     if (st == VC_OK) st = t->inf.ensure(std::max<size_t>(n, 1));
     if (st != VC_OK) {

@@ -236,9 +236,9 @@ static int msm_device_acc(vc_ctx* ctx, int id, size_t offset, const void* d_sc, 
     return vk::msm_run(ctx, t, offset, d_sc, n, mont, acc, part, parts);
 }
 
-int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows) {
+int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows, int* terms_per_point) {
     if (!valid_curve(curve) || !window_bits || !windows) return VC_E_INVALID;
-    return vk::msm_windows(curve, n, window_bits, windows);
+    return vk::msm_windows(curve, n, window_bits, windows, terms_per_point);
 }
 
 int vc_msm_device_window_part(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont, int part,

@@ -52,6 +52,9 @@ struct Table {
     // fixed-base window tables for batched commits
     int fb_c = 0, fb_W = 0;
     DevBuf fb;
+    // 1: every base lies in the prime-order subgroup (the GLV endomorphism acts as lambda, so
+    // msm.hip may split scalars), 0: some base does not, -1: not checked yet
+    int subgroup = -1;
 };
 
 enum WsSlot {
@@ -89,6 +92,9 @@ enum WsSlot {
     WS_NXT,
     WS_NXT2,
     WS_CHAIN,
+    WS_GLV_SC,
+    WS_GLV_PHI,
+    WS_GLV_FLAG,
     WS_COUNT_
 };
 
@@ -148,7 +154,7 @@ struct vc_ctx {
 namespace vk {
 // implemented per translation unit with explicit instantiations
 int device_mad_rate(vc_ctx* ctx, double* tera_per_s);
-int msm_windows(int curve, size_t n, int* c, int* W);
+int msm_windows(int curve, size_t n, int* c, int* W, int* terms);
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
             uint32_t* out_acc, int part = 0, int parts = 1);
 int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out_inf);

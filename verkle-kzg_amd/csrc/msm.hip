@@ -63,11 +63,64 @@ __device__ __forceinline__ void for_each_digit(fe<Fr> s, int c, int W, Fn&& f) {
     }
 }
 
+// Digits of a 4-limb magnitude (GLV halves, < 2^127), same recoding.
+template <class Fn>
+__device__ __forceinline__ void for_each_digit4(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3, int c, int W,
+                                                Fn&& f) {
+    const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+        uint32_t raw = (s0 & mask) + carry;
+        s0 = (s0 >> c) | (s1 << (32 - c));
+        s1 = (s1 >> c) | (s2 << (32 - c));
+        s2 = (s2 >> c) | (s3 << (32 - c));
+        s3 >>= c;
+        int32_t d;
+        if (raw > half) {
+            d = (int32_t)raw - (int32_t)(1u << c);
+            carry = 1;
+        } else {
+            d = (int32_t)raw;
+            carry = 0;
+        }
+        f(w, d);
+    }
+}
+
+// Digit sources of the sort: entry i of the MSM -> its signed digits (nothing for an identity base).
+template <class Fr>
+struct ScalarDigits {  // plain scalars, canonical or Montgomery
+    const uint32_t* sc;
+    const uint8_t* inf;
+    int mont;
+    template <class Fn>
+    __device__ __forceinline__ void operator()(uint32_t i, int c, int W, Fn&& f) const {
+        if (inf != nullptr && inf[i]) return;
+        fe<Fr> s = load_scalar<Fr>(sc, i);
+        if (mont) s = fe_from_mont<Fr>(s);
+        for_each_digit<Fr>(s, c, W, f);
+    }
+};
+// GLV halves (k_glv_split): entry i < n is k1 of scalar i against P_i, entry n + i is k2 against
+// phi(P_i); magnitude in bits 0..126, sign in bit 127 (a negative half negates every digit)
+struct GlvDigits {
+    const uint4* k;
+    const uint8_t* inf;
+    uint32_t n;
+    template <class Fn>
+    __device__ __forceinline__ void operator()(uint32_t i, int c, int W, Fn&& f) const {
+        if (inf != nullptr && inf[i < n ? i : i - n]) return;
+        const uint4 v = k[i];
+        const bool neg = (v.w >> 31) != 0;
+        for_each_digit4(v.x, v.y, v.z, v.w & 0x7fffffffu, c, W, [&](int w, int32_t d) { f(w, neg ? -d : d); });
+    }
+};
+
 // Two-pass MSD counting sort of the n*W (window, bucket) keys, all in LDS -- no global atomics
 // (global atomics execute memory-side on CDNA4, ~26 G/s for scattered words, which made the
 // one-pass global-histogram sort cost 2.2 ms at 2^20 x 16 windows).
 //   coarse bin g = w * NBC + (b >> FB)          (NBC = NB >> FB coarse bins per window)
-//   k_sort_hist     block = CHUNK scalars: LDS histogram of coarse bins -> counts[g][block]
+//   k_sort_hist     block = CHUNK entries: LDS histogram of coarse bins -> counts[g][block]
 //   hipcub scan     counts -> base[g][block] (global position of the block's run in bin g)
 //   k_sort_coarse   same digits again, LDS cursors from base: tmp[pos] = fine<<32 | i | sign<<31
 //   k_sort_fine     block = coarse bin: LDS histogram of the 2^FB fine buckets -> bucket
@@ -75,9 +128,8 @@ __device__ __forceinline__ void for_each_digit(fe<Fr> s, int c, int W, Fn&& f) {
 // Order inside a bucket is arbitrary (EC addition is commutative and exact).
 constexpr uint32_t SORT_CHUNK = 1024;
 
-template <class Fr>
-__global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
-                                                  uint32_t n, int c, int wb, int we, int mont, uint32_t FB,
+template <class Src>
+__global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
                                                   uint32_t NBC, uint32_t nblk, uint32_t* __restrict__ counts) {
     extern __shared__ uint32_t hist[];
     const uint32_t bins = (uint32_t)(we - wb) * NBC;
@@ -85,10 +137,7 @@ __global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ 
     __syncthreads();
     const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        if (inf != nullptr && inf[i]) continue;
-        fe<Fr> s = load_scalar<Fr>(sc, i);
-        if (mont) s = fe_from_mont<Fr>(s);
-        for_each_digit<Fr>(s, c, we, [&](int w, int32_t d) {
+        src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb)
                 atomicAdd(&hist[(uint32_t)(w - wb) * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
         });
@@ -97,9 +146,8 @@ __global__ void __launch_bounds__(256) k_sort_hist(const uint32_t* __restrict__ 
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(size_t)k * nblk + blockIdx.x] = hist[k];
 }
 
-template <class Fr>
-__global__ void __launch_bounds__(256) k_sort_coarse(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
-                                                    uint32_t n, int c, int wb, int we, int mont, uint32_t FB,
+template <class Src>
+__global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
                                                     uint32_t NBC, uint32_t nblk, const uint32_t* __restrict__ base,
                                                     uint64_t* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
@@ -109,10 +157,7 @@ __global__ void __launch_bounds__(256) k_sort_coarse(const uint32_t* __restrict_
     const uint32_t fmask = (1u << FB) - 1;
     const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        if (inf != nullptr && inf[i]) continue;
-        fe<Fr> s = load_scalar<Fr>(sc, i);
-        if (mont) s = fe_from_mont<Fr>(s);
-        for_each_digit<Fr>(s, c, we, [&](int w, int32_t d) {
+        src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb) {
                 uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
                 uint32_t pos = atomicAdd(&cur[(uint32_t)(w - wb) * NBC + (b >> FB)], 1u);
@@ -160,8 +205,8 @@ __global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ 
 // ------------------------------------------------------------------ bucket accumulation
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_accumulate(
-    const typename C::Aff* __restrict__ bases, const uint32_t* __restrict__ sorted,
-    const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
+    const typename C::Aff* __restrict__ bases, const typename C::Aff* __restrict__ phi, uint32_t nphi,
+    const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename C::Acc* __restrict__ buckets, typename C::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename C::Acc* __restrict__ owner_piece,
     uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max) {
@@ -185,14 +230,16 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(
     uint32_t bend = offsets[b + 1];
     bool left_open = offsets[b] < k;
     Acc acc = C::zero();
+    // entry j < nphi: bases[j]; j >= nphi: phi[j - nphi] (the GLV endomorphism images)
+    auto base_of = [&](uint32_t j) -> const Aff* { return j < nphi ? bases + j : phi + (j - nphi); };
     uint32_t idx = sorted[k];
-    Aff P = bases[idx & 0x7fffffffu];
+    Aff P = *base_of(idx & 0x7fffffffu);
     while (true) {
         uint32_t cur = idx;
         Aff Q = P;
         if (k + 1 < e) {  // prefetch next base
             idx = sorted[k + 1];
-            P = bases[idx & 0x7fffffffu];
+            P = *base_of(idx & 0x7fffffffu);
         }
         acc = C::madd(acc, Q, (cur >> 31) != 0);
         k++;
@@ -222,7 +269,235 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(
     }
 }
 
+// ------------------------------------------------------------------ GLV endomorphism (BLS12-381 G1)
+// phi(x, y) = (beta x, y) acts on the prime-order subgroup as multiplication by
+// lambda = z^2 - 1 (z = -0xd201000000010000), and r = lambda^2 + lambda + 1. A scalar splits as
+// k = k1 + lambda k2 with |k1|, |k2| <= lambda/2 + 1 < 2^127, so an n-term MSM is a 2n-term MSM
+// of 127-bit scalars over (P_i, phi(P_i)): the same number of accumulate entries (2n x 8
+// windows instead of n x 16 at c = 16) but half the buckets, half the bucket reduction and
+// half the Horner doublings. Used only when every base of the table is in the subgroup
+// (checked once per table: phi^2(P) = -z^2 P, which non-subgroup points fail), so the result
+// is the same group element as the reference's sum of k_i P_i for any input.
+struct GlvK {
+    uint64_t lam[2];
+    uint64_t mu[3];  // floor(2^256 / lambda)
+    uint64_t r[4];
+};
+constexpr size_t GLV_MIN_N = 4096;
+constexpr int GLV_BITS = 128;  // |k1|, |k2| < 2^127, plus the recoding's spare bit
+
+typedef unsigned __int128 u128;
+
+template <class Fr>
+__global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ sc, uint32_t n, int mont, GlvK K,
+                                                  uint4* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe<Fr> f = load_scalar<Fr>(sc, i);
+    if (mont) f = fe_from_mont<Fr>(f);
+    uint64_t s[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) s[k] = (uint64_t)f.v[2 * k] | ((uint64_t)f.v[2 * k + 1] << 32);
+    // s mod r (inputs are < 2^256 < 3r)
+    for (int rep = 0; rep < 2; rep++) {
+        bool ge = true;
+        for (int k = 3; k >= 0; k--)
+            if (s[k] != K.r[k]) {
+                ge = s[k] > K.r[k];
+                break;
+            }
+        if (!ge) break;
+        uint64_t br = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            u128 d = (u128)s[k] - K.r[k] - br;
+            s[k] = (uint64_t)d;
+            br = (uint64_t)(d >> 64) & 1;
+        }
+    }
+    // q = floor(s mu / 2^256): floor(s / lambda) or up to 2 less
+    uint64_t p[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int b = 0; b < 3; b++) {
+            u128 t = (u128)s[a] * K.mu[b] + p[a + b] + carry;
+            p[a + b] = (uint64_t)t;
+            carry = (uint64_t)(t >> 64);
+        }
+        p[a + 3] = carry;
+    }
+    u128 q = ((u128)p[5] << 64) | p[4];
+    const u128 lam = ((u128)K.lam[1] << 64) | K.lam[0];
+    // rem = s - q lambda (< 3 lambda: 3 limbs)
+    uint64_t ql[4] = {0, 0, 0, 0};
+    const uint64_t qv[2] = {(uint64_t)q, (uint64_t)(q >> 64)};
+#pragma unroll
+    for (int a = 0; a < 2; a++) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+            u128 t = (u128)qv[a] * K.lam[b] + ql[a + b] + carry;
+            ql[a + b] = (uint64_t)t;
+            carry = (uint64_t)(t >> 64);
+        }
+        ql[a + 2] = carry;
+    }
+    uint64_t rm[3];
+    {
+        uint64_t br = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            u128 d = (u128)s[k] - ql[k] - br;
+            rm[k] = (uint64_t)d;
+            br = (uint64_t)(d >> 64) & 1;
+        }
+    }
+    for (int it = 0; it < 4; it++) {  // at most 2 corrections
+        const u128 lo = ((u128)rm[1] << 64) | rm[0];
+        if (rm[2] == 0 && lo < lam) break;
+        const u128 d = lo - lam;
+        if (lo < lam) rm[2] -= 1;
+        rm[0] = (uint64_t)d;
+        rm[1] = (uint64_t)(d >> 64);
+        q += 1;
+    }
+    u128 rem = ((u128)rm[1] << 64) | rm[0];
+    // balance: k = rem + lambda q with rem in [0, lambda), q in [0, lambda + 1]
+    //   q > lambda/2:   (rem - 1) + lambda (q - lambda - 1)   (= k - r)
+    //   rem > lambda/2: (rem - lambda) + lambda (q + 1)
+    const u128 half = lam >> 1;
+    bool nq = false, nr = false;
+    if (q > half) {
+        q = lam + 1 - q;  // magnitude of q - lambda - 1
+        nq = true;
+        if (rem == 0) {
+            rem = 1;
+            nr = true;
+        } else {
+            rem -= 1;
+        }
+    }
+    if (!nr && rem > half) {
+        rem = lam - rem;
+        nr = true;
+        if (!nq) {
+            q += 1;
+        } else if (q == 0) {
+            q = 1;
+            nq = false;
+        } else {
+            q -= 1;
+        }
+    }
+    out[i] = make_uint4((uint32_t)rem, (uint32_t)(rem >> 32), (uint32_t)(rem >> 64),
+                        (uint32_t)(rem >> 96) | (nr ? 0x80000000u : 0u));
+    out[n + i] = make_uint4((uint32_t)q, (uint32_t)(q >> 32), (uint32_t)(q >> 64),
+                            (uint32_t)(q >> 96) | (nq ? 0x80000000u : 0u));
+}
+
+template <class C>
+__global__ void __launch_bounds__(256) k_glv_phi(const typename C::Aff* __restrict__ bases, uint32_t n,
+                                                fe<typename C::F> beta, typename C::Aff* __restrict__ phi) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    typename C::Aff p = bases[i];
+    p.x = fe_mul<typename C::F>(p.x, beta);
+    phi[i] = p;
+}
+
+// bad |= some base with phi^2(P) + z^2 P != 0 (phi^2 = (beta^2 x, y) has eigenvalue lambda^2 = -z^2)
+template <class C>
+__global__ void __launch_bounds__(256) k_glv_check(const typename C::Aff* __restrict__ bases,
+                                                  const uint8_t* __restrict__ inf, uint32_t n,
+                                                  fe<typename C::F> beta2, uint64_t z2lo, uint64_t z2hi,
+                                                  uint32_t* __restrict__ bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || inf[i]) return;
+    typename C::Aff p = bases[i];
+    typename C::Acc acc = C::zero();
+    for (int b = 127; b >= 0; b--) {
+        acc = C::dbl(acc);
+        const uint64_t w = b >= 64 ? z2hi : z2lo;
+        if ((w >> (b & 63)) & 1) acc = C::madd(acc, p, false);
+    }
+    p.x = fe_mul<typename C::F>(p.x, beta2);
+    acc = C::madd(acc, p, false);
+    if (!C::is_zero(acc)) atomicOr(bad, 1u);
+}
+
+static GlvK glv_consts() {
+    return GlvK{{0x00000000ffffffffull, 0xac45a4010001a402ull},
+                {0x63f6e522f6cfee30ull, 0x7c6becf1e01faaddull, 0x1ull},
+                {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull, 0x73eda753299d7d48ull}};
+}
+static const uint64_t GLV_BETA[6] = {0x8bfd00000000aaacull, 0x409427eb4f49fffdull, 0x897d29650fb85f9bull,
+                                     0xaa0d857d89759ad4ull, 0xec02408663d4de85ull, 0x1a0111ea397fe699ull};
+static const uint64_t GLV_BETA2[6] = {0x2e01fffffffefffeull, 0xde17d813620a0002ull, 0xddb3a93be6f89688ull,
+                                      0xba69c6076a0f77eaull, 0x5f19672fdf76ce51ull, 0x0ull};
+static fe<BLS381Fq> bls_fq_mont(const uint64_t* w) {
+    fe<BLS381Fq> r;
+    memcpy(r.v, w, sizeof(r.v));
+    return fe_to_mont<BLS381Fq>(r);
+}
+static const uint64_t GLV_Z2[2] = {0x0000000100000000ull, 0xac45a4010001a402ull};  // z^2 = lambda + 1
+
+// is every base of t in the prime-order subgroup? (checked once per table, cached)
+static int glv_table_ok(vc_ctx* ctx, Table* t, bool* ok) {
+    using C = BLS381G1;
+    if (t->subgroup < 0) {
+        VK_TRY(ctx->ws[WS_GLV_FLAG].ensure(4));
+        uint32_t* d_bad = ctx->ws[WS_GLV_FLAG].as<uint32_t>();
+        VK_CHECK_HIP(hipMemsetAsync(d_bad, 0, 4, ctx->stream));
+        if (t->n > 0)
+            VK_LAUNCH(ctx, "glv_check", (k_glv_check<C>), (t->n + 255) / 256, 256, 0, t->bases.as<C::Aff>(),
+                      t->inf.as<uint8_t>(), (uint32_t)t->n, bls_fq_mont(GLV_BETA2), GLV_Z2[0], GLV_Z2[1],
+                      d_bad);
+        uint32_t bad = 0;
+        VK_CHECK_HIP(hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        t->subgroup = bad ? 0 : 1;
+    }
+    *ok = t->subgroup == 1;
+    return VC_OK;
+}
+
+template <class Src>
+static int sort_entries(vc_ctx* ctx, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB, uint32_t NBC,
+                        uint32_t nblk, size_t ncnt, uint32_t* counts, uint32_t* base, uint64_t* tmp,
+                        uint32_t* offsets, uint32_t* sorted) {
+    hipStream_t st = ctx->stream;
+    const uint32_t bins = (uint32_t)(we - wb) * NBC;
+    const size_t lds = (size_t)bins * 4;
+    if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
+    VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
+    VK_LAUNCH(ctx, "msm_sort_hist", (k_sort_hist<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk, counts);
+    size_t tmp_bytes = 0;
+    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
+    VK_TRY(ctx->ws[WS_SCAN_TMP].ensure(tmp_bytes));
+    {
+        hipEvent_t ev = nullptr;
+        if (ctx->timing) ctx->timer_begin("msm_scan", &ev);
+        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
+        if (ctx->timing) ctx->timer_end("msm_scan", ev);
+    }
+    VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk, base,
+              tmp);
+    VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
+    return VC_OK;
+}
+
 // ------------------------------------------------------------------ host side
+// GLV halves are < 2^127: window sizes whose top window still spans most of its digit range
+// (16 -> 8 windows, top 15 of 16 bits; 13 -> 10, top 10; 10 -> 13, top 7). A nearly empty
+// top window (c = 15 leaves 7 bits, c = 14 one) piles all its entries into a few buckets:
+// one fine-sort block and long fix-up chains (measured 0.25 + 0.23 ms at 2^16 with c = 15).
+static int glv_window(size_t nv) {
+    if (nv >= (1u << 19)) return 16;
+    if (nv >= (1u << 15)) return 13;
+    return 10;
+}
 static int choose_window(size_t n) {
     if (n >= (1u << 19)) return 16;
     if (n >= (1u << 17)) return 15;
@@ -245,8 +520,14 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     }
     if (n >= 0x7fffffffu) return VC_E_INVALID;
     if (parts < 1 || part < 0 || part >= parts) return VC_E_INVALID;
-    const int c = choose_window(n);
-    const int Wfull = (Fr::BITS + 1 + c - 1) / c;  // one spare bit absorbs the final carry
+    bool glv = false;
+    if constexpr (std::is_same<C, BLS381G1>::value) {
+        if (n >= GLV_MIN_N && n < (1u << 30)) VK_TRY(glv_table_ok(ctx, t, &glv));
+    }
+    const size_t nv = glv ? 2 * n : n;  // MSM terms after the endomorphism split
+    const int c = glv ? glv_window(nv) : choose_window(nv);
+    // one spare bit absorbs the final carry of the signed recoding
+    const int Wfull = glv ? (GLV_BITS + c - 1) / c : (Fr::BITS + 1 + c - 1) / c;
     // window slice [wb, we) of this call (parts > 1: the MSM split by windows across GPUs;
     // the slices' results add up to the whole MSM)
     const int wb = part * Wfull / parts, we = (part + 1) * Wfull / parts;
@@ -258,12 +539,17 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     }
     const uint32_t NB = 1u << (c - 1);
     const uint32_t NBtot = NB * W;
-    const size_t maxL = n * (size_t)W;
+    const size_t maxL = nv * (size_t)W;
     // sorted entries per accumulate thread: 64 at 2^20 x 16 windows (2 rounds of 2048 waves),
     // fewer for window slices / small MSMs so the grid still fills the chip
     // (not below 16: a bucket then straddles more threads and the fix-up's serial merge chain
     // costs more than the emptier accumulate rounds -- measured at 2 windows of 2^20)
-    const uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    // ... and at least twice the mean bucket load, so few buckets straddle more than two
+    // threads (the GLV 2^20 MSM has 64 entries per bucket: M = 128 drops the fix-up's
+    // pointer-jumping rounds, 0.23 -> 0.06 ms, for 0.1 ms more accumulate)
+    if (nv / NB > M / 2 && M < 128) M *= 2;
+    if (const char* em = getenv("VKZG_MSM_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe
     // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 8, or
     // 4 when the segments (one lane each) would not give every SIMD a wave
     uint32_t Lseg = NB >= 64 ? 8 : (NB >= 4 ? 2 : 1);
@@ -277,9 +563,9 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
     uint32_t lgNB = (uint32_t)c - 1;
     const uint32_t FB = lgNB < 8 ? lgNB : 8;
-    const uint32_t NBC = NB >> FB, bins = (uint32_t)W * NBC;
-    const uint32_t nblk = (uint32_t)((n + SORT_CHUNK - 1) / SORT_CHUNK);
-    const size_t ncnt = (size_t)bins * nblk + 1;
+    const uint32_t NBC = NB >> FB;
+    const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
+    const size_t ncnt = (size_t)W * NBC * nblk + 1;
 
     VK_TRY(ctx->ws[WS_DIGITS].ensure(maxL * 8));
     VK_TRY(ctx->ws[WS_COUNTS].ensure(ncnt * 4));
@@ -313,30 +599,34 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
 
     const Aff* bases = t->bases.as<Aff>() + offset;
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
+    const Aff* phi = bases;
+    uint32_t nphi = 0xffffffffu;  // entry j < nphi reads bases[j], else phi[j - nphi]
 
-    const size_t lds = (size_t)bins * 4;
-    if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
-    VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
-    VK_LAUNCH(ctx, "msm_sort_hist", (k_sort_hist<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, wb, we, mont, FB,
-              NBC, nblk, counts);
-    size_t tmp_bytes = 0;
-    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
-    VK_TRY(ctx->ws[WS_SCAN_TMP].ensure(tmp_bytes));
-    {
-        hipEvent_t ev = nullptr;
-        if (ctx->timing) ctx->timer_begin("msm_scan", &ev);
-        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
-        if (ctx->timing) ctx->timer_end("msm_scan", ev);
+    if (glv) {
+        if constexpr (std::is_same<C, BLS381G1>::value) {
+            VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 16));
+            VK_TRY(ctx->ws[WS_GLV_PHI].ensure(n * sizeof(Aff)));
+            uint4* halves = ctx->ws[WS_GLV_SC].as<uint4>();
+            Aff* dphi = ctx->ws[WS_GLV_PHI].as<Aff>();
+            VK_LAUNCH(ctx, "glv_split", (k_glv_split<Fr>), (n + 255) / 256, 256, 0, d_sc, (uint32_t)n, mont,
+                      glv_consts(), halves);
+            VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), (n + 255) / 256, 256, 0, bases, (uint32_t)n,
+                      bls_fq_mont(GLV_BETA), dphi);
+            VK_TRY(sort_entries(ctx, GlvDigits{halves, inf, (uint32_t)n}, (uint32_t)nv, c, wb, we, FB, NBC, nblk,
+                                ncnt, counts, base, tmp, offsets, sorted));
+            phi = dphi;
+            nphi = (uint32_t)n;
+        }
+    } else {
+        VK_TRY(sort_entries(ctx, ScalarDigits<Fr>{d_sc, inf, mont}, (uint32_t)nv, c, wb, we, FB, NBC, nblk, ncnt,
+                            counts, base, tmp, offsets, sorted));
     }
-    VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Fr>), nblk, 256, lds, d_sc, inf, (uint32_t)n, c, wb, we, mont,
-              FB, NBC, nblk, base, tmp);
-    VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
-    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= n*W
+    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W
     VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
     uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
     VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-    VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, sorted, offsets,
-              NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
+    VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted,
+              offsets, NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
     VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max));
     VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
     std::vector<Acc> ht((size_t)W * (J + 1));
@@ -538,8 +828,8 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
         uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
         VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab,
-                  d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(),
+        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab, tab,
+                  0xffffffffu, d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(),
                   d_carry.as<Acc>(), d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max);
         VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
                                  d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max));
@@ -568,10 +858,13 @@ int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_pt
     return VC_E_INVALID;
 }
 
-int msm_windows(int curve, size_t n, int* c, int* W) {
+int msm_windows(int curve, size_t n, int* c, int* W, int* terms) {
     int bits = curve == VC_CURVE_BN254 ? BN254Fr::BITS : curve == VC_CURVE_BLS12_381 ? BLS381Fr::BITS : BandFr::BITS;
-    *c = choose_window(n);
-    *W = (bits + 1 + *c - 1) / *c;
+    // BLS12-381 tables of subgroup points take the GLV split (2n terms of 127-bit scalars)
+    const bool glv = curve == VC_CURVE_BLS12_381 && n >= GLV_MIN_N && n < (1u << 30);
+    *c = glv ? glv_window(2 * n) : choose_window(n);
+    *W = glv ? (GLV_BITS + *c - 1) / *c : (bits + 1 + *c - 1) / *c;
+    if (terms) *terms = glv ? 2 : 1;
     return VC_OK;
 }
 

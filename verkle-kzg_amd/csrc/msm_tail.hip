@@ -119,26 +119,24 @@ __device__ __forceinline__ typename C::Acc shfl_acc(const typename C::Acc& v, ui
 
 // stage 1: lane sums K (msm_bitsum_k) selected items of one (w, q) sum serially, then the wave
 // folds its 64 lane sums (xor butterfly) -- K + 6 iterations of one add:
-//   q < J: R_s over s with bit q set (S/2 items);  q == J: acc_s (S items).
-// partial[(w * (J + 1) + q) * PW + wave_in_sum], PW = ceil(S / (64 K)).
-// Cost model: a wave-level BLS12-381 EC add is ~18 us of one SIMD's issue (a lone wave
-// saturates the SIMD: tools/microbench), priced in SIMD rounds.
+//   q < J: R_s over s with bit q set (S/2 items, nb1 waves);  q == J: acc_s (S items, nb2 waves).
+// Waves are laid out compactly (window by window: J x nb1 bit-sum waves, then nb2), so the grid
+// holds only busy waves and every CU gets at most one block (a grid with idle waves let the
+// dispatcher stack two busy blocks on some CUs: their SIMDs ran two waves, twice as long).
 template <class C>
 __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __restrict__ accs,
                                                    const typename C::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
-                                                   uint32_t K, uint32_t PW, uint32_t n_waves,
+                                                   uint32_t K, uint32_t nb1, uint32_t nb2, uint32_t n_waves,
                                                    typename C::Acc* __restrict__ partial) {
     using Acc = typename C::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
-    const uint32_t sum = gw / PW, wv = gw % PW;
-    const uint32_t w = sum / (J + 1), q = sum % (J + 1);
+    const uint32_t per_w = J * nb1 + nb2;
+    const uint32_t w = gw / per_w, r = gw % per_w;
+    const uint32_t q = r < J * nb1 ? r / nb1 : J;
+    const uint32_t wv = r < J * nb1 ? r % nb1 : r - J * nb1;
     const uint32_t n_items = q < J ? S / 2 : S;
     const uint32_t base = wv * 64 * K;
-    if (base >= n_items) {  // whole wave idle (uniform branch)
-        if (lane == 0) partial[gw] = C::zero();
-        return;
-    }
     const Acc* src = (q < J ? Rs : accs) + (size_t)w * S;
     Acc v = C::zero();
     for (uint32_t it = 0; it < K + 6; it++) {
@@ -155,24 +153,28 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __res
     if (lane == 0) partial[gw] = v;
 }
 
-// stage 2: one wave per sum folds its PW partials (ceil(PW/64) per lane, then the butterfly)
+// stage 2: one wave per (w, q) sum folds its partials (nb1 or nb2: ceil(n/64) per lane, then
+// the butterfly)
 template <class C>
-__global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __restrict__ partial, uint32_t PW,
-                                                   typename C::Acc* __restrict__ out) {
+__global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __restrict__ partial, uint32_t J,
+                                                   uint32_t nb1, uint32_t nb2, typename C::Acc* __restrict__ out) {
     using Acc = typename C::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
+    const uint32_t w = sum / (J + 1), q = sum % (J + 1);
+    const uint32_t cnt = q < J ? nb1 : nb2;
+    const size_t start = (size_t)w * (J * nb1 + nb2) + (q < J ? q * nb1 : J * nb1);
     uint32_t span = 1, lg = 0;
-    while (span < PW && span < 64) {
+    while (span < cnt && span < 64) {
         span <<= 1;
         lg++;
     }
-    const uint32_t nk = (PW + 63) / 64;
+    const uint32_t nk = (cnt + 63) / 64;
     Acc v = C::zero();
     for (uint32_t it = 0; it < nk + lg; it++) {
         Acc o;
         if (it < nk) {
             const uint32_t k = lane + it * 64;
-            o = k < PW ? partial[(size_t)sum * PW + k] : C::zero();
+            o = k < cnt ? partial[start + k] : C::zero();
         } else {
             o = shfl_acc<C>(v, 1u << (it - nk));
         }
@@ -222,10 +224,11 @@ int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t*
               Lseg, S, accs, Rs);
     const uint32_t sums = (uint32_t)W * (J + 1);
     const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);
-    const uint32_t PW = msm_bitsum_pw(S, K);
-    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (sums * PW * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, PW,
-              sums * PW, partial);
-    VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<CI>), sums, 64, 0, partial, PW, out);
+    const uint32_t nb1 = msm_bitsum_pw(S / 2, K), nb2 = msm_bitsum_pw(S, K);
+    const uint32_t n_waves = (uint32_t)W * (J * nb1 + nb2);
+    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
+              n_waves, partial);
+    VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<CI>), sums, 64, 0, partial, J, nb1, nb2, out);
     return VC_OK;
 }
 

@@ -4,16 +4,21 @@
 #include "ec.hpp"
 
 namespace vk {
-// items per lane of the bit-sum stage: as many as keep >= 1024 waves (one per SIMD) busy,
-// within [2, 8]: each wave also pays a 6-add butterfly, so K = 1 doubles the waves for one
-// add less per lane (measured: 2-window slices of 2^20, K = 1 -> 2 cut the stage ~2x)
+// items per lane of the bit-sum stage: the smallest K in [2, 16] whose busy waves (a wave per
+// 64 K items of each of the W (J + 1) sums) fit one wave per SIMD (1024): a wave costs K + 6
+// serial adds (its butterfly included) and a SIMD's second wave doubles its time, so fewer,
+// longer waves win until every SIMD has one (measured: 1192 busy waves at K = 7 took 2x the
+// 960 of K = 8 on a GLV 2^20 MSM)
 inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J) {
-    const uint64_t items = (uint64_t)W * ((uint64_t)J * (S / 2) + S);
-    uint64_t k = items / (1024ull * 64);
-    return (uint32_t)(k < 2 ? 2 : (k > 8 ? 8 : k));
+    for (uint32_t k = 2; k < 16; k++) {
+        const uint64_t per = 64ull * k;
+        const uint64_t busy = (uint64_t)W * ((uint64_t)J * ((S / 2 + per - 1) / per) + (S + per - 1) / per);
+        if (busy <= 1024) return k;
+    }
+    return 16;
 }
-// partial slots per (window, bit) sum of the bit-sum stage (K items per lane, 64 lanes)
-inline uint32_t msm_bitsum_pw(uint32_t S, uint32_t K) { return (S + 64 * K - 1) / (64 * K); }
+// waves (= partial slots) of one bit-stage sum over `items` items (K per lane, 64 lanes)
+inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K) { return (items + 64 * K - 1) / (64 * K); }
 template <class C>
 int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
                    typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,

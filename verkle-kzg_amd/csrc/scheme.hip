@@ -668,6 +668,7 @@ int vc_kzg_setup(vc_ctx* ctx, size_t max_items, const uint64_t* secret, int* tab
         delete t;
         return st;
     }
+    t->subgroup = 1;  // l_j(s) * G
     ctx->tables.push_back(t);
     *table_id = (int)ctx->tables.size() - 1;
     if (size) *size = n;

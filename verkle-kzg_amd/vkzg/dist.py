@@ -62,14 +62,16 @@ def all_gather_partials(part_words, world, device=None):
     return torch.stack(outs).cpu().numpy().view(np.uint32)
 
 
-def window_count(curve, n):
-    """(window bits c, window count W) the engine picks for an n-term MSM (vc_msm_windows)."""
+def window_count(curve, n, with_terms=False):
+    """(window bits c, window count W[, terms per point]) the engine picks for an n-term MSM
+    (vc_msm_windows); terms per point = 2 when the GLV split applies."""
     import ctypes
     from ._lib import check, lib
     from .engine import CURVE_IDS
-    c, w = ctypes.c_int(0), ctypes.c_int(0)
-    check(lib().vc_msm_windows(CURVE_IDS[curve], n, ctypes.byref(c), ctypes.byref(w)), "vc_msm_windows")
-    return c.value, w.value
+    c, w, t = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    check(lib().vc_msm_windows(CURVE_IDS[curve], n, ctypes.byref(c), ctypes.byref(w), ctypes.byref(t)),
+          "vc_msm_windows")
+    return (c.value, w.value, t.value) if with_terms else (c.value, w.value)
 
 
 def all_gather_commitments(xy, inf, total, world):
