@@ -215,10 +215,11 @@ def test_msm_window_parts(engines, oracle_c, curve, n, parts):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("width,batch,c", [(256, 700, 8), (64, 3000, 12), (255, 520, 16)])
+@pytest.mark.parametrize("width,batch,c", [(256, 700, 8), (64, 3000, 12), (255, 520, 16), (5, 30000, 20)])
 def test_batch_commit_persistent(engines, oracle_c, curve, width, batch, c):
-    """large batches take the persistent equal-run path (runs straddling two commits, piece
-    combine); sampled commits vs the oracle, for three table window sizes"""
+    """large batches take the chunk-major path (width cut into chunks, one piece per (chunk,
+    commit), piece combine); sampled commits vs the oracle, for four table window sizes up to
+    the 20-bit windows of the bench's config-3 table"""
     import vkzg
     e = engines[curve]
     rng = np.random.default_rng(31 + c)

@@ -172,43 +172,31 @@ __global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __rest
 }
 
 // ------------------------------------------------------------------ the batched commit
-// Persistent item ranges: the batch x width (commit, base) items are cut into nlanes equal
-// runs of K consecutive items (K <= width, so a run touches at most two commits), one run
-// per lane, with nlanes = what the chip holds in ONE round (occupancy x CUs). A run keeps
-// one accumulator per commit it touches and stores them as two pieces; k_fb_combine adds
-// the ~width/K pieces of each commit. (A thread-group-per-commit mapping left the last
-// round 20 % full at 10k commits: 61 % of the chip.)
+// Chunk-major runs: the width is cut into nch chunks of <= K bases and run r = chunk * batch + g
+// adds commit g's items of chunk `chunk`. The 64 lanes of a wave are 64 commits at the same base
+// and window, so each gather instruction stays inside one (base, window) block of the table
+// (3 MB at c = 16) instead of touching 64 blocks spread over the whole table (GBs): far fewer
+// distinct pages per instruction, and the identity-base skip is wave-uniform.
 template <class C, class Fr>
-__global__ void __launch_bounds__(256) k_fb_commit(const FbE<C>* __restrict__ tab,
-                                                  const uint8_t* __restrict__ inf, uint32_t width,
-                                                  int c, int W, const uint32_t* __restrict__ sc,
-                                                  uint32_t batch, int mont, uint32_t K, uint32_t nlanes,
-                                                  typename C::Acc* __restrict__ piece) {
+__global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>* __restrict__ tab,
+                                                     const uint8_t* __restrict__ inf, uint32_t width,
+                                                     int c, int W, const uint32_t* __restrict__ sc,
+                                                     uint32_t batch, int mont, uint32_t K, uint32_t nruns,
+                                                     typename C::Acc* __restrict__ piece) {
     using Acc = typename C::Acc;
-    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= nlanes) return;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nruns) return;
+    const uint32_t chunk = r / batch, g = r - chunk * batch;
     const uint32_t NBk = 1u << (c - 1);
     const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
-    const size_t items = (size_t)batch * width;
-    const size_t it0 = (size_t)l * K, it1 = min(it0 + K, items);
-    uint32_t g_cur = (uint32_t)(it0 / width);
-    int slot = 0;
+    const uint32_t i0 = chunk * K, i1 = min(i0 + K, width);
     Acc acc = C::zero();
-    for (size_t it = it0; it < it1; it++) {
-        const uint32_t g = (uint32_t)(it / width), i = (uint32_t)(it - (size_t)g * width);
-        if (g != g_cur) {  // run crosses into the next commit (at most once: K <= width)
-            piece[2 * (size_t)l] = acc;
-            acc = C::zero();
-            slot = 1;
-            g_cur = g;
-        }
+    for (uint32_t i = i0; i < i1; i++) {
         if (inf[i]) continue;
-        fe<Fr> s = load_scalar_fb<Fr>(sc, it);
+        fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
         if (mont) s = fe_from_mont<Fr>(s);
         const FbE<C>* ti = tab + (size_t)i * W * NBk;
         uint32_t carry = 0;
-        // digit of the next window computed one step ahead so its table entry is in flight
-        // while the current mixed add runs (random 96 B reads from a 0.1-13 GB table)
         auto next_digit = [&]() -> int32_t {
             uint32_t raw = (s.v[0] & mask) + carry;
 #pragma unroll
@@ -229,21 +217,17 @@ __global__ void __launch_bounds__(256) k_fb_commit(const FbE<C>* __restrict__ ta
             if (d != 0) acc = C::madd(acc, P, d < 0);
         }
     }
-    piece[2 * (size_t)l + slot] = acc;
+    piece[r] = acc;
 }
 
-// commit g = sum of its pieces: lanes l0..l1 cover items [g*width, (g+1)*width)
+// commit g = sum over chunks of piece[chunk * batch + g] (coalesced across g)
 template <class C>
-__global__ void __launch_bounds__(256) k_fb_combine(const typename C::Acc* __restrict__ piece, uint32_t width,
-                                                   uint32_t batch, uint32_t K, typename C::Acc* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_fb_combine_cm(const typename C::Acc* __restrict__ piece, uint32_t nch,
+                                                      uint32_t batch, typename C::Acc* __restrict__ out) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= batch) return;
-    const size_t l0 = (size_t)g * width / K, l1 = ((size_t)(g + 1) * width - 1) / K;
-    typename C::Acc acc = C::zero();
-    for (size_t l = l0; l <= l1; l++) {
-        const uint32_t gl = (uint32_t)(l * K / width);  // first commit of lane l's run
-        acc = C::add(acc, piece[2 * l + (gl == g ? 0 : 1)]);
-    }
+    typename C::Acc acc = piece[g];
+    for (uint32_t k = 1; k < nch; k++) acc = C::add(acc, piece[(size_t)k * batch + g]);
     out[g] = acc;
 }
 
@@ -340,7 +324,7 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c) {
     using Fr = typename std::conditional<std::is_same<C, BN254G1>::value, BN254Fr,
                                          typename std::conditional<std::is_same<C, BLS381G1>::value, BLS381Fr,
                                                                    BandFr>::type>::type;
-    if (c < 4 || c > 16) return VC_E_INVALID;
+    if (c < 4 || c > 20) return VC_E_INVALID;
     const uint32_t n = (uint32_t)t->n;
     const int W = (Fr::BITS + 1 + c - 1) / c;
     const uint32_t NBk = 1u << (c - 1);
@@ -380,7 +364,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (batch == 0) return VC_OK;
     VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
     static uint32_t lanes_cache = 0;
-    if (!lanes_cache) lanes_cache = resident_lanes(k_fb_commit<C, Fr>, 256);
+    if (!lanes_cache) lanes_cache = resident_lanes(k_fb_commit_cm<C, Fr>, 256);
     const size_t items = batch * width;
     const size_t lanes = lanes_cache ? lanes_cache : 131072;
     const int W = t->fb_W;
@@ -411,17 +395,25 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // host staging vectors die on return
         return VC_OK;
     }
-    size_t K = (items + lanes - 1) / lanes;
-    K = std::max<size_t>(1, std::min<size_t>(K, width));
-    const size_t nlanes = (items + K - 1) / K;
-    if (nlanes >= (1ull << 31)) return VC_E_RANGE;
-    VK_TRY(ctx->ws[WS_PIECE].ensure(2 * nlanes * sizeof(Acc)));
-    VK_LAUNCH(ctx, "fb_commit", (k_fb_commit<C, Fr>), (nlanes + 255) / 256, 256, 0,
+    // chunk-major: the chunk count minimising rounds-of-resident-lanes x items-per-run
+    // (fewest chunks on ties: fewer pieces to combine)
+    size_t K = width, best = SIZE_MAX;
+    for (size_t nc = 1; nc <= width; nc++) {
+        const size_t k = (width + nc - 1) / nc;
+        if ((width + k - 1) / k != nc) continue;  // same K as a smaller chunk count
+        const size_t cost = ((nc * batch + lanes - 1) / lanes) * k;
+        if (cost < best) best = cost, K = k;
+    }
+    const size_t nch = (width + K - 1) / K;
+    const size_t nruns = nch * batch;
+    if (nruns >= (1ull << 31)) return VC_E_RANGE;
+    VK_TRY(ctx->ws[WS_PIECE].ensure(nruns * sizeof(Acc)));
+    VK_LAUNCH(ctx, "fb_commit", (k_fb_commit_cm<C, Fr>), (nruns + 255) / 256, 256, 0,
               t->fb.as<FbE<C>>(), t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, t->fb_W,
-              reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, (uint32_t)K, (uint32_t)nlanes,
+              reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, (uint32_t)K, (uint32_t)nruns,
               ctx->ws[WS_PIECE].as<Acc>());
-    VK_LAUNCH(ctx, "fb_combine", (k_fb_combine<C>), (batch + 255) / 256, 256, 0, ctx->ws[WS_PIECE].as<Acc>(),
-              (uint32_t)width, (uint32_t)batch, (uint32_t)K, ctx->ws[WS_OUT].as<Acc>());
+    VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_cm<C>), (batch + 255) / 256, 256, 0,
+              ctx->ws[WS_PIECE].as<Acc>(), (uint32_t)nch, (uint32_t)batch, ctx->ws[WS_OUT].as<Acc>());
     VK_LAUNCH(ctx, "fb_normalize_out", (k_normalize<C>), (batch + 255) / 256, 256, 0,
               ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
               reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);

@@ -13,6 +13,17 @@
 #include <string.h>
 
 #define VK_HD __host__ __device__ __forceinline__
+// occupancy targets for the two VALU-heavy kernels (waves per SIMD; 0 = compiler's choice)
+#if defined(VK_COMMIT_WPE) && VK_COMMIT_WPE > 0
+#define VK_COMMIT_OCC __attribute__((amdgpu_waves_per_eu(VK_COMMIT_WPE)))
+#else
+#define VK_COMMIT_OCC
+#endif
+#if defined(VK_ACC_WPE) && VK_ACC_WPE > 0
+#define VK_ACC_OCC __attribute__((amdgpu_waves_per_eu(VK_ACC_WPE)))
+#else
+#define VK_ACC_OCC
+#endif
 
 namespace vk {
 

@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ 
 
 // ------------------------------------------------------------------ bucket accumulation
 template <class C>
-__global__ void __launch_bounds__(256) k_msm_accumulate(
+__global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     const typename C::Aff* __restrict__ bases, const typename C::Aff* __restrict__ phi, uint32_t nphi,
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename C::Acc* __restrict__ buckets, typename C::Acc* __restrict__ carry_in,
