@@ -55,6 +55,9 @@ struct Table {
     // 1: every base lies in the prime-order subgroup (the GLV endomorphism acts as lambda, so
     // msm.hip may split scalars), 0: some base does not, -1: not checked yet
     int subgroup = -1;
+    // GLV: phi(P) = (beta x, y) of every base, computed by the first MSM that splits scalars
+    int phi_ok = 0;
+    DevBuf phi;
 };
 
 enum WsSlot {
@@ -93,7 +96,6 @@ enum WsSlot {
     WS_NXT2,
     WS_CHAIN,
     WS_GLV_SC,
-    WS_GLV_PHI,
     WS_GLV_FLAG,
     WS_COUNT_
 };

@@ -550,10 +550,12 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     // pointer-jumping rounds, 0.23 -> 0.06 ms, for 0.1 ms more accumulate)
     if (nv / NB > M / 2 && M < 128) M *= 2;
     if (const char* em = getenv("VKZG_MSM_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe
-    // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 8, or
-    // 4 when the segments (one lane each) would not give every SIMD a wave
-    uint32_t Lseg = NB >= 64 ? 8 : (NB >= 4 ? 2 : 1);
-    if (Lseg == 8 && (size_t)(NB / Lseg) * W < 65536) Lseg = 4;
+    // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 4, or 2
+    // when the segments (one lane each) would not give every SIMD a wave (GLV 2^20: 4 at 8
+    // windows, 2 for the 1-4 window slices of multi-GPU runs; 8 measured 0.1-0.15 ms slower)
+    uint32_t Lseg = NB >= 64 ? 4 : (NB >= 4 ? 2 : 1);
+    if (Lseg == 4 && (size_t)(NB / Lseg) * W < 65536) Lseg = 2;
+    if (const char* el = getenv("VKZG_MSM_LSEG")) Lseg = (uint32_t)std::max(1, atoi(el));  // tuning probe
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
     while ((1u << J) < S) J++;
@@ -605,13 +607,16 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     if (glv) {
         if constexpr (std::is_same<C, BLS381G1>::value) {
             VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 16));
-            VK_TRY(ctx->ws[WS_GLV_PHI].ensure(n * sizeof(Aff)));
             uint4* halves = ctx->ws[WS_GLV_SC].as<uint4>();
-            Aff* dphi = ctx->ws[WS_GLV_PHI].as<Aff>();
+            if (!t->phi_ok) {  // phi of the whole table, once (bases never change under it)
+                VK_TRY(t->phi.ensure(t->n * sizeof(Aff)));
+                VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), (t->n + 255) / 256, 256, 0, t->bases.as<Aff>(),
+                          (uint32_t)t->n, bls_fq_mont(GLV_BETA), t->phi.as<Aff>());
+                t->phi_ok = 1;
+            }
+            const Aff* dphi = t->phi.as<Aff>() + offset;
             VK_LAUNCH(ctx, "glv_split", (k_glv_split<Fr>), (n + 255) / 256, 256, 0, d_sc, (uint32_t)n, mont,
                       glv_consts(), halves);
-            VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), (n + 255) / 256, 256, 0, bases, (uint32_t)n,
-                      bls_fq_mont(GLV_BETA), dphi);
             VK_TRY(sort_entries(ctx, GlvDigits{halves, inf, (uint32_t)n}, (uint32_t)nv, c, wb, we, FB, NBC, nblk,
                                 ncnt, counts, base, tmp, offsets, sorted));
             phi = dphi;
@@ -627,11 +632,22 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
     VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted,
               offsets, NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
-    VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max));
+    const uint32_t guard = msm_fixup_guard_rounds(nv, NB, M);
+    VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max,
+                             guard));
     VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
     std::vector<Acc> ht((size_t)W * (J + 1));
+    uint32_t Lmax = 0;
     VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipMemcpyAsync(&Lmax, chain_max, 4, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));
+    if (Lmax > (1u << guard)) {  // rare (heavily repeated scalars): finish the chains, redo the tail
+        VK_TRY(msm_tail_fixup_more<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, guard,
+                                      Lmax));
+        VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
+        VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
+        VK_CHECK_HIP(hipStreamSynchronize(st));
+    }
     // MSM = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host, 64-bit limbs)
     int lg_seg = 0;
     while ((1u << lg_seg) < Lseg) lg_seg++;

@@ -36,11 +36,14 @@ __global__ void __launch_bounds__(256) k_fixup_jump(const typename C::Acc* __res
                                                    const uint8_t* __restrict__ through, uint32_t Tmax,
                                                    const uint32_t* __restrict__ Lp, uint32_t M,
                                                    typename C::Acc* __restrict__ val_out,
-                                                   uint32_t* __restrict__ nxt_out) {
+                                                   uint32_t* __restrict__ nxt_out, uint32_t span,
+                                                   const uint32_t* __restrict__ chain_max) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t T = (*Lp + M - 1) / M;
     if (u >= T || u >= Tmax || through[u] == 0) return;  // no carry piece in thread u
-    const uint32_t n = nxt_in[u];
+    // device-guarded round (launched before the host knows the longest chain): a round the
+    // chains do not need passes its input through unchanged
+    const uint32_t n = (chain_max && span >= *chain_max) ? NONE_T : nxt_in[u];
     if (n == NONE_T) {
         val_out[u] = val_in[u];
         nxt_out[u] = NONE_T;
@@ -127,6 +130,7 @@ template <class C>
 __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __restrict__ accs,
                                                    const typename C::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
                                                    uint32_t K, uint32_t nb1, uint32_t nb2, uint32_t n_waves,
+                                                   const uint32_t* __restrict__ offsets,
                                                    typename C::Acc* __restrict__ partial) {
     using Acc = typename C::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
@@ -144,7 +148,11 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __res
         if (it < K) {
             const uint32_t m = base + it * 64 + lane;  // lane-interleaved rows
             const uint32_t idx = q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m;
-            o = m < n_items ? src[idx] : C::zero();
+            // Lseg = 1 (no segment stage): the items are the buckets themselves (offsets != null),
+            // an empty bucket was never written
+            const size_t g = (size_t)w * S + idx;
+            const bool live = m < n_items && (!offsets || offsets[g + 1] > offsets[g]);
+            o = live ? src[idx] : C::zero();
         } else {
             o = shfl_acc<C>(v, 1u << (it - K));
         }
@@ -183,33 +191,72 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __res
     if (lane == 0) out[sum] = v;
 }
 
+// pointer-jumping rounds r0 <= r < r1 (span 2^r) for a host-known Lmax, or -- guarded -- rounds
+// whose kernels compare span with the device's chain_max: no host sync in the pipeline;
+// msm_tail_fixup_more finishes the rare longer chains afterwards. The carry pieces ping-pong
+// between `carry` and WS_CARRY2 (links: WS_NXT / WS_NXT2), so the parity of r0 says where the
+// latest state is.
+template <class C>
+static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* carry,
+                        const uint8_t* through, uint32_t r0, uint32_t r1, const uint32_t* d_chain_max,
+                        const typename C::Acc** sum) {
+    using CI = typename C::Inl;
+    using Acc = typename C::Acc;
+    VK_TRY(ctx->ws[WS_CARRY2].ensure((size_t)(T + 8) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_NXT].ensure((size_t)(T + 8) * 4));
+    VK_TRY(ctx->ws[WS_NXT2].ensure((size_t)(T + 8) * 4));
+    Acc* va = carry;
+    Acc* vb = ctx->ws[WS_CARRY2].as<Acc>();
+    uint32_t* na = ctx->ws[WS_NXT].as<uint32_t>();
+    uint32_t* nb = ctx->ws[WS_NXT2].as<uint32_t>();
+    if (r0 & 1) {  // continuing after an odd number of rounds: the latest state is in the second pair
+        std::swap(va, vb);
+        std::swap(na, nb);
+    }
+    if (r0 == 0) VK_LAUNCH(ctx, "msm_fixup_init", (k_fixup_init<CI>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
+    for (uint32_t r = r0; r < r1; r++) {
+        VK_LAUNCH(ctx, "msm_fixup_jump", (k_fixup_jump<CI>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
+                  nb, 1u << r, d_chain_max);
+        std::swap(va, vb);
+        std::swap(na, nb);
+    }
+    *sum = va;
+    return VC_OK;
+}
+
 template <class C>
 int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
                    typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
-                   const uint32_t* owner_b, const uint32_t* d_chain_max) {
+                   const uint32_t* owner_b, const uint32_t* d_chain_max, uint32_t guarded) {
     using CI = typename C::Inl;
     using Acc = typename C::Acc;
-    uint32_t Lmax = 0;
-    VK_CHECK_HIP(hipMemcpyAsync(&Lmax, d_chain_max, 4, hipMemcpyDeviceToHost, ctx->stream));
-    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     const Acc* sum = carry;
-    if (Lmax >= 2) {
-        VK_TRY(ctx->ws[WS_CARRY2].ensure((size_t)(T + 8) * sizeof(Acc)));
-        VK_TRY(ctx->ws[WS_NXT].ensure((size_t)(T + 8) * 4));
-        VK_TRY(ctx->ws[WS_NXT2].ensure((size_t)(T + 8) * 4));
-        Acc* va = carry;
-        Acc* vb = ctx->ws[WS_CARRY2].as<Acc>();
-        uint32_t* na = ctx->ws[WS_NXT].as<uint32_t>();
-        uint32_t* nb = ctx->ws[WS_NXT2].as<uint32_t>();
-        VK_LAUNCH(ctx, "msm_fixup_init", (k_fixup_init<CI>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
-        for (uint32_t span = 1; span < Lmax; span <<= 1) {
-            VK_LAUNCH(ctx, "msm_fixup_jump", (k_fixup_jump<CI>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
-                      nb);
-            std::swap(va, vb);
-            std::swap(na, nb);
-        }
-        sum = va;
+    if (guarded) {
+        VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, 0, guarded, d_chain_max, &sum));
+    } else {
+        uint32_t Lmax = 0;
+        VK_CHECK_HIP(hipMemcpyAsync(&Lmax, d_chain_max, 4, hipMemcpyDeviceToHost, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        uint32_t r1 = 0;
+        while (Lmax >= 2 && (1u << r1) < Lmax) r1++;
+        if (r1 > 0) VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, 0, r1, nullptr, &sum));
     }
+    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<CI>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
+    return VC_OK;
+}
+
+// after `guarded` guarded rounds: chains longer than 2^guarded threads (Lmax read back with the
+// results) get their remaining rounds, then the owners are rewritten (idempotent)
+template <class C>
+int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
+                        typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
+                        const uint32_t* owner_b, uint32_t guarded, uint32_t Lmax) {
+    using CI = typename C::Inl;
+    using Acc = typename C::Acc;
+    uint32_t r1 = guarded;
+    while ((1u << r1) < Lmax) r1++;
+    const Acc* sum = carry;
+    VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, guarded, r1, nullptr, &sum));
     VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<CI>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
     return VC_OK;
 }
@@ -220,21 +267,29 @@ int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t*
                     uint32_t Lseg, uint32_t S, uint32_t J, typename C::Acc* accs, typename C::Acc* Rs,
                     typename C::Acc* partial, typename C::Acc* out) {
     using CI = typename C::Inl;
-    VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<CI>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB, W,
-              Lseg, S, accs, Rs);
+    const uint32_t* live = nullptr;
+    if (Lseg == 1) {  // segments of one bucket: R_s = acc_s = B_s, read in place
+        accs = Rs = const_cast<typename C::Acc*>(buckets);
+        live = offsets;
+    } else {
+        VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<CI>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB,
+                  W, Lseg, S, accs, Rs);
+    }
     const uint32_t sums = (uint32_t)W * (J + 1);
     const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);
     const uint32_t nb1 = msm_bitsum_pw(S / 2, K), nb2 = msm_bitsum_pw(S, K);
     const uint32_t n_waves = (uint32_t)W * (J * nb1 + nb2);
     VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
-              n_waves, partial);
+              n_waves, live, partial);
     VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<CI>), sums, 64, 0, partial, J, nb1, nb2, out);
     return VC_OK;
 }
 
 #define VK_INST_TAIL(C)                                                                                        \
     template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, C::Acc*, const uint8_t*,  \
-                                   const C::Acc*, const uint32_t*, const uint32_t*);                           \
+                                   const C::Acc*, const uint32_t*, const uint32_t*, uint32_t);                     \
+    template int msm_tail_fixup_more<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, C::Acc*,          \
+                                        const uint8_t*, const C::Acc*, const uint32_t*, uint32_t, uint32_t);            \
     template int msm_tail_reduce<C>(vc_ctx*, const C::Acc*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
                                     uint32_t, C::Acc*, C::Acc*, C::Acc*, C::Acc*);
 VK_INST_TAIL(BN254G1)

@@ -19,10 +19,25 @@ inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J) {
 }
 // waves (= partial slots) of one bit-stage sum over `items` items (K per lane, 64 lanes)
 inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K) { return (items + 64 * K - 1) / (64 * K); }
+// guarded = 0: read the longest chain back (host sync) and run exactly the rounds it needs;
+// guarded = r > 0: r device-guarded rounds, no sync (chains up to 2^r threads; longer ones are
+// finished by msm_tail_fixup_more once the caller has read chain_max with its results)
 template <class C>
 int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
                    typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
-                   const uint32_t* owner_b, const uint32_t* d_chain_max);
+                   const uint32_t* owner_b, const uint32_t* d_chain_max, uint32_t guarded = 0);
+template <class C>
+int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
+                        typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
+                        const uint32_t* owner_b, uint32_t guarded, uint32_t Lmax);
+// guarded rounds for nv entries over NB buckets per window at M entries per thread: covers a
+// bucket of 4x the mean load (the top window of a GLV split uses half its buckets: 2x)
+inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {
+    const size_t chain = 4 * nv / ((size_t)NB * M) + 2;
+    uint32_t r = 1;
+    while ((1ull << r) < chain && r < 6) r++;
+    return r;
+}
 template <class C>
 int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, typename C::Acc* accs, typename C::Acc* Rs,
