@@ -1,0 +1,74 @@
+"""Radix-2^29 Montgomery arithmetic of the accumulate / commit loops (csrc/ff29.hpp), checked on
+the host against Python integers: congruences mod p, the output bounds the kernels' bound
+analysis relies on (ec29.hpp header), limb normalisation, the packed form and the conversions
+to and from the 32-bit-limb Montgomery form. Includes max-limb stress operands (column
+accumulator overflow would show as a wrong residue)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIELDS = {
+    "bls12_381_fq": (0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab, 14, 12),
+    "bn254_fq": (21888242871839275222246405745257275088696311157297823662689037894645226208583, 9, 8),
+    "bls12_381_fr": (0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001, 9, 8),
+}
+M29 = (1 << 29) - 1
+
+
+def val(limbs):
+    return sum(v << (29 * j) for j, v in enumerate(limbs))
+
+
+@pytest.fixture(scope="module")
+def lines(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("ff29") / "ff29_check"
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                           os.path.join(HERE, "cpp", "ff29_check.cpp"), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)], text=True)
+    return [json.loads(ln) for ln in out.splitlines()]
+
+
+def test_ff29_ops(lines):
+    seen = set()
+    for d in lines:
+        p, L, N = FIELDS[d["f"]]
+        Rp = 1 << (29 * L)
+        R = 1 << (32 * N)
+        r = val(d["r"])
+        op = d["op"]
+        seen.add((d["f"], op))
+        if op == "mul":
+            a, b = val(d["a"]), val(d["b"])
+            assert (r * Rp - a * b) % p == 0
+            assert r < a * b // Rp + p
+            assert all(v <= M29 for v in d["r"][:-1])
+        elif op == "add":
+            assert r == val(d["a"]) + val(d["b"])
+            assert all(v <= M29 + 7 for v in d["r"][:-1])
+        elif op in ("sub4", "sub16"):
+            k = int(op[3:])
+            a, b = val(d["a"]), val(d["b"])
+            assert r == a - b + k * p
+            assert all(v <= M29 + 7 for v in d["r"][:-1])
+        elif op == "canon":
+            assert r < p and (r - val(d["a"])) % p == 0
+        elif op == "unpack":
+            assert r == val(d["a"])
+        elif op == "mont":
+            v = val(d["a"])
+            assert (r - v * Rp * pow(R, -1, p)) % p == 0
+            back = sum(w << (32 * k) for k, w in enumerate(d["back"]))
+            assert back == v
+    assert len(seen) == 3 * 7
+
+
+def test_ff29_zero_test(lines):
+    """is_zero_mo29 (product outputs below 2p) agrees with the residue"""
+    for d in lines:
+        if d["op"] == "mont":
+            p = FIELDS[d["f"]][0]
+            # "a" of a mont record is canon(r) of the same iteration's product
+            assert d["zero_mo"] == (1 if val(d["a"]) % p == 0 else 0)

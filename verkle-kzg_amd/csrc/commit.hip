@@ -19,6 +19,7 @@
 
 #include "ctx.hpp"
 #include "ec.hpp"
+#include "ec29.hpp"
 
 namespace vk {
 
@@ -30,14 +31,15 @@ struct FbEntryNoPad {
 template <class C>
 using FbE = FbEntryNoPad<C>;  // padding 96 -> 128 B measured slower (4.54 -> 4.93 ms at c = 16)
 
-// copy one window's normalised multiples into the table: tab[(i*W + w)*NBk + k] = aff[i*NBk + k]
+// copy one window's normalised multiples into the table: tab[(i*W + w)*NBk + k] = aff[i*NBk + k],
+// in the packed-29 form the commit loops read
 template <class C>
 __global__ void k_fb_place(const typename C::Aff* __restrict__ aff, uint32_t n, uint32_t NBk, int W, int w,
                            FbE<C>* __restrict__ tab) {
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= (size_t)n * NBk) return;
     size_t i = j / NBk, k = j - i * NBk;
-    tab[(i * W + w) * NBk + k].a = aff[j];
+    Fast29<C>::type::pack_aff(aff[j], &tab[(i * W + w) * NBk + k].a);  // packed-29 (ec29.hpp)
 }
 
 template <class Fr>
@@ -183,14 +185,14 @@ __global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>
                                                      int c, int W, const uint32_t* __restrict__ sc,
                                                      uint32_t batch, int mont, uint32_t K, uint32_t nruns,
                                                      typename C::Acc* __restrict__ piece) {
-    using Acc = typename C::Acc;
+    using FC = typename Fast29<C>::type;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nruns) return;
     const uint32_t chunk = r / batch, g = r - chunk * batch;
     const uint32_t NBk = 1u << (c - 1);
     const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
     const uint32_t i0 = chunk * K, i1 = min(i0 + K, width);
-    Acc acc = C::zero();
+    typename FC::Acc acc = FC::zero();
     for (uint32_t i = i0; i < i1; i++) {
         if (inf[i]) continue;
         fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
@@ -214,10 +216,10 @@ __global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>
                 dn = next_digit();
                 Pn = ti[(size_t)(w + 1) * NBk + (dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0)].a;
             }
-            if (d != 0) acc = C::madd(acc, P, d < 0);
+            if (d != 0) acc = FC::madd(acc, FC::load(&P), d < 0);
         }
     }
-    piece[r] = acc;
+    piece[r] = FC::store(acc);
 }
 
 // commit g = sum over chunks of piece[chunk * batch + g] (coalesced across g)
@@ -261,6 +263,7 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
                                                         int W, const uint32_t* __restrict__ sc, int mont,
                                                         uint32_t bpc, int wpt, typename C::Acc* __restrict__ part) {
     using Acc = typename C::Acc;
+    using FC = typename Fast29<C>::type;
     __shared__ Acc wsum[4];
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
     const uint32_t WG = (uint32_t)(W + wpt - 1) / wpt;
@@ -268,7 +271,7 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
     const uint32_t i = j / WG, wg = j % WG;
     const uint32_t NBk = 1u << (c - 1);
     const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
-    Acc acc = C::zero();
+    typename FC::Acc fa = FC::zero();
     if (i < width && !inf[i]) {
         fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
         if (mont) s = fe_from_mont<Fr>(s);
@@ -283,10 +286,10 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
             carry = raw > half ? 1u : 0u;
             const int32_t d = carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
             if (w >= wb && d != 0)
-                acc = C::madd(acc, ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].a, d < 0);
+                fa = FC::madd(fa, FC::load(&ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].a), d < 0);
         }
     }
-    acc = fb_wave_sum<C>(acc);
+    Acc acc = fb_wave_sum<C>(FC::store(fa));
     const int wave = threadIdx.x / 64;
     if ((threadIdx.x & 63) == 0) wsum[wave] = acc;
     __syncthreads();
@@ -426,7 +429,7 @@ static int table_from_acc_t(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) 
     t->curve = ctx->curve;
     t->n = n;
     t->fb_c = t->fb_W = 0;
-    t->phi_ok = 0;
+    t->fast_ok = t->phi_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(typename C::Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
     if (n == 0) return VC_OK;

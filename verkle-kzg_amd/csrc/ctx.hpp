@@ -55,9 +55,10 @@ struct Table {
     // 1: every base lies in the prime-order subgroup (the GLV endomorphism acts as lambda, so
     // msm.hip may split scalars), 0: some base does not, -1: not checked yet
     int subgroup = -1;
-    // GLV: phi(P) = (beta x, y) of every base, computed by the first MSM that splits scalars
-    int phi_ok = 0;
-    DevBuf phi;
+    // packed-29 copies (ec29.hpp) read by the accumulate: the bases at [0, n) and, once a GLV
+    // MSM has run, phi(P) = (beta x, y) of every base at [n, 2n); built on first use
+    int fast_ok = 0, phi_ok = 0;
+    DevBuf fast;
 };
 
 enum WsSlot {
@@ -97,6 +98,9 @@ enum WsSlot {
     WS_CHAIN,
     WS_GLV_SC,
     WS_GLV_FLAG,
+    WS_RAW_B,  // radix-29 accumulators written by k_msm_accumulate (converted by k_fast_store)
+    WS_RAW_C,
+    WS_RAW_O,
     WS_COUNT_
 };
 

@@ -1,0 +1,184 @@
+// Mixed additions over the radix-2^29 fields (ff29.hpp) for the VALU-bound inner loops:
+// Pippenger bucket accumulation (k_msm_accumulate) and the fixed-base commits (commit.hip).
+// Points in HBM stay in the ec.hpp layouts; the tables these loops read hold x R' mod p
+// ("packed 29" form, made once per table by k_to_fast), accumulators are converted back to
+// the ec.hpp form (x R) when stored. Same group law and exceptional-case handling as ec.hpp.
+//
+// Value bounds (ff29.hpp keeps residues loosely reduced; rho = p / R'):
+//  SW (XYZZ, a = 0): X < 11p, Y < 7p, ZZ, ZZZ < 1.1p between adds (BN254's rho = 2^-7.4 is
+//    the tight case; BLS12-381's 2^-25 leaves every product output below 1.0001 p).
+//  TE (extended, a = -5, Bandersnatch over BLS12-381 Fr, rho = 2^-6.1): every coordinate is
+//    a product output < 1.9p (fixed point of the bounds with inputs < 2p).
+#pragma once
+#include "ec.hpp"
+#include "ff29.hpp"
+
+namespace vk {
+
+template <class C, class P>
+struct SW29 {
+    using OAcc = typename C::Acc;
+    using OAff = typename C::Aff;
+    using F = typename C::F;
+    struct Aff {
+        f29<P> x, y;
+    };
+    struct Acc {
+        f29<P> x, y, zz, zzz;
+        bool inf;
+    };
+    VK_HD static Acc zero() {
+        Acc r;
+        r.x = r.y = r.zz = r.zzz = zero29<P>();
+        r.inf = true;
+        return r;
+    }
+    // a packed-29 table point
+    VK_HD static Aff load(const OAff* p) {
+        Aff a;
+        a.x = unpack29<P>(p->x.v);
+        a.y = unpack29<P>(p->y.v);
+        return a;
+    }
+    VK_HD static Acc dbl_aff(const f29<P>& x, const f29<P>& y) {
+        const f29<P> U = add29<P>(y, y);
+        const f29<P> V = sqr29<P>(U);
+        const f29<P> W = mul29<P>(U, V);
+        const f29<P> S = mul29<P>(x, V);
+        const f29<P> X2 = sqr29<P>(x);
+        const f29<P> M = add29<P>(add29<P>(X2, X2), X2);
+        Acc r;
+        r.x = sub29<P, 8>(sqr29<P>(M), add29<P>(S, S));
+        r.y = sub29<P, 4>(mul29<P>(M, sub29<P, 16>(S, r.x)), mul29<P>(W, y));
+        r.zz = V;
+        r.zzz = W;
+        r.inf = false;
+        return r;
+    }
+    // madd-2008-s: acc + (x2, +-y2)
+    VK_HD static Acc madd(const Acc& p, const Aff& q, bool neg) {
+        const f29<P> y2 = neg ? neg29<P, 2>(q.y) : q.y;
+        if (p.inf) {
+            Acc r;
+            r.x = q.x;
+            r.y = y2;
+            r.zz = one29<P>();
+            r.zzz = one29<P>();
+            r.inf = false;
+            return r;
+        }
+        const f29<P> U2 = mul29<P>(q.x, p.zz);
+        const f29<P> S2 = mul29<P>(y2, p.zzz);
+        const f29<P> Pd = sub29<P, 16>(U2, p.x);
+        const f29<P> R = sub29<P, 16>(S2, p.y);
+        const f29<P> PP = sqr29<P>(Pd);
+        const f29<P> PPP = mul29<P>(Pd, PP);
+        const f29<P> Q = mul29<P>(p.x, PP);
+        Acc r;
+        r.x = sub2_29<P, 8>(sqr29<P>(R), PPP, add29<P>(Q, Q));
+        r.y = sub29<P, 4>(mul29<P>(R, sub29<P, 16>(Q, r.x)), mul29<P>(p.y, PPP));
+        r.zz = mul29<P>(p.zz, PP);
+        r.zzz = mul29<P>(p.zzz, PPP);
+        r.inf = false;
+        if (is_zero_mo29<P>(r.zz)) {  // P == 0 mod p: q = +-acc (rare)
+            if (is_zero_mo29<P>(mul29<P>(R, one29<P>()))) return dbl_aff(q.x, y2);
+            return zero();
+        }
+        return r;
+    }
+    // back to the ec.hpp accumulator (x R, canonical)
+    VK_HD static OAcc store(const Acc& a) {
+        if (a.inf) return C::zero();
+        OAcc r;
+        r.x = to_mont32<P, F>(a.x);
+        r.y = to_mont32<P, F>(a.y);
+        r.zz = to_mont32<P, F>(a.zz);
+        r.zzz = to_mont32<P, F>(a.zzz);
+        return r;
+    }
+    // ec.hpp affine point (x R) -> packed 29 (x R')
+    VK_HD static void pack_aff(const OAff& a, OAff* out) {
+        OAff o;
+        pack29<P>(canon29<P>(from_mont32<P, F>(a.x)), o.x.v);
+        pack29<P>(canon29<P>(from_mont32<P, F>(a.y)), o.y.v);
+        *out = o;
+    }
+};
+
+template <class C, class P>
+struct TE29 {
+    using OAcc = typename C::Acc;
+    using OAff = typename C::Aff;
+    using F = typename C::F;
+    struct Aff {
+        f29<P> x, y, kt;
+    };
+    struct Acc {
+        f29<P> X, Y, T, Z;
+    };
+    VK_HD static Acc zero() {
+        Acc r;
+        r.X = r.T = zero29<P>();
+        r.Y = r.Z = one29<P>();
+        return r;
+    }
+    VK_HD static Aff load(const OAff* p) {
+        Aff a;
+        a.x = unpack29<P>(p->x.v);
+        a.y = unpack29<P>(p->y.v);
+        a.kt = unpack29<P>(p->kt.v);
+        return a;
+    }
+    // unified mixed add (add-2008-hwcd, Z2 = 1, kt = d x2 y2): complete, no exceptions
+    VK_HD static Acc madd(const Acc& p, const Aff& q, bool neg) {
+        const f29<P> x2 = neg ? neg29<P, 2>(q.x) : q.x;
+        const f29<P> kt = neg ? neg29<P, 2>(q.kt) : q.kt;
+        const f29<P> A = mul29<P>(p.X, x2);
+        const f29<P> B = mul29<P>(p.Y, q.y);
+        const f29<P> Cc = mul29<P>(p.T, kt);
+        const f29<P> E = sub2_29<P, 8>(mul29<P>(add29<P>(p.X, p.Y), add29<P>(x2, q.y)), A, B);
+        const f29<P> Fv = sub29<P, 4>(p.Z, Cc);
+        const f29<P> G = add29<P>(p.Z, Cc);
+        const f29<P> A2 = add29<P>(A, A);
+        const f29<P> H = add29<P>(B, add29<P>(add29<P>(A2, A2), A));  // B - a A, a = -5
+        Acc r;
+        r.X = mul29<P>(E, Fv);
+        r.Y = mul29<P>(G, H);
+        r.T = mul29<P>(E, H);
+        r.Z = mul29<P>(Fv, G);
+        return r;
+    }
+    VK_HD static OAcc store(const Acc& a) {
+        OAcc r;
+        r.X = to_mont32<P, F>(a.X);
+        r.Y = to_mont32<P, F>(a.Y);
+        r.T = to_mont32<P, F>(a.T);
+        r.Z = to_mont32<P, F>(a.Z);
+        return r;
+    }
+    VK_HD static void pack_aff(const OAff& a, OAff* out) {
+        OAff o;
+        pack29<P>(canon29<P>(from_mont32<P, F>(a.x)), o.x.v);
+        pack29<P>(canon29<P>(from_mont32<P, F>(a.y)), o.y.v);
+        pack29<P>(canon29<P>(from_mont32<P, F>(a.kt)), o.kt.v);
+        *out = o;
+    }
+};
+
+// curve of ec.hpp -> its radix-2^29 mixed-add engine
+template <class C>
+struct Fast29;
+template <>
+struct Fast29<BLS381G1> {
+    using type = SW29<BLS381G1, F29BLS381Fq>;
+};
+template <>
+struct Fast29<BN254G1> {
+    using type = SW29<BN254G1, F29BN254Fq>;
+};
+template <>
+struct Fast29<Bandersnatch> {
+    using type = TE29<Bandersnatch, F29BLS381Fr>;
+};
+
+}  // namespace vk

@@ -24,6 +24,7 @@
 #include "ctx.hpp"
 #include "ec.hpp"
 #include "msm_tail.hpp"
+#include "ec29.hpp"
 
 namespace vk {
 
@@ -203,14 +204,18 @@ __global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ 
 }
 
 // ------------------------------------------------------------------ bucket accumulation
+// The bases / phi / fixed-base tables read here are in the packed-29 form (x R', ec29.hpp)
+// and the adds run in radix-2^29 arithmetic. Buckets and pieces are stored raw (radix-29) and
+// converted to the ec.hpp form by k_fast_store: a conversion (4 multiplies) inlined at the
+// three store sites put ~50 KB of rarely-run code into the loop and cost 7 % of the kernel.
 template <class C>
 __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     const typename C::Aff* __restrict__ bases, const typename C::Aff* __restrict__ phi, uint32_t nphi,
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
-    typename C::Acc* __restrict__ buckets, typename C::Acc* __restrict__ carry_in,
-    uint8_t* __restrict__ through, typename C::Acc* __restrict__ owner_piece,
+    typename Fast29<C>::type::Acc* __restrict__ buckets, typename Fast29<C>::type::Acc* __restrict__ carry_in,
+    uint8_t* __restrict__ through, typename Fast29<C>::type::Acc* __restrict__ owner_piece,
     uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max) {
-    using Acc = typename C::Acc;
+    using FC = typename Fast29<C>::type;
     using Aff = typename C::Aff;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t L = offsets[NBtot];  // entry count, read on the device: no host round trip
@@ -229,19 +234,19 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     uint32_t b = lo;
     uint32_t bend = offsets[b + 1];
     bool left_open = offsets[b] < k;
-    Acc acc = C::zero();
+    typename FC::Acc acc = FC::zero();
     // entry j < nphi: bases[j]; j >= nphi: phi[j - nphi] (the GLV endomorphism images)
     auto base_of = [&](uint32_t j) -> const Aff* { return j < nphi ? bases + j : phi + (j - nphi); };
     uint32_t idx = sorted[k];
     Aff P = *base_of(idx & 0x7fffffffu);
     while (true) {
         uint32_t cur = idx;
-        Aff Q = P;
+        const typename FC::Aff Q = FC::load(&P);
         if (k + 1 < e) {  // prefetch next base
             idx = sorted[k + 1];
             P = *base_of(idx & 0x7fffffffu);
         }
-        acc = C::madd(acc, Q, (cur >> 31) != 0);
+        acc = FC::madd(acc, Q, (cur >> 31) != 0);
         k++;
         if (k == bend || k == e) {
             bool right_open = (k == e) && (bend > e);
@@ -260,13 +265,45 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
             }
             if (k == e) break;
             left_open = false;
-            acc = C::zero();
+            acc = FC::zero();
             do {
                 b++;
                 bend = offsets[b + 1];
             } while (bend <= k);
         }
     }
+}
+
+// radix-29 accumulators -> ec.hpp form: the non-empty buckets of a0 (offsets off0), then [0, n1) of
+// a1, then [0, n2) of a2
+template <class C>
+__global__ void __launch_bounds__(256) k_fast_store(const typename Fast29<C>::type::Acc* __restrict__ a0, uint32_t n0,
+                                                   typename C::Acc* __restrict__ o0, const uint32_t* __restrict__ off0,
+                                                   const typename Fast29<C>::type::Acc* __restrict__ a1, uint32_t n1,
+                                                   typename C::Acc* __restrict__ o1,
+                                                   const typename Fast29<C>::type::Acc* __restrict__ a2, uint32_t n2,
+                                                   typename C::Acc* __restrict__ o2) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n0) {  // buckets: only those the accumulate wrote (empty ones keep what the caller put there)
+        if (off0[i + 1] > off0[i]) o0[i] = Fast29<C>::type::store(a0[i]);
+        return;
+    }
+    i -= n0;
+    if (i < n1) {
+        o1[i] = Fast29<C>::type::store(a1[i]);
+        return;
+    }
+    i -= n1;
+    if (i < n2) o2[i] = Fast29<C>::type::store(a2[i]);
+}
+
+// ec.hpp affine points -> packed-29 form (the tables the accumulate / commit loops read)
+template <class C>
+__global__ void __launch_bounds__(256) k_to_fast(const typename C::Aff* __restrict__ in, size_t n,
+                                                typename C::Aff* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fast29<C>::type::pack_aff(in[i], out + i);
 }
 
 // ------------------------------------------------------------------ GLV endomorphism (BLS12-381 G1)
@@ -463,6 +500,58 @@ static int glv_table_ok(vc_ctx* ctx, Table* t, bool* ok) {
     return VC_OK;
 }
 
+// k_msm_accumulate into raw radix-29 buffers, then k_fast_store into the ec.hpp-form buckets /
+// carry pieces / owner pieces the fix-up and the reduction read
+template <class C>
+static int accumulate_run(vc_ctx* ctx, const char* name, uint32_t Tmax, const typename C::Aff* bases,
+                          const typename C::Aff* phi, uint32_t nphi, const uint32_t* sorted, const uint32_t* offsets,
+                          uint32_t NBtot, uint32_t M, typename C::Acc* buckets, typename C::Acc* carry,
+                          uint8_t* through, typename C::Acc* owner, uint32_t* owner_b, uint32_t* chain_max) {
+    using FAcc = typename Fast29<C>::type::Acc;
+    VK_TRY(ctx->ws[WS_RAW_B].ensure((size_t)std::max<uint32_t>(NBtot, 1) * sizeof(FAcc)));
+    VK_TRY(ctx->ws[WS_RAW_C].ensure((size_t)(Tmax + 8) * sizeof(FAcc)));
+    VK_TRY(ctx->ws[WS_RAW_O].ensure((size_t)(Tmax + 8) * sizeof(FAcc)));
+    FAcc* rb = ctx->ws[WS_RAW_B].as<FAcc>();
+    FAcc* rc = ctx->ws[WS_RAW_C].as<FAcc>();
+    FAcc* ro = ctx->ws[WS_RAW_O].as<FAcc>();
+    VK_LAUNCH(ctx, name, (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted, offsets, NBtot,
+              M, rb, rc, through, ro, owner_b, chain_max);
+    const size_t tot = (size_t)NBtot + 2 * (size_t)Tmax;
+    VK_LAUNCH(ctx, "msm_store", (k_fast_store<C>), (tot + 255) / 256, 256, 0, rb, NBtot, buckets, offsets, rc, Tmax,
+              carry, ro, Tmax, owner);
+    return VC_OK;
+}
+
+// the packed-29 copies of a table's bases (and of phi(bases) for GLV MSMs), made once
+template <class C>
+static int fast_tables(vc_ctx* ctx, Table* t, bool with_phi) {
+    using Aff = typename C::Aff;
+    const size_t need = (with_phi ? 2 : 1) * std::max<size_t>(t->n, 1) * sizeof(Aff);
+    if (t->fast.cap < need) {
+        t->fast_ok = t->phi_ok = 0;
+        t->fast.release();
+        VK_TRY(t->fast.ensure(need));
+    }
+    if (!t->fast_ok && t->n > 0) {
+        VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), (t->n + 255) / 256, 256, 0, t->bases.as<Aff>(), t->n,
+                  t->fast.as<Aff>());
+        t->fast_ok = 1;
+    }
+    if constexpr (std::is_same<C, BLS381G1>::value) {
+        if (with_phi && !t->phi_ok && t->n > 0) {
+            DevBuf phi;
+            VK_TRY(phi.ensure(t->n * sizeof(Aff)));
+            VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), (t->n + 255) / 256, 256, 0, t->bases.as<Aff>(), (uint32_t)t->n,
+                      bls_fq_mont(GLV_BETA), phi.as<Aff>());
+            VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), (t->n + 255) / 256, 256, 0, phi.as<Aff>(), t->n,
+                      t->fast.as<Aff>() + t->n);
+            VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // before phi's buffer is freed
+            t->phi_ok = 1;
+        }
+    }
+    return VC_OK;
+}
+
 template <class Src>
 static int sort_entries(vc_ctx* ctx, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB, uint32_t NBC,
                         uint32_t nblk, size_t ncnt, uint32_t* counts, uint32_t* base, uint64_t* tmp,
@@ -599,7 +688,8 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     Acc* bsum_part = ctx->ws[WS_WIN].as<Acc>();
     Acc* tail = ctx->ws[WS_TAIL].as<Acc>();
 
-    const Aff* bases = t->bases.as<Aff>() + offset;
+    VK_TRY(fast_tables<C>(ctx, t, glv));
+    const Aff* bases = t->fast.as<Aff>() + offset;  // packed-29 copies (ec29.hpp)
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
     const Aff* phi = bases;
     uint32_t nphi = 0xffffffffu;  // entry j < nphi reads bases[j], else phi[j - nphi]
@@ -608,13 +698,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         if constexpr (std::is_same<C, BLS381G1>::value) {
             VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 16));
             uint4* halves = ctx->ws[WS_GLV_SC].as<uint4>();
-            if (!t->phi_ok) {  // phi of the whole table, once (bases never change under it)
-                VK_TRY(t->phi.ensure(t->n * sizeof(Aff)));
-                VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), (t->n + 255) / 256, 256, 0, t->bases.as<Aff>(),
-                          (uint32_t)t->n, bls_fq_mont(GLV_BETA), t->phi.as<Aff>());
-                t->phi_ok = 1;
-            }
-            const Aff* dphi = t->phi.as<Aff>() + offset;
+            const Aff* dphi = t->fast.as<Aff>() + t->n + offset;
             VK_LAUNCH(ctx, "glv_split", (k_glv_split<Fr>), (n + 255) / 256, 256, 0, d_sc, (uint32_t)n, mont,
                       glv_consts(), halves);
             VK_TRY(sort_entries(ctx, GlvDigits{halves, inf, (uint32_t)n}, (uint32_t)nv, c, wb, we, FB, NBC, nblk,
@@ -630,8 +714,8 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
     uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
     VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-    VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted,
-              offsets, NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
+    VK_TRY(accumulate_run<C>(ctx, "msm_accumulate", Tmax, bases, phi, nphi, sorted, offsets, NBtot, M, buckets, carry,
+                             through, owner, owner_b, chain_max));
     const uint32_t guard = msm_fixup_guard_rounds(nv, NB, M);
     VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max,
                              guard));
@@ -844,9 +928,9 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
         uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
         VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab, tab,
-                  0xffffffffu, d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(),
-                  d_carry.as<Acc>(), d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max);
+        VK_TRY(accumulate_run<C>(ctx, "sparse_accumulate", Tmax, tab, tab, 0xffffffffu, d_ent.as<uint32_t>(),
+                                 d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
+                                 d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max));
         VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
                                  d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max));
     }
