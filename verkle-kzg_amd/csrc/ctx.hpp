@@ -98,9 +98,7 @@ enum WsSlot {
     WS_CHAIN,
     WS_GLV_SC,
     WS_GLV_FLAG,
-    WS_RAW_B,  // radix-29 accumulators written by k_msm_accumulate (converted by k_fast_store)
-    WS_RAW_C,
-    WS_RAW_O,
+    WS_RAW_B,  // radix-29 row sums of the sparse accumulate (converted by k_fast_store)
     WS_COUNT_
 };
 

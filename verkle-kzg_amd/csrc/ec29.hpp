@@ -86,6 +86,48 @@ struct SW29 {
         }
         return r;
     }
+    // dbl-2008-s-1
+    VK_HD static Acc dbl(const Acc& p) {
+        if (p.inf) return p;
+        const f29<P> U = add29<P>(p.y, p.y);
+        const f29<P> V = sqr29<P>(U);
+        const f29<P> W = mul29<P>(U, V);
+        const f29<P> S = mul29<P>(p.x, V);
+        const f29<P> X2 = sqr29<P>(p.x);
+        const f29<P> M = add29<P>(add29<P>(X2, X2), X2);
+        Acc r;
+        r.x = sub29<P, 8>(sqr29<P>(M), add29<P>(S, S));
+        r.y = sub29<P, 4>(mul29<P>(M, sub29<P, 16>(S, r.x)), mul29<P>(W, p.y));
+        r.zz = mul29<P>(V, p.zz);
+        r.zzz = mul29<P>(W, p.zzz);
+        r.inf = is_zero_mo29<P>(r.zz);  // y == 0: 2P = O
+        return r;
+    }
+    // add-2008-s (both operands general XYZZ accumulators)
+    VK_HD static Acc add(const Acc& p, const Acc& q) {
+        if (p.inf) return q;
+        if (q.inf) return p;
+        const f29<P> U1 = mul29<P>(p.x, q.zz);
+        const f29<P> U2 = mul29<P>(q.x, p.zz);
+        const f29<P> S1 = mul29<P>(p.y, q.zzz);
+        const f29<P> S2 = mul29<P>(q.y, p.zzz);
+        const f29<P> Pd = sub29<P, 4>(U2, U1);
+        const f29<P> R = sub29<P, 4>(S2, S1);
+        const f29<P> PP = sqr29<P>(Pd);
+        const f29<P> PPP = mul29<P>(Pd, PP);
+        const f29<P> Q = mul29<P>(U1, PP);
+        Acc r;
+        r.x = sub2_29<P, 8>(sqr29<P>(R), PPP, add29<P>(Q, Q));
+        r.y = sub29<P, 4>(mul29<P>(R, sub29<P, 16>(Q, r.x)), mul29<P>(S1, PPP));
+        r.zz = mul29<P>(mul29<P>(p.zz, q.zz), PP);
+        r.zzz = mul29<P>(mul29<P>(p.zzz, q.zzz), PPP);
+        r.inf = false;
+        if (is_zero_mo29<P>(r.zz)) {  // P == 0 mod p: q = +-p (rare)
+            if (is_zero_mo29<P>(mul29<P>(R, one29<P>()))) return dbl(p);
+            return zero();
+        }
+        return r;
+    }
     // back to the ec.hpp accumulator (x R, canonical)
     VK_HD static OAcc store(const Acc& a) {
         if (a.inf) return C::zero();
@@ -141,6 +183,27 @@ struct TE29 {
         const f29<P> G = add29<P>(p.Z, Cc);
         const f29<P> A2 = add29<P>(A, A);
         const f29<P> H = add29<P>(B, add29<P>(add29<P>(A2, A2), A));  // B - a A, a = -5
+        Acc r;
+        r.X = mul29<P>(E, Fv);
+        r.Y = mul29<P>(G, H);
+        r.T = mul29<P>(E, H);
+        r.Z = mul29<P>(Fv, G);
+        return r;
+    }
+    // unified add (add-2008-hwcd): 10 multiplies (d T1 T2 as two)
+    VK_HD static Acc add(const Acc& p, const Acc& q) {
+        f29<P> d;
+#pragma unroll
+        for (int j = 0; j < P::L; j++) d.v[j] = P::band_d(j);
+        const f29<P> A = mul29<P>(p.X, q.X);
+        const f29<P> B = mul29<P>(p.Y, q.Y);
+        const f29<P> Cc = mul29<P>(mul29<P>(p.T, q.T), d);
+        const f29<P> D = mul29<P>(p.Z, q.Z);
+        const f29<P> E = sub2_29<P, 8>(mul29<P>(add29<P>(p.X, p.Y), add29<P>(q.X, q.Y)), A, B);
+        const f29<P> Fv = sub29<P, 4>(D, Cc);
+        const f29<P> G = add29<P>(D, Cc);
+        const f29<P> A2 = add29<P>(A, A);
+        const f29<P> H = add29<P>(B, add29<P>(add29<P>(A2, A2), A));
         Acc r;
         r.X = mul29<P>(E, Fv);
         r.Y = mul29<P>(G, H);

@@ -205,9 +205,10 @@ __global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ 
 
 // ------------------------------------------------------------------ bucket accumulation
 // The bases / phi / fixed-base tables read here are in the packed-29 form (x R', ec29.hpp)
-// and the adds run in radix-2^29 arithmetic. Buckets and pieces are stored raw (radix-29) and
-// converted to the ec.hpp form by k_fast_store: a conversion (4 multiplies) inlined at the
-// three store sites put ~50 KB of rarely-run code into the loop and cost 7 % of the kernel.
+// and the adds run in radix-2^29 arithmetic. Buckets and pieces are stored raw (radix-29) for
+// the fix-up and the reduction (msm_tail.hip), which run the same arithmetic; converting them
+// to the ec.hpp form at the three store sites (4 multiplies each) put ~50 KB of rarely-run code
+// into the loop and cost 7 % of the kernel.
 template <class C>
 __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     const typename C::Aff* __restrict__ bases, const typename C::Aff* __restrict__ phi, uint32_t nphi,
@@ -274,27 +275,13 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     }
 }
 
-// radix-29 accumulators -> ec.hpp form: the non-empty buckets of a0 (offsets off0), then [0, n1) of
-// a1, then [0, n2) of a2
+// radix-29 bucket accumulators -> ec.hpp form, non-empty buckets only (empty ones keep what the
+// caller put there)
 template <class C>
-__global__ void __launch_bounds__(256) k_fast_store(const typename Fast29<C>::type::Acc* __restrict__ a0, uint32_t n0,
-                                                   typename C::Acc* __restrict__ o0, const uint32_t* __restrict__ off0,
-                                                   const typename Fast29<C>::type::Acc* __restrict__ a1, uint32_t n1,
-                                                   typename C::Acc* __restrict__ o1,
-                                                   const typename Fast29<C>::type::Acc* __restrict__ a2, uint32_t n2,
-                                                   typename C::Acc* __restrict__ o2) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n0) {  // buckets: only those the accumulate wrote (empty ones keep what the caller put there)
-        if (off0[i + 1] > off0[i]) o0[i] = Fast29<C>::type::store(a0[i]);
-        return;
-    }
-    i -= n0;
-    if (i < n1) {
-        o1[i] = Fast29<C>::type::store(a1[i]);
-        return;
-    }
-    i -= n1;
-    if (i < n2) o2[i] = Fast29<C>::type::store(a2[i]);
+__global__ void __launch_bounds__(256) k_fast_store(const FAcc<C>* __restrict__ a, uint32_t n,
+                                                   const uint32_t* __restrict__ offsets, typename C::Acc* __restrict__ o) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && offsets[i + 1] > offsets[i]) o[i] = Fast29<C>::type::store(a[i]);
 }
 
 // ec.hpp affine points -> packed-29 form (the tables the accumulate / commit loops read)
@@ -500,28 +487,6 @@ static int glv_table_ok(vc_ctx* ctx, Table* t, bool* ok) {
     return VC_OK;
 }
 
-// k_msm_accumulate into raw radix-29 buffers, then k_fast_store into the ec.hpp-form buckets /
-// carry pieces / owner pieces the fix-up and the reduction read
-template <class C>
-static int accumulate_run(vc_ctx* ctx, const char* name, uint32_t Tmax, const typename C::Aff* bases,
-                          const typename C::Aff* phi, uint32_t nphi, const uint32_t* sorted, const uint32_t* offsets,
-                          uint32_t NBtot, uint32_t M, typename C::Acc* buckets, typename C::Acc* carry,
-                          uint8_t* through, typename C::Acc* owner, uint32_t* owner_b, uint32_t* chain_max) {
-    using FAcc = typename Fast29<C>::type::Acc;
-    VK_TRY(ctx->ws[WS_RAW_B].ensure((size_t)std::max<uint32_t>(NBtot, 1) * sizeof(FAcc)));
-    VK_TRY(ctx->ws[WS_RAW_C].ensure((size_t)(Tmax + 8) * sizeof(FAcc)));
-    VK_TRY(ctx->ws[WS_RAW_O].ensure((size_t)(Tmax + 8) * sizeof(FAcc)));
-    FAcc* rb = ctx->ws[WS_RAW_B].as<FAcc>();
-    FAcc* rc = ctx->ws[WS_RAW_C].as<FAcc>();
-    FAcc* ro = ctx->ws[WS_RAW_O].as<FAcc>();
-    VK_LAUNCH(ctx, name, (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted, offsets, NBtot,
-              M, rb, rc, through, ro, owner_b, chain_max);
-    const size_t tot = (size_t)NBtot + 2 * (size_t)Tmax;
-    VK_LAUNCH(ctx, "msm_store", (k_fast_store<C>), (tot + 255) / 256, 256, 0, rb, NBtot, buckets, offsets, rc, Tmax,
-              carry, ro, Tmax, owner);
-    return VC_OK;
-}
-
 // the packed-29 copies of a table's bases (and of phi(bases) for GLV MSMs), made once
 template <class C>
 static int fast_tables(vc_ctx* ctx, Table* t, bool with_phi) {
@@ -663,14 +628,16 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_TRY(ctx->ws[WS_CURSOR].ensure(ncnt * 4));
     VK_TRY(ctx->ws[WS_OFFSETS].ensure((size_t)(NBtot + 1) * 4));
     VK_TRY(ctx->ws[WS_SORTED].ensure(maxL * 4));
-    VK_TRY(ctx->ws[WS_BUCKETS].ensure((size_t)NBtot * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_CARRY].ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    using RAcc = FAcc<C>;  // raw radix-29 accumulators of the accumulate / fix-up / reduction
+    VK_TRY(ctx->ws[WS_BUCKETS].ensure((size_t)NBtot * sizeof(RAcc)));
+    VK_TRY(ctx->ws[WS_CARRY].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
     VK_TRY(ctx->ws[WS_THROUGH].ensure((size_t)(Tmax + 8)));
-    VK_TRY(ctx->ws[WS_OWNER].ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_OWNER].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
     VK_TRY(ctx->ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
-    VK_TRY(ctx->ws[WS_SEG].ensure((size_t)S * W * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_TREE].ensure((size_t)S * W * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)W, J)) * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_SEG].ensure((size_t)S * W * sizeof(RAcc)));
+    VK_TRY(ctx->ws[WS_TREE].ensure((size_t)S * W * sizeof(RAcc)));
+    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)W, J)) *
+                                  sizeof(RAcc)));
     VK_TRY(ctx->ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
 
     uint64_t* tmp = ctx->ws[WS_DIGITS].as<uint64_t>();
@@ -678,14 +645,14 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     uint32_t* base = ctx->ws[WS_CURSOR].as<uint32_t>();
     uint32_t* offsets = ctx->ws[WS_OFFSETS].as<uint32_t>();
     uint32_t* sorted = ctx->ws[WS_SORTED].as<uint32_t>();
-    Acc* buckets = ctx->ws[WS_BUCKETS].as<Acc>();
-    Acc* carry = ctx->ws[WS_CARRY].as<Acc>();
+    RAcc* buckets = ctx->ws[WS_BUCKETS].as<RAcc>();
+    RAcc* carry = ctx->ws[WS_CARRY].as<RAcc>();
     uint8_t* through = ctx->ws[WS_THROUGH].as<uint8_t>();
-    Acc* owner = ctx->ws[WS_OWNER].as<Acc>();
+    RAcc* owner = ctx->ws[WS_OWNER].as<RAcc>();
     uint32_t* owner_b = ctx->ws[WS_OWNER_B].as<uint32_t>();
-    Acc* seg = ctx->ws[WS_SEG].as<Acc>();
-    Acc* rs = ctx->ws[WS_TREE].as<Acc>();
-    Acc* bsum_part = ctx->ws[WS_WIN].as<Acc>();
+    RAcc* seg = ctx->ws[WS_SEG].as<RAcc>();
+    RAcc* rs = ctx->ws[WS_TREE].as<RAcc>();
+    RAcc* bsum_part = ctx->ws[WS_WIN].as<RAcc>();
     Acc* tail = ctx->ws[WS_TAIL].as<Acc>();
 
     VK_TRY(fast_tables<C>(ctx, t, glv));
@@ -714,8 +681,8 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
     uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
     VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-    VK_TRY(accumulate_run<C>(ctx, "msm_accumulate", Tmax, bases, phi, nphi, sorted, offsets, NBtot, M, buckets, carry,
-                             through, owner, owner_b, chain_max));
+    VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted,
+              offsets, NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
     const uint32_t guard = msm_fixup_guard_rounds(nv, NB, M);
     VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max,
                              guard));
@@ -896,9 +863,9 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_TRY(d_ent.ensure(std::max<size_t>(maxL, 1) * 4));
     VK_TRY(d_off.ensure((nch + 1) * 4));
     VK_TRY(d_rows.ensure(batch * sizeof(Acc)));
-    VK_TRY(d_carry.ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(d_carry.ensure((size_t)(Tmax + 8) * sizeof(FAcc<C>)));
     VK_TRY(d_thr.ensure((size_t)(Tmax + 8)));
-    VK_TRY(d_own.ensure((size_t)(Tmax + 8) * sizeof(Acc)));
+    VK_TRY(d_own.ensure((size_t)(Tmax + 8) * sizeof(FAcc<C>)));
     VK_TRY(d_ownb.ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(d_xy.ensure(batch * 2 * C::F::N * 4));
     VK_TRY(d_inf.ensure(batch));
@@ -928,11 +895,16 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
         uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
         VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-        VK_TRY(accumulate_run<C>(ctx, "sparse_accumulate", Tmax, tab, tab, 0xffffffffu, d_ent.as<uint32_t>(),
-                                 d_off.as<uint32_t>(), (uint32_t)nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
-                                 d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max));
-        VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_chunks.as<Acc>(), d_carry.as<Acc>(),
-                                 d_thr.as<uint8_t>(), d_own.as<Acc>(), d_ownb.as<uint32_t>(), chain_max));
+        using RAcc = FAcc<C>;
+        DevBuf& d_raw = ctx->ws[WS_RAW_B];
+        VK_TRY(d_raw.ensure(nch * sizeof(RAcc)));
+        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
+                  d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
+                  d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max);
+        VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
+                                 d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max));
+        VK_LAUNCH(ctx, "sparse_store", (k_fast_store<C>), (nch + 255) / 256, 256, 0, d_raw.as<RAcc>(), (uint32_t)nch,
+                  d_off.as<uint32_t>(), d_chunks.as<Acc>());
     }
     VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
               d_rc.as<uint32_t>(), d_rows.as<Acc>());

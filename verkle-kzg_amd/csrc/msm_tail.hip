@@ -1,12 +1,16 @@
-// Latency-bound tail of the Pippenger MSM (split from msm.hip so the inlined field
-// multiplies these kernels use -- the compiler can then interleave independent multiplies,
-// which halves the latency of a serial EC chain -- do not slow every rebuild of msm.hip).
+// Latency-bound tail of the Pippenger MSM (split from msm.hip to keep rebuilds short). The
+// kernels run the radix-2^29 point arithmetic of ec29.hpp on the raw accumulators of
+// k_msm_accumulate (A = Fast29<C>::type): a serial add chain in one wave is bound by its
+// instruction count (~4.4 cycles per wave64 instruction alone on a SIMD), and the radix-29
+// add is ~20 % shorter than the 32-bit-limb one. Only the W x (J + 1) outputs are converted
+// back to the ec.hpp form (for the host Horner pass).
 #include <hip/hip_runtime.h>
 
 #include <utility>
 
 #include "ctx.hpp"
 #include "ec.hpp"
+#include "ec29.hpp"
 #include "msm_tail.hpp"
 
 namespace vk {
@@ -30,12 +34,12 @@ __global__ void __launch_bounds__(256) k_fixup_init(const uint8_t* __restrict__ 
     nxt[u] = through[u] == 2 && u + 1 < T ? u + 1 : NONE_T;
 }
 
-template <class C>
-__global__ void __launch_bounds__(256) k_fixup_jump(const typename C::Acc* __restrict__ val_in,
+template <class A>
+__global__ void __launch_bounds__(256) k_fixup_jump(const typename A::Acc* __restrict__ val_in,
                                                    const uint32_t* __restrict__ nxt_in,
                                                    const uint8_t* __restrict__ through, uint32_t Tmax,
                                                    const uint32_t* __restrict__ Lp, uint32_t M,
-                                                   typename C::Acc* __restrict__ val_out,
+                                                   typename A::Acc* __restrict__ val_out,
                                                    uint32_t* __restrict__ nxt_out, uint32_t span,
                                                    const uint32_t* __restrict__ chain_max) {
     uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -49,14 +53,14 @@ __global__ void __launch_bounds__(256) k_fixup_jump(const typename C::Acc* __res
         nxt_out[u] = NONE_T;
         return;
     }
-    val_out[u] = C::add(val_in[u], val_in[n]);
+    val_out[u] = A::add(val_in[u], val_in[n]);
     nxt_out[u] = nxt_in[n];
 }
 
-template <class C>
-__global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__ buckets,
-                                                  const typename C::Acc* __restrict__ chain_sum,
-                                                  const typename C::Acc* __restrict__ owner_piece,
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_fixup(typename A::Acc* __restrict__ buckets,
+                                                  const typename A::Acc* __restrict__ chain_sum,
+                                                  const typename A::Acc* __restrict__ owner_piece,
                                                   const uint32_t* __restrict__ owner_bucket,
                                                   uint32_t Tmax, const uint32_t* __restrict__ Lp, uint32_t M) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -65,7 +69,7 @@ __global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__
     uint32_t b = owner_bucket[t];
     if (b == NONE_T) return;
     // an owner piece exists only when the bucket continues into t + 1 (< T by construction)
-    buckets[b] = C::add(owner_piece[t], chain_sum[t + 1]);
+    buckets[b] = A::add(owner_piece[t], chain_sum[t + 1]);
 }
 
 // ------------------------------------------------------------------ bucket reduction
@@ -81,17 +85,17 @@ __global__ void __launch_bounds__(256) k_msm_fixup(typename C::Acc* __restrict__
 // I-cache note: an inlined BLS12-381 EC add is ~34 KB of straight-line code (14 asm multiplies),
 // so a kernel with two add call sites in its loop streams ~70 KB per iteration through a 64 KB
 // instruction cache. Every kernel below has ONE add call site: operands are selected first.
-template <class C>
-__global__ void __launch_bounds__(256) k_msm_segsum(const typename C::Acc* __restrict__ buckets,
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_segsum(const typename A::Acc* __restrict__ buckets,
                                                    const uint32_t* __restrict__ offsets, uint32_t NB, int W,
-                                                   uint32_t Lseg, uint32_t S, typename C::Acc* __restrict__ accs,
-                                                   typename C::Acc* __restrict__ Rs) {
-    using Acc = typename C::Acc;
+                                                   uint32_t Lseg, uint32_t S, typename A::Acc* __restrict__ accs,
+                                                   typename A::Acc* __restrict__ Rs) {
+    using Acc = typename A::Acc;
     uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t w = gid / S, s = gid % S;
     if (w >= (uint32_t)W) return;
     uint32_t lo = s * Lseg, hi = min(lo + Lseg, NB);
-    Acc R = C::zero(), acc = C::zero();
+    Acc R = A::zero(), acc = A::zero();
     // buckets from the top: R += B_j, then acc += R (2 (hi - lo) adds through one call site)
     for (uint32_t it = 0; it < 2 * (hi - lo); it++) {
         const bool second = (it & 1) != 0;
@@ -100,9 +104,9 @@ __global__ void __launch_bounds__(256) k_msm_segsum(const typename C::Acc* __res
             y = R;
         } else {
             const size_t g = (size_t)w * NB + (hi - 1 - it / 2);
-            y = offsets[g + 1] > offsets[g] ? buckets[g] : C::zero();
+            y = offsets[g + 1] > offsets[g] ? buckets[g] : A::zero();
         }
-        const Acc r = C::add(second ? acc : R, y);
+        const Acc r = A::add(second ? acc : R, y);
         if (second) acc = r;
         else R = r;
     }
@@ -110,13 +114,14 @@ __global__ void __launch_bounds__(256) k_msm_segsum(const typename C::Acc* __res
     Rs[gid] = R;
 }
 
-template <class C>
-__device__ __forceinline__ typename C::Acc shfl_acc(const typename C::Acc& v, uint32_t m) {
-    typename C::Acc o;
+template <class A>
+__device__ __forceinline__ typename A::Acc shfl_acc(const typename A::Acc& v, uint32_t m) {
+    static_assert(sizeof(typename A::Acc) % 4 == 0, "");
+    typename A::Acc o;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
-    for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
+    for (int k = 0; k < (int)(sizeof(typename A::Acc) / 4); k++) dst[k] = __shfl_xor(src[k], m, 64);
     return o;
 }
 
@@ -126,13 +131,13 @@ __device__ __forceinline__ typename C::Acc shfl_acc(const typename C::Acc& v, ui
 // Waves are laid out compactly (window by window: J x nb1 bit-sum waves, then nb2), so the grid
 // holds only busy waves and every CU gets at most one block (a grid with idle waves let the
 // dispatcher stack two busy blocks on some CUs: their SIMDs ran two waves, twice as long).
-template <class C>
-__global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __restrict__ accs,
-                                                   const typename C::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __restrict__ accs,
+                                                   const typename A::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
                                                    uint32_t K, uint32_t nb1, uint32_t nb2, uint32_t n_waves,
                                                    const uint32_t* __restrict__ offsets,
-                                                   typename C::Acc* __restrict__ partial) {
-    using Acc = typename C::Acc;
+                                                   typename A::Acc* __restrict__ partial) {
+    using Acc = typename A::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
     const uint32_t per_w = J * nb1 + nb2;
@@ -142,7 +147,7 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __res
     const uint32_t n_items = q < J ? S / 2 : S;
     const uint32_t base = wv * 64 * K;
     const Acc* src = (q < J ? Rs : accs) + (size_t)w * S;
-    Acc v = C::zero();
+    Acc v = A::zero();
     for (uint32_t it = 0; it < K + 6; it++) {
         Acc o;
         if (it < K) {
@@ -152,21 +157,21 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename C::Acc* __res
             // an empty bucket was never written
             const size_t g = (size_t)w * S + idx;
             const bool live = m < n_items && (!offsets || offsets[g + 1] > offsets[g]);
-            o = live ? src[idx] : C::zero();
+            o = live ? src[idx] : A::zero();
         } else {
-            o = shfl_acc<C>(v, 1u << (it - K));
+            o = shfl_acc<A>(v, 1u << (it - K));
         }
-        v = C::add(v, o);
+        v = A::add(v, o);
     }
     if (lane == 0) partial[gw] = v;
 }
 
 // stage 2: one wave per (w, q) sum folds its partials (nb1 or nb2: ceil(n/64) per lane, then
 // the butterfly)
-template <class C>
-__global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __restrict__ partial, uint32_t J,
+template <class C, class A>
+__global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __restrict__ partial, uint32_t J,
                                                    uint32_t nb1, uint32_t nb2, typename C::Acc* __restrict__ out) {
-    using Acc = typename C::Acc;
+    using Acc = typename A::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
     const uint32_t w = sum / (J + 1), q = sum % (J + 1);
     const uint32_t cnt = q < J ? nb1 : nb2;
@@ -177,31 +182,31 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename C::Acc* __res
         lg++;
     }
     const uint32_t nk = (cnt + 63) / 64;
-    Acc v = C::zero();
+    Acc v = A::zero();
     for (uint32_t it = 0; it < nk + lg; it++) {
         Acc o;
         if (it < nk) {
             const uint32_t k = lane + it * 64;
-            o = k < cnt ? partial[start + k] : C::zero();
+            o = k < cnt ? partial[start + k] : A::zero();
         } else {
-            o = shfl_acc<C>(v, 1u << (it - nk));
+            o = shfl_acc<A>(v, 1u << (it - nk));
         }
-        v = C::add(v, o);
+        v = A::add(v, o);
     }
-    if (lane == 0) out[sum] = v;
+    if (lane == 0) out[sum] = A::store(v);
 }
 
 // pointer-jumping rounds r0 <= r < r1 (span 2^r) for a host-known Lmax, or -- guarded -- rounds
 // whose kernels compare span with the device's chain_max: no host sync in the pipeline;
 // msm_tail_fixup_more finishes the rare longer chains afterwards. The carry pieces ping-pong
 // between `carry` and WS_CARRY2 (links: WS_NXT / WS_NXT2), so the parity of r0 says where the
-// latest state is.
+// latest state is. Buffers hold the raw radix-29 accumulators (FAcc<C>).
 template <class C>
-static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* carry,
+static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* carry,
                         const uint8_t* through, uint32_t r0, uint32_t r1, const uint32_t* d_chain_max,
-                        const typename C::Acc** sum) {
-    using CI = typename C::Inl;
-    using Acc = typename C::Acc;
+                        const FAcc<C>** sum) {
+    using A = typename Fast29<C>::type;
+    using Acc = FAcc<C>;
     VK_TRY(ctx->ws[WS_CARRY2].ensure((size_t)(T + 8) * sizeof(Acc)));
     VK_TRY(ctx->ws[WS_NXT].ensure((size_t)(T + 8) * 4));
     VK_TRY(ctx->ws[WS_NXT2].ensure((size_t)(T + 8) * 4));
@@ -213,9 +218,9 @@ static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M,
         std::swap(va, vb);
         std::swap(na, nb);
     }
-    if (r0 == 0) VK_LAUNCH(ctx, "msm_fixup_init", (k_fixup_init<CI>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
+    if (r0 == 0) VK_LAUNCH(ctx, "msm_fixup_init", (k_fixup_init<A>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
     for (uint32_t r = r0; r < r1; r++) {
-        VK_LAUNCH(ctx, "msm_fixup_jump", (k_fixup_jump<CI>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
+        VK_LAUNCH(ctx, "msm_fixup_jump", (k_fixup_jump<A>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
                   nb, 1u << r, d_chain_max);
         std::swap(va, vb);
         std::swap(na, nb);
@@ -225,12 +230,11 @@ static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M,
 }
 
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
-                   typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
-                   const uint32_t* owner_b, const uint32_t* d_chain_max, uint32_t guarded) {
-    using CI = typename C::Inl;
-    using Acc = typename C::Acc;
-    const Acc* sum = carry;
+int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets, FAcc<C>* carry,
+                   const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
+                   const uint32_t* d_chain_max, uint32_t guarded) {
+    using A = typename Fast29<C>::type;
+    const FAcc<C>* sum = carry;
     if (guarded) {
         VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, 0, guarded, d_chain_max, &sum));
     } else {
@@ -241,57 +245,56 @@ int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, type
         while (Lmax >= 2 && (1u << r1) < Lmax) r1++;
         if (r1 > 0) VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, 0, r1, nullptr, &sum));
     }
-    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<CI>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
+    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<A>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
     return VC_OK;
 }
 
 // after `guarded` guarded rounds: chains longer than 2^guarded threads (Lmax read back with the
 // results) get their remaining rounds, then the owners are rewritten (idempotent)
 template <class C>
-int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
-                        typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
-                        const uint32_t* owner_b, uint32_t guarded, uint32_t Lmax) {
-    using CI = typename C::Inl;
-    using Acc = typename C::Acc;
+int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
+                        FAcc<C>* carry, const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
+                        uint32_t guarded, uint32_t Lmax) {
+    using A = typename Fast29<C>::type;
     uint32_t r1 = guarded;
     while ((1u << r1) < Lmax) r1++;
-    const Acc* sum = carry;
+    const FAcc<C>* sum = carry;
     VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, guarded, r1, nullptr, &sum));
-    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<CI>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
+    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<A>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
     return VC_OK;
 }
 
-// outputs W x (J + 1) points: [w][q] = T_wq (q < J), A_w (q == J)
+// outputs W x (J + 1) points in ec.hpp form: [w][q] = T_wq (q < J), A_w (q == J)
 template <class C>
-int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t* offsets, uint32_t NB, int W,
-                    uint32_t Lseg, uint32_t S, uint32_t J, typename C::Acc* accs, typename C::Acc* Rs,
-                    typename C::Acc* partial, typename C::Acc* out) {
-    using CI = typename C::Inl;
+int msm_tail_reduce(vc_ctx* ctx, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
+                    uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
+                    typename C::Acc* out) {
+    using A = typename Fast29<C>::type;
     const uint32_t* live = nullptr;
     if (Lseg == 1) {  // segments of one bucket: R_s = acc_s = B_s, read in place
-        accs = Rs = const_cast<typename C::Acc*>(buckets);
+        accs = Rs = const_cast<FAcc<C>*>(buckets);
         live = offsets;
     } else {
-        VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<CI>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB,
+        VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB,
                   W, Lseg, S, accs, Rs);
     }
     const uint32_t sums = (uint32_t)W * (J + 1);
     const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);
     const uint32_t nb1 = msm_bitsum_pw(S / 2, K), nb2 = msm_bitsum_pw(S, K);
     const uint32_t n_waves = (uint32_t)W * (J * nb1 + nb2);
-    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<CI>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
+    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
               n_waves, live, partial);
-    VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<CI>), sums, 64, 0, partial, J, nb1, nb2, out);
+    VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
     return VC_OK;
 }
 
-#define VK_INST_TAIL(C)                                                                                        \
-    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, C::Acc*, const uint8_t*,  \
-                                   const C::Acc*, const uint32_t*, const uint32_t*, uint32_t);                     \
-    template int msm_tail_fixup_more<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, C::Acc*, C::Acc*,          \
-                                        const uint8_t*, const C::Acc*, const uint32_t*, uint32_t, uint32_t);            \
-    template int msm_tail_reduce<C>(vc_ctx*, const C::Acc*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
-                                    uint32_t, C::Acc*, C::Acc*, C::Acc*, C::Acc*);
+#define VK_INST_TAIL(C)                                                                                      \
+    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,           \
+                                   const uint8_t*, const FAcc<C>*, const uint32_t*, const uint32_t*, uint32_t); \
+    template int msm_tail_fixup_more<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,      \
+                                        const uint8_t*, const FAcc<C>*, const uint32_t*, uint32_t, uint32_t);   \
+    template int msm_tail_reduce<C>(vc_ctx*, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
+                                    uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*);
 VK_INST_TAIL(BN254G1)
 VK_INST_TAIL(BLS381G1)
 VK_INST_TAIL(Bandersnatch)

@@ -2,6 +2,7 @@
 #pragma once
 #include "ctx.hpp"
 #include "ec.hpp"
+#include "ec29.hpp"
 
 namespace vk {
 // items per lane of the bit-sum stage: the smallest K in [2, 16] whose busy waves (a wave per
@@ -22,14 +23,17 @@ inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K) { return (items + 64 *
 // guarded = 0: read the longest chain back (host sync) and run exactly the rounds it needs;
 // guarded = r > 0: r device-guarded rounds, no sync (chains up to 2^r threads; longer ones are
 // finished by msm_tail_fixup_more once the caller has read chain_max with its results)
+// raw radix-29 accumulator of curve C (what k_msm_accumulate writes)
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
-                   typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
-                   const uint32_t* owner_b, const uint32_t* d_chain_max, uint32_t guarded = 0);
+using FAcc = typename Fast29<C>::type::Acc;
 template <class C>
-int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, typename C::Acc* buckets,
-                        typename C::Acc* carry, const uint8_t* through, const typename C::Acc* owner,
-                        const uint32_t* owner_b, uint32_t guarded, uint32_t Lmax);
+int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets, FAcc<C>* carry,
+                   const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
+                   const uint32_t* d_chain_max, uint32_t guarded = 0);
+template <class C>
+int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
+                        FAcc<C>* carry, const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
+                        uint32_t guarded, uint32_t Lmax);
 // guarded rounds for nv entries over NB buckets per window at M entries per thread: covers a
 // bucket of 4x the mean load (the top window of a GLV split uses half its buckets: 2x)
 inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {
@@ -39,7 +43,7 @@ inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {
     return r;
 }
 template <class C>
-int msm_tail_reduce(vc_ctx* ctx, const typename C::Acc* buckets, const uint32_t* offsets, uint32_t NB, int W,
-                    uint32_t Lseg, uint32_t S, uint32_t J, typename C::Acc* accs, typename C::Acc* Rs,
-                    typename C::Acc* partial, typename C::Acc* out);
+int msm_tail_reduce(vc_ctx* ctx, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
+                    uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
+                    typename C::Acc* out);
 }  // namespace vk
