@@ -37,8 +37,7 @@ BYTES_PER_POINT = {"bls12_381": 96 + 32, "bn254": 64 + 32, "bandersnatch": 64 + 
 OUT_BYTES = {"bls12_381": 96, "bn254": 64, "bandersnatch": 64}
 # VALU roofline: field multiplies per mixed add in the accumulate kernel
 # (XYZZ 8M+2S; extended Edwards 8M) x 2 N^2 v_mad_u64_u32 per N-limb Montgomery multiply
-MULS_PER_MADD = {"bls12_381": 10, "bn254": 10, "bandersnatch": 8}
-LIMBS32 = {"bls12_381": 12, "bn254": 8, "bandersnatch": 8}
+CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD"}  # kernel-name match
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
 # (tools_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
@@ -385,16 +384,29 @@ def main():
     # algorithmic bytes of this rank's share of the MSM (n*(96+32) + 96 per MSM)
     shard_bytes = (n * BYTES_PER_POINT[curve] + OUT_BYTES[curve]) / world
     achieved = shard_bytes / acc_s / 1e9 if acc_s else None
-    # VALU roofline: mixed adds of this rank's window slice (one per nonzero digit ~ n per window)
+    # VALU roofline: the accumulate's executed VALU instructions (PMC SQ_INSTS_VALU per launch,
+    # wave-level, from the committed profile of this same command) x 64 lanes / its live time,
+    # against the live issue peak of 4-cycle VALU work (v_mad_u64_u32; VCC adds issue the same,
+    # plain 32-bit adds in half: tools/issueprobe.hip), i.e. lanes x SIMDs x clock / 4
     from vkzg.dist import window_count
     c_bits, w_total, terms = window_count(curve, n, with_terms=True)
     w_rank = (rank + 1) * w_total // world - rank * w_total // world
-    mads = terms * n * w_rank * MULS_PER_MADD[curve] * 2 * LIMBS32[curve] ** 2
+    madds = terms * n * w_rank
     mad_peak = eng.device_mad_rate()
-    valu = {"achieved": mads / acc_s / 1e12 if acc_s else None, "peak": mad_peak, "unit": "T v_mad_u64_u32/s",
-            "frac": (mads / acc_s / 1e12 / mad_peak) if acc_s else None,
-            "work": f"{terms * n}x{w_rank} mixed adds x {MULS_PER_MADD[curve]} Fq mults x {2 * LIMBS32[curve] ** 2} mads",
-            "peak_source": "vc_device_mad_rate, measured live on this GPU"}
+    pmc = json.load(open(PMC_SUMMARY)) if os.path.exists(PMC_SUMMARY) else None
+    insts = None
+    if pmc and world == 1 and pmc.get("config", {}).get("log_n") == a.log_n:
+        key = [k for k in pmc["kernels"] if k.startswith("vk::k_msm_accumulate") and CURVE_TAG[curve] in k]
+        if key:
+            insts = pmc["kernels"][key[0]].get("SQ_INSTS_VALU_per_launch")
+    ach = insts * 64 / acc_s / 1e12 if (insts and acc_s) else None
+    valu = {"achieved": ach, "peak": mad_peak, "unit": "T VALU lane-instructions/s",
+            "frac": (ach / mad_peak) if ach else None,
+            "work": f"{madds} mixed adds (radix-2^29 XYZZ, 10 field multiplies each); "
+                    f"{insts / madds * 64 if insts else float('nan'):.0f} VALU lane-instructions per mixed add (PMC)",
+            "madds_per_s": madds / acc_s if acc_s else None,
+            "peak_source": "vc_device_mad_rate: v_mad_u64_u32 issue rate measured live on this GPU",
+            "insts_source": os.path.relpath(PMC_SUMMARY, ROOT) if insts else None}
     traffic, traffic_src = None, None
     if world == 1 and os.path.exists(PMC_SUMMARY):
         pmc = json.load(open(PMC_SUMMARY))

@@ -13,5 +13,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/fetch -o run
 echo fetch-done
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/bench_write.json
 echo write-done
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES -d $OUT/valu -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline "$@" > $OUT/bench_valu.json
+echo valu-done
 python3 $R/verkle-kzg_amd/tools/prof_summary.py $OUT $OUT/summary.json
 echo profile-done

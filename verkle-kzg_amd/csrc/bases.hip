@@ -342,21 +342,33 @@ int point_words(int curve) {
 int aff_limbs64(int curve) { return curve == VC_CURVE_BLS12_381 ? 6 : 4; }
 
 // ------------------------------------------------------------------ VALU peak probe
-// v_mad_u64_u32 throughput (8 independent chains per lane, 16 waves per SIMD): the peak the
-// MSM kernels' VALU roofline is priced against.
+// Issue rate of v_mad_u64_u32 (64 independent mads per iteration in asm, 8 waves per SIMD): a
+// wave64 64-bit mad issues in 4 cycles per SIMD on gfx950 (tools/issueprobe.hip), like the VCC
+// carry adds; plain 32-bit adds issue in 2. The MSM kernels' VALU roofline is priced against
+// this rate (lane-operations per second).
+#define VK_MADS8_                                              \
+    "v_mad_u64_u32 v[10:11], s[98:99], %0, %1, v[20:21]\n\t" \
+    "v_mad_u64_u32 v[12:13], s[98:99], %0, %1, v[22:23]\n\t" \
+    "v_mad_u64_u32 v[14:15], s[98:99], %0, %1, v[24:25]\n\t" \
+    "v_mad_u64_u32 v[16:17], s[98:99], %0, %1, v[26:27]\n\t" \
+    "v_mad_u64_u32 v[18:19], s[98:99], %0, %1, v[28:29]\n\t" \
+    "v_mad_u64_u32 v[30:31], s[98:99], %0, %1, v[20:21]\n\t" \
+    "v_mad_u64_u32 v[32:33], s[98:99], %0, %1, v[22:23]\n\t" \
+    "v_mad_u64_u32 v[34:35], s[98:99], %0, %1, v[24:25]\n\t"
 __global__ void __launch_bounds__(256) k_mad_probe(uint32_t* out, uint32_t seed, int iters) {
     uint32_t x = seed + threadIdx.x, y = seed * 3 + blockIdx.x;
-    uint64_t a0 = x, a1 = y, a2 = x ^ y, a3 = x + y, a4 = 5, a5 = 7, a6 = 9, a7 = 11;
     for (int i = 0; i < iters; i++) {
-#define VK_MAD_(a) a = (uint64_t)(uint32_t)a * x + (a >> 32);
-        VK_MAD_(a0) VK_MAD_(a1) VK_MAD_(a2) VK_MAD_(a3) VK_MAD_(a4) VK_MAD_(a5) VK_MAD_(a6) VK_MAD_(a7)
-#undef VK_MAD_
+        asm volatile(VK_MADS8_ VK_MADS8_ VK_MADS8_ VK_MADS8_ VK_MADS8_ VK_MADS8_ VK_MADS8_ VK_MADS8_
+                     :: "v"(x), "v"(y)
+                     : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v30", "v31", "v32",
+                       "v33", "v34", "v35", "s98", "s99");
     }
-    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x ^ y;
 }
+#undef VK_MADS8_
 
 int device_mad_rate(vc_ctx* ctx, double* tera_per_s) {
-    const int blocks = 4096, iters = 4096;
+    const int blocks = 8192, iters = 512;
     DevBuf out;
     VK_TRY(out.ensure((size_t)blocks * 256 * 4));
     hipEvent_t a, b;
@@ -371,7 +383,7 @@ int device_mad_rate(vc_ctx* ctx, double* tera_per_s) {
     VK_CHECK_HIP(hipEventElapsedTime(&ms, a, b));
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    *tera_per_s = (double)blocks * 256 * iters * 8 / (ms * 1e-3) / 1e12;
+    *tera_per_s = (double)blocks * 256 * iters * 64 / (ms * 1e-3) / 1e12;
     return VC_OK;
 }
 

@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>
                                                      const uint8_t* __restrict__ inf, uint32_t width,
                                                      int c, int W, const uint32_t* __restrict__ sc,
                                                      uint32_t batch, int mont, uint32_t K, uint32_t nruns,
-                                                     typename C::Acc* __restrict__ piece) {
+                                                     typename Fast29<C>::type::Acc* __restrict__ piece) {
     using FC = typename Fast29<C>::type;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nruns) return;
@@ -219,18 +219,46 @@ __global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>
             if (d != 0) acc = FC::madd(acc, FC::load(&P), d < 0);
         }
     }
-    piece[r] = FC::store(acc);
+    piece[r] = acc;
 }
 
-// commit g = sum over chunks of piece[chunk * batch + g] (coalesced across g)
+// commit g = sum over chunks of the raw pieces piece[chunk * batch + g]: a thread per commit
+// (coalesced across g) for large batches, or a wave per commit (lanes fold a strided share,
+// then an xor butterfly) for small ones, which the chip spreads over up to `width` chunks per
+// commit: a serial chain of 257 adds cost ~2 ms (IPA prover rounds)
 template <class C>
-__global__ void __launch_bounds__(256) k_fb_combine_cm(const typename C::Acc* __restrict__ piece, uint32_t nch,
-                                                      uint32_t batch, typename C::Acc* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_fb_combine_cm(const typename Fast29<C>::type::Acc* __restrict__ piece,
+                                                      uint32_t nch, uint32_t batch, typename C::Acc* __restrict__ out) {
+    using FC = typename Fast29<C>::type;
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= batch) return;
-    typename C::Acc acc = piece[g];
-    for (uint32_t k = 1; k < nch; k++) acc = C::add(acc, piece[(size_t)k * batch + g]);
-    out[g] = acc;
+    typename FC::Acc acc = piece[g];
+    for (uint32_t k = 1; k < nch; k++) acc = FC::add(acc, piece[(size_t)k * batch + g]);
+    out[g] = FC::store(acc);
+}
+template <class C>
+__global__ void __launch_bounds__(64) k_fb_combine_wave(const typename Fast29<C>::type::Acc* __restrict__ piece,
+                                                       uint32_t nch, uint32_t batch, typename C::Acc* __restrict__ out) {
+    using FC = typename Fast29<C>::type;
+    const uint32_t g = blockIdx.x, lane = threadIdx.x;
+    uint32_t span = 1, lg = 0;
+    while (span < nch && span < 64) {
+        span <<= 1;
+        lg++;
+    }
+    const uint32_t nk = (nch + 63) / 64;
+    typename FC::Acc v = FC::zero();
+    for (uint32_t it = 0; it < nk + lg; it++) {  // one add call site
+        typename FC::Acc o;
+        if (it < nk) {
+            const uint32_t k = lane + it * 64;
+            o = k < nch ? piece[(size_t)k * batch + g] : FC::zero();
+        } else {
+            o = shfl_xor_pod(v, 1u << (it - nk));
+        }
+        v = FC::add(v, o);
+    }
+    if (lane == 0) out[g] = FC::store(v);
 }
 
 // ---- latency path for small batches (the IPA prover's L/R, multiproof D/E): every thread
@@ -410,13 +438,25 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     const size_t nch = (width + K - 1) / K;
     const size_t nruns = nch * batch;
     if (nruns >= (1ull << 31)) return VC_E_RANGE;
-    VK_TRY(ctx->ws[WS_PIECE].ensure(nruns * sizeof(Acc)));
+    VK_TRY(ctx->ws[WS_PIECE].ensure(nruns * sizeof(typename Fast29<C>::type::Acc)));
     VK_LAUNCH(ctx, "fb_commit", (k_fb_commit_cm<C, Fr>), (nruns + 255) / 256, 256, 0,
               t->fb.as<FbE<C>>(), t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, t->fb_W,
               reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, (uint32_t)K, (uint32_t)nruns,
-              ctx->ws[WS_PIECE].as<Acc>());
-    VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_cm<C>), (batch + 255) / 256, 256, 0,
-              ctx->ws[WS_PIECE].as<Acc>(), (uint32_t)nch, (uint32_t)batch, ctx->ws[WS_OUT].as<Acc>());
+              ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>());
+    // serial adds per SIMD: a thread per commit (nch adds, batch / 64 waves) vs a wave per commit
+    // (ceil(nch / 64) + log2 adds, batch waves) -- 1024 SIMDs
+    size_t lg = 0;
+    while ((1ull << lg) < std::min<size_t>(nch, 64)) lg++;
+    const size_t cost_thread = nch * ((batch + 65535) / 65536);
+    const size_t cost_wave = ((batch + 1023) / 1024) * ((nch + 63) / 64 + lg);
+    if (cost_thread <= cost_wave)
+        VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_cm<C>), (batch + 255) / 256, 256, 0,
+                  ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>(), (uint32_t)nch, (uint32_t)batch,
+                  ctx->ws[WS_OUT].as<Acc>());
+    else
+        VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_wave<C>), batch, 64, 0,
+                  ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>(), (uint32_t)nch, (uint32_t)batch,
+                  ctx->ws[WS_OUT].as<Acc>());
     VK_LAUNCH(ctx, "fb_normalize_out", (k_normalize<C>), (batch + 255) / 256, 256, 0,
               ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
               reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);

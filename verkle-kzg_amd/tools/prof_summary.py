@@ -1,5 +1,5 @@
 """Summarise a tools_profile.sh run: kernel durations (trace pass) + HBM bytes per launch
-from the FETCH_SIZE / WRITE_SIZE PMC passes, with the gfx950 correction of
+from the FETCH_SIZE / WRITE_SIZE PMC passes (+ SQ_INSTS_VALU, wave-level VALU instructions), with the gfx950 correction of
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts 64 B per 128-B read request, so it is
 doubled; WRITE_SIZE is taken as is.  usage: prof_summary.py <prof dir> <out json>"""
 import csv
@@ -22,7 +22,7 @@ def main(d, out):
             stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                       "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
     pmc = defaultdict(lambda: defaultdict(list))
-    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"), ("valu", "SQ_INSTS_VALU")):
         try:
             with open(f"{d}/{sub}/run_counter_collection.csv") as f:
                 for r in csv.DictReader(f):
@@ -38,6 +38,8 @@ def main(d, out):
             e["FETCH_SIZE_KB_per_launch_raw"] = sum(p["FETCH_SIZE"]) / len(p["FETCH_SIZE"])
         if p.get("WRITE_SIZE"):
             e["WRITE_SIZE_KB_per_launch"] = sum(p["WRITE_SIZE"]) / len(p["WRITE_SIZE"])
+        if p.get("SQ_INSTS_VALU"):
+            e["SQ_INSTS_VALU_per_launch"] = sum(p["SQ_INSTS_VALU"]) / len(p["SQ_INSTS_VALU"])
         if "FETCH_SIZE_KB_per_launch_raw" in e and "WRITE_SIZE_KB_per_launch" in e:
             e["hbm_bytes_per_launch"] = 1024.0 * (2.0 * e["FETCH_SIZE_KB_per_launch_raw"]
                                                   + e["WRITE_SIZE_KB_per_launch"])
