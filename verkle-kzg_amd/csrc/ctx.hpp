@@ -102,6 +102,13 @@ enum WsSlot {
     WS_COUNT_
 };
 
+// a stream and the workspace its launches use: the MSM runs two window slices concurrently
+// (lane 0 = the context's stream + ws, lane 1 = side_stream + ws2)
+struct Lane {
+    hipStream_t st;
+    DevBuf* ws;
+};
+
 struct PendingTimer {
     hipEvent_t a, b;
     std::string name;
@@ -118,6 +125,7 @@ struct vc_ctx {
     std::mutex mu;
     std::vector<vk::Table*> tables;
     vk::DevBuf ws[vk::WS_COUNT_];
+    vk::DevBuf ws2[vk::WS_COUNT_];  // workspace of lane 1 (side_stream)
     bool timing = false;
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
@@ -130,6 +138,7 @@ struct vc_ctx {
     void timer_begin(const char* name, hipEvent_t* a, hipStream_t s = nullptr);
     void timer_end(const char* name, hipEvent_t a, hipStream_t s = nullptr);
     void collect_timers();  // call after the stream is synchronised
+    vk::Lane lane(int i) { return i == 0 ? vk::Lane{stream, ws} : vk::Lane{side_stream, ws2}; }
     vk::Table* table(int id) {
         if (id < 0 || id >= (int)tables.size() || !tables[id]) return nullptr;
         return tables[id];

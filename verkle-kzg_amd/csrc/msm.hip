@@ -518,27 +518,28 @@ static int fast_tables(vc_ctx* ctx, Table* t, bool with_phi) {
 }
 
 template <class Src>
-static int sort_entries(vc_ctx* ctx, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB, uint32_t NBC,
-                        uint32_t nblk, size_t ncnt, uint32_t* counts, uint32_t* base, uint64_t* tmp,
+static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
+                        uint32_t NBC, uint32_t nblk, size_t ncnt, uint32_t* counts, uint32_t* base, uint64_t* tmp,
                         uint32_t* offsets, uint32_t* sorted) {
-    hipStream_t st = ctx->stream;
+    hipStream_t st = L.st;
     const uint32_t bins = (uint32_t)(we - wb) * NBC;
     const size_t lds = (size_t)bins * 4;
     if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
     VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
-    VK_LAUNCH(ctx, "msm_sort_hist", (k_sort_hist<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk, counts);
+    VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
+                 counts);
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
-    VK_TRY(ctx->ws[WS_SCAN_TMP].ensure(tmp_bytes));
+    VK_TRY(L.ws[WS_SCAN_TMP].ensure(tmp_bytes));
     {
         hipEvent_t ev = nullptr;
-        if (ctx->timing) ctx->timer_begin("msm_scan", &ev);
-        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
-        if (ctx->timing) ctx->timer_end("msm_scan", ev);
+        if (ctx->timing) ctx->timer_begin("msm_scan", &ev, st);
+        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(L.ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
+        if (ctx->timing) ctx->timer_end("msm_scan", ev, st);
     }
-    VK_LAUNCH(ctx, "msm_sort_coarse", (k_sort_coarse<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk, base,
-              tmp);
-    VK_LAUNCH(ctx, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
+    VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
+                 base, tmp);
+    VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
     return VC_OK;
 }
 
@@ -560,6 +561,168 @@ static int choose_window(size_t n) {
     if (n >= (1u << 9)) return 9;
     if (n >= 64) return 7;
     return 5;
+}
+
+// One window slice [wb, we) of an MSM enqueued on a lane: sort, accumulate, fix-up, reduction and
+// the read-back of its W (J + 1) reduced points; slice_finish waits for it and folds them by
+// Horner over bit positions. msm_run_t can run two slices of a (rank's) window range on the two
+// lanes, staggered: slice 1's sort beside slice 0's accumulate, slice 1's accumulate after slice
+// 0's (an event), beside slice 0's latency-bound fix-up and reduction (off by default, see below).
+template <class C>
+struct MsmSlice {
+    using Acc = typename C::Acc;
+    Lane L{};
+    int c = 0, wb = 0, we = 0, W = 0;
+    uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
+    uint32_t* offsets = nullptr;
+    uint32_t* chain_max = nullptr;
+    uint8_t* through = nullptr;
+    uint32_t* owner_b = nullptr;
+    FAcc<C>* buckets = nullptr;
+    FAcc<C>* carry = nullptr;
+    FAcc<C>* owner = nullptr;
+    FAcc<C>* seg = nullptr;
+    FAcc<C>* rs = nullptr;
+    FAcc<C>* bsum_part = nullptr;
+    Acc* tail = nullptr;
+    std::vector<Acc> ht;
+    uint32_t Lmax = 0;
+};
+
+template <class C, class Src>
+static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const typename C::Aff* bases,
+                         const typename C::Aff* phi, uint32_t nphi, hipEvent_t acc_wait, hipEvent_t acc_done) {
+    using Acc = typename C::Acc;
+    using RAcc = FAcc<C>;  // raw radix-29 accumulators of the accumulate / fix-up / reduction
+    const Lane L = sl.L;
+    const int c = sl.c, W = sl.W;
+    const uint32_t NB = 1u << (c - 1);
+    const uint32_t NBtot = NB * (uint32_t)W;
+    const size_t maxL = nv * (size_t)W;
+    // sorted entries per accumulate thread: 64 at 2^20 x 16 windows (2 rounds of 2048 waves),
+    // fewer for window slices / small MSMs so the grid still fills the chip
+    // (not below 16: a bucket then straddles more threads and the fix-up's serial merge chain
+    // costs more than the emptier accumulate rounds -- measured at 2 windows of 2^20)
+    uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    // ... and at least twice the mean bucket load, so few buckets straddle more than two
+    // threads (the GLV 2^20 MSM has 64 entries per bucket: M = 128 drops the fix-up's
+    // pointer-jumping rounds, 0.23 -> 0.06 ms, for 0.1 ms more accumulate)
+    if (nv / NB > M / 2 && M < 128) M *= 2;
+    if (const char* em = getenv("VKZG_MSM_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe
+    // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 4, or 2
+    // when the segments (one lane each) would not give every SIMD a wave (GLV 2^20: 4 at 8
+    // windows, 2 for the 1-4 window slices of multi-GPU runs; 8 measured 0.1-0.15 ms slower)
+    uint32_t Lseg = NB >= 64 ? 4 : (NB >= 4 ? 2 : 1);
+    if (Lseg == 4 && (size_t)(NB / Lseg) * W < 65536) Lseg = 2;
+    if (const char* el = getenv("VKZG_MSM_LSEG")) Lseg = (uint32_t)std::max(1, atoi(el));  // tuning probe
+    const uint32_t S = NB / Lseg;  // power of two
+    uint32_t J = 0;
+    while ((1u << J) < S) J++;
+    const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
+    hipStream_t st = L.st;
+
+    // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
+    uint32_t lgNB = (uint32_t)c - 1;
+    const uint32_t FB = lgNB < 8 ? lgNB : 8;
+    const uint32_t NBC = NB >> FB;
+    const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
+    const size_t ncnt = (size_t)W * NBC * nblk + 1;
+
+    DevBuf* ws = L.ws;
+    VK_TRY(ws[WS_DIGITS].ensure(maxL * 8));
+    VK_TRY(ws[WS_COUNTS].ensure(ncnt * 4));
+    VK_TRY(ws[WS_CURSOR].ensure(ncnt * 4));
+    VK_TRY(ws[WS_OFFSETS].ensure((size_t)(NBtot + 1) * 4));
+    VK_TRY(ws[WS_SORTED].ensure(maxL * 4));
+    VK_TRY(ws[WS_BUCKETS].ensure((size_t)NBtot * sizeof(RAcc)));
+    VK_TRY(ws[WS_CARRY].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
+    VK_TRY(ws[WS_THROUGH].ensure((size_t)(Tmax + 8)));
+    VK_TRY(ws[WS_OWNER].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
+    VK_TRY(ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
+    VK_TRY(ws[WS_SEG].ensure((size_t)S * W * sizeof(RAcc)));
+    VK_TRY(ws[WS_TREE].ensure((size_t)S * W * sizeof(RAcc)));
+    VK_TRY(ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)W, J)) * sizeof(RAcc)));
+    VK_TRY(ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
+    VK_TRY(ws[WS_CHAIN].ensure(4));
+
+    sl.NB = NB;
+    sl.NBtot = NBtot;
+    sl.Tmax = Tmax;
+    sl.M = M;
+    sl.Lseg = Lseg;
+    sl.S = S;
+    sl.J = J;
+    sl.offsets = ws[WS_OFFSETS].as<uint32_t>();
+    sl.chain_max = ws[WS_CHAIN].as<uint32_t>();
+    sl.through = ws[WS_THROUGH].as<uint8_t>();
+    sl.owner_b = ws[WS_OWNER_B].as<uint32_t>();
+    sl.buckets = ws[WS_BUCKETS].as<RAcc>();
+    sl.carry = ws[WS_CARRY].as<RAcc>();
+    sl.owner = ws[WS_OWNER].as<RAcc>();
+    sl.seg = ws[WS_SEG].as<RAcc>();
+    sl.rs = ws[WS_TREE].as<RAcc>();
+    sl.bsum_part = ws[WS_WIN].as<RAcc>();
+    sl.tail = ws[WS_TAIL].as<Acc>();
+
+    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, ncnt, ws[WS_COUNTS].as<uint32_t>(),
+                        ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].as<uint64_t>(), sl.offsets,
+                        ws[WS_SORTED].as<uint32_t>()));
+    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W
+    VK_CHECK_HIP(hipMemsetAsync(sl.chain_max, 0, 4, st));
+    if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
+    VK_LAUNCH_ON(ctx, st, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi,
+                 ws[WS_SORTED].as<uint32_t>(), sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
+                 sl.owner_b, sl.chain_max);
+    if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
+    sl.guard = msm_fixup_guard_rounds(nv, NB, M);
+    VK_TRY(msm_tail_fixup<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
+                             sl.owner_b, sl.chain_max, sl.guard));
+    VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, W, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
+                              sl.tail));
+    return VC_OK;
+}
+
+// read back (after every slice has been enqueued: a copy into pageable memory may block the host)
+template <class C>
+static int slice_fetch(MsmSlice<C>& sl) {
+    sl.ht.resize((size_t)sl.W * (sl.J + 1));
+    VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(typename C::Acc), hipMemcpyDeviceToHost,
+                                sl.L.st));
+    VK_CHECK_HIP(hipMemcpyAsync(&sl.Lmax, sl.chain_max, 4, hipMemcpyDeviceToHost, sl.L.st));
+    return VC_OK;
+}
+
+template <class C>
+static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
+    using Acc = typename C::Acc;
+    VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
+    if (sl.Lmax > (1u << sl.guard)) {  // rare (heavily repeated scalars): finish the chains, redo the tail
+        VK_TRY(msm_tail_fixup_more<C>(ctx, sl.L, sl.Tmax, sl.offsets + sl.NBtot, sl.M, sl.buckets, sl.carry,
+                                      sl.through, sl.owner, sl.owner_b, sl.guard, sl.Lmax));
+        VK_TRY(msm_tail_reduce<C>(ctx, sl.L, sl.buckets, sl.offsets, sl.NB, sl.W, sl.Lseg, sl.S, sl.J, sl.seg, sl.rs,
+                                  sl.bsum_part, sl.tail));
+        VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(Acc), hipMemcpyDeviceToHost,
+                                    sl.L.st));
+        VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
+    }
+    // slice = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host, 64-bit limbs)
+    const uint32_t J = sl.J;
+    int lg_seg = 0;
+    while ((1u << lg_seg) < sl.Lseg) lg_seg++;
+    const int maxpos = sl.c * (sl.we - 1) + lg_seg + (int)J;
+    std::vector<std::vector<int>> at(maxpos + 1);
+    for (int w = 0; w < sl.W; w++) {
+        const int p0 = sl.c * (sl.wb + w);  // absolute bit position of window wb + w
+        at[p0].push_back(w * (int)(J + 1) + (int)J);
+        for (uint32_t j = 0; j < J; j++) at[p0 + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
+    }
+    Acc r = C::zero();
+    for (int pos = maxpos; pos >= 0; pos--) {
+        if (!C::is_zero(r)) r = C::dbl(r);
+        for (int idx : at[pos]) r = C::add(r, sl.ht[idx]);
+    }
+    *res = r;
+    return VC_OK;
 }
 
 template <class C, class Fr>
@@ -591,76 +754,24 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         memcpy(out_acc, &z, sizeof(Acc));
         return VC_OK;
     }
-    const uint32_t NB = 1u << (c - 1);
-    const uint32_t NBtot = NB * W;
-    const size_t maxL = nv * (size_t)W;
-    // sorted entries per accumulate thread: 64 at 2^20 x 16 windows (2 rounds of 2048 waves),
-    // fewer for window slices / small MSMs so the grid still fills the chip
-    // (not below 16: a bucket then straddles more threads and the fix-up's serial merge chain
-    // costs more than the emptier accumulate rounds -- measured at 2 windows of 2^20)
-    uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
-    // ... and at least twice the mean bucket load, so few buckets straddle more than two
-    // threads (the GLV 2^20 MSM has 64 entries per bucket: M = 128 drops the fix-up's
-    // pointer-jumping rounds, 0.23 -> 0.06 ms, for 0.1 ms more accumulate)
-    if (nv / NB > M / 2 && M < 128) M *= 2;
-    if (const char* em = getenv("VKZG_MSM_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe
-    // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 4, or 2
-    // when the segments (one lane each) would not give every SIMD a wave (GLV 2^20: 4 at 8
-    // windows, 2 for the 1-4 window slices of multi-GPU runs; 8 measured 0.1-0.15 ms slower)
-    uint32_t Lseg = NB >= 64 ? 4 : (NB >= 4 ? 2 : 1);
-    if (Lseg == 4 && (size_t)(NB / Lseg) * W < 65536) Lseg = 2;
-    if (const char* el = getenv("VKZG_MSM_LSEG")) Lseg = (uint32_t)std::max(1, atoi(el));  // tuning probe
-    const uint32_t S = NB / Lseg;  // power of two
-    uint32_t J = 0;
-    while ((1u << J) < S) J++;
-    const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
-    hipStream_t st = ctx->stream;
-
-    // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
-    uint32_t lgNB = (uint32_t)c - 1;
-    const uint32_t FB = lgNB < 8 ? lgNB : 8;
-    const uint32_t NBC = NB >> FB;
-    const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
-    const size_t ncnt = (size_t)W * NBC * nblk + 1;
-
-    VK_TRY(ctx->ws[WS_DIGITS].ensure(maxL * 8));
-    VK_TRY(ctx->ws[WS_COUNTS].ensure(ncnt * 4));
-    VK_TRY(ctx->ws[WS_CURSOR].ensure(ncnt * 4));
-    VK_TRY(ctx->ws[WS_OFFSETS].ensure((size_t)(NBtot + 1) * 4));
-    VK_TRY(ctx->ws[WS_SORTED].ensure(maxL * 4));
-    using RAcc = FAcc<C>;  // raw radix-29 accumulators of the accumulate / fix-up / reduction
-    VK_TRY(ctx->ws[WS_BUCKETS].ensure((size_t)NBtot * sizeof(RAcc)));
-    VK_TRY(ctx->ws[WS_CARRY].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
-    VK_TRY(ctx->ws[WS_THROUGH].ensure((size_t)(Tmax + 8)));
-    VK_TRY(ctx->ws[WS_OWNER].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
-    VK_TRY(ctx->ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
-    VK_TRY(ctx->ws[WS_SEG].ensure((size_t)S * W * sizeof(RAcc)));
-    VK_TRY(ctx->ws[WS_TREE].ensure((size_t)S * W * sizeof(RAcc)));
-    VK_TRY(ctx->ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)W, J)) *
-                                  sizeof(RAcc)));
-    VK_TRY(ctx->ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
-
-    uint64_t* tmp = ctx->ws[WS_DIGITS].as<uint64_t>();
-    uint32_t* counts = ctx->ws[WS_COUNTS].as<uint32_t>();
-    uint32_t* base = ctx->ws[WS_CURSOR].as<uint32_t>();
-    uint32_t* offsets = ctx->ws[WS_OFFSETS].as<uint32_t>();
-    uint32_t* sorted = ctx->ws[WS_SORTED].as<uint32_t>();
-    RAcc* buckets = ctx->ws[WS_BUCKETS].as<RAcc>();
-    RAcc* carry = ctx->ws[WS_CARRY].as<RAcc>();
-    uint8_t* through = ctx->ws[WS_THROUGH].as<uint8_t>();
-    RAcc* owner = ctx->ws[WS_OWNER].as<RAcc>();
-    uint32_t* owner_b = ctx->ws[WS_OWNER_B].as<uint32_t>();
-    RAcc* seg = ctx->ws[WS_SEG].as<RAcc>();
-    RAcc* rs = ctx->ws[WS_TREE].as<RAcc>();
-    RAcc* bsum_part = ctx->ws[WS_WIN].as<RAcc>();
-    Acc* tail = ctx->ws[WS_TAIL].as<Acc>();
-
     VK_TRY(fast_tables<C>(ctx, t, glv));
     const Aff* bases = t->fast.as<Aff>() + offset;  // packed-29 copies (ec29.hpp)
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
-    const Aff* phi = bases;
-    uint32_t nphi = 0xffffffffu;  // entry j < nphi reads bases[j], else phi[j - nphi]
-
+    // VKZG_MSM_SLICES=2 runs two staggered slices on the two lanes (tuning probe): measured no
+    // faster at 2^20 BLS12-381 (4.09-4.29 vs 3.98-4.06 ms) -- a 4-window slice's accumulate fills
+    // one wave per SIMD (6-13 % below two), and the overlapped tail shares the same SIMDs
+    static const int slices_env = getenv("VKZG_MSM_SLICES") ? atoi(getenv("VKZG_MSM_SLICES")) : 1;
+    const int nsl = (slices_env == 2 && W >= 2 && nv * (size_t)W >= (1u << 22)) ? 2 : 1;
+    MsmSlice<C> sl[2];
+    for (int k = 0; k < nsl; k++) {
+        sl[k].L = ctx->lane(k);
+        sl[k].c = c;
+        sl[k].wb = wb + k * W / nsl;
+        sl[k].we = wb + (k + 1) * W / nsl;
+        sl[k].W = sl[k].we - sl[k].wb;
+    }
+    hipEvent_t fork = nullptr, join = nullptr, acc0 = nullptr;
+    if (nsl == 2) acc0 = ctx->get_event();
     if (glv) {
         if constexpr (std::is_same<C, BLS381G1>::value) {
             VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 16));
@@ -668,51 +779,39 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
             const Aff* dphi = t->fast.as<Aff>() + t->n + offset;
             VK_LAUNCH(ctx, "glv_split", (k_glv_split<Fr>), (n + 255) / 256, 256, 0, d_sc, (uint32_t)n, mont,
                       glv_consts(), halves);
-            VK_TRY(sort_entries(ctx, GlvDigits{halves, inf, (uint32_t)n}, (uint32_t)nv, c, wb, we, FB, NBC, nblk,
-                                ncnt, counts, base, tmp, offsets, sorted));
-            phi = dphi;
-            nphi = (uint32_t)n;
+            if (nsl == 2) {
+                fork = ctx->get_event();
+                VK_CHECK_HIP(hipEventRecord(fork, ctx->stream));
+                VK_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, fork, 0));
+            }
+            for (int k = 0; k < nsl; k++)
+                VK_TRY(slice_enqueue<C>(ctx, sl[k], GlvDigits{halves, inf, (uint32_t)n}, nv, bases, dphi,
+                                        (uint32_t)n, k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
         }
     } else {
-        VK_TRY(sort_entries(ctx, ScalarDigits<Fr>{d_sc, inf, mont}, (uint32_t)nv, c, wb, we, FB, NBC, nblk, ncnt,
-                            counts, base, tmp, offsets, sorted));
+        if (nsl == 2) {
+            fork = ctx->get_event();
+            VK_CHECK_HIP(hipEventRecord(fork, ctx->stream));
+            VK_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, fork, 0));
+        }
+        for (int k = 0; k < nsl; k++)
+            VK_TRY(slice_enqueue<C>(ctx, sl[k], ScalarDigits<Fr>{d_sc, inf, mont}, nv, bases, bases, 0xffffffffu,
+                                    k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
     }
-    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W
-    VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
-    uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
-    VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
-    VK_LAUNCH(ctx, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi, sorted,
-              offsets, NBtot, M, buckets, carry, through, owner, owner_b, chain_max);
-    const uint32_t guard = msm_fixup_guard_rounds(nv, NB, M);
-    VK_TRY(msm_tail_fixup<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, chain_max,
-                             guard));
-    VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
-    std::vector<Acc> ht((size_t)W * (J + 1));
-    uint32_t Lmax = 0;
-    VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipMemcpyAsync(&Lmax, chain_max, 4, hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipStreamSynchronize(st));
-    if (Lmax > (1u << guard)) {  // rare (heavily repeated scalars): finish the chains, redo the tail
-        VK_TRY(msm_tail_fixup_more<C>(ctx, Tmax, offsets + NBtot, M, buckets, carry, through, owner, owner_b, guard,
-                                      Lmax));
-        VK_TRY(msm_tail_reduce<C>(ctx, buckets, offsets, NB, W, Lseg, S, J, seg, rs, bsum_part, tail));
-        VK_CHECK_HIP(hipMemcpyAsync(ht.data(), tail, ht.size() * sizeof(Acc), hipMemcpyDeviceToHost, st));
-        VK_CHECK_HIP(hipStreamSynchronize(st));
-    }
-    // MSM = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host, 64-bit limbs)
-    int lg_seg = 0;
-    while ((1u << lg_seg) < Lseg) lg_seg++;
-    const int maxpos = c * (we - 1) + lg_seg + (int)J;
-    std::vector<std::vector<int>> at(maxpos + 1);
-    for (int w = 0; w < W; w++) {
-        const int p0 = c * (wb + w);  // absolute bit position of window wb + w
-        at[p0].push_back(w * (int)(J + 1) + (int)J);
-        for (uint32_t j = 0; j < J; j++) at[p0 + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
-    }
+    for (int k = 0; k < nsl; k++) VK_TRY(slice_fetch<C>(sl[k]));
     Acc res = C::zero();
-    for (int pos = maxpos; pos >= 0; pos--) {
-        if (!C::is_zero(res)) res = C::dbl(res);
-        for (int idx : at[pos]) res = C::add(res, ht[idx]);
+    for (int k = 0; k < nsl; k++) {
+        Acc r;
+        VK_TRY(slice_finish<C>(ctx, sl[k], &r));
+        res = C::add(res, r);
+    }
+    if (nsl == 2) {  // later work on the context's stream stays ordered after lane 1
+        join = ctx->get_event();
+        VK_CHECK_HIP(hipEventRecord(join, ctx->side_stream));
+        VK_CHECK_HIP(hipStreamWaitEvent(ctx->stream, join, 0));
+        ctx->event_pool.push_back(fork);  // a wait binds the record it saw: safe to re-record
+        ctx->event_pool.push_back(join);
+        ctx->event_pool.push_back(acc0);
     }
     memcpy(out_acc, &res, sizeof(Acc));
     return VC_OK;
@@ -901,7 +1000,7 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
                   d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
                   d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max);
-        VK_TRY(msm_tail_fixup<C>(ctx, Tmax, d_off.as<uint32_t>() + nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
+        VK_TRY(msm_tail_fixup<C>(ctx, ctx->lane(0), Tmax, d_off.as<uint32_t>() + nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
                                  d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max));
         VK_LAUNCH(ctx, "sparse_store", (k_fast_store<C>), (nch + 255) / 256, 256, 0, d_raw.as<RAcc>(), (uint32_t)nch,
                   d_off.as<uint32_t>(), d_chunks.as<Acc>());

@@ -202,25 +202,25 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
 // between `carry` and WS_CARRY2 (links: WS_NXT / WS_NXT2), so the parity of r0 says where the
 // latest state is. Buffers hold the raw radix-29 accumulators (FAcc<C>).
 template <class C>
-static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* carry,
+static int fixup_rounds(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* carry,
                         const uint8_t* through, uint32_t r0, uint32_t r1, const uint32_t* d_chain_max,
                         const FAcc<C>** sum) {
     using A = typename Fast29<C>::type;
     using Acc = FAcc<C>;
-    VK_TRY(ctx->ws[WS_CARRY2].ensure((size_t)(T + 8) * sizeof(Acc)));
-    VK_TRY(ctx->ws[WS_NXT].ensure((size_t)(T + 8) * 4));
-    VK_TRY(ctx->ws[WS_NXT2].ensure((size_t)(T + 8) * 4));
+    VK_TRY(L.ws[WS_CARRY2].ensure((size_t)(T + 8) * sizeof(Acc)));
+    VK_TRY(L.ws[WS_NXT].ensure((size_t)(T + 8) * 4));
+    VK_TRY(L.ws[WS_NXT2].ensure((size_t)(T + 8) * 4));
     Acc* va = carry;
-    Acc* vb = ctx->ws[WS_CARRY2].as<Acc>();
-    uint32_t* na = ctx->ws[WS_NXT].as<uint32_t>();
-    uint32_t* nb = ctx->ws[WS_NXT2].as<uint32_t>();
+    Acc* vb = L.ws[WS_CARRY2].as<Acc>();
+    uint32_t* na = L.ws[WS_NXT].as<uint32_t>();
+    uint32_t* nb = L.ws[WS_NXT2].as<uint32_t>();
     if (r0 & 1) {  // continuing after an odd number of rounds: the latest state is in the second pair
         std::swap(va, vb);
         std::swap(na, nb);
     }
-    if (r0 == 0) VK_LAUNCH(ctx, "msm_fixup_init", (k_fixup_init<A>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
+    if (r0 == 0) VK_LAUNCH_ON(ctx, L.st, "msm_fixup_init", (k_fixup_init<A>), (T + 255) / 256, 256, 0, through, T, Lp, M, na);
     for (uint32_t r = r0; r < r1; r++) {
-        VK_LAUNCH(ctx, "msm_fixup_jump", (k_fixup_jump<A>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
+        VK_LAUNCH_ON(ctx, L.st, "msm_fixup_jump", (k_fixup_jump<A>), (T + 255) / 256, 256, 0, va, na, through, T, Lp, M, vb,
                   nb, 1u << r, d_chain_max);
         std::swap(va, vb);
         std::swap(na, nb);
@@ -230,43 +230,43 @@ static int fixup_rounds(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M,
 }
 
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets, FAcc<C>* carry,
+int msm_tail_fixup(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets, FAcc<C>* carry,
                    const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
                    const uint32_t* d_chain_max, uint32_t guarded) {
     using A = typename Fast29<C>::type;
     const FAcc<C>* sum = carry;
     if (guarded) {
-        VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, 0, guarded, d_chain_max, &sum));
+        VK_TRY(fixup_rounds<C>(ctx, L, T, Lp, M, carry, through, 0, guarded, d_chain_max, &sum));
     } else {
         uint32_t Lmax = 0;
-        VK_CHECK_HIP(hipMemcpyAsync(&Lmax, d_chain_max, 4, hipMemcpyDeviceToHost, ctx->stream));
-        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        VK_CHECK_HIP(hipMemcpyAsync(&Lmax, d_chain_max, 4, hipMemcpyDeviceToHost, L.st));
+        VK_CHECK_HIP(hipStreamSynchronize(L.st));
         uint32_t r1 = 0;
         while (Lmax >= 2 && (1u << r1) < Lmax) r1++;
-        if (r1 > 0) VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, 0, r1, nullptr, &sum));
+        if (r1 > 0) VK_TRY(fixup_rounds<C>(ctx, L, T, Lp, M, carry, through, 0, r1, nullptr, &sum));
     }
-    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<A>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
+    VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup<A>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
     return VC_OK;
 }
 
 // after `guarded` guarded rounds: chains longer than 2^guarded threads (Lmax read back with the
 // results) get their remaining rounds, then the owners are rewritten (idempotent)
 template <class C>
-int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
+int msm_tail_fixup_more(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
                         FAcc<C>* carry, const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
                         uint32_t guarded, uint32_t Lmax) {
     using A = typename Fast29<C>::type;
     uint32_t r1 = guarded;
     while ((1u << r1) < Lmax) r1++;
     const FAcc<C>* sum = carry;
-    VK_TRY(fixup_rounds<C>(ctx, T, Lp, M, carry, through, guarded, r1, nullptr, &sum));
-    VK_LAUNCH(ctx, "msm_fixup", (k_msm_fixup<A>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
+    VK_TRY(fixup_rounds<C>(ctx, L, T, Lp, M, carry, through, guarded, r1, nullptr, &sum));
+    VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup<A>), (T + 255) / 256, 256, 0, buckets, sum, owner, owner_b, T, Lp, M);
     return VC_OK;
 }
 
 // outputs W x (J + 1) points in ec.hpp form: [w][q] = T_wq (q < J), A_w (q == J)
 template <class C>
-int msm_tail_reduce(vc_ctx* ctx, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
+int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
                     typename C::Acc* out) {
     using A = typename Fast29<C>::type;
@@ -275,25 +275,25 @@ int msm_tail_reduce(vc_ctx* ctx, const FAcc<C>* buckets, const uint32_t* offsets
         accs = Rs = const_cast<FAcc<C>*>(buckets);
         live = offsets;
     } else {
-        VK_LAUNCH(ctx, "msm_segsum", (k_msm_segsum<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB,
+        VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segsum<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB,
                   W, Lseg, S, accs, Rs);
     }
     const uint32_t sums = (uint32_t)W * (J + 1);
     const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);
     const uint32_t nb1 = msm_bitsum_pw(S / 2, K), nb2 = msm_bitsum_pw(S, K);
     const uint32_t n_waves = (uint32_t)W * (J * nb1 + nb2);
-    VK_LAUNCH(ctx, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
+    VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
               n_waves, live, partial);
-    VK_LAUNCH(ctx, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
+    VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
     return VC_OK;
 }
 
 #define VK_INST_TAIL(C)                                                                                      \
-    template int msm_tail_fixup<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,           \
+    template int msm_tail_fixup<C>(vc_ctx*, Lane, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,           \
                                    const uint8_t*, const FAcc<C>*, const uint32_t*, const uint32_t*, uint32_t); \
-    template int msm_tail_fixup_more<C>(vc_ctx*, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,      \
+    template int msm_tail_fixup_more<C>(vc_ctx*, Lane, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,      \
                                         const uint8_t*, const FAcc<C>*, const uint32_t*, uint32_t, uint32_t);   \
-    template int msm_tail_reduce<C>(vc_ctx*, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
+    template int msm_tail_reduce<C>(vc_ctx*, Lane, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
                                     uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*);
 VK_INST_TAIL(BN254G1)
 VK_INST_TAIL(BLS381G1)

@@ -27,11 +27,11 @@ inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K) { return (items + 64 *
 template <class C>
 using FAcc = typename Fast29<C>::type::Acc;
 template <class C>
-int msm_tail_fixup(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets, FAcc<C>* carry,
+int msm_tail_fixup(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets, FAcc<C>* carry,
                    const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
                    const uint32_t* d_chain_max, uint32_t guarded = 0);
 template <class C>
-int msm_tail_fixup_more(vc_ctx* ctx, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
+int msm_tail_fixup_more(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
                         FAcc<C>* carry, const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
                         uint32_t guarded, uint32_t Lmax);
 // guarded rounds for nv entries over NB buckets per window at M entries per thread: covers a
@@ -43,7 +43,7 @@ inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {
     return r;
 }
 template <class C>
-int msm_tail_reduce(vc_ctx* ctx, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
+int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
                     typename C::Acc* out);
 }  // namespace vk
