@@ -37,6 +37,8 @@ static void run(const char* name) {
         f29<P> a = rand29<P>(mode), b = rand29<P>(mode);
         f29<P> r = mul29<P>(a, b);
         printf("{\"f\":\"%s\",\"op\":\"mul\",", name); pr("a", a); printf(","); pr("b", b); printf(","); pr("r", r); printf("}\n");
+        f29<P> q = sqr29<P>(a);
+        printf("{\"f\":\"%s\",\"op\":\"mul\",", name); pr("a", a); printf(","); pr("b", a); printf(","); pr("r", q); printf("}\n");
         f29<P> s = add29<P>(a, b);
         printf("{\"f\":\"%s\",\"op\":\"add\",", name); pr("a", a); printf(","); pr("b", b); printf(","); pr("r", s); printf("}\n");
         // subtrahend below p (a mul output): sub2 / sub4 / sub16

@@ -117,9 +117,40 @@ VK_HD f29<P> mul29(const f29<P>& a, const f29<P>& b) {
     r.v[L - 1] = (uint32_t)t[L - 1];
     return r;
 }
+// Montgomery square a^2 / R': the product half by symmetry (L(L+1)/2 mads: a_i * 2a_j for i < j
+// plus the diagonal, into 2L - 1 columns), then L reduction rows (separated operand scanning);
+// the L result limbs are columns L .. 2L - 1.
+// Columns stay below 2^63 (<= L/2 cross products of 2^59, L reduction products of 2^58).
 template <class P>
 VK_HD f29<P> sqr29(const f29<P>& a) {
-    return mul29<P>(a, a);
+    constexpr int L = P::L;
+    uint32_t d[L];
+#pragma unroll
+    for (int j = 0; j < L; j++) d[j] = a.v[j] << 1;
+    uint64_t T[2 * L];
+#pragma unroll
+    for (int k = 0; k < 2 * L; k++) T[k] = 0;
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+        T[2 * i] += (uint64_t)a.v[i] * a.v[i];
+#pragma unroll
+        for (int j = i + 1; j < L; j++) T[i + j] += (uint64_t)a.v[i] * d[j];
+    }
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+        const uint32_t m = ((uint32_t)T[i] * P::inv) & M29;
+#pragma unroll
+        for (int j = 0; j < L; j++) T[i + j] += (uint64_t)m * P::p(j);
+        T[i + 1] += T[i] >> 29;
+    }
+    f29<P> r;
+#pragma unroll
+    for (int j = L; j < 2 * L - 1; j++) {
+        T[j + 1] += T[j] >> 29;
+        r.v[j - L] = (uint32_t)T[j] & M29;
+    }
+    r.v[L - 1] = (uint32_t)T[2 * L - 1];
+    return r;
 }
 
 template <class P>
