@@ -127,7 +127,10 @@ struct GlvDigits {
 //   k_sort_fine     block = coarse bin: LDS histogram of the 2^FB fine buckets -> bucket
 //                   offsets (written directly), then scatter into sorted[]
 // Order inside a bucket is arbitrary (EC addition is commutative and exact).
-constexpr uint32_t SORT_CHUNK = 1024;
+#ifndef VK_SORT_CHUNK
+#define VK_SORT_CHUNK 1024
+#endif
+constexpr uint32_t SORT_CHUNK = VK_SORT_CHUNK;
 
 template <class Src>
 __global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
