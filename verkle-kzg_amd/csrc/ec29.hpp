@@ -228,6 +228,7 @@ struct TE29 {
     }
 };
 
+#ifdef __HIPCC__
 // xor-shuffle of a POD accumulator across the wave (word by word)
 template <class T>
 __device__ __forceinline__ T shfl_xor_pod(const T& v, uint32_t m) {
@@ -239,6 +240,7 @@ __device__ __forceinline__ T shfl_xor_pod(const T& v, uint32_t m) {
     for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = __shfl_xor(src[k], m, 64);
     return o;
 }
+#endif
 
 // curve of ec.hpp -> its radix-2^29 mixed-add engine
 template <class C>
