@@ -677,9 +677,11 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
                  ws[WS_SORTED].as<uint32_t>(), sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
                  sl.owner_b, sl.chain_max);
     if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
+    // chains up to 2^guard carry pieces are walked serially by their owners; longer ones
+    // (adversarial scalars) take the pointer-jumping path in slice_finish
     sl.guard = msm_fixup_guard_rounds(nv, NB, M);
-    VK_TRY(msm_tail_fixup<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
-                             sl.owner_b, sl.chain_max, sl.guard));
+    VK_TRY(msm_tail_fixup_walk<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
+                                  sl.owner_b, 1u << sl.guard));
     VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, W, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
                               sl.tail));
     return VC_OK;
@@ -699,9 +701,9 @@ template <class C>
 static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     using Acc = typename C::Acc;
     VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
-    if (sl.Lmax > (1u << sl.guard)) {  // rare (heavily repeated scalars): finish the chains, redo the tail
-        VK_TRY(msm_tail_fixup_more<C>(ctx, sl.L, sl.Tmax, sl.offsets + sl.NBtot, sl.M, sl.buckets, sl.carry,
-                                      sl.through, sl.owner, sl.owner_b, sl.guard, sl.Lmax));
+    if (sl.Lmax > (1u << sl.guard)) {  // rare (heavily repeated scalars): pointer jumping, redo the tail
+        VK_TRY(msm_tail_fixup<C>(ctx, sl.L, sl.Tmax, sl.offsets + sl.NBtot, sl.M, sl.buckets, sl.carry, sl.through,
+                                 sl.owner, sl.owner_b, sl.chain_max, 0));
         VK_TRY(msm_tail_reduce<C>(ctx, sl.L, sl.buckets, sl.offsets, sl.NB, sl.W, sl.Lseg, sl.S, sl.J, sl.seg, sl.rs,
                                   sl.bsum_part, sl.tail));
         VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(Acc), hipMemcpyDeviceToHost,
