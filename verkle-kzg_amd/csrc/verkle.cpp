@@ -9,6 +9,7 @@
 #include <array>
 #include <cstring>
 #include <map>
+#include <thread>
 #include <vector>
 
 #include "../../include/vc_scheme.h"
@@ -262,6 +263,11 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
         std::vector<uint64_t> ptr{0};
         std::vector<uint32_t> cols;
         std::vector<uint64_t> vals;
+        void reserve(size_t rows, size_t nnz) {
+            ptr.reserve(rows + 1);
+            cols.reserve(nnz);
+            vals.reserve(4 * nnz);
+        }
         void add(uint32_t col, const uint64_t* v) {
             if (!(v[0] | v[1] | v[2] | v[3])) return;  // zero scalars contribute nothing
             cols.push_back(col);
@@ -269,6 +275,47 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
         }
         void end_row() { ptr.push_back(cols.size()); }
         size_t n() const { return ptr.size() - 1; }
+        // append another builder's rows (row pointers shifted)
+        void append(const Rows& o) {
+            const uint64_t base = cols.size();
+            for (size_t i = 1; i < o.ptr.size(); i++) ptr.push_back(base + o.ptr[i]);
+            cols.insert(cols.end(), o.cols.begin(), o.cols.end());
+            vals.insert(vals.end(), o.vals.begin(), o.vals.end());
+        }
+    };
+    // rows of items [0, count) built by fn(i, Rows&) on up to 16 host threads, in item order
+    // (the node walks are pointer-chasing std::map code: ~100-200 ns per node on one thread)
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto build_rows = [&](size_t count, size_t nnz_per, auto fn) {
+        Rows out;
+        const unsigned T = count >= 4096 ? hw : 1;
+        if (T == 1) {
+            out.reserve(count, count * nnz_per);
+            for (size_t i = 0; i < count; i++) fn(i, out);
+            return out;
+        }
+        std::vector<Rows> part(T);
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < T; k++)
+            th.emplace_back([&, k] {
+                const size_t lo = count * k / T, hi = count * (k + 1) / T;
+                part[k].reserve(hi - lo, (hi - lo) * nnz_per);
+                for (size_t i = lo; i < hi; i++) fn(i, part[k]);
+            });
+        for (auto& x : th) x.join();
+        out.reserve(count, count * nnz_per);
+        for (auto& r : part) out.append(r);
+        return out;
+    };
+    // fn(i) for i in [0, count) on the same threads (independent per-item writes)
+    auto for_each = [&](size_t count, auto fn) {
+        const unsigned T = count >= 4096 ? hw : 1;
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < T; k++)
+            th.emplace_back([&, k] {
+                for (size_t i = count * k / T; i < count * (k + 1) / T; i++) fn(i);
+            });
+        for (auto& x : th) x.join();
     };
     lap("collect dirty");
     auto commit_rows = [&](const Rows& r, std::vector<uint64_t>& xy, std::vector<uint8_t>& inf,
@@ -290,24 +337,21 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
     // extension nodes: c1, c2 (width N), then [1, stem, c1, c2] (width 4)
     if (!exts.empty()) {
         const size_t E = exts.size();
-        Rows r12;
         // (position, value) writes of c1 / c2 in leaf order; a later write to the same
         // position overwrites, as c1_values[index] = ... does (node.rs:226-239)
-        std::vector<std::pair<uint32_t, std::array<uint64_t, 4>>> half[2];
-        auto put = [&](int h, uint32_t pos, const uint64_t* v) {
-            for (auto& pv : half[h])
-                if (pv.first == pos) {
-                    memcpy(pv.second.data(), v, 32);
-                    return;
-                }
-            std::array<uint64_t, 4> a;
-            memcpy(a.data(), v, 32);
-            half[h].push_back({pos, a});
-        };
-        for (size_t e = 0; e < E; e++) {
+        Rows r12 = build_rows(E, (size_t)N, [&](size_t e, Rows& r) {
+            std::vector<std::pair<uint32_t, std::array<uint64_t, 4>>> half[2];
+            auto put = [&](int h, uint32_t pos, const uint64_t* v) {
+                for (auto& pv : half[h])
+                    if (pv.first == pos) {
+                        memcpy(pv.second.data(), v, 32);
+                        return;
+                    }
+                std::array<uint64_t, 4> a;
+                memcpy(a.data(), v, 32);
+                half[h].push_back({pos, a});
+            };
             const VNode& n = t->nodes[exts[e]];
-            half[0].clear();
-            half[1].clear();
             for (auto& kv : n.leaves) {
                 const size_t index = kv.first;
                 uint64_t lo[4], hi[4];
@@ -318,47 +362,45 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
                 put(h, (uint32_t)((2 * index + 1) % N), hi);
             }
             for (int h = 0; h < 2; h++) {
-                for (auto& pv : half[h]) r12.add(pv.first, pv.second.data());
-                r12.end_row();
+                for (auto& pv : half[h]) r.add(pv.first, pv.second.data());
+                r.end_row();
             }
-        }
+        });
         VK_TRY(commit_rows(r12, xy, inf, items));
-        Rows rx;
-        for (size_t e = 0; e < E; e++) {
+        Rows rx = build_rows(E, 4, [&](size_t e, Rows& r) {
             const VNode& n = t->nodes[exts[e]];
             uint64_t one[4] = {1, 0, 0, 0}, stem_item[4];
             item_of_bytes(n.stem.data(), N, stem_item);  // bytes_to_item(stem.to_bytes())
-            rx.add(0, one);
-            rx.add(1, stem_item);
-            rx.add(2, &items[(2 * e) * 4]);
-            rx.add(3, &items[(2 * e + 1) * 4]);
-            rx.end_row();
-        }
+            r.add(0, one);
+            r.add(1, stem_item);
+            r.add(2, &items[(2 * e) * 4]);
+            r.add(3, &items[(2 * e + 1) * 4]);
+            r.end_row();
+        });
         VK_TRY(commit_rows(rx, xy2, inf2, items2));
-        for (size_t e = 0; e < E; e++) {
+        for_each(E, [&](size_t e) {
             VNode& n = t->nodes[exts[e]];
             memcpy(n.cxy, &xy2[e * 8], 64);
             n.cinf = inf2[e];
             memcpy(n.item, &items2[e * 4], 32);
             n.has_commit = true;
-        }
+        });
     }
     // internal nodes, deepest level first (HACK in the reference: width hard-coded 256)
     for (int depth = (int)internals.size() - 1; depth >= 0; depth--) {
         const std::vector<int>& lv = internals[depth];
-        Rows ri;
-        for (int id : lv) {
-            for (auto& kv : t->nodes[id].children) ri.add(kv.first, t->nodes[kv.second].item);
-            ri.end_row();
-        }
+        Rows ri = build_rows(lv.size(), 4, [&](size_t b, Rows& r) {
+            for (auto& kv : t->nodes[lv[b]].children) r.add(kv.first, t->nodes[kv.second].item);
+            r.end_row();
+        });
         VK_TRY(commit_rows(ri, xy, inf, items));
-        for (size_t b = 0; b < lv.size(); b++) {
+        for_each(lv.size(), [&](size_t b) {
             VNode& n = t->nodes[lv[b]];
             memcpy(n.cxy, &xy[b * 8], 64);
             n.cinf = inf[b];
             memcpy(n.item, &items[b * 4], 32);
             n.has_commit = true;
-        }
+        });
     }
     memcpy(out_xy, t->nodes[0].cxy, 64);
     *out_inf = t->nodes[0].cinf;
