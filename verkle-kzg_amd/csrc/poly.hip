@@ -45,22 +45,43 @@ __global__ void k_powers(fe<F> w, size_t n, fe<F>* __restrict__ out) {
     out[i] = r;
 }
 
-// out[k] = 1 / in[k] for k < n (zeros map to zero), chunks of CH per thread:
-// prefix products, one binary-Euclid inversion per chunk, backward substitution
+// out[k] = 1 / in[k] for k < n (zeros map to zero). Montgomery's trick at two levels: each
+// thread multiplies a chunk of CH, a workgroup scans its 256 chunk products (prefix and suffix,
+// LDS) and inverts their product once (binary Euclid, one lane), then every chunk's inverse is
+// inv(total) * prefix * suffix and the chunk is substituted backwards. One inversion per 256 CH
+// elements (per chunk before: 65,536 inversions for a 2^20 KZG quotient, 0.46 ms).
 template <class F>
 __global__ void __launch_bounds__(256) k_batch_inv(const fe<F>* __restrict__ in, fe<F>* __restrict__ out, size_t n,
                                                   int CH) {
-    size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t lo = c * CH;
-    if (lo >= n) return;
-    size_t hi = lo + CH < n ? lo + CH : n;
+    __shared__ fe<F> pre[256], suf[256];
+    __shared__ fe<F> tinv;
+    const uint32_t t = threadIdx.x;
+    const size_t lo = ((size_t)blockIdx.x * 256 + t) * CH;
+    const size_t hi = lo + CH < n ? lo + CH : n;
     fe<F> acc = fe_one<F>();
     for (size_t k = lo; k < hi; k++) {
         fe<F> v = in[k];
         if (!fe_is_zero<F>(v)) acc = fe_mul<F>(acc, v);
-        out[k] = acc;
+        out[k] = acc;  // chunk prefix products
     }
-    fe<F> inv = fe_inv_bin<F>(acc);
+    pre[t] = acc;
+    suf[t] = acc;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        fe<F> p = pre[t], q = suf[t];
+        if (t >= off) p = fe_mul<F>(pre[t - off], p);
+        if (t + off < 256) q = fe_mul<F>(q, suf[t + off]);
+        __syncthreads();
+        pre[t] = p;
+        suf[t] = q;
+        __syncthreads();
+    }
+    if (t == 0) tinv = fe_inv_bin<F>(pre[255]);
+    __syncthreads();
+    if (lo >= n) return;
+    fe<F> inv = tinv;  // 1 / (this chunk's product)
+    if (t > 0) inv = fe_mul<F>(inv, pre[t - 1]);
+    if (t < 255) inv = fe_mul<F>(inv, suf[t + 1]);
     for (size_t k = hi; k-- > lo;) {
         fe<F> v = in[k];
         if (fe_is_zero<F>(v)) {
@@ -202,7 +223,7 @@ int domain_powers(vc_ctx* ctx, const fe<F>& w, size_t n, fe<F>* d_out) {
 
 template <class F>
 int batch_inverse(vc_ctx* ctx, const fe<F>* d_in, fe<F>* d_out, size_t n) {
-    const int CH = 16;
+    const int CH = n >= (1u << 18) ? 16 : 4;
     size_t chunks = (n + CH - 1) / CH;
     VK_LAUNCH(ctx, "batch_inv", (k_batch_inv<F>), (chunks + 255) / 256, 256, 0, d_in, d_out, n, CH);
     return VC_OK;

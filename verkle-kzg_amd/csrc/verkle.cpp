@@ -21,11 +21,43 @@ namespace {
 
 using vk::Fr;
 
+// unit -> V, sorted by unit in one vector: the std::map API subset the tree uses, without a heap
+// node per entry (pointer chasing made the commitment's node walks ~150 ns per node)
+template <class V>
+struct FlatMap {
+    std::vector<std::pair<uint8_t, V>> v;
+    using iterator = typename std::vector<std::pair<uint8_t, V>>::iterator;
+    using const_iterator = typename std::vector<std::pair<uint8_t, V>>::const_iterator;
+    iterator begin() { return v.begin(); }
+    iterator end() { return v.end(); }
+    const_iterator begin() const { return v.begin(); }
+    const_iterator end() const { return v.end(); }
+    iterator lower(uint8_t k) {
+        return std::lower_bound(v.begin(), v.end(), k, [](const std::pair<uint8_t, V>& a, uint8_t b) { return a.first < b; });
+    }
+    const_iterator lower(uint8_t k) const {
+        return std::lower_bound(v.begin(), v.end(), k, [](const std::pair<uint8_t, V>& a, uint8_t b) { return a.first < b; });
+    }
+    iterator find(uint8_t k) {
+        auto it = lower(k);
+        return (it != v.end() && it->first == k) ? it : v.end();
+    }
+    const_iterator find(uint8_t k) const {
+        auto it = lower(k);
+        return (it != v.end() && it->first == k) ? it : v.end();
+    }
+    V& operator[](uint8_t k) {
+        auto it = lower(k);
+        if (it == v.end() || it->first != k) it = v.insert(it, {k, V{}});
+        return it->second;
+    }
+};
+
 struct VNode {
     bool ext = false;
-    std::vector<uint8_t> stem;                               // extension: the full key (node.rs:45)
-    std::map<uint8_t, std::array<uint8_t, 32>> leaves;      // extension: unit -> value
-    std::map<uint8_t, int> children;                         // internal: unit -> node
+    std::array<uint8_t, 32> stem{};                          // extension: the full key (node.rs:45)
+    FlatMap<std::array<uint8_t, 32>> leaves;                 // extension: unit -> value
+    FlatMap<int> children;                                   // internal: unit -> node
     bool has_commit = false;
     uint64_t cxy[8] = {0};
     uint8_t cinf = 1;
@@ -75,7 +107,7 @@ namespace {
 int new_ext(vc_verkle* t, const uint8_t* stem, uint8_t unit, const uint8_t* value) {
     VNode n;
     n.ext = true;
-    n.stem.assign(stem, stem + t->N);
+    memcpy(n.stem.data(), stem, t->N);
     std::array<uint8_t, 32> v;
     memcpy(v.data(), value, 32);
     n.leaves[unit] = v;
@@ -84,7 +116,7 @@ int new_ext(vc_verkle* t, const uint8_t* stem, uint8_t unit, const uint8_t* valu
 }
 
 // first d > cur with a[d] != b[d] (or N) -- KeyMethods::next_diff_depth (lib.rs:49-58)
-int next_diff_depth(const std::vector<uint8_t>& a, const uint8_t* b, int cur, int N) {
+int next_diff_depth(const uint8_t* a, const uint8_t* b, int cur, int N) {
     int d = cur + 1;
     while (d < N && a[d] == b[d]) d++;
     return d;
@@ -150,7 +182,7 @@ int vc_verkle_insert(vc_verkle* t, const uint8_t* key, const uint8_t* value) {
         if (c.ext && !(memcmp(c.stem.data(), stem, N) == 0 || depth == N - 2)) {
             // the reference indexes stem[d] out of bounds (panics) when no unit after `depth`
             // differs -- reachable only through its level-skipping splits
-            if (next_diff_depth(c.stem, stem, depth, N) >= N) return VC_E_INVALID;
+            if (next_diff_depth(c.stem.data(), stem, depth, N) >= N) return VC_E_INVALID;
             action = SPLIT;
             parent_k = k;
             break;
@@ -174,8 +206,8 @@ int vc_verkle_insert(vc_verkle* t, const uint8_t* key, const uint8_t* value) {
     // SPLIT: new internal keyed by the first differing unit d (which may skip levels, as in
     // the reference: node.rs:176-185)
     const int old = t->nodes[cur].children[(uint8_t)parent_k];
-    const std::vector<uint8_t> old_stem = t->nodes[old].stem;
-    const int d = next_diff_depth(old_stem, stem, depth, N);
+    const std::array<uint8_t, 32> old_stem = t->nodes[old].stem;
+    const int d = next_diff_depth(old_stem.data(), stem, depth, N);
     int e = new_ext(t, stem, unit, value);
     VNode in;
     in.children[stem[d]] = e;
@@ -310,6 +342,10 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
     // fn(i) for i in [0, count) on the same threads (independent per-item writes)
     auto for_each = [&](size_t count, auto fn) {
         const unsigned T = count >= 4096 ? hw : 1;
+        if (T == 1) {
+            for (size_t i = 0; i < count; i++) fn(i);
+            return;
+        }
         std::vector<std::thread> th;
         for (unsigned k = 0; k < T; k++)
             th.emplace_back([&, k] {

@@ -24,7 +24,10 @@ class VerkleTree:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().vc_verkle_free(self.h)
+            try:
+                lib().vc_verkle_free(self.h)
+            except TypeError:  # interpreter shutdown: module globals already cleared
+                pass
             self.h = None
 
     def insert_single(self, key, value):
