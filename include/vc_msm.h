@@ -116,7 +116,8 @@ int vc_msm_batch_device(vc_ctx* ctx, int table_id, size_t width, const void* d_s
  * (verkle internal nodes commit ~5 non-zero children of 256, node.rs:262-271). */
 int vc_msm_batch_sparse(vc_ctx* ctx, int table_id, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                         const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
-/* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 16]. */
+/* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 20]
+ * (n x ceil(bits/c) x 2^(c-1) affine points: 167 GB for 256 Bandersnatch bases at c = 20). */
 int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
 
 #ifdef __cplusplus
