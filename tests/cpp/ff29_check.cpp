@@ -47,6 +47,14 @@ static void run(const char* name) {
         f29<P> d2 = sub29<P, 4>(a, c), d16 = sub29<P, 16>(r, c2);
         printf("{\"f\":\"%s\",\"op\":\"sub4\",", name); pr("a", a); printf(","); pr("b", c); printf(","); pr("r", d2); printf("}\n");
         printf("{\"f\":\"%s\",\"op\":\"sub16\",", name); pr("a", r); printf(","); pr("b", c2); printf(","); pr("r", d16); printf("}\n");
+        // lazy sum of products (mul2sum29), as in the Y3 formulas (d = 4p - a product output),
+        // and with four max-limb operands (column bound)
+        f29<P> nc = neg29<P, 4>(c);
+        f29<P> m2 = mul2sum29<P>(a, b, r, nc), m3 = mul2sum29<P>(a, b, b, a);
+        printf("{\"f\":\"%s\",\"op\":\"mul2\",", name); pr("a", a); printf(","); pr("b", b); printf(",");
+        pr("c", r); printf(","); pr("d", nc); printf(","); pr("r", m2); printf("}\n");
+        printf("{\"f\":\"%s\",\"op\":\"mul2\",", name); pr("a", a); printf(","); pr("b", b); printf(",");
+        pr("c", b); printf(","); pr("d", a); printf(","); pr("r", m3); printf("}\n");
         f29<P> cn = canon29<P>(r);
         printf("{\"f\":\"%s\",\"op\":\"canon\",", name); pr("a", r); printf(","); pr("r", cn); printf("}\n");
         uint32_t w[P::N];

@@ -45,6 +45,11 @@ def test_ff29_ops(lines):
             assert (r * Rp - a * b) % p == 0
             assert r < a * b // Rp + p
             assert all(v <= M29 for v in d["r"][:-1])
+        elif op == "mul2":
+            s = val(d["a"]) * val(d["b"]) + val(d["c"]) * val(d["d"])
+            assert (r * Rp - s) % p == 0
+            assert r < s // Rp + p
+            assert all(v <= M29 for v in d["r"][:-1])
         elif op == "add":
             assert r == val(d["a"]) + val(d["b"])
             assert all(v <= M29 + 7 for v in d["r"][:-1])
@@ -62,7 +67,7 @@ def test_ff29_ops(lines):
             assert (r - v * Rp * pow(R, -1, p)) % p == 0
             back = sum(w << (32 * k) for k, w in enumerate(d["back"]))
             assert back == v
-    assert len(seen) == 3 * 7
+    assert len(seen) == 3 * 8
 
 
 def test_ff29_zero_test(lines):

@@ -45,6 +45,33 @@ def test_transcript_matches_oracle_multistep():
     assert a.digest("t") == b.digest("t")
 
 
+def test_multiproof_transcript_matches_oracle():
+    """vc_multiproof_begin's challenge r (multiproof.rs:106-114) over Q = 9000 queries -- the
+    records are serialised on several host threads at this size -- against the oracle's
+    transcript fed query by query; identity commitments included."""
+    import numpy as np
+    import vkzg
+    from pyoracle import arkser
+    from vkzg import scheme
+    from vkzg._lib import lib
+    gold = [P(c["point"]) for c in load("transcript.json")["compressed"]]
+    Q, N = 9000, 256
+    pts = [None if i % 97 == 5 else gold[i % len(gold)] for i in range(Q)]
+    z = np.array([(i * 37) % N for i in range(Q)], dtype=np.uint64)
+    ys = [(i * 0x9E3779B97F4A7C15 + 11) % (1 << 250) for i in range(Q)]
+    a = arkser.TranscriptHasher("multiproof")
+    for p, zi, yi in zip(pts, z, ys):
+        a.append_point(p, "C")
+        a.append_usize(int(zi), "z")
+        a.append_fr(yi, "y")
+    want = a.digest("r")
+    cxy, cinf = vkzg.points_to_arrays("bn254", pts)
+    tr, r, rows = scheme.multiproof_begin(N, cxy, cinf, z, vkzg.ints_to_limbs(ys))
+    lib().vc_transcript_free(tr)
+    assert sum(int(v) << (64 * k) for k, v in enumerate(r)) == want
+    assert rows == len(set(int(v) for v in z))
+
+
 def test_compress_and_to_data_item_golden():
     from pyoracle import arkser
     from vkzg import scheme

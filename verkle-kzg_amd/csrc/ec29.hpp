@@ -6,7 +6,9 @@
 //
 // Value bounds (ff29.hpp keeps residues loosely reduced; rho = p / R'):
 //  SW (XYZZ, a = 0): X < 11p, Y < 7p, ZZ, ZZZ < 1.1p between adds (BN254's rho = 2^-7.4 is
-//    the tight case; BLS12-381's 2^-25 leaves every product output below 1.0001 p).
+//    the tight case; BLS12-381's 2^-25 leaves every product output below 1.0001 p). The add
+//    paths' Y3 = R (Q - X3) + Y1 (4p - PPP) is one lazy sum of products (mul2sum29):
+//    < (17p 17p + 7p 4p) rho + p = 2.9p at BN254, 1.0001p at BLS12-381.
 //  TE (extended, a = -5, Bandersnatch over BLS12-381 Fr, rho = 2^-6.1): every coordinate is
 //    a product output < 1.9p (fixed point of the bounds with inputs < 2p).
 #pragma once
@@ -76,7 +78,8 @@ struct SW29 {
         const f29<P> Q = mul29<P>(p.x, PP);
         Acc r;
         r.x = sub2_29<P, 8>(sqr29<P>(R), PPP, add29<P>(Q, Q));
-        r.y = sub29<P, 4>(mul29<P>(R, sub29<P, 16>(Q, r.x)), mul29<P>(p.y, PPP));
+        // Y3 = R (Q - X3) + Y1 (4p - PPP) with one reduction (mul2sum29)
+        r.y = mul2sum29<P>(R, sub29<P, 16>(Q, r.x), p.y, neg29<P, 4>(PPP));
         r.zz = mul29<P>(p.zz, PP);
         r.zzz = mul29<P>(p.zzz, PPP);
         r.inf = false;
@@ -118,7 +121,7 @@ struct SW29 {
         const f29<P> Q = mul29<P>(U1, PP);
         Acc r;
         r.x = sub2_29<P, 8>(sqr29<P>(R), PPP, add29<P>(Q, Q));
-        r.y = sub29<P, 4>(mul29<P>(R, sub29<P, 16>(Q, r.x)), mul29<P>(S1, PPP));
+        r.y = mul2sum29<P>(R, sub29<P, 16>(Q, r.x), S1, neg29<P, 4>(PPP));
         r.zz = mul29<P>(mul29<P>(p.zz, q.zz), PP);
         r.zzz = mul29<P>(mul29<P>(p.zzz, q.zzz), PPP);
         r.inf = false;

@@ -117,6 +117,43 @@ VK_HD f29<P> mul29(const f29<P>& a, const f29<P>& b) {
     r.v[L - 1] = (uint32_t)t[L - 1];
     return r;
 }
+// Montgomery sum of two products (a b + c d) / R' with ONE reduction (lazy reduction): every
+// row takes a b_i and c d_i before its reduction step, so the pair costs 2L^2 + L^2 mads
+// instead of 2 x 2L^2. A column (absolute position k) collects at most L rows x 3 products
+// (a b, c d, m p) of < 2^58.0001 plus the row carry: < 2^63.4 at L = 14. Output fully
+// normalised, value < (a b + c d) / R' + p.
+template <class P>
+VK_HD f29<P> mul2sum29(const f29<P>& a, const f29<P>& b, const f29<P>& c, const f29<P>& d) {
+    constexpr int L = P::L;
+    static_assert(3 * L <= 42, "column bound");
+    uint64_t t[L];
+#pragma unroll
+    for (int j = 0; j < L; j++) t[j] = (uint64_t)a.v[j] * b.v[0] + (uint64_t)c.v[j] * d.v[0];
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+        if (i > 0) {
+#pragma unroll
+            for (int j = 0; j < L; j++) t[j] += (uint64_t)a.v[j] * b.v[i] + (uint64_t)c.v[j] * d.v[i];
+        }
+        const uint32_t m = ((uint32_t)t[0] * P::inv) & M29;
+#pragma unroll
+        for (int j = 0; j < L; j++) t[j] += (uint64_t)m * P::p(j);
+        const uint64_t cy = t[0] >> 29;
+#pragma unroll
+        for (int j = 0; j < L - 1; j++) t[j] = t[j + 1];
+        t[L - 1] = 0;
+        t[0] += cy;
+    }
+    f29<P> r;
+#pragma unroll
+    for (int j = 0; j < L - 1; j++) {
+        t[j + 1] += t[j] >> 29;
+        r.v[j] = (uint32_t)t[j] & M29;
+    }
+    r.v[L - 1] = (uint32_t)t[L - 1];
+    return r;
+}
+
 // Montgomery square a^2 / R': the product half by symmetry (L(L+1)/2 mads: a_i * 2a_j for i < j
 // plus the diagonal, into 2L - 1 columns), then L reduction rows (separated operand scanning);
 // the L result limbs are columns L .. 2L - 1.

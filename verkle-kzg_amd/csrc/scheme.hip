@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
@@ -740,14 +741,34 @@ struct MpPrep {
     std::vector<Fr> rpow;
 };
 
+// multiproof.rs:106-112: per query "C" || compress(C) || "z" || z (u64 LE) || "y" || y -- 75
+// bytes at offset 75 i, so the records are written straight into the transcript on up to 16
+// host threads (the point compression is the costly part); the SHA-256 over them stays serial.
 static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                                     const uint64_t* y) {
+    constexpr size_t REC = 75;
     vc_transcript* tr = vc_transcript_new("multiproof");
-    vc_transcript_reserve(tr, Q * 75 + 64);
-    for (size_t i = 0; i < Q; i++) {
-        vc_transcript_append_point(tr, com_xy + 8 * i, com_inf[i], "C");
-        vc_transcript_append_u64(tr, z[i], "z");
-        vc_transcript_append_fr(tr, y + 4 * i, "y");
+    vc_transcript_reserve(tr, Q * REC + 64);
+    uint8_t* out = transcript_extend(tr, Q * REC);
+    auto fill = [&](size_t lo, size_t hi) {
+        static const uint64_t zero[8] = {0};
+        for (size_t i = lo; i < hi; i++) {
+            uint8_t* o = out + REC * i;
+            o[0] = 'C';
+            compress_g1(com_inf[i] ? zero : com_xy + 8 * i, com_inf[i] != 0, o + 1);
+            o[33] = 'z';
+            for (int k = 0; k < 8; k++) o[34 + k] = (uint8_t)(z[i] >> (8 * k));
+            o[42] = 'y';
+            memcpy(o + 43, y + 4 * i, 32);
+        }
+    };
+    const unsigned T = Q >= 8192 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1;
+    if (T == 1) {
+        fill(0, Q);
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < T; k++) th.emplace_back(fill, Q * k / T, Q * (k + 1) / T);
+        for (auto& x : th) x.join();
     }
     return tr;
 }

@@ -221,6 +221,11 @@ Fr transcript_digest(vc_transcript* t, const char* label) {
     if (label) t->state.insert(t->state.end(), label, label + strlen(label));
     return r;
 }
+uint8_t* transcript_extend(vc_transcript* t, size_t n) {
+    const size_t at = t->state.size();
+    t->state.resize(at + n);
+    return t->state.data() + at;
+}
 void transcript_append_point(vc_transcript* t, const uint64_t* xy, bool inf, const char* label) {
     vc_transcript_append_point(t, xy, inf ? 1 : 0, label);
 }
