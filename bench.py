@@ -409,7 +409,7 @@ def main():
     ach = insts * 64 / acc_s / 1e12 if (insts and acc_s) else None
     valu = {"achieved": ach, "peak": mad_peak, "unit": "T VALU lane-instructions/s",
             "frac": (ach / mad_peak) if ach else None,
-            "work": f"{madds} mixed adds (radix-2^29 XYZZ, 10 field multiplies each); "
+            "work": f"{madds} mixed adds (radix-2^29 XYZZ: 8 products + 2 squares, 9 Montgomery reductions -- Y3 is one lazy sum of two products); "
                     f"{insts / madds * 64 if insts else float('nan'):.0f} VALU lane-instructions per mixed add (PMC)",
             "madds_per_s": madds / acc_s if acc_s else None,
             "peak_source": "vc_device_mad_rate: v_mad_u64_u32 issue rate measured live on this GPU",
