@@ -173,7 +173,7 @@ static int fill_t(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf,
     t->n = n;
     t->fb_c = t->fb_W = 0;  // any fixed-base tables are stale now
     t->subgroup = -1;
-    t->fast_ok = t->phi_ok = 0;
+    t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
     if (n == 0) return VC_OK;

@@ -469,7 +469,7 @@ static int table_from_acc_t(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) 
     t->curve = ctx->curve;
     t->n = n;
     t->fb_c = t->fb_W = 0;
-    t->fast_ok = t->phi_ok = 0;
+    t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(typename C::Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
     if (n == 0) return VC_OK;

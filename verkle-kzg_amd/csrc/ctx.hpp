@@ -59,6 +59,11 @@ struct Table {
     // MSM has run, phi(P) = (beta x, y) of every base at [n, 2n); built on first use
     int fast_ok = 0, phi_ok = 0;
     DevBuf fast;
+    // GLV MSMs over the whole table: packed-29 copies of 2^(c w) P and 2^(c w) phi(P) for every
+    // window w ([w][2n] layout), so all windows share one set of buckets (msm.hip, "shared
+    // windows"); built on first use for the window size c in win_c
+    int win_ok = 0, win_c = 0, win_W = 0;
+    DevBuf win;
 };
 
 enum WsSlot {

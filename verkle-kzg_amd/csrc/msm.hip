@@ -127,6 +127,8 @@ struct GlvDigits {
 //   k_sort_fine     block = coarse bin: LDS histogram of the 2^FB fine buckets -> bucket
 //                   offsets (written directly), then scatter into sorted[]
 // Order inside a bucket is arbitrary (EC addition is commutative and exact).
+// Shared windows (stride != 0): every window's digits go to ONE set of buckets and the entry
+// names the point 2^(c w) P_i by its index w * stride + i in the window copies (Table::win).
 #ifndef VK_SORT_CHUNK
 #define VK_SORT_CHUNK 1024
 #endif
@@ -134,16 +136,18 @@ constexpr uint32_t SORT_CHUNK = VK_SORT_CHUNK;
 
 template <class Src>
 __global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
-                                                  uint32_t NBC, uint32_t nblk, uint32_t* __restrict__ counts) {
+                                                  uint32_t NBC, uint32_t nblk, uint32_t stride,
+                                                  uint32_t* __restrict__ counts) {
     extern __shared__ uint32_t hist[];
-    const uint32_t bins = (uint32_t)(we - wb) * NBC;
+    const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb)
-                atomicAdd(&hist[(uint32_t)(w - wb) * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
+                atomicAdd(&hist[(stride ? 0u : (uint32_t)(w - wb)) * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)],
+                          1u);
         });
     }
     __syncthreads();
@@ -152,10 +156,10 @@ __global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, i
 
 template <class Src>
 __global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
-                                                    uint32_t NBC, uint32_t nblk, const uint32_t* __restrict__ base,
-                                                    uint64_t* __restrict__ tmp) {
+                                                    uint32_t NBC, uint32_t nblk, uint32_t stride,
+                                                    const uint32_t* __restrict__ base, uint64_t* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
-    const uint32_t bins = (uint32_t)(we - wb) * NBC;
+    const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + blockIdx.x];
     __syncthreads();
     const uint32_t fmask = (1u << FB) - 1;
@@ -164,8 +168,9 @@ __global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c,
         src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb) {
                 uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-                uint32_t pos = atomicAdd(&cur[(uint32_t)(w - wb) * NBC + (b >> FB)], 1u);
-                tmp[pos] = ((uint64_t)(b & fmask) << 32) | i | (d < 0 ? 0x80000000u : 0u);
+                uint32_t pos = atomicAdd(&cur[(stride ? 0u : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
+                const uint32_t e = stride ? i + (uint32_t)w * stride : i;
+                tmp[pos] = ((uint64_t)(b & fmask) << 32) | e | (d < 0 ? 0x80000000u : 0u);
             }
         });
     }
@@ -520,17 +525,67 @@ static int fast_tables(vc_ctx* ctx, Table* t, bool with_phi) {
     return VC_OK;
 }
 
+// out[i] = 2^c in[i] (identity bases stay the identity)
+template <class C>
+__global__ void __launch_bounds__(256) k_win_next(const typename C::Aff* __restrict__ in,
+                                                 const uint8_t* __restrict__ inf, uint32_t n, int c,
+                                                 typename C::Acc* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    typename C::Acc a = inf[i] ? C::zero() : C::from_aff(in[i], false);
+    for (int k = 0; k < c; k++) a = C::dbl(a);
+    out[i] = a;
+}
+
+// Shared-window copies of a GLV table (Table::win): for w < W, 2^(c w) P_i at [w][i] and
+// 2^(c w) phi(P_i) at [w][n + i], packed-29. A GLV MSM over the whole table then sends every
+// window's digits to one set of 2^(c-1) buckets -- the same mixed adds, but one bucket reduction
+// instead of W and no doublings in the host fold. 2 W n points (1.6 GB at n = 2^20, c = 16),
+// built once per table and window size: W - 1 steps of c doublings + a batch normalisation.
+template <class C>
+static int win_tables(vc_ctx* ctx, Table* t, int c, int W) {
+    using Aff = typename C::Aff;
+    using Acc = typename C::Acc;
+    if (t->win_ok && t->win_c == c && t->win_W >= W) return VC_OK;
+    const size_t n = t->n;
+    t->win_ok = 0;
+    VK_TRY(t->win.ensure((size_t)W * 2 * n * sizeof(Aff)));
+    Table cur;  // 2^(c w) P (affine, Montgomery): normalised by table_from_acc (commit.hip)
+    DevBuf nxt, acc;
+    VK_TRY(nxt.ensure(n * sizeof(Aff)));
+    VK_TRY(acc.ensure(n * sizeof(Acc)));
+    Aff* win = t->win.as<Aff>();
+    const unsigned g = (unsigned)((n + 255) / 256);
+    for (int w = 0; w < W; w++) {
+        const Aff* src = t->bases.as<Aff>();
+        if (w > 0) {
+            VK_LAUNCH(ctx, "win_next", (k_win_next<C>), g, 256, 0, w == 1 ? t->bases.as<Aff>() : cur.bases.as<Aff>(),
+                      t->inf.as<uint8_t>(), (uint32_t)n, c, acc.as<Acc>());
+            VK_TRY(table_from_acc(ctx, &cur, acc.p, n));
+            src = cur.bases.as<Aff>();
+        }
+        VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, src, n, win + (size_t)w * 2 * n);
+        VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), g, 256, 0, src, (uint32_t)n, bls_fq_mont(GLV_BETA), nxt.as<Aff>());
+        VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, nxt.as<Aff>(), n, win + (size_t)w * 2 * n + n);
+    }
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // before the staging buffers are freed
+    t->win_ok = 1;
+    t->win_c = c;
+    t->win_W = W;
+    return VC_OK;
+}
+
 template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
-                        uint32_t NBC, uint32_t nblk, size_t ncnt, uint32_t* counts, uint32_t* base, uint64_t* tmp,
-                        uint32_t* offsets, uint32_t* sorted) {
+                        uint32_t NBC, uint32_t nblk, uint32_t stride, size_t ncnt, uint32_t* counts, uint32_t* base,
+                        uint64_t* tmp, uint32_t* offsets, uint32_t* sorted) {
     hipStream_t st = L.st;
-    const uint32_t bins = (uint32_t)(we - wb) * NBC;
+    const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     const size_t lds = (size_t)bins * 4;
     if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
     VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
     VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
-                 counts);
+                 stride, counts);
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
     VK_TRY(L.ws[WS_SCAN_TMP].ensure(tmp_bytes));
@@ -541,7 +596,7 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
         if (ctx->timing) ctx->timer_end("msm_scan", ev, st);
     }
     VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
-                 base, tmp);
+                 stride, base, tmp);
     VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
     return VC_OK;
 }
@@ -576,6 +631,8 @@ struct MsmSlice {
     using Acc = typename C::Acc;
     Lane L{};
     int c = 0, wb = 0, we = 0, W = 0;
+    bool shared = false;  // all windows into one bucket set (Table::win copies)
+    int Wr = 0;           // bucket sets reduced: 1 shared, W otherwise
     uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
     uint32_t* offsets = nullptr;
     uint32_t* chain_max = nullptr;
@@ -599,9 +656,12 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     using RAcc = FAcc<C>;  // raw radix-29 accumulators of the accumulate / fix-up / reduction
     const Lane L = sl.L;
     const int c = sl.c, W = sl.W;
+    const int Wr = sl.shared ? 1 : W;
+    sl.Wr = Wr;
     const uint32_t NB = 1u << (c - 1);
-    const uint32_t NBtot = NB * (uint32_t)W;
+    const uint32_t NBtot = NB * (uint32_t)Wr;
     const size_t maxL = nv * (size_t)W;
+    const size_t load = maxL / Wr;  // entries per bucket set
     // sorted entries per accumulate thread: 64 at 2^20 x 16 windows (2 rounds of 2048 waves),
     // fewer for window slices / small MSMs so the grid still fills the chip
     // (not below 16: a bucket then straddles more threads and the fix-up's serial merge chain
@@ -610,13 +670,14 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // ... and at least twice the mean bucket load, so few buckets straddle more than two
     // threads (the GLV 2^20 MSM has 64 entries per bucket: M = 128 drops the fix-up's
     // pointer-jumping rounds, 0.23 -> 0.06 ms, for 0.1 ms more accumulate)
-    if (nv / NB > M / 2 && M < 128) M *= 2;
+    if (load / NB > M / 2 && M < 128) M *= 2;
     if (const char* em = getenv("VKZG_MSM_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe
     // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 4, or 2
     // when the segments (one lane each) would not give every SIMD a wave (GLV 2^20: 4 at 8
     // windows, 2 for the 1-4 window slices of multi-GPU runs; 8 measured 0.1-0.15 ms slower)
     uint32_t Lseg = NB >= 64 ? 4 : (NB >= 4 ? 2 : 1);
-    if (Lseg == 4 && (size_t)(NB / Lseg) * W < 65536) Lseg = 2;
+    if (Lseg == 4 && (size_t)(NB / Lseg) * Wr < 65536) Lseg = 2;
+    if (sl.shared) Lseg = 1;  // one bucket set: the bit sums straight over the buckets (measured)
     if (const char* el = getenv("VKZG_MSM_LSEG")) Lseg = (uint32_t)std::max(1, atoi(el));  // tuning probe
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
@@ -626,10 +687,12 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
 
     // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
     uint32_t lgNB = (uint32_t)c - 1;
-    const uint32_t FB = lgNB < 8 ? lgNB : 8;
+    uint32_t FB = lgNB < 8 ? lgNB : 8;
+    // shared windows: ~16K entries per coarse bin (one k_sort_fine block each), as per window
+    while (sl.shared && FB > 1 && (load >> 14) > (size_t)(NB >> FB)) FB--;
     const uint32_t NBC = NB >> FB;
     const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
-    const size_t ncnt = (size_t)W * NBC * nblk + 1;
+    const size_t ncnt = (size_t)Wr * NBC * nblk + 1;
 
     DevBuf* ws = L.ws;
     VK_TRY(ws[WS_DIGITS].ensure(maxL * 8));
@@ -642,10 +705,10 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     VK_TRY(ws[WS_THROUGH].ensure((size_t)(Tmax + 8)));
     VK_TRY(ws[WS_OWNER].ensure((size_t)(Tmax + 8) * sizeof(RAcc)));
     VK_TRY(ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
-    VK_TRY(ws[WS_SEG].ensure((size_t)S * W * sizeof(RAcc)));
-    VK_TRY(ws[WS_TREE].ensure((size_t)S * W * sizeof(RAcc)));
-    VK_TRY(ws[WS_WIN].ensure((size_t)W * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)W, J)) * sizeof(RAcc)));
-    VK_TRY(ws[WS_TAIL].ensure((size_t)W * (J + 1) * sizeof(Acc)));
+    VK_TRY(ws[WS_SEG].ensure((size_t)S * Wr * sizeof(RAcc)));
+    VK_TRY(ws[WS_TREE].ensure((size_t)S * Wr * sizeof(RAcc)));
+    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)Wr, J)) * sizeof(RAcc)));
+    VK_TRY(ws[WS_TAIL].ensure((size_t)Wr * (J + 1) * sizeof(Acc)));
     VK_TRY(ws[WS_CHAIN].ensure(4));
 
     sl.NB = NB;
@@ -667,7 +730,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.bsum_part = ws[WS_WIN].as<RAcc>();
     sl.tail = ws[WS_TAIL].as<Acc>();
 
-    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, ncnt, ws[WS_COUNTS].as<uint32_t>(),
+    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, sl.shared ? (uint32_t)nv : 0u, ncnt,
+                        ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].as<uint64_t>(), sl.offsets,
                         ws[WS_SORTED].as<uint32_t>()));
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W
@@ -679,10 +743,15 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
     // chains up to 2^guard carry pieces are walked serially by their owners; longer ones
     // (adversarial scalars) take the pointer-jumping path in slice_finish
-    sl.guard = msm_fixup_guard_rounds(nv, NB, M);
-    VK_TRY(msm_tail_fixup_walk<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
-                                  sl.owner_b, 1u << sl.guard));
-    VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, W, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
+    sl.guard = msm_fixup_guard_rounds(load, NB, M);
+    static const int fix_env = getenv("VKZG_MSM_FIXUP") ? atoi(getenv("VKZG_MSM_FIXUP")) : 0;  // tuning probe
+    if (fix_env == 1)  // guarded pointer-jumping rounds instead of the owner walk
+        VK_TRY(msm_tail_fixup<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
+                                 sl.owner_b, sl.chain_max, sl.guard));
+    else
+        VK_TRY(msm_tail_fixup_walk<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through,
+                                      sl.owner, sl.owner_b, 1u << sl.guard));
+    VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, Wr, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
                               sl.tail));
     return VC_OK;
 }
@@ -690,7 +759,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
 // read back (after every slice has been enqueued: a copy into pageable memory may block the host)
 template <class C>
 static int slice_fetch(MsmSlice<C>& sl) {
-    sl.ht.resize((size_t)sl.W * (sl.J + 1));
+    sl.ht.resize((size_t)sl.Wr * (sl.J + 1));
     VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(typename C::Acc), hipMemcpyDeviceToHost,
                                 sl.L.st));
     VK_CHECK_HIP(hipMemcpyAsync(&sl.Lmax, sl.chain_max, 4, hipMemcpyDeviceToHost, sl.L.st));
@@ -704,20 +773,21 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     if (sl.Lmax > (1u << sl.guard)) {  // rare (heavily repeated scalars): pointer jumping, redo the tail
         VK_TRY(msm_tail_fixup<C>(ctx, sl.L, sl.Tmax, sl.offsets + sl.NBtot, sl.M, sl.buckets, sl.carry, sl.through,
                                  sl.owner, sl.owner_b, sl.chain_max, 0));
-        VK_TRY(msm_tail_reduce<C>(ctx, sl.L, sl.buckets, sl.offsets, sl.NB, sl.W, sl.Lseg, sl.S, sl.J, sl.seg, sl.rs,
-                                  sl.bsum_part, sl.tail));
+        VK_TRY(msm_tail_reduce<C>(ctx, sl.L, sl.buckets, sl.offsets, sl.NB, sl.Wr, sl.Lseg, sl.S, sl.J, sl.seg,
+                                  sl.rs, sl.bsum_part, sl.tail));
         VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(Acc), hipMemcpyDeviceToHost,
                                     sl.L.st));
         VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
     }
-    // slice = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host, 64-bit limbs)
+    // slice = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host); with
+    // shared windows the one bucket set already holds the 2^(c w) factors: A + Lseg sum_j 2^j T_j
     const uint32_t J = sl.J;
     int lg_seg = 0;
     while ((1u << lg_seg) < sl.Lseg) lg_seg++;
-    const int maxpos = sl.c * (sl.we - 1) + lg_seg + (int)J;
+    const int maxpos = (sl.shared ? 0 : sl.c * (sl.we - 1)) + lg_seg + (int)J;
     std::vector<std::vector<int>> at(maxpos + 1);
-    for (int w = 0; w < sl.W; w++) {
-        const int p0 = sl.c * (sl.wb + w);  // absolute bit position of window wb + w
+    for (int w = 0; w < sl.Wr; w++) {
+        const int p0 = sl.shared ? 0 : sl.c * (sl.wb + w);  // absolute bit position of window wb + w
         at[p0].push_back(w * (int)(J + 1) + (int)J);
         for (uint32_t j = 0; j < J; j++) at[p0 + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
     }
@@ -761,6 +831,20 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     }
     VK_TRY(fast_tables<C>(ctx, t, glv));
     const Aff* bases = t->fast.as<Aff>() + offset;  // packed-29 copies (ec29.hpp)
+    // shared windows (GLV MSM over the whole table): every window into one bucket set through
+    // the 2^(c w) copies of the bases (Table::win, built once; up to 8 GB of HBM). VKZG_MSM_SHARED=0
+    // keeps the per-window buckets (tuning probe / memory-tight callers).
+    bool shared = false;
+    if constexpr (std::is_same<C, BLS381G1>::value) {
+        static const bool shared_env = !(getenv("VKZG_MSM_SHARED") && atoi(getenv("VKZG_MSM_SHARED")) == 0);
+        const size_t win_bytes = (size_t)Wfull * 2 * t->n * sizeof(Aff);
+        if (glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
+            const int st = win_tables<C>(ctx, t, c, Wfull);
+            if (st == VC_OK) shared = true;
+            else if (st != VC_E_OOM) return st;  // out of memory: per-window buckets instead
+            else t->win.release();
+        }
+    }
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
     // VKZG_MSM_SLICES=2 runs two staggered slices on the two lanes (tuning probe): measured no
     // faster at 2^20 BLS12-381 (4.09-4.29 vs 3.98-4.06 ms) -- a 4-window slice's accumulate fills
@@ -774,6 +858,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         sl[k].wb = wb + k * W / nsl;
         sl[k].we = wb + (k + 1) * W / nsl;
         sl[k].W = sl[k].we - sl[k].wb;
+        sl[k].shared = shared;
     }
     hipEvent_t fork = nullptr, join = nullptr, acc0 = nullptr;
     if (nsl == 2) acc0 = ctx->get_event();
@@ -789,9 +874,11 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                 VK_CHECK_HIP(hipEventRecord(fork, ctx->stream));
                 VK_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, fork, 0));
             }
+            const Aff* win = t->win.as<Aff>();  // [w][2n]: entry w * 2n + i (sort_entries' stride)
             for (int k = 0; k < nsl; k++)
-                VK_TRY(slice_enqueue<C>(ctx, sl[k], GlvDigits{halves, inf, (uint32_t)n}, nv, bases, dphi,
-                                        (uint32_t)n, k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
+                VK_TRY(slice_enqueue<C>(ctx, sl[k], GlvDigits{halves, inf, (uint32_t)n}, nv, shared ? win : bases,
+                                        shared ? win : dphi, shared ? 0xffffffffu : (uint32_t)n,
+                                        k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
         }
     } else {
         if (nsl == 2) {

@@ -92,9 +92,17 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk(typename A::Acc* __restr
     if (b == NONE_T) return;
     typename A::Acc acc = owner_piece[t];
     uint32_t u = t + 1;
+    typename A::Acc nx = carry[u];  // the next piece is loaded while the current add runs
+    uint8_t nth = through[u];
     for (uint32_t k = 0; k < limit && u < T; k++, u++) {
-        acc = A::add(acc, carry[u]);
-        if (through[u] == 1) {  // the piece that ends the bucket
+        const typename A::Acc cur = nx;
+        const uint8_t th = nth;
+        if (th != 1 && u + 1 < T) {
+            nx = carry[u + 1];
+            nth = through[u + 1];
+        }
+        acc = A::add(acc, cur);
+        if (th == 1) {  // the piece that ends the bucket
             buckets[b] = acc;
             return;
         }
