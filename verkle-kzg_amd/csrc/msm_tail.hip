@@ -72,41 +72,28 @@ __global__ void __launch_bounds__(256) k_msm_fixup(typename A::Acc* __restrict__
     buckets[b] = A::add(owner_piece[t], chain_sum[t + 1]);
 }
 
-// Common case: the owner thread of each straddling bucket walks its chain of carry pieces
-// serially (t+1, t+2, ... up to the piece that ends the bucket), at most `limit` of them: one
-// kernel, one add call site, a few serial adds when chains are short (mean bucket load ~ M).
-// A bucket over more than `limit` carry pieces is left unwritten here; the accumulate's
-// chain_max tells the host, which then runs the pointer-jumping path (msm_tail_fixup with the
-// known Lmax) from the untouched carry pieces and redoes the reduction.
+// Common case: a lane per bucket. A bucket b over accumulate threads t0 < t1 (t = entry / M)
+// has its owner piece in t0 and carry pieces in t0 + 1 .. t1; the lane adds them serially (at
+// most `limit` carry pieces): one kernel, one add call site, every lane of a wave busy (a lane
+// per accumulate thread left 3 of 4 lanes idle at 512 entries per bucket and ran the waves in
+// two rounds). A longer bucket is left unwritten here; the accumulate's chain_max tells the
+// host, which then runs the pointer-jumping path (msm_tail_fixup with the known Lmax) from the
+// untouched carry pieces and redoes the reduction.
 template <class A>
 __global__ void __launch_bounds__(256) k_msm_fixup_walk(typename A::Acc* __restrict__ buckets,
                                                        const typename A::Acc* __restrict__ carry,
-                                                       const uint8_t* __restrict__ through,
                                                        const typename A::Acc* __restrict__ owner_piece,
-                                                       const uint32_t* __restrict__ owner_bucket, uint32_t Tmax,
-                                                       const uint32_t* __restrict__ Lp, uint32_t M, uint32_t limit) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t T = (*Lp + M - 1) / M;
-    if (t >= T || t >= Tmax) return;
-    const uint32_t b = owner_bucket[t];
-    if (b == NONE_T) return;
-    typename A::Acc acc = owner_piece[t];
-    uint32_t u = t + 1;
-    typename A::Acc nx = carry[u];  // the next piece is loaded while the current add runs
-    uint8_t nth = through[u];
-    for (uint32_t k = 0; k < limit && u < T; k++, u++) {
-        const typename A::Acc cur = nx;
-        const uint8_t th = nth;
-        if (th != 1 && u + 1 < T) {
-            nx = carry[u + 1];
-            nth = through[u + 1];
-        }
-        acc = A::add(acc, cur);
-        if (th == 1) {  // the piece that ends the bucket
-            buckets[b] = acc;
-            return;
-        }
-    }
+                                                       const uint32_t* __restrict__ offsets, uint32_t NBtot,
+                                                       uint32_t M, uint32_t limit) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= NBtot) return;
+    const uint32_t lo = offsets[b], hi = offsets[b + 1];
+    if (hi <= lo) return;  // empty
+    const uint32_t t0 = lo / M, t1 = (hi - 1) / M;
+    if (t0 == t1 || t1 - t0 > limit) return;  // inside one thread (written) / long chain (host path)
+    typename A::Acc acc = owner_piece[t0];
+    for (uint32_t u = t0 + 1; u <= t1; u++) acc = A::add(acc, carry[u]);
+    buckets[b] = acc;
 }
 
 // ------------------------------------------------------------------ bucket reduction
@@ -288,12 +275,11 @@ int msm_tail_fixup(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t
 
 // the serial walk of every owner over at most `limit` carry pieces (see k_msm_fixup_walk)
 template <class C>
-int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t M, FAcc<C>* buckets,
-                        const FAcc<C>* carry, const uint8_t* through, const FAcc<C>* owner, const uint32_t* owner_b,
-                        uint32_t limit) {
+int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t NBtot, uint32_t M, FAcc<C>* buckets,
+                        const FAcc<C>* carry, const FAcc<C>* owner, uint32_t limit) {
     using A = typename Fast29<C>::type;
-    VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk<A>), (T + 255) / 256, 256, 0, buckets, carry, through,
-                 owner, owner_b, T, Lp, M, limit);
+    VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk<A>), (NBtot + 255) / 256, 256, 0, buckets, carry, owner,
+                 offsets, NBtot, M, limit);
     return VC_OK;
 }
 
@@ -341,8 +327,8 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
                                    const uint8_t*, const FAcc<C>*, const uint32_t*, const uint32_t*, uint32_t); \
     template int msm_tail_fixup_more<C>(vc_ctx*, Lane, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,      \
                                         const uint8_t*, const FAcc<C>*, const uint32_t*, uint32_t, uint32_t);   \
-    template int msm_tail_fixup_walk<C>(vc_ctx*, Lane, uint32_t, const uint32_t*, uint32_t, FAcc<C>*,              \
-                                        const FAcc<C>*, const uint8_t*, const FAcc<C>*, const uint32_t*, uint32_t); \
+    template int msm_tail_fixup_walk<C>(vc_ctx*, Lane, const uint32_t*, uint32_t, uint32_t, FAcc<C>*, const FAcc<C>*, \
+                                        const FAcc<C>*, uint32_t);                                             \
     template int msm_tail_reduce<C>(vc_ctx*, Lane, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
                                     uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*);
 VK_INST_TAIL(BN254G1)
