@@ -62,7 +62,7 @@ struct Table {
     // GLV MSMs over the whole table: packed-29 copies of 2^(c w) P and 2^(c w) phi(P) for every
     // window w ([w][2n] layout), so all windows share one set of buckets (msm.hip, "shared
     // windows"); built on first use for the window size c in win_c
-    int win_ok = 0, win_c = 0, win_W = 0;
+    int win_ok = 0, win_c = 0, win_W = 0, win_ts = 0;
     DevBuf win;
 };
 

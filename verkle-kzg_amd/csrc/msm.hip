@@ -103,17 +103,24 @@ struct ScalarDigits {  // plain scalars, canonical or Montgomery
     }
 };
 // GLV halves (k_glv_split): entry i < n is k1 of scalar i against P_i, entry n + i is k2 against
-// phi(P_i); magnitude in bits 0..126, sign in bit 127 (a negative half negates every digit)
+// phi(P_i); magnitude in bits 0..126, sign in bit 127 (a negative half negates every digit).
+// Shared windows with a short top window (tw >= 0): its digits are scaled by 2^ts -- the window
+// copy of that window holds 2^(c tw - ts) P -- so they spread over the whole bucket range
+// instead of piling into the lowest 2^-ts of it.
 struct GlvDigits {
     const uint4* k;
     const uint8_t* inf;
     uint32_t n;
+    int tw = -1, ts = 0;
     template <class Fn>
     __device__ __forceinline__ void operator()(uint32_t i, int c, int W, Fn&& f) const {
         if (inf != nullptr && inf[i < n ? i : i - n]) return;
         const uint4 v = k[i];
         const bool neg = (v.w >> 31) != 0;
-        for_each_digit4(v.x, v.y, v.z, v.w & 0x7fffffffu, c, W, [&](int w, int32_t d) { f(w, neg ? -d : d); });
+        for_each_digit4(v.x, v.y, v.z, v.w & 0x7fffffffu, c, W, [&](int w, int32_t d) {
+            if (w == tw) d *= (1 << ts);
+            f(w, neg ? -d : d);
+        });
     }
 };
 
@@ -543,10 +550,10 @@ __global__ void __launch_bounds__(256) k_win_next(const typename C::Aff* __restr
 // instead of W and no doublings in the host fold. 2 W n points (1.6 GB at n = 2^20, c = 16),
 // built once per table and window size: W - 1 steps of c doublings + a batch normalisation.
 template <class C>
-static int win_tables(vc_ctx* ctx, Table* t, int c, int W) {
+static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
     using Aff = typename C::Aff;
     using Acc = typename C::Acc;
-    if (t->win_ok && t->win_c == c && t->win_W >= W) return VC_OK;
+    if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts) return VC_OK;
     const size_t n = t->n;
     t->win_ok = 0;
     VK_TRY(t->win.ensure((size_t)W * 2 * n * sizeof(Aff)));
@@ -559,8 +566,9 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W) {
     for (int w = 0; w < W; w++) {
         const Aff* src = t->bases.as<Aff>();
         if (w > 0) {
+            // the top window's copy is 2^(c w - ts) P (its digits are scaled by 2^ts, GlvDigits)
             VK_LAUNCH(ctx, "win_next", (k_win_next<C>), g, 256, 0, w == 1 ? t->bases.as<Aff>() : cur.bases.as<Aff>(),
-                      t->inf.as<uint8_t>(), (uint32_t)n, c, acc.as<Acc>());
+                      t->inf.as<uint8_t>(), (uint32_t)n, w == W - 1 ? c - ts : c, acc.as<Acc>());
             VK_TRY(table_from_acc(ctx, &cur, acc.p, n));
             src = cur.bases.as<Aff>();
         }
@@ -572,6 +580,7 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W) {
     t->win_ok = 1;
     t->win_c = c;
     t->win_W = W;
+    t->win_ts = ts;
     return VC_OK;
 }
 
@@ -610,6 +619,15 @@ static int glv_window(size_t nv) {
     if (nv >= (1u << 19)) return 16;
     if (nv >= (1u << 15)) return 13;
     return 10;
+}
+// shared windows (msm_run_t): a short top window's digits are scaled to span the bucket range
+// (GlvDigits::ts), so c need not divide 128. Measured at 2^21 terms: c = 19 (7 windows) cuts
+// the accumulate by 0.3-0.45 ms but its 2^18-bucket reduction, the top window's hot buckets in
+// the fix-up and the sort give it all back (3.61 vs 3.60 ms) -- c = 16 stays.
+static int glv_window_shared(size_t nv) {
+    static const int env = getenv("VKZG_MSM_C") ? atoi(getenv("VKZG_MSM_C")) : 0;  // tuning probe
+    if (env >= 8 && env <= 20) return env;
+    return glv_window(nv);
 }
 static int choose_window(size_t n) {
     if (n >= (1u << 19)) return 16;
@@ -671,13 +689,17 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // threads (the GLV 2^20 MSM has 64 entries per bucket: M = 128 drops the fix-up's
     // pointer-jumping rounds, 0.23 -> 0.06 ms, for 0.1 ms more accumulate)
     if (load / NB > M / 2 && M < 128) M *= 2;
+    // shared windows: the fix-up is a lane per bucket, so M just fills one round of two waves
+    // per SIMD (131072 lanes)
+    if (sl.shared) M = (uint32_t)std::max<size_t>(16, (maxL + 131071) / 131072);
     if (const char* em = getenv("VKZG_MSM_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe
     // buckets per reduction segment (the segment sum is a serial chain of 2*Lseg adds): 4, or 2
     // when the segments (one lane each) would not give every SIMD a wave (GLV 2^20: 4 at 8
     // windows, 2 for the 1-4 window slices of multi-GPU runs; 8 measured 0.1-0.15 ms slower)
     uint32_t Lseg = NB >= 64 ? 4 : (NB >= 4 ? 2 : 1);
     if (Lseg == 4 && (size_t)(NB / Lseg) * Wr < 65536) Lseg = 2;
-    if (sl.shared) Lseg = 1;  // one bucket set: the bit sums straight over the buckets (measured)
+    // one bucket set: the bit sums straight over 2^15 buckets (measured), segments of 4 at 2^18
+    if (sl.shared) Lseg = NB >= (1u << 17) ? 4 : 1;
     if (const char* el = getenv("VKZG_MSM_LSEG")) Lseg = (uint32_t)std::max(1, atoi(el));  // tuning probe
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
@@ -744,6 +766,9 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // chains up to 2^guard carry pieces are walked serially by their owners; longer ones
     // (adversarial scalars) take the pointer-jumping path in slice_finish
     sl.guard = msm_fixup_guard_rounds(load, NB, M);
+    // shared windows: a short top window's digits load 2^-tb of the buckets several times the
+    // mean (c = 19: ~310 entries vs 56), so the walk takes chains of up to 16 pieces
+    if (sl.shared) sl.guard = std::max<uint32_t>(sl.guard, 4);
     static const int fix_env = getenv("VKZG_MSM_FIXUP") ? atoi(getenv("VKZG_MSM_FIXUP")) : 0;  // tuning probe
     if (fix_env == 1)  // guarded pointer-jumping rounds instead of the owner walk
         VK_TRY(msm_tail_fixup<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
@@ -816,7 +841,36 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         if (n >= GLV_MIN_N && n < (1u << 30)) VK_TRY(glv_table_ok(ctx, t, &glv));
     }
     const size_t nv = glv ? 2 * n : n;  // MSM terms after the endomorphism split
-    const int c = glv ? glv_window(nv) : choose_window(nv);
+    VK_TRY(fast_tables<C>(ctx, t, glv));
+    const Aff* bases = t->fast.as<Aff>() + offset;  // packed-29 copies (ec29.hpp)
+    // shared windows (GLV MSM over the whole table): every window into one bucket set through
+    // the 2^(c w) copies of the bases (Table::win, built once; up to 8 GB of HBM). The window
+    // size then only trades mixed adds (W per term) against one bucket reduction: c = 19 at
+    // 2^21 terms (7 windows instead of 8). VKZG_MSM_SHARED=0 keeps per-window buckets (probe).
+    bool shared = false;
+    int top_shift = 0;
+    int c = glv ? glv_window(nv) : choose_window(nv);
+    if constexpr (std::is_same<C, BLS381G1>::value) {
+        static const bool shared_env = !(getenv("VKZG_MSM_SHARED") && atoi(getenv("VKZG_MSM_SHARED")) == 0);
+        const int cs = glv_window_shared(nv);
+        const int Ws = (GLV_BITS + cs - 1) / cs;
+        // top window: GLV_BITS - cs (Ws - 1) bits -> digits up to 2^tb; scaled to fill 2^(cs-1)
+        const int tb = GLV_BITS - cs * (Ws - 1);
+        const int ts = std::max(0, (cs - 1) - tb);
+        const size_t win_bytes = (size_t)Ws * 2 * t->n * sizeof(Aff);
+        if (glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
+            const int st = win_tables<C>(ctx, t, cs, Ws, ts);
+            if (st == VC_OK) {
+                shared = true;
+                c = cs;
+                top_shift = ts;
+            } else if (st != VC_E_OOM) {
+                return st;
+            } else {
+                t->win.release();  // out of memory: per-window buckets instead
+            }
+        }
+    }
     // one spare bit absorbs the final carry of the signed recoding
     const int Wfull = glv ? (GLV_BITS + c - 1) / c : (Fr::BITS + 1 + c - 1) / c;
     // window slice [wb, we) of this call (parts > 1: the MSM split by windows across GPUs;
@@ -827,22 +881,6 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         Acc z = C::zero();
         memcpy(out_acc, &z, sizeof(Acc));
         return VC_OK;
-    }
-    VK_TRY(fast_tables<C>(ctx, t, glv));
-    const Aff* bases = t->fast.as<Aff>() + offset;  // packed-29 copies (ec29.hpp)
-    // shared windows (GLV MSM over the whole table): every window into one bucket set through
-    // the 2^(c w) copies of the bases (Table::win, built once; up to 8 GB of HBM). VKZG_MSM_SHARED=0
-    // keeps the per-window buckets (tuning probe / memory-tight callers).
-    bool shared = false;
-    if constexpr (std::is_same<C, BLS381G1>::value) {
-        static const bool shared_env = !(getenv("VKZG_MSM_SHARED") && atoi(getenv("VKZG_MSM_SHARED")) == 0);
-        const size_t win_bytes = (size_t)Wfull * 2 * t->n * sizeof(Aff);
-        if (glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
-            const int st = win_tables<C>(ctx, t, c, Wfull);
-            if (st == VC_OK) shared = true;
-            else if (st != VC_E_OOM) return st;  // out of memory: per-window buckets instead
-            else t->win.release();
-        }
     }
     const uint8_t* inf = t->inf.as<uint8_t>() + offset;
     // VKZG_MSM_SLICES=2 runs two staggered slices on the two lanes (tuning probe): measured no
@@ -874,8 +912,13 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                 VK_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, fork, 0));
             }
             const Aff* win = t->win.as<Aff>();  // [w][2n]: entry w * 2n + i (sort_entries' stride)
+            GlvDigits src{halves, inf, (uint32_t)n};
+            if (shared && top_shift > 0) {
+                src.tw = Wfull - 1;
+                src.ts = top_shift;
+            }
             for (int k = 0; k < nsl; k++)
-                VK_TRY(slice_enqueue<C>(ctx, sl[k], GlvDigits{halves, inf, (uint32_t)n}, nv, shared ? win : bases,
+                VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, shared ? win : bases,
                                         shared ? win : dphi, shared ? 0xffffffffu : (uint32_t)n,
                                         k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
         }
@@ -1124,7 +1167,8 @@ int msm_windows(int curve, size_t n, int* c, int* W, int* terms) {
     int bits = curve == VC_CURVE_BN254 ? BN254Fr::BITS : curve == VC_CURVE_BLS12_381 ? BLS381Fr::BITS : BandFr::BITS;
     // BLS12-381 tables of subgroup points take the GLV split (2n terms of 127-bit scalars)
     const bool glv = curve == VC_CURVE_BLS12_381 && n >= GLV_MIN_N && n < (1u << 30);
-    *c = glv ? glv_window(2 * n) : choose_window(n);
+    // (a GLV MSM over a whole table takes the shared-window size, msm_run_t)
+    *c = glv ? glv_window_shared(2 * n) : choose_window(n);
     *W = glv ? (GLV_BITS + *c - 1) / *c : (bits + 1 + *c - 1) / *c;
     if (terms) *terms = glv ? 2 : 1;
     return VC_OK;
