@@ -29,6 +29,27 @@ int DevBuf::ensure(size_t bytes) {
     return VC_OK;
 }
 
+int PinBuf::ensure(size_t bytes) {
+    if (bytes <= cap && p) return VC_OK;
+    release();
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        p = nullptr;
+        cap = 0;
+        return VC_E_OOM;
+    }
+    cap = bytes;
+    return VC_OK;
+}
+
+void PinBuf::release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
 void DevBuf::release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -150,6 +171,8 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         for (auto* t : ctx->tables) delete t;
         ctx->tables.clear();
         for (auto& b : ctx->ws) b.release();
+        for (auto& b : ctx->ws2) b.release();
+        for (auto& b : ctx->pin) b.release();
         for (auto& p : ctx->pending) {
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);

@@ -44,6 +44,23 @@ struct DevBuf {
     DevBuf& operator=(const DevBuf&) = delete;
 };
 
+// page-locked host staging (one per lane): device->host copies into pageable memory go through a
+// bounce buffer and start late (measured ~25 us before the MSM's second small read-back)
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes);
+    void release();
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+    ~PinBuf() { release(); }
+    PinBuf() = default;
+    PinBuf(const PinBuf&) = delete;
+    PinBuf& operator=(const PinBuf&) = delete;
+};
+
 struct Table {
     int curve = 0;
     size_t n = 0;
@@ -112,6 +129,7 @@ enum WsSlot {
 struct Lane {
     hipStream_t st;
     DevBuf* ws;
+    PinBuf* pin;
 };
 
 struct PendingTimer {
@@ -131,6 +149,7 @@ struct vc_ctx {
     std::vector<vk::Table*> tables;
     vk::DevBuf ws[vk::WS_COUNT_];
     vk::DevBuf ws2[vk::WS_COUNT_];  // workspace of lane 1 (side_stream)
+    vk::PinBuf pin[2];              // read-back staging of lanes 0 / 1
     bool timing = false;
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
@@ -143,7 +162,7 @@ struct vc_ctx {
     void timer_begin(const char* name, hipEvent_t* a, hipStream_t s = nullptr);
     void timer_end(const char* name, hipEvent_t a, hipStream_t s = nullptr);
     void collect_timers();  // call after the stream is synchronised
-    vk::Lane lane(int i) { return i == 0 ? vk::Lane{stream, ws} : vk::Lane{side_stream, ws2}; }
+    vk::Lane lane(int i) { return i == 0 ? vk::Lane{stream, ws, &pin[0]} : vk::Lane{side_stream, ws2, &pin[1]}; }
     vk::Table* table(int id) {
         if (id < 0 || id >= (int)tables.size() || !tables[id]) return nullptr;
         return tables[id];

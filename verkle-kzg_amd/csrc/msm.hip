@@ -159,12 +159,32 @@ __global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, i
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(size_t)k * nblk + blockIdx.x] = hist[k];
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(size_t)bins * nblk] = 0;  // the scan's terminal slot
 }
 
-template <class Src>
+// Coarse entries: u64 = fine << 32 | e | sign << 31, or -- when e < 2^(31 - FB), e.g. the
+// shared-window 2^20 MSM (e < 2^24, FB = 5) -- u32 = fine << (31 - FB) | e | sign << 31, which
+// halves the scatter's and the fine pass's traffic.
+template <class T>
+__device__ __forceinline__ T sort_pack(uint32_t fine, uint32_t e, bool neg, uint32_t FB) {
+    if constexpr (sizeof(T) == 8) return ((uint64_t)fine << 32) | e | (neg ? 0x80000000u : 0u);
+    else return (fine << (31 - FB)) | e | (neg ? 0x80000000u : 0u);
+}
+template <class T>
+__device__ __forceinline__ uint32_t sort_fine_of(T x, uint32_t FB) {
+    if constexpr (sizeof(T) == 8) return (uint32_t)(x >> 32);
+    else return (x & 0x7fffffffu) >> (31 - FB);
+}
+template <class T>
+__device__ __forceinline__ uint32_t sort_entry_of(T x, uint32_t FB) {
+    if constexpr (sizeof(T) == 8) return (uint32_t)x;
+    else return x & (0x80000000u | ((1u << (31 - FB)) - 1));
+}
+
+template <class Src, class T>
 __global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
                                                     uint32_t NBC, uint32_t nblk, uint32_t stride,
-                                                    const uint32_t* __restrict__ base, uint64_t* __restrict__ tmp) {
+                                                    const uint32_t* __restrict__ base, T* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
     const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + blockIdx.x];
@@ -177,23 +197,27 @@ __global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c,
                 uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
                 uint32_t pos = atomicAdd(&cur[(stride ? 0u : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
                 const uint32_t e = stride ? i + (uint32_t)w * stride : i;
-                tmp[pos] = ((uint64_t)(b & fmask) << 32) | e | (d < 0 ? 0x80000000u : 0u);
+                tmp[pos] = sort_pack<T>(b & fmask, e, d < 0, FB);
             }
         });
     }
 }
 
-// one block per coarse bin; offsets[g * 2^FB + f] = start of fine bucket f of bin g
-__global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ tmp, const uint32_t* __restrict__ base,
+// one block per coarse bin; offsets[g * 2^FB + f] = start of fine bucket f of bin g. Block 0
+// also clears the accumulate's chain_max word (no separate memset in the pipeline).
+template <class T>
+__global__ void __launch_bounds__(256) k_sort_fine(const T* __restrict__ tmp, const uint32_t* __restrict__ base,
                                                   uint32_t nblk, uint32_t bins, uint32_t FB,
-                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
+                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
+                                                  uint32_t* __restrict__ zero_word) {
     __shared__ uint32_t h[256], x[256];
     const uint32_t g = blockIdx.x, F = 1u << FB, t = threadIdx.x;
+    if (zero_word != nullptr && g == 0 && t == 0) *zero_word = 0;
     const uint32_t start = base[(size_t)g * nblk];
     const uint32_t end = base[(size_t)(g + 1) * nblk];  // base has bins*nblk + 1 entries
     h[t] = 0;
     __syncthreads();
-    for (uint32_t p = start + t; p < end; p += blockDim.x) atomicAdd(&h[(uint32_t)(tmp[p] >> 32)], 1u);
+    for (uint32_t p = start + t; p < end; p += blockDim.x) atomicAdd(&h[sort_fine_of<T>(tmp[p], FB)], 1u);
     __syncthreads();
     // inclusive Hillis-Steele scan over 256 counters
     uint32_t v = h[t];
@@ -212,9 +236,9 @@ __global__ void __launch_bounds__(256) k_sort_fine(const uint64_t* __restrict__ 
     h[t] = excl;  // cursors
     __syncthreads();
     for (uint32_t p = start + t; p < end; p += blockDim.x) {
-        uint64_t e = tmp[p];
-        uint32_t pos = start + atomicAdd(&h[(uint32_t)(e >> 32)], 1u);
-        sorted[pos] = (uint32_t)e;
+        const T e = tmp[p];
+        uint32_t pos = start + atomicAdd(&h[sort_fine_of<T>(e, FB)], 1u);
+        sorted[pos] = sort_entry_of<T>(e, FB);
     }
 }
 
@@ -587,12 +611,15 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
 template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
                         uint32_t NBC, uint32_t nblk, uint32_t stride, size_t ncnt, uint32_t* counts, uint32_t* base,
-                        uint64_t* tmp, uint32_t* offsets, uint32_t* sorted) {
+                        void* tmp, uint32_t* offsets, uint32_t* sorted, uint32_t* zero_word) {
     hipStream_t st = L.st;
     const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     const size_t lds = (size_t)bins * 4;
     if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
-    VK_CHECK_HIP(hipMemsetAsync(counts + ncnt - 1, 0, 4, st));
+    if (ncnt != (size_t)bins * nblk + 1) return VC_E_INVALID;
+    // largest entry index e: i < nv, or w * stride + i with shared windows
+    const uint64_t emax = stride ? (uint64_t)we * stride : (uint64_t)nv;
+    const bool narrow = emax <= (1ull << (31 - FB));
     VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
                  stride, counts);
     size_t tmp_bytes = 0;
@@ -604,9 +631,17 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
         VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(L.ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
         if (ctx->timing) ctx->timer_end("msm_scan", ev, st);
     }
-    VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
-                 stride, base, tmp);
-    VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine, bins, 256, 0, tmp, base, nblk, bins, FB, offsets, sorted);
+    if (narrow) {
+        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, 256, lds, src, nv, c, wb, we, FB,
+                     NBC, nblk, stride, base, static_cast<uint32_t*>(tmp));
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, 256, 0, static_cast<const uint32_t*>(tmp),
+                     base, nblk, bins, FB, offsets, sorted, zero_word);
+    } else {
+        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, 256, lds, src, nv, c, wb, we, FB,
+                     NBC, nblk, stride, base, static_cast<uint64_t*>(tmp));
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, 256, 0, static_cast<const uint64_t*>(tmp),
+                     base, nblk, bins, FB, offsets, sorted, zero_word);
+    }
     return VC_OK;
 }
 
@@ -653,7 +688,8 @@ struct MsmSlice {
     int Wr = 0;           // bucket sets reduced: 1 shared, W otherwise
     uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
     uint32_t* offsets = nullptr;
-    uint32_t* chain_max = nullptr;
+    uint32_t* chain_max = nullptr;  // in the WS_TAIL buffer, tail_bytes after the tail points
+    size_t tail_bytes = 0;
     uint8_t* through = nullptr;
     uint32_t* owner_b = nullptr;
     FAcc<C>* buckets = nullptr;
@@ -730,8 +766,9 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     VK_TRY(ws[WS_SEG].ensure((size_t)S * Wr * sizeof(RAcc)));
     VK_TRY(ws[WS_TREE].ensure((size_t)S * Wr * sizeof(RAcc)));
     VK_TRY(ws[WS_WIN].ensure((size_t)Wr * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)Wr, J)) * sizeof(RAcc)));
-    VK_TRY(ws[WS_TAIL].ensure((size_t)Wr * (J + 1) * sizeof(Acc)));
-    VK_TRY(ws[WS_CHAIN].ensure(4));
+    // tail points, then the chain_max word: one read-back
+    const size_t tail_bytes = ((size_t)Wr * (J + 1) * sizeof(Acc) + 15) & ~(size_t)15;
+    VK_TRY(ws[WS_TAIL].ensure(tail_bytes + 16));
 
     sl.NB = NB;
     sl.NBtot = NBtot;
@@ -741,7 +778,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.S = S;
     sl.J = J;
     sl.offsets = ws[WS_OFFSETS].as<uint32_t>();
-    sl.chain_max = ws[WS_CHAIN].as<uint32_t>();
+    sl.tail_bytes = tail_bytes;
+    sl.chain_max = reinterpret_cast<uint32_t*>(ws[WS_TAIL].as<uint8_t>() + tail_bytes);
     sl.through = ws[WS_THROUGH].as<uint8_t>();
     sl.owner_b = ws[WS_OWNER_B].as<uint32_t>();
     sl.buckets = ws[WS_BUCKETS].as<RAcc>();
@@ -754,10 +792,10 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
 
     VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, sl.shared ? (uint32_t)nv : 0u, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
-                        ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].as<uint64_t>(), sl.offsets,
-                        ws[WS_SORTED].as<uint32_t>()));
-    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W
-    VK_CHECK_HIP(hipMemsetAsync(sl.chain_max, 0, 4, st));
+                        ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
+                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max));
+    // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W;
+    // chain_max was cleared by k_sort_fine
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
     VK_LAUNCH_ON(ctx, st, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi,
                  ws[WS_SORTED].as<uint32_t>(), sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
@@ -784,9 +822,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
 template <class C>
 static int slice_fetch(MsmSlice<C>& sl) {
     sl.ht.resize((size_t)sl.Wr * (sl.J + 1));
-    VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(typename C::Acc), hipMemcpyDeviceToHost,
-                                sl.L.st));
-    VK_CHECK_HIP(hipMemcpyAsync(&sl.Lmax, sl.chain_max, 4, hipMemcpyDeviceToHost, sl.L.st));
+    VK_TRY(sl.L.pin->ensure(sl.tail_bytes + 16));
+    VK_CHECK_HIP(hipMemcpyAsync(sl.L.pin->p, sl.tail, sl.tail_bytes + 4, hipMemcpyDeviceToHost, sl.L.st));
     return VC_OK;
 }
 
@@ -794,6 +831,8 @@ template <class C>
 static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     using Acc = typename C::Acc;
     VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
+    memcpy(sl.ht.data(), sl.L.pin->p, sl.ht.size() * sizeof(Acc));
+    memcpy(&sl.Lmax, static_cast<const uint8_t*>(sl.L.pin->p) + sl.tail_bytes, 4);
     if (sl.Lmax > (1u << sl.guard)) {  // rare (heavily repeated scalars): pointer jumping, redo the tail
         VK_TRY(msm_tail_fixup<C>(ctx, sl.L, sl.Tmax, sl.offsets + sl.NBtot, sl.M, sl.buckets, sl.carry, sl.through,
                                  sl.owner, sl.owner_b, sl.chain_max, 0));
