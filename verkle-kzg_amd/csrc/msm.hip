@@ -141,6 +141,15 @@ struct GlvDigits {
 #endif
 constexpr uint32_t SORT_CHUNK = VK_SORT_CHUNK;
 
+// XCD-aware run order: blocks are dispatched round-robin over the 8 XCDs (block b on XCD b % 8),
+// each with its own L2. A block's run inside every coarse bin sits at its slot in this order, so
+// the runs of one XCD's blocks are adjacent and the partial-line writes of the scatter merge in
+// ONE L2 instead of being written back as masked partial lines by several.
+__device__ __forceinline__ uint32_t sort_slot(uint32_t b, uint32_t nblk) {
+    const uint32_t q = nblk / 8, rem = nblk % 8, x = b % 8;
+    return x * q + min(x, rem) + b / 8;
+}
+
 template <class Src>
 __global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
                                                   uint32_t NBC, uint32_t nblk, uint32_t stride,
@@ -158,7 +167,8 @@ __global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, i
         });
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(size_t)k * nblk + blockIdx.x] = hist[k];
+    const uint32_t slot = sort_slot(blockIdx.x, nblk);
+    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) counts[(size_t)k * nblk + slot] = hist[k];
     if (blockIdx.x == 0 && threadIdx.x == 0) counts[(size_t)bins * nblk] = 0;  // the scan's terminal slot
 }
 
@@ -187,7 +197,8 @@ __global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c,
                                                     const uint32_t* __restrict__ base, T* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
     const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
-    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + blockIdx.x];
+    const uint32_t slot = sort_slot(blockIdx.x, nblk);
+    for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + slot];
     __syncthreads();
     const uint32_t fmask = (1u << FB) - 1;
     const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
