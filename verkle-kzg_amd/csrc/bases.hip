@@ -177,7 +177,7 @@ static int fill_t(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf,
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
     if (n == 0) return VC_OK;
-    DevBuf dxy, dinf, dbad;
+    DevBuf dxy(ctx), dinf(ctx), dbad(ctx);
     VK_TRY(dxy.ensure(n * 2 * F::N * 4));
     VK_TRY(dinf.ensure(n));
     VK_TRY(dbad.ensure(4));

@@ -14,10 +14,50 @@ hipError_t& last_hip_error() {
     return e;
 }
 
+// pooled blocks: best fit within 2x (+1 MiB) of the request; at most VK_POOL_MAX cached bytes
+constexpr size_t VK_POOL_MAX = 16ull << 30;
+
+int pool_take(vc_ctx* ctx, size_t bytes, void** p, size_t* cap) {
+    auto it = ctx->pool_free.lower_bound(bytes);
+    if (it != ctx->pool_free.end() && it->first <= 2 * bytes + (1u << 20)) {
+        *p = it->second;
+        *cap = it->first;
+        ctx->pool_bytes -= it->first;
+        ctx->pool_free.erase(it);
+        return VC_OK;
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory && !ctx->pool_free.empty()) {  // give the cached blocks back, retry
+        (void)hipGetLastError();
+        for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
+        ctx->pool_free.clear();
+        ctx->pool_bytes = 0;
+        e = hipMalloc(p, bytes);
+    }
+    if (e != hipSuccess) {
+        last_hip_error() = e;
+        *p = nullptr;
+        *cap = 0;
+        return VC_E_OOM;
+    }
+    *cap = bytes;
+    return VC_OK;
+}
+
+void pool_put(vc_ctx* ctx, void* p, size_t cap) {
+    if (ctx->pool_bytes + cap > VK_POOL_MAX) {
+        (void)hipFree(p);
+        return;
+    }
+    ctx->pool_free.emplace(cap, p);
+    ctx->pool_bytes += cap;
+}
+
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap && p) return VC_OK;
     release();
     if (bytes == 0) bytes = 16;
+    if (pool) return pool_take(pool, bytes, &p, &cap);
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {
         last_hip_error() = e;
@@ -51,7 +91,8 @@ void PinBuf::release() {
 }
 
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p && pool) pool_put(pool, p, cap);
+    else if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
 }
@@ -173,6 +214,8 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         for (auto& b : ctx->ws) b.release();
         for (auto& b : ctx->ws2) b.release();
         for (auto& b : ctx->pin) b.release();
+        for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
+        ctx->pool_free.clear();
         for (auto& p : ctx->pending) {
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
@@ -192,7 +235,10 @@ int vc_ctx_curve(const vc_ctx* ctx) { return ctx ? ctx->curve : VC_E_INVALID; }
 int vc_ctx_set_stream(vc_ctx* ctx, void* s) {
     if (!ctx) return VC_E_INVALID;
     Guard g(ctx);
-    ctx->stream = s ? reinterpret_cast<hipStream_t>(s) : ctx->own_stream;
+    hipStream_t ns = s ? reinterpret_cast<hipStream_t>(s) : ctx->own_stream;
+    // pooled scratch freed by work still queued on the old stream must not be reused on the new one
+    if (ns != ctx->stream && ctx->stream) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->stream = ns;
     return VC_OK;
 }
 

@@ -28,12 +28,19 @@
 namespace vk {
 
 hipError_t& last_hip_error();
+int pool_take(vc_ctx* ctx, size_t bytes, void** p, size_t* cap);
+void pool_put(vc_ctx* ctx, void* p, size_t cap);
 
+// Device buffer. DevBuf(ctx) draws from / returns to the context's stream-ordered block pool
+// (per-call scratch of the scheme paths: a hipMalloc + hipFree pair per buffer per call cost
+// tens of us each, and hipFree synchronises the device); DevBuf() owns its memory outright.
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    vc_ctx* pool = nullptr;
     int ensure(size_t bytes);
     void release();
+    explicit DevBuf(vc_ctx* ctx) : pool(ctx) {}
     template <class T>
     T* as() const {
         return reinterpret_cast<T*>(p);
@@ -150,6 +157,11 @@ struct vc_ctx {
     vk::DevBuf ws[vk::WS_COUNT_];
     vk::DevBuf ws2[vk::WS_COUNT_];  // workspace of lane 1 (side_stream)
     vk::PinBuf pin[2];              // read-back staging of lanes 0 / 1
+    // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
+    // (or are synchronised), so a block freed by one call is safely reused by the next in
+    // stream order; vc_ctx_set_stream drains the old stream first
+    std::multimap<size_t, void*> pool_free;
+    size_t pool_bytes = 0;
     bool timing = false;
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;

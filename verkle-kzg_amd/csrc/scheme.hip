@@ -117,7 +117,7 @@ static int msm_points(vc_ctx* ctx, const std::vector<uint64_t>& xy, const std::v
                       const std::vector<Fr>& sc, Acc* out) {
     size_t n = sc.size();
     VK_TRY(bases_fill(ctx, &ctx->scratch, xy.data(), inf.data(), n));
-    DevBuf d;
+    DevBuf d(ctx);
     VK_TRY(d.ensure(std::max<size_t>(n, 1) * 32));
     VK_CHECK_HIP(hipMemcpyAsync(d.p, sc.data(), n * 32, hipMemcpyHostToDevice, ctx->stream));
     VK_TRY(msm_run(ctx, &ctx->scratch, 0, d.p, n, 1, reinterpret_cast<uint32_t*>(out)));
@@ -314,7 +314,7 @@ static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals
                        int part = 0, int parts = 1, uint32_t* out_acc = nullptr) {
     if (!is_pow2(size) || max > size) return VC_E_INVALID;
     if (t && t->n < size) return VC_E_RANGE;
-    DevBuf d_f, d_q, pw, tmp, part_buf;
+    DevBuf d_f(ctx), d_q(ctx), pw(ctx), tmp(ctx), part_buf(ctx);
     VK_TRY(d_f.ensure(size * 32));
     VK_TRY(d_q.ensure(size * 32));
     VK_TRY(tmp.ensure(size * 32));
@@ -444,7 +444,7 @@ int vc_to_data_item_batch(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, s
     if (ctx->curve != VC_CURVE_BN254) return VC_E_INVALID;
     Guard g(ctx);
     if (n == 0) return VC_OK;
-    DevBuf dxy, dinf, dout;
+    DevBuf dxy(ctx), dinf(ctx), dout(ctx);
     VK_TRY(dxy.ensure(n * 64));
     VK_TRY(dinf.ensure(n));
     VK_TRY(dout.ensure(n * 32));
@@ -637,7 +637,7 @@ int vc_kzg_setup(vc_ctx* ctx, size_t max_items, const uint64_t* secret, int* tab
     Guard g(ctx);
     size_t n = 1;
     while (n < max_items) n <<= 1;
-    DevBuf acc;
+    DevBuf acc(ctx);
     Table* t = new Table();
     int st = VC_OK;
     if (ctx->curve == VC_CURVE_BN254) {
@@ -890,7 +890,7 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     }
     const uint32_t nch = (uint32_t)(be.size() / 2);
     zc[Z] = nch;
-    DevBuf d_rp, d_order, d_be, d_zc, d_part;
+    DevBuf d_rp(ctx), d_order(ctx), d_be(ctx), d_zc(ctx), d_part(ctx);
     VK_TRY(d_rp.ensure(Qs * 32));
     VK_TRY(d_order.ensure(Qs * 4));
     VK_TRY(d_be.ensure(be.size() * 4));
@@ -924,7 +924,7 @@ static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vec
     if (!is_pow2(N) || G < 1 || zval.empty()) return VC_E_INVALID;
     hipStream_t st = ctx->stream;
     const uint32_t Z = (uint32_t)zval.size();
-    DevBuf d_zv, d_S, d_den, d_inv, d_Q, d_pw, d_pwi, d_g, d_h, d_it;
+    DevBuf d_zv(ctx), d_S(ctx), d_den(ctx), d_inv(ctx), d_Q(ctx), d_pw(ctx), d_pwi(ctx), d_g(ctx), d_h(ctx), d_it(ctx);
     VK_TRY(d_zv.ensure(Z * 4));
     VK_TRY(d_S.ensure((size_t)Z * N * 32));
     VK_TRY(d_den.ensure((size_t)Z * N * 32));
@@ -995,7 +995,7 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     Fr r;
     VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
     std::vector<uint32_t> zval = mp_points(Q, z);
-    DevBuf d_data, d_S;
+    DevBuf d_data(ctx), d_S(ctx);
     int st = d_data.ensure(Q * N * 32);
     if (st == VC_OK) st = d_S.ensure(zval.size() * N * 32);
     if (st == VC_OK && hipMemcpyAsync(d_data.p, data, Q * N * 32, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
