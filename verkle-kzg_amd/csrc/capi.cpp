@@ -214,6 +214,8 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         for (auto& b : ctx->ws) b.release();
         for (auto& b : ctx->ws2) b.release();
         for (auto& b : ctx->pin) b.release();
+        ctx->pin_io.release();
+        ctx->pin_small.release();
         for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
         ctx->pool_free.clear();
         for (auto& p : ctx->pending) {
@@ -397,7 +399,10 @@ int vc_msm_batch(vc_ctx* ctx, int id, size_t width, const uint64_t* scalars, siz
     uint8_t* dinf = dxy + batch * 2 * nl * 8;
     VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[vk::WS_SCALARS].p, scalars, batch * width * 32,
                                 hipMemcpyHostToDevice, ctx->stream));
-    VK_TRY(vk::msm_batch_run(ctx, t, width, ctx->ws[vk::WS_SCALARS].p, batch, mont, dxy, dinf));
+    bool on_host = false;
+    VK_TRY(vk::msm_batch_run(ctx, t, width, ctx->ws[vk::WS_SCALARS].p, batch, mont, dxy, dinf, out_xy, out_inf,
+                             &on_host));
+    if (on_host) return VC_OK;
     VK_CHECK_HIP(hipMemcpyAsync(out_xy, dxy, batch * 2 * nl * 8, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipMemcpyAsync(out_inf, dinf, batch, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));

@@ -388,7 +388,7 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c) {
 
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
-                       void* d_out_xy, uint8_t* d_out_inf) {
+                       void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host) {
     using Acc = typename C::Acc;
     if (width > t->n) return VC_E_RANGE;
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
@@ -409,17 +409,26 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
                   bpc, wpt, ctx->ws[WS_PIECE].as<Acc>());
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
-        std::vector<Acc> parts((size_t)batch * bpc);
-        VK_CHECK_HIP(hipMemcpyAsync(parts.data(), ctx->ws[WS_PIECE].p, parts.size() * sizeof(Acc),
+        // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the
+        // upload / second read-back round trip)
+        VK_TRY(ctx->pin_small.ensure((size_t)batch * bpc * sizeof(Acc)));
+        const Acc* parts = ctx->pin_small.as<Acc>();
+        VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_small.p, ctx->ws[WS_PIECE].p, (size_t)batch * bpc * sizeof(Acc),
                                     hipMemcpyDeviceToHost, ctx->stream));
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         const int nl = (int)(C::F::N / 2);
-        std::vector<uint64_t> oxy((size_t)batch * 2 * nl);
-        std::vector<uint8_t> oinf(batch);
+        std::vector<uint64_t> oxy(h_out_xy ? 0 : (size_t)batch * 2 * nl);
+        std::vector<uint8_t> oinf(h_out_xy ? 0 : batch);
+        uint64_t* rxy = h_out_xy ? h_out_xy : oxy.data();
+        uint8_t* rinf = h_out_xy ? h_out_inf : oinf.data();
         for (size_t g = 0; g < batch; g++) {
             Acc a = parts[g * bpc];
             for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
-            VK_TRY(acc_to_affine(ctx->curve, reinterpret_cast<const uint32_t*>(&a), &oxy[g * 2 * nl], &oinf[g]));
+            VK_TRY(acc_to_affine(ctx->curve, reinterpret_cast<const uint32_t*>(&a), rxy + g * 2 * nl, rinf + g));
+        }
+        if (h_out_xy) {
+            *on_host = true;
+            return VC_OK;
         }
         VK_CHECK_HIP(hipMemcpyAsync(d_out_xy, oxy.data(), oxy.size() * 8, hipMemcpyHostToDevice, ctx->stream));
         VK_CHECK_HIP(hipMemcpyAsync(d_out_inf, oinf.data(), batch, hipMemcpyHostToDevice, ctx->stream));
@@ -514,11 +523,21 @@ int fixed_base_precompute(vc_ctx* ctx, Table* t, int c) {
 }
 
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
-                  void* d_out_xy, uint8_t* d_out_inf) {
+                  void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host) {
+    bool dummy = false;
+    if (!on_host) on_host = &dummy;
+    *on_host = false;
+    if (h_out_xy && !h_out_inf) return VC_E_INVALID;
     switch (t->curve) {
-        case VC_CURVE_BN254: return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf);
-        case VC_CURVE_BLS12_381: return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf);
-        case VC_CURVE_BANDERSNATCH: return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf);
+        case VC_CURVE_BN254:
+            return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
+                                                 h_out_inf, on_host);
+        case VC_CURVE_BLS12_381:
+            return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
+                                                   h_out_inf, on_host);
+        case VC_CURVE_BANDERSNATCH:
+            return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
+                                                     h_out_inf, on_host);
     }
     return VC_E_INVALID;
 }

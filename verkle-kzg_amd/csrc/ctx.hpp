@@ -157,6 +157,8 @@ struct vc_ctx {
     vk::DevBuf ws[vk::WS_COUNT_];
     vk::DevBuf ws2[vk::WS_COUNT_];  // workspace of lane 1 (side_stream)
     vk::PinBuf pin[2];              // read-back staging of lanes 0 / 1
+    vk::PinBuf pin_io;              // host <-> device staging of the scheme paths (commit_batch)
+    vk::PinBuf pin_small;           // block partials of the small-batch commit path
     // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
     // (or are synchronised), so a block freed by one call is safely reused by the next in
     // stream order; vc_ctx_set_stream drains the old stream first
@@ -219,6 +221,9 @@ int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void
 int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                      const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
 int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
+// h_out_xy / h_out_inf (optional): host destinations -- when the small-batch latency path ran,
+// the results are written there instead of d_out_* and *on_host is set
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
-                  int mont, void* d_out_xy, uint8_t* d_out_inf);
+                  int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
+                  uint8_t* h_out_inf = nullptr, bool* on_host = nullptr);
 }  // namespace vk

@@ -100,15 +100,23 @@ static bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
 // width-w fixed-base commitments of Montgomery scalars (host) -> canonical affine (host)
 static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
                         uint8_t* out_inf) {
-    VK_TRY(ctx->ws[WS_SCALARS].ensure(batch * width * 32));
-    VK_TRY(ctx->ws[WS_MISC].ensure(batch * 65));
+    const size_t in_bytes = batch * width * 32, out_bytes = batch * 65;
+    VK_TRY(ctx->ws[WS_SCALARS].ensure(in_bytes));
+    VK_TRY(ctx->ws[WS_MISC].ensure(out_bytes));
     uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
     uint8_t* dinf = dxy + batch * 64;
-    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_SCALARS].p, sc, batch * width * 32, hipMemcpyHostToDevice, ctx->stream));
-    VK_TRY(msm_batch_run(ctx, t, width, ctx->ws[WS_SCALARS].p, batch, 1, dxy, dinf));
-    VK_CHECK_HIP(hipMemcpyAsync(out_xy, dxy, batch * 64, hipMemcpyDeviceToHost, ctx->stream));
-    VK_CHECK_HIP(hipMemcpyAsync(out_inf, dinf, batch, hipMemcpyDeviceToHost, ctx->stream));
+    // pinned staging both ways (the IPA rounds call this 8 times per proof: pageable copies went
+    // through bounce buffers), points and flags read back in one copy
+    VK_TRY(ctx->pin_io.ensure(std::max(in_bytes, out_bytes)));
+    memcpy(ctx->pin_io.p, sc, in_bytes);
+    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_SCALARS].p, ctx->pin_io.p, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    bool on_host = false;
+    VK_TRY(msm_batch_run(ctx, t, width, ctx->ws[WS_SCALARS].p, batch, 1, dxy, dinf, out_xy, out_inf, &on_host));
+    if (on_host) return VC_OK;
+    VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_io.p, dxy, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    memcpy(out_xy, ctx->pin_io.p, batch * 64);
+    memcpy(out_inf, static_cast<const uint8_t*>(ctx->pin_io.p) + batch * 64, batch);
     return VC_OK;
 }
 
