@@ -290,7 +290,7 @@ static int acc_to_affine_t(const uint32_t* accw, uint64_t* out_xy, uint8_t* out_
     typename C::Acc a;
     memcpy(&a, accw, sizeof a);
     fe<F> x, y;
-    bool fin = C::to_aff(a, x, y);
+    bool fin = C::template to_aff<true>(a, x, y);
     if (!fin) {
         memset(out_xy, 0, 2 * F::N * 4);
         if (C::is_te) out_xy[0 + F::N / 2] = 1;  // y = 1
