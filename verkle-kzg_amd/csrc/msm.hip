@@ -758,7 +758,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     uint32_t lgNB = (uint32_t)c - 1;
     uint32_t FB = lgNB < 8 ? lgNB : 8;
     // shared windows: ~16K entries per coarse bin (one k_sort_fine block each), as per window
-    while (sl.shared && FB > 1 && (load >> 14) > (size_t)(NB >> FB)) FB--;
+    static const int bin_lg = getenv("VKZG_SORT_BIN_LG") ? atoi(getenv("VKZG_SORT_BIN_LG")) : 14;  // tuning probe
+    while (sl.shared && FB > 1 && (load >> bin_lg) > (size_t)(NB >> FB)) FB--;
     const uint32_t NBC = NB >> FB;
     const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
     const size_t ncnt = (size_t)Wr * NBC * nblk + 1;
