@@ -215,36 +215,38 @@ __global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c,
 }
 
 // one block per coarse bin; offsets[g * 2^FB + f] = start of fine bucket f of bin g. Block 0
-// also clears the accumulate's chain_max word (no separate memset in the pipeline).
+// also clears the accumulate's chain_max word (no separate memset in the pipeline). Blocks of
+// 256 or 1024 threads (large bins): the 256 fine counters are scanned by the first 256.
 template <class T>
-__global__ void __launch_bounds__(256) k_sort_fine(const T* __restrict__ tmp, const uint32_t* __restrict__ base,
-                                                  uint32_t nblk, uint32_t bins, uint32_t FB,
-                                                  uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
-                                                  uint32_t* __restrict__ zero_word) {
+__global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, const uint32_t* __restrict__ base,
+                                                   uint32_t nblk, uint32_t bins, uint32_t FB,
+                                                   uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
+                                                   uint32_t* __restrict__ zero_word) {
     __shared__ uint32_t h[256], x[256];
     const uint32_t g = blockIdx.x, F = 1u << FB, t = threadIdx.x;
+    const bool cnt_lane = t < 256;
     if (zero_word != nullptr && g == 0 && t == 0) *zero_word = 0;
     const uint32_t start = base[(size_t)g * nblk];
     const uint32_t end = base[(size_t)(g + 1) * nblk];  // base has bins*nblk + 1 entries
-    h[t] = 0;
+    if (cnt_lane) h[t] = 0;
     __syncthreads();
     for (uint32_t p = start + t; p < end; p += blockDim.x) atomicAdd(&h[sort_fine_of<T>(tmp[p], FB)], 1u);
     __syncthreads();
     // inclusive Hillis-Steele scan over 256 counters
-    uint32_t v = h[t];
-    x[t] = v;
+    const uint32_t v = cnt_lane ? h[t] : 0u;
+    if (cnt_lane) x[t] = v;
     __syncthreads();
     for (uint32_t o = 1; o < 256; o <<= 1) {
-        uint32_t a = t >= o ? x[t - o] : 0u;
+        const uint32_t a = (cnt_lane && t >= o) ? x[t - o] : 0u;
         __syncthreads();
-        x[t] += a;
+        if (cnt_lane) x[t] += a;
         __syncthreads();
     }
-    const uint32_t excl = x[t] - v;
+    const uint32_t excl = cnt_lane ? x[t] - v : 0u;
     if (t < F) offsets[(size_t)g * F + t] = start + excl;
     if (g == bins - 1 && t == 0) offsets[(size_t)bins * F] = end;
     __syncthreads();
-    h[t] = excl;  // cursors
+    if (cnt_lane) h[t] = excl;  // cursors
     __syncthreads();
     for (uint32_t p = start + t; p < end; p += blockDim.x) {
         const T e = tmp[p];
@@ -642,15 +644,19 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
         VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(L.ws[WS_SCAN_TMP].p, tmp_bytes, counts, base, ncnt, st));
         if (ctx->timing) ctx->timer_end("msm_scan", ev, st);
     }
+    // fine-pass block: 1024 threads once bins average >= 2^15 entries (one block per bin)
+    static const int fine_env = getenv("VKZG_SORT_FINE_BLOCK") ? atoi(getenv("VKZG_SORT_FINE_BLOCK")) : 0;  // probe
+    const uint64_t total = stride ? (uint64_t)(we - wb) * stride : (uint64_t)nv * (uint32_t)(we - wb);
+    const int fblk = fine_env == 256 || fine_env == 1024 ? fine_env : (total / bins >= (1u << 15) ? 1024 : 256);
     if (narrow) {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, 256, lds, src, nv, c, wb, we, FB,
                      NBC, nblk, stride, base, static_cast<uint32_t*>(tmp));
-        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, 256, 0, static_cast<const uint32_t*>(tmp),
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, 0, static_cast<const uint32_t*>(tmp),
                      base, nblk, bins, FB, offsets, sorted, zero_word);
     } else {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, 256, lds, src, nv, c, wb, we, FB,
                      NBC, nblk, stride, base, static_cast<uint64_t*>(tmp));
-        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, 256, 0, static_cast<const uint64_t*>(tmp),
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, fblk, 0, static_cast<const uint64_t*>(tmp),
                      base, nblk, bins, FB, offsets, sorted, zero_word);
     }
     return VC_OK;
@@ -757,9 +763,13 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
     uint32_t lgNB = (uint32_t)c - 1;
     uint32_t FB = lgNB < 8 ? lgNB : 8;
-    // shared windows: ~16K entries per coarse bin (one k_sort_fine block each), as per window
-    static const int bin_lg = getenv("VKZG_SORT_BIN_LG") ? atoi(getenv("VKZG_SORT_BIN_LG")) : 14;  // tuning probe
+    // shared windows: ~64K entries per coarse bin (one 1024-thread k_sort_fine block each) but at
+    // least 256 bins (a fine block per CU). Measured at 2^21 x 8 entries (hist + coarse + fine):
+    // 0.233 ms at 2^14 entries per bin (256-thread fine blocks), 0.222 at 2^15, 0.204 at 2^16,
+    // 0.295 at 2^17 -- bigger bins shorten the scatter's partial-line writes
+    static const int bin_lg = getenv("VKZG_SORT_BIN_LG") ? atoi(getenv("VKZG_SORT_BIN_LG")) : 16;  // tuning probe
     while (sl.shared && FB > 1 && (load >> bin_lg) > (size_t)(NB >> FB)) FB--;
+    while (sl.shared && FB > 1 && (NB >> FB) < 256) FB--;
     const uint32_t NBC = NB >> FB;
     const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
     const size_t ncnt = (size_t)Wr * NBC * nblk + 1;
