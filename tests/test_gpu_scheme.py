@@ -181,6 +181,39 @@ def test_kzg_256_golden(eng):
         assert pr["proof"] == P(op["proof"]) and hex(pr["y"]) == op["y"]
 
 
+def test_scratch_pool_reuse_and_stream_switch():
+    """Per-call scratch comes from the context's stream-ordered pool (ctx.hpp DevBuf(ctx)):
+    repeated KZG opens of different sizes, interleaved IPA proofs, and a switch to another
+    stream (vc_ctx_set_stream drains the old one) must reproduce the golden openings exactly."""
+    import torch
+    import vkzg
+    from vkzg import scheme
+    g = load("kzg_256.json")
+    e = vkzg.Engine("bn254")
+    try:
+        kz = scheme.KZG(e, 256, secret=100)
+        small = scheme.KZG(e, 16)
+        data = scheme.LagrangeBasis([H(x) for x in g["evals"]], 256)
+        com = kz.commit(data)
+        ops = [op for op in g["openings"] if "error" not in op]
+        want = [(P(op["proof"]), H(op["y"])) for op in ops]
+        rng = random.Random(5)
+        d16 = scheme.LagrangeBasis([rng.randrange(scheme.R_BN254) for _ in range(8)], 16)
+        c16 = small.commit(d16)
+        first16 = small.prove(c16, 3, d16)
+        for rep in range(3):
+            if rep == 2:  # another stream: pooled blocks freed on the old one must not race
+                side = torch.cuda.Stream()
+                e.set_stream(side.cuda_stream)
+            for op, (pw, yw) in zip(ops, want):
+                pr = kz.prove(com, op["point"], data)
+                assert pr["proof"] == pw and pr["y"] == yw, (rep, op["point"])
+                assert small.prove(c16, 3, d16) == first16
+        e.set_stream(None)
+    finally:
+        e.close()
+
+
 def test_reference_kzg_test_restated(eng):
     """kzg/mod.rs:278-297: CRS 16, data 8; every index proves (trapdoor check), y = 0 on 8..16, 17 out."""
     from pyoracle import protocol
