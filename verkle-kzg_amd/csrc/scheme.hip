@@ -149,9 +149,25 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     while ((1ull << K) < N) K++;
     Fr omega = bn254_group_gen(N);
     std::vector<IpaState> st(B);
-    for (size_t p = 0; p < B; p++) {
+    for (size_t p = 0; p < B; p++)
         if (proofs[p].rounds < K || !proofs[p].l_xy || !proofs[p].r_xy || !proofs[p].l_inf || !proofs[p].r_inf)
             return VC_E_INVALID;
+    // the per-proof host work (barycentric weights, transcripts, scalar rows, folds: ~600 field
+    // multiplies per proof per round) is independent across proofs: up to 16 host threads
+    const unsigned T = B >= 16 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+    auto par_for = [&](auto fn) {
+        if (T == 1) {
+            for (size_t p = 0; p < B; p++) fn(p);
+            return;
+        }
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < T; k++)
+            th.emplace_back([&, k] {
+                for (size_t p = B * k / T; p < B * (k + 1) / T; p++) fn(p);
+            });
+        for (auto& x : th) x.join();
+    };
+    par_for([&](size_t p) {
         IpaState& s = st[p];
         s.a = data[p];
         s.b = barycentric(N, points[p], omega);
@@ -166,14 +182,14 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
         transcript_append_fr(s.tr, s.eval, "output point");
         s.w = transcript_digest(s.tr, "w");
         s.coeff.assign(N, fe_one<F>());
-    }
+    });
     const size_t W = N + 1;
     std::vector<Fr> sc(2 * B * W);
     std::vector<uint64_t> oxy(2 * B * 8);
     std::vector<uint8_t> oinf(2 * B);
     for (size_t r = 0; r < K; r++) {
         const size_t m = N >> r, half = m / 2;
-        for (size_t p = 0; p < B; p++) {
+        par_for([&](size_t p) {
             IpaState& s = st[p];
             Fr* sL = &sc[(2 * p) * W];
             Fr* sR = &sc[(2 * p + 1) * W];
@@ -190,9 +206,9 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
             // q' * <a_L, b_R> = q * (w <a_L, b_R>)
             sL[N] = fe_mul<F>(s.w, inner(&s.a[0], &s.b[half], half));
             sR[N] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
-        }
+        });
         VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data()));
-        for (size_t p = 0; p < B; p++) {
+        par_for([&](size_t p) {
             IpaState& s = st[p];
             const uint64_t* Lxy = &oxy[(2 * p) * 8];
             const uint64_t* Rxy = &oxy[(2 * p + 1) * 8];
@@ -212,7 +228,7 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
             s.b.resize(half);
             for (size_t i = 0; i < N; i++)
                 if ((i % m) < half) s.coeff[i] = fe_mul<F>(s.coeff[i], x);
-        }
+        });
     }
     for (size_t p = 0; p < B; p++) {
         proofs[p].rounds = K;

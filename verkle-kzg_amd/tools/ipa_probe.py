@@ -11,6 +11,7 @@ import vkzg  # noqa: E402
 from vkzg import scheme  # noqa: E402
 from vkzg._lib import lib  # noqa: E402
 import ctypes  # noqa: E402
+import numpy as np  # noqa: E402
 
 e = vkzg.Engine("bn254", 0)
 e.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -45,3 +46,34 @@ for name, f in (("commit", lambda: ipa.commit(data)), ("prove", lambda: ipa.prov
     print(f"{name}: wall {wall:.3f} ms, timed kernels {tot:.3f} ms")
     for k, ms, c in rows:
         print(f"   {k:16s} {ms:.4f} ms  {c:.1f} launches")
+
+# 256 independent proofs in one call (bench.py ipa_line batch_prove)
+B = 256
+datas = [scheme.LagrangeBasis([(r0 * (k + 1) + i) % scheme.R_BN254 for i in range(N)]) for k in range(B)]
+coms = ipa.commit_batch(datas)
+pts = [(31 * k) % N for k in range(B)]
+ipa.prove_batch_points(coms, pts, datas)
+t0 = time.perf_counter()
+ipa.prove_batch_points(coms, pts, datas)
+wall = (time.perf_counter() - t0) * 1e3
+e.enable_timing(True)
+e.reset_timing()
+ipa.prove_batch_points(coms, pts, datas)
+e.enable_timing(False)
+rows = []
+for k in ("fb_commit", "fb_commit_small", "fb_combine", "fb_normalize_out", "normalize_out", "fb_commit_cm"):
+    ms, cnt = e.kernel_time(k)
+    if cnt:
+        rows.append((k, ms, cnt))
+print(f"batch {B}: wall {wall:.2f} ms, timed kernels {sum(r[1] for r in rows):.3f} ms")
+for k, ms, c in rows:
+    print(f"   {k:16s} {ms:.4f} ms  {c} launches")
+t0 = time.perf_counter()
+ipa.prove_batch_points(coms, pts, datas)
+print(f"batch {B} again: {(time.perf_counter() - t0) * 1e3:.2f} ms")
+t0 = time.perf_counter()
+d = np.concatenate([x.limbs(N)[:N] for x in datas])
+print(f"python limbs of {B} datas: {(time.perf_counter() - t0) * 1e3:.2f} ms")
+t0 = time.perf_counter()
+cxy, cinf = scheme._pt_arrays(coms)
+print(f"python commitment arrays: {(time.perf_counter() - t0) * 1e3:.2f} ms")

@@ -24,15 +24,18 @@ def _ptr(a):
 
 
 def ints_to_limbs(vals, nl=4):
-    out = np.zeros((len(vals), nl), dtype=np.uint64)
-    for i, v in enumerate(vals):
-        v = int(v)
-        for j in range(nl):
-            out[i, j] = (v >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
-    return out
+    """Python ints -> (len, nl) little-endian u64 limbs (values taken mod 2^(64 nl), two's
+    complement for negatives). One to_bytes per value: ~10x faster than per-limb shifts, which
+    dominated the Python side of batched calls (256 x 256 scalars: 20 ms)."""
+    nb = 8 * nl
+    mask = (1 << (64 * nl)) - 1
+    buf = b"".join((int(v) & mask).to_bytes(nb, "little") for v in vals)
+    return np.frombuffer(buf, dtype="<u8").reshape(len(vals), nl).astype(np.uint64)
 
 
 def limbs_to_int(row):
+    if isinstance(row, np.ndarray):
+        return int.from_bytes(np.ascontiguousarray(row, dtype="<u8").tobytes(), "little")
     return sum(int(x) << (64 * j) for j, x in enumerate(row))
 
 
