@@ -41,7 +41,8 @@ CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
 # (tools_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r02", "r01"))
+                    if os.path.exists(p)), os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"))
 
 
 def parse():
@@ -64,7 +65,21 @@ def parse():
     ap.add_argument("--no-ipa", action="store_true", help="skip the single IPA prove/verify line (benches/ipa.rs)")
     ap.add_argument("--verkle-keys", type=int, default=1 << 16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
+    ap.add_argument("--no-variable-base", action="store_true",
+                    help="skip the variable-base (no shared-window copies) MSM sub-line")
+    ap.add_argument("--no-check", action="store_true", help="skip the one-time 2^20 result check")
     return ap.parse_args()
+
+
+def kernel_table(eng):
+    """mean device ms per launch of the MSM pipeline's kernels (HIP events on the launch stream)"""
+    out = {}
+    for k in ("glv_split", "glv_phi", "msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine",
+              "msm_accumulate", "msm_fixup", "msm_segsum", "msm_bitsum", "msm_sumpart"):
+        ms, cnt = eng.kernel_time(k)
+        if cnt:
+            out[k] = round(ms / cnt, 4)
+    return out
 
 
 def cpu_baseline(curve, n_full, sample):
@@ -381,12 +396,72 @@ def main():
 
     # dominant kernel (bucket accumulation) device time, HIP events on the launch stream
     acc_ms, acc_n = eng.kernel_time("msm_accumulate")
-    kernels = {}
-    for k in ("glv_split", "glv_phi", "msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate", "msm_fixup",
-              "msm_segsum", "msm_bitsum", "msm_sumpart"):
-        ms, cnt = eng.kernel_time(k)
-        if cnt:
-            kernels[k] = round(ms / cnt, 4)
+    kernels = kernel_table(eng)
+
+    # one-time result check, outside the timed region: the bases are P_i = s_i G with s_i
+    # re-derived on the host (vkzg.random_base_scalars), so sum k_i P_i = t P_0 with
+    # t = (sum k_i s_i) / s_0 mod r -- a 1-term MSM on the same table (tests/test_gpu_fullsize.py
+    # pins the same identity against the oracle's group law)
+    check = None
+    if not a.no_check:
+        r_mod = vkzg.SCALAR_R[curve]
+        s_all = vkzg.random_base_scalars(curve, 2024, n)
+        t = vkzg.dot_mod(scalars, s_all, r_mod) * pow(vkzg.limbs_to_int(s_all[0]), -1, r_mod) % r_mod
+        want = eng.msm(table, vkzg.ints_to_limbs([t]), offset=0)
+        ok = bool(int(res[1]) == want[1] and np.array_equal(np.asarray(res[0]), want[0]))
+        check = {"ok": ok, "method": "sum k_i P_i == ((sum k_i s_i) / s_0 mod r) P_0, P_i = s_i G (host-derived s_i)"}
+        if not ok:
+            raise SystemExit(f"bench: 2^{a.log_n} MSM result check FAILED: {res} vs {want}")
+
+    # variable-base sub-line: the same MSM without the per-table shifted window copies
+    # (VC_OPT_MSM_SHARED_WINDOWS = 0): plain Pippenger, W bucket sets, no precomputation
+    variable = None
+    if not a.no_variable_base and curve == "bls12_381":
+        eng.set_option(eng.OPT_MSM_SHARED_WINDOWS, 0)
+        for _ in range(max(1, a.warmup)):
+            vres = step()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        eng.reset_timing()
+        eng.enable_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            vres = step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        vdt = time.perf_counter() - t0
+        eng.enable_timing(False)
+        if world > 1:
+            tt = torch.tensor([vdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            vdt = float(tt.item())
+        vacc_ms, vacc_n = eng.kernel_time("msm_accumulate")
+        eng.set_option(eng.OPT_MSM_SHARED_WINDOWS, 1)
+        vsame = bool(int(vres[1]) == int(res[1]) and np.array_equal(np.asarray(vres[0]), np.asarray(res[0])))
+        vk_ms = vacc_ms / vacc_n if vacc_n else None
+        variable = {"ms_per_msm": vdt / a.steps * 1e3, "value": a.steps / vdt, "unit": "2^20-pt MSM/s",
+                    "precomputed_bases": None, "same_result": vsame,
+                    "kernel_ms": kernel_table(eng),
+                    "roofline": {"kernel": "msm_accumulate", "kernel_ms": vk_ms,
+                                 "achieved": (n * BYTES_PER_POINT[curve] + OUT_BYTES[curve]) / world / (vk_ms * 1e-3) / 1e9
+                                 if vk_ms else None, "peak": HBM_PEAK_GBS, "unit": "GB/s"}}
+        if variable["roofline"]["achieved"]:
+            variable["roofline"]["frac"] = variable["roofline"]["achieved"] / HBM_PEAK_GBS
+
+    # host-scalar latency: vc_msm with the scalars in (pageable) host memory -- the entry point
+    # INTEGRATION.md's Rust binding calls; adds the 32 MB H2D copy over PCIe to every MSM
+    host_line = None
+    if world == 1:
+        eng.msm(table, scalars)
+        t0 = time.perf_counter()
+        hreps = 5
+        for _ in range(hreps):
+            eng.msm(table, scalars)
+        hdt = (time.perf_counter() - t0) / hreps
+        host_line = {"ms_per_msm": hdt * 1e3, "h2d_bytes": int(scalars.nbytes),
+                     "note": "vc_msm, scalars in pageable host memory (PCIe copy inside the call); not `value`"}
     acc_s = acc_ms / acc_n * 1e-3 if acc_n else None
     # algorithmic bytes of this rank's share of the MSM (n*(96+32) + 96 per MSM)
     shard_bytes = (n * BYTES_PER_POINT[curve] + OUT_BYTES[curve]) / world
@@ -437,31 +512,34 @@ def main():
         "data": "synthetic (random subgroup bases s_i*G generated on device, uniform scalars < r)",
         "config": {"workload": f"single 2^{a.log_n}-point {curve} G1 Pippenger MSM (configs[1])",
                    "n_points": n, "curve": curve, "parallelism": f"Pippenger-window slices x{world}",
-                   "window_bits": c_bits, "windows": w_total},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "window_bits": c_bits, "windows": w_total,
+                   "precomputed_bases": (f"{w_total} x 2n shifted window copies 2^(c w) P_i, 2^(c w) phi(P_i) "
+                                         f"({w_total * 2 * n * 96 / 1e9:.2f} GB), built once per base table "
+                                         "(a fixed CRS), untimed; `variable_base` is the same MSM without them")
+                   if curve == "bls12_381" else None},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": "msm_accumulate",
                      "kernel_ms": (acc_ms / acc_n) if acc_n else None,
                      "algorithmic_bytes_per_launch": shard_bytes,
                      "valu": valu,
-                     "note": "EC MSM is VALU integer-multiply bound, not HBM bound (SURVEY 8(d)); "
-                             "the valu object is the binding roofline"},
+                     "note": "EC MSM is VALU integer-multiply bound, not HBM bound (SURVEY 8(d)): achieved/peak/"
+                             "frac are the algorithmic-HBM figures BASELINE.json's metric asks for; the "
+                             "valu object is the binding roofline"},
         "kernel_ms": kernels,
         "result_inf": int(res[1]),
+        "result_check": check,
+        "variable_base": variable,
+        "host_scalars": host_line,
     }
 
     if not a.no_secondary:
-        # config 3: batched width-256 commits (fixed-base tables), batch split across ranks
+        # config 3: batched width-256 commits (fixed-base tables), batch split across ranks; timed
+        # on the c = commit_window table (167 GB at c = 20) and on the deployable c = 16 one (12.9 GB)
         ceng = vkzg.Engine("bandersnatch", local)
         ceng.set_stream(stream.cuda_stream)
         ctab = ceng.random_bases(256, seed=3)
-        cw = a.commit_window
-        try:
-            ceng.fixed_base_precompute(ctab, cw)
-        except vkzg.VCError:  # table does not fit next to the rest: the 12.9 GB c = 16 one
-            cw = 16
-            ceng.fixed_base_precompute(ctab, cw)
         B = a.commit_batch
         blo, bhi = vdist.shard_range(B, rank, world)
         Bl = bhi - blo
@@ -476,32 +554,45 @@ def main():
                 return vdist.all_gather_commitments(dxy[:Bl], dinf[:Bl], B, world)
             return dxy, dinf
 
-        for _ in range(2):
-            cstep()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        ceng.enable_timing(True)
-        t0 = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            cstep()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        cdt = (time.perf_counter() - t0) / reps
-        if world > 1:
-            tt = torch.tensor([cdt], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            cdt = float(tt.item())
-        fb_ms, fb_n = ceng.kernel_time("fb_commit")
+        def ctime(cw):
+            try:
+                ceng.fixed_base_precompute(ctab, cw)
+            except vkzg.VCError:  # table does not fit next to the rest
+                return None
+            for _ in range(2):
+                cstep()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            ceng.reset_timing()
+            ceng.enable_timing(True)
+            t0 = time.perf_counter()
+            reps = 5
+            for _ in range(reps):
+                cstep()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            cdt = (time.perf_counter() - t0) / reps
+            ceng.enable_timing(False)
+            if world > 1:
+                tt = torch.tensor([cdt], dtype=torch.float64, device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                cdt = float(tt.item())
+            fb_ms, fb_n = ceng.kernel_time("fb_commit")
+            return {"window_bits": cw, "commits_per_s": B / cdt, "ms_per_batch": cdt * 1e3,
+                    "fb_commit_kernel_ms": fb_ms / fb_n if fb_n else None,
+                    "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
+                    "table_bytes": 256 * ((253 + 1 + cw - 1) // cw) * (1 << (cw - 1)) * 96}
+
+        big = ctime(a.commit_window)
+        small = ctime(16) if a.commit_window != 16 else big
+        head = big or small
         out["secondary"] = {
-            "workload": f"{B} batched width-256 Bandersnatch commits (configs[2]), fixed-base c={cw}, "
+            "workload": f"{B} batched width-256 Bandersnatch commits (configs[2]), fixed-base c={head['window_bits']}, "
                         f"batch split over {world} rank(s)",
-            "commits_per_s": B / cdt, "ms_per_batch": cdt * 1e3,
-            "fb_commit_kernel_ms": fb_ms / fb_n if fb_n else None,
-            "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
-            "table_bytes": 256 * ((253 + 1 + cw - 1) // cw) * (1 << (cw - 1)) * 96,
+            **head,
+            "c16": small,
         }
         ceng.close()
 

@@ -60,6 +60,17 @@ void vc_ctx_destroy(vc_ctx* ctx);
 int vc_ctx_curve(const vc_ctx* ctx);
 /* Launch on an external stream (e.g. torch.cuda.current_stream().cuda_stream); NULL = own. */
 int vc_ctx_set_stream(vc_ctx* ctx, void* hip_stream);
+/* Engine knobs (per context; defaults in brackets). None changes a result, only the path:
+ *   VC_OPT_MSM_SHARED_WINDOWS [1]: a GLV MSM (BLS12-381, n >= 4096) over a WHOLE table sends all
+ *     windows to one bucket set through per-table shifted copies 2^(c w) P_i, 2^(c w) phi(P_i)
+ *     (W x 2n points, 1.6 GB at n = 2^20, built once per table on first use and kept -- a
+ *     fixed-base precomputation over the CRS). 0: plain variable-base Pippenger, no copies.
+ *   VC_OPT_MSM_CHUNK_POINTS [2^27]: MSMs of more points run as summed chunks of this many
+ *     (keeps the u32 entry space of the bucket sort from wrapping). */
+#define VC_OPT_MSM_SHARED_WINDOWS 1
+#define VC_OPT_MSM_CHUNK_POINTS 2
+int vc_ctx_set_option(vc_ctx* ctx, int option, int64_t value);
+int vc_ctx_get_option(vc_ctx* ctx, int option, int64_t* value);
 /* Per-kernel device timing (HIP events around each launch on the ctx stream). */
 int vc_ctx_enable_timing(vc_ctx* ctx, int on);
 /* name: "msm_accumulate", "msm_digits", ... ; returns total ms and launch count */

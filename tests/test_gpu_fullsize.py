@@ -1,0 +1,277 @@
+"""GPU parity at the sizes bench.py measures (BASELINE.json configs[1]-[4]).
+
+The oracle cannot run a 2^20-term naive MSM in test time, so full-size results are pinned by
+properties that are exact for these inputs:
+  configs[1]  2^20-point BLS12-381 MSM over synthetic bases P_i = s_i G (vc_bases_random; the
+              s_i are re-derived on the host and 64 sampled P_i are checked against the oracle's
+              s_i G), so sum k_i P_i = (sum k_i s_i mod r) G exactly -- on the shared-window
+              path the bench times, on the plain variable-base path, and in point chunks;
+  configs[2]  10k x width-256 Bandersnatch commits on the c = 20 fixed-base table (the bench's),
+              16 sampled commits against the C oracle (utils.rs:16-19 restated);
+  configs[3]  KZG commit + open at d = 2^20 on BLS12-381: the trapdoor identity
+              pi (s - z) = C - y G (s = 100, kzg/mod.rs:115-154) in and outside the domain;
+  configs[4]  IPA multiproof over Q = 2^16 width-256 queries: verify_multiproof accepts, D / y
+              tampering rejects (multiproof.rs:178-215), and the 8-shard three-phase prover
+              (8 ranks simulated on one GPU) gives the unsharded proof.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _pt(curve, xy, inf):
+    import vkzg
+    return vkzg.arrays_to_points(curve, np.asarray(xy)[None, :], np.array([inf], dtype=np.uint8))[0]
+
+
+@pytest.fixture(scope="module")
+def bls():
+    import vkzg
+    e = vkzg.Engine("bls12_381")
+    yield e
+    e.close()
+
+
+def _check_synthetic_bases(e, curve, tid, seed, n, samples=64):
+    """P_i = s_i G for sampled i (oracle group law) -- pins the host mirror of the seed derivation."""
+    import vkzg
+    from pyoracle.curves import CURVES
+    C = CURVES[curve]
+    s = vkzg.random_base_scalars(curve, seed, n)
+    xy, inf = e.download_bases(tid)
+    idx = np.random.default_rng(seed).choice(n, size=min(samples, n), replace=False)
+    for i in list(idx) + [0, n - 1]:
+        assert not inf[i]
+        assert _pt(curve, xy[i], 0) == C.mul(C.g, vkzg.limbs_to_int(s[i])), i
+    return s
+
+
+@pytest.mark.parametrize("path", ["shared_windows", "variable_base", "chunked"])
+def test_msm_2e20_bls12_381(bls, path):
+    """configs[1] at full size: the bench's inputs (seeds 2024 / 1234) and geometry (GLV, c = 16,
+    8 windows; shared windows = one 2^15-bucket set, narrow sort entries, 1024-thread fine sort)."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    n = 1 << 20
+    e = bls
+    tid = e.random_bases(n, seed=2024)
+    s = _check_synthetic_bases(e, "bls12_381", tid, 2024, n, samples=16)
+    k = vkzg.random_scalars("bls12_381", n, np.random.default_rng(1234))
+    want = C.mul(C.g, vkzg.dot_mod(k, s, C.r))
+    d_k = torch.from_numpy(k.view(np.int64).copy()).cuda()
+    e.set_option(e.OPT_MSM_SHARED_WINDOWS, 0 if path == "variable_base" else 1)
+    e.set_option(e.OPT_MSM_CHUNK_POINTS, 300_000 if path == "chunked" else 1 << 27)
+    try:
+        got = e.msm_device(tid, d_k.data_ptr(), n)
+        assert _pt("bls12_381", *got) == want
+        # twice: the second call reuses the shared-window copies and the workspaces
+        got = e.msm_device(tid, d_k.data_ptr(), n)
+        assert _pt("bls12_381", *got) == want
+        # host-scalar entry point (the one INTEGRATION.md's binding calls)
+        got = e.msm(tid, k)
+        assert _pt("bls12_381", *got) == want
+    finally:
+        e.set_option(e.OPT_MSM_SHARED_WINDOWS, 1)
+        e.set_option(e.OPT_MSM_CHUNK_POINTS, 1 << 27)
+
+
+def test_msm_2e20_window_parts_sum(bls):
+    """the 8-rank window split of the bench (vc_msm_device_window_part) at 2^20 adds up to the
+    same linearity-pinned point."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    n = 1 << 20
+    e = bls
+    tid = e.random_bases(n, seed=2024)
+    s = vkzg.random_base_scalars("bls12_381", 2024, n)
+    k = vkzg.random_scalars("bls12_381", n, np.random.default_rng(99))
+    want = C.mul(C.g, vkzg.dot_mod(k, s, C.r))
+    d_k = torch.from_numpy(k.view(np.int64).copy()).cuda()
+    for parts in (2, 8):
+        accs = np.stack([e.msm_device_window_part(tid, d_k.data_ptr(), n, p, parts) for p in range(parts)])
+        assert _pt("bls12_381", *e.partials_sum(accs)) == want
+
+
+@pytest.mark.parametrize("curve", ["bn254", "bandersnatch"])
+def test_msm_2e20_other_curves(curve):
+    """2^20 without GLV (BN254: c = 16, 17 windows; Bandersnatch: Edwards adds), by linearity."""
+    import torch
+    import vkzg
+    from pyoracle.curves import CURVES
+    C = CURVES[curve]
+    n = 1 << 20
+    e = vkzg.Engine(curve)
+    try:
+        tid = e.random_bases(n, seed=11)
+        s = _check_synthetic_bases(e, curve, tid, 11, n, samples=8)
+        k = vkzg.random_scalars(curve, n, np.random.default_rng(12))
+        d_k = torch.from_numpy(k.view(np.int64).copy()).cuda()
+        got = e.msm_device(tid, d_k.data_ptr(), n)
+        assert _pt(curve, *got) == C.mul(C.g, vkzg.dot_mod(k, s, C.r))
+    finally:
+        e.close()
+
+
+def test_msm_chunk_option_small(oracle_c):
+    """chunked MSMs (VC_OPT_MSM_CHUNK_POINTS) equal the oracle at sizes it runs directly."""
+    import vkzg
+    e = vkzg.Engine("bn254")
+    try:
+        n = 5000
+        tid = e.random_bases(n, seed=3)
+        xy, inf = e.download_bases(tid)
+        k = vkzg.random_scalars("bn254", n, np.random.default_rng(4))
+        want = oracle_c.msm_arrays("bn254", xy, inf, k, 16)
+        for chunk in (1, 7, 1000, 4999, 5000):
+            e.set_option(e.OPT_MSM_CHUNK_POINTS, chunk)
+            assert e.get_option(e.OPT_MSM_CHUNK_POINTS) == chunk
+            got = e.msm(tid, k)
+            assert got[1] == want[1] and np.array_equal(got[0], want[0]), chunk
+        with pytest.raises(vkzg.VCError):
+            e.set_option(e.OPT_MSM_CHUNK_POINTS, 0)
+    finally:
+        e.close()
+
+
+def test_commit_10k_width256_c20(oracle_c):
+    """configs[2]: 10,000 width-256 Bandersnatch commits on the bench's c = 20 table (167 GB;
+    c = 16 if it does not fit next to the rest), 16 sampled commits against the oracle."""
+    import torch
+    import vkzg
+    e = vkzg.Engine("bandersnatch")
+    try:
+        tab = e.random_bases(256, seed=3)
+        xy, inf = e.download_bases(tab)
+        try:
+            e.fixed_base_precompute(tab, 20)
+        except vkzg.VCError:
+            e.fixed_base_precompute(tab, 16)
+        B = 10_000
+        sc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(5))
+        d_sc = torch.from_numpy(sc.view(np.int64).copy()).cuda()
+        d_xy = torch.zeros((B, 8), dtype=torch.int64, device="cuda")
+        d_inf = torch.zeros(B, dtype=torch.uint8, device="cuda")
+        e.msm_batch_device(tab, 256, d_sc.data_ptr(), B, d_xy.data_ptr(), d_inf.data_ptr())
+        got_xy = d_xy.cpu().numpy().view(np.uint64)
+        got_inf = d_inf.cpu().numpy()
+        for j in list(np.random.default_rng(6).choice(B, 14, replace=False)) + [0, B - 1]:
+            want = oracle_c.msm_arrays("bandersnatch", xy, inf, sc[j * 256:(j + 1) * 256], 1)
+            assert got_inf[j] == want[1] and np.array_equal(got_xy[j], want[0]), j
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("where", ["in_domain", "outside"])
+def test_kzg_commit_open_2e20_trapdoor(where):
+    """configs[3]: commit + open at d = 2^20 on BLS12-381 (the bench's workload), checked by the
+    trapdoor identity pi (100 - z) = C - y G with the oracle's group law; in-domain y = f_m."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    from vkzg._lib import check, lib
+    d = 1 << 20
+    e = vkzg.Engine("bls12_381")
+    try:
+        secret = vkzg.ints_to_limbs([100])[0].copy()
+        tid, size = ctypes.c_int(), ctypes.c_size_t()
+        check(lib().vc_kzg_setup(e.h, d, ctypes.c_void_p(secret.ctypes.data), ctypes.byref(tid),
+                                 ctypes.byref(size)), "vc_kzg_setup")
+        tid = tid.value
+        assert size.value == d
+        ev = vkzg.random_scalars("bls12_381", d, np.random.default_rng(44))
+        d_ev = torch.from_numpy(ev.view(np.int64).copy()).cuda()
+        com = _pt("bls12_381", *e.msm_device(tid, d_ev.data_ptr(), d))
+        if where == "in_domain":
+            m = d // 3
+            point_int = m
+            zval = pow(pow(7, (C.r - 1) // d, C.r), m, C.r)
+        else:
+            point_int = d + 987654321
+            zval = point_int
+        pt = vkzg.ints_to_limbs([point_int])[0].copy()
+        pxy = np.zeros(12, dtype=np.uint64)
+        pinf = np.zeros(1, dtype=np.uint8)
+        y = np.zeros(4, dtype=np.uint64)
+        P = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+        check(lib().vc_kzg_prove_device(e.h, tid, d, ctypes.c_void_p(d_ev.data_ptr()), d, P(pt), P(pxy), P(pinf),
+                                        P(y)), "vc_kzg_prove_device")
+        yv = vkzg.limbs_to_int(y)
+        if where == "in_domain":
+            assert yv == vkzg.limbs_to_int(ev[m])
+        proof = _pt("bls12_381", pxy, pinf[0])
+        assert C.mul(proof, (100 - zval) % C.r) == C.add(com, C.neg(C.mul(C.g, yv)))
+    finally:
+        e.close()
+
+
+def _mp_inputs(eng, ipa, Q, N=256, seed=77):
+    """The bench's multiproof inputs: data < 2^252, commitments (batched commits), z, y = f(z)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 1 << 63, size=(Q * N, 4), dtype=np.uint64)
+    data[:, 3] &= np.uint64((1 << 60) - 1)
+    z = rng.integers(0, N, size=Q, dtype=np.uint64)
+    y = data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)].copy()
+    d_all = torch.from_numpy(data.view(np.int64)).cuda()
+    cxy_d = torch.zeros((Q, 8), dtype=torch.int64, device="cuda")
+    cinf_d = torch.zeros(Q, dtype=torch.uint8, device="cuda")
+    eng.msm_batch_device(ipa.table, N, d_all.data_ptr(), Q, cxy_d.data_ptr(), cinf_d.data_ptr())
+    torch.cuda.synchronize()
+    return data, d_all, cxy_d.cpu().numpy().view(np.uint64).copy(), cinf_d.cpu().numpy().copy(), z, y
+
+
+def test_multiproof_2e16_verify_tamper_and_shards():
+    """configs[4] at Q = 2^16: prove, verify (accept), tamper D and one y (reject), and the
+    three-phase prover over 8 query shards == the unsharded proof."""
+    import torch
+    import vkzg
+    from vkzg import dist as vdist
+    from vkzg import scheme
+    from vkzg._lib import check, lib
+    N, Q = 256, 1 << 16
+    eng = vkzg.Engine("bn254")
+    try:
+        ipa = scheme.IPA(eng, N, scheme.ipa_crs(N + 1, max_=512))
+        data, d_all, cxy, cinf, z, y = _mp_inputs(eng, ipa, Q)
+        P = scheme._p
+        dxy = np.zeros(8, dtype=np.uint64)
+        dinf = np.zeros(1, dtype=np.uint8)
+        b, arrs = scheme.IPAProof._alloc(8)
+        check(lib().vc_multiproof_prove(eng.h, 0, ipa.table, N, Q, P(data), P(cxy), P(cinf), P(z), P(y), P(dxy),
+                                        P(dinf), ctypes.byref(b), None, None, None), "vc_multiproof_prove")
+        proof = scheme.IPAProof._from(b, arrs)
+
+        def verify(dxy_, y_):
+            bb, _ = proof._to()
+            res = ctypes.c_int(-1)
+            check(lib().vc_multiproof_verify_ipa(eng.h, ipa.table, N, Q, P(cxy), P(cinf), P(z), P(y_), P(dxy_),
+                                                 int(dinf[0]), ctypes.byref(bb), ctypes.byref(res)), "verify")
+            return res.value
+
+        assert verify(dxy, y) == 1
+        bad_y = y.copy()
+        bad_y[Q // 2, 0] ^= np.uint64(1)
+        assert verify(dxy, bad_y) == 0
+        from pyoracle.curves import BN254
+        D = _pt("bn254", dxy, dinf[0])
+        bad_d, _ = vkzg.points_to_arrays("bn254", [BN254.add(D, BN254.g)])
+        assert verify(bad_d[0], y) == 0
+        # 8 shards, accumulated separately as 8 ranks would, then one finish over the summed S
+        G = 8
+        tr, r, rows = scheme.multiproof_begin(N, cxy, cinf, z, y)
+        parts = torch.zeros((G, rows, N, 4), dtype=torch.int64, device="cuda")
+        for k in range(G):
+            lo, hi = vdist.shard_range(Q, k, G)
+            scheme.multiproof_accumulate(eng, N, z, lo, hi - lo, d_all[lo * N:].data_ptr(), r, parts[k].data_ptr())
+        torch.cuda.synchronize()
+        mp = scheme.multiproof_finish_ipa(ipa, z, parts.data_ptr(), G, tr)
+        assert mp["d"] == D
+        assert mp["proof"].l == proof.l and mp["proof"].r == proof.r
+        assert mp["proof"].tip == proof.tip and mp["proof"].y == proof.y
+    finally:
+        eng.close()

@@ -294,3 +294,62 @@ def test_multiproof_sharded_phases_golden(eng, crs, G):
     pr = mp["proof"]
     assert pr.l == [P(x) for x in want["l"]] and pr.r == [P(x) for x in want["r"]]
     assert pr.tip == H(want["tip"]) and pr.y == H(want["y"])
+
+
+def test_ipa_point_on_domain_element_is_domain_error(eng, crs):
+    """compute_barycentric_coefficients divides by (point - w^i) (precompute.rs:85): at a domain
+    element w^i that is not below N as an integer the reference panics; the engine returns
+    VC_E_DOMAIN for both prove and verify instead of all-zero weights (which would let verify
+    accept y = 0 for any commitment)."""
+    import vkzg
+    from vkzg import scheme
+    N = 32
+    ipa = scheme.IPA(eng, N, crs[:N + 1])
+    r = scheme.R_BN254
+    omega = pow(5, (r - 1) // N, r)
+    data = scheme.LagrangeBasis(list(range(N)))
+    com = ipa.commit(data)
+    for i in (1, 3, 31):
+        pt = pow(omega, i, r)
+        assert pt >= N
+        with pytest.raises(vkzg.VCError) as ex:
+            ipa.prove_point(com, pt, data)
+        assert ex.value.status == -8
+        good = ipa.prove_point(com, 1000, data)
+        with pytest.raises(vkzg.VCError) as ex:
+            ipa.verify_point(com, pt, scheme.IPAProof(good.l, good.r, good.tip, 0))
+        assert ex.value.status == -8
+    # omega^0 = 1 < N is the one-hot branch (precompute.rs:75-79), not an error
+    pr = ipa.prove_point(com, 1, data)
+    assert pr.y == 1 and ipa.verify_point(com, 1, pr)
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_kzg_multiproof_sharded_golden(eng, G):
+    """the three-phase prover with the KZG finish (vc_multiproof_finish scheme 1) over G query
+    shards == the golden KZG multiproof (multiproof.rs:99-176 over KZG, :310-357)."""
+    import numpy as np
+    import torch
+    from vkzg import dist as vdist
+    from vkzg import scheme
+    g = load("multiproof_32.json")["kzg"]
+    vc = scheme.KZG(eng, 32)
+    queries = []
+    for q in g["queries"]:
+        d = scheme.LagrangeBasis([H(x) for x in q["data"]])
+        queries.append((d, vc.commit(d), q["z"], H(q["y"])))
+    Q, data, cxy, cinf, z, y = scheme._queries(queries, 32)
+    d_data = torch.from_numpy(data.view(np.int64).copy()).cuda()
+    if G == 1:
+        mp = vdist.multiproof_prove_sharded(vc, cxy, cinf, z, y, d_data.data_ptr(), 0, 1)
+    else:
+        tr, r, rows = scheme.multiproof_begin(32, cxy, cinf, z, y)
+        parts = torch.zeros((G, rows, 32, 4), dtype=torch.int64, device="cuda")
+        for k in range(G):
+            lo, hi = vdist.shard_range(Q, k, G)
+            scheme.multiproof_accumulate(eng, 32, z, lo, hi - lo, d_data[lo * 32:].data_ptr(), r,
+                                         parts[k].data_ptr())
+        torch.cuda.synchronize()
+        mp = scheme.multiproof_finish(vc, z, parts.data_ptr(), G, tr)
+    assert mp["d"] == P(g["d"])
+    assert mp["proof"]["proof"] == P(g["proof"]["proof"]) and mp["proof"]["y"] == H(g["proof"]["y"])

@@ -244,6 +244,31 @@ int vc_ctx_set_stream(vc_ctx* ctx, void* s) {
     return VC_OK;
 }
 
+int vc_ctx_set_option(vc_ctx* ctx, int option, int64_t value) {
+    if (!ctx) return VC_E_INVALID;
+    Guard g(ctx);
+    switch (option) {
+        case VC_OPT_MSM_SHARED_WINDOWS:
+            ctx->opt_shared_windows = value != 0;
+            return VC_OK;
+        case VC_OPT_MSM_CHUNK_POINTS:
+            if (value < 1 || value > (int64_t(1) << 27)) return VC_E_INVALID;
+            ctx->opt_msm_chunk = (size_t)value;
+            return VC_OK;
+    }
+    return VC_E_INVALID;
+}
+
+int vc_ctx_get_option(vc_ctx* ctx, int option, int64_t* value) {
+    if (!ctx || !value) return VC_E_INVALID;
+    Guard g(ctx);
+    switch (option) {
+        case VC_OPT_MSM_SHARED_WINDOWS: *value = ctx->opt_shared_windows; return VC_OK;
+        case VC_OPT_MSM_CHUNK_POINTS: *value = (int64_t)ctx->opt_msm_chunk; return VC_OK;
+    }
+    return VC_E_INVALID;
+}
+
 int vc_ctx_enable_timing(vc_ctx* ctx, int on) {
     if (!ctx) return VC_E_INVALID;
     Guard g(ctx);

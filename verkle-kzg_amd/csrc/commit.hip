@@ -272,16 +272,16 @@ __global__ void __launch_bounds__(64) k_fb_combine_wave(const typename Fast29<C>
 constexpr int FB_WPT = 1;
 static int fb_wpt() { return FB_WPT; }
 
-template <class C>
-__device__ __forceinline__ typename C::Acc fb_wave_sum(typename C::Acc v) {
-    for (int m = 1; m < 64; m <<= 1) {
-        typename C::Acc o;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
-#pragma unroll
-        for (int k = 0; k < C::ACC_WORDS; k++) dst[k] = __shfl_xor(src[k], m, 64);
-        v = C::add(v, o);
-    }
+// xor butterfly over the wave on the radix-29 accumulators (the add the tails run too). The
+// shuffle moves sizeof(Acc) / 4 words (shfl_xor_pod): SW29::Acc is 4 L limbs of 29 bits plus the
+// `inf` flag -- 37 words at BN254 (L = 9), 57 at BLS12-381 -- not the 4 N words of the ec.hpp
+// accumulator (C::ACC_WORDS = 32 / 48). An earlier version shuffled C::ACC_WORDS words of the
+// radix-29 accumulator, which left zz / zzz partly and `inf` entirely lane-local: every commit
+// with more than one non-identity lane came out wrong (batched-commit parity failed at the first
+// non-zero commit on the GPU while the host tests of the add formulas passed).
+template <class FC>
+__device__ __forceinline__ typename FC::Acc fb_wave_sum29(typename FC::Acc v) {
+    for (uint32_t m = 1; m < 64; m <<= 1) v = FC::add(v, shfl_xor_pod(v, m));
     return v;
 }
 
@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
                 fa = FC::madd(fa, FC::load(&ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].a), d < 0);
         }
     }
-    Acc acc = fb_wave_sum<C>(FC::store(fa));
+    Acc acc = FC::store(fb_wave_sum29<FC>(fa));
     const int wave = threadIdx.x / 64;
     if ((threadIdx.x & 63) == 0) wsum[wave] = acc;
     __syncthreads();
@@ -394,10 +394,10 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
     if (batch == 0) return VC_OK;
     VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
-    static uint32_t lanes_cache = 0;
-    if (!lanes_cache) lanes_cache = resident_lanes(k_fb_commit_cm<C, Fr>, 256);
+    // resident lanes of this context's device (cached per ctx: the Guard's mutex serialises it)
+    if (!ctx->fb_lanes) ctx->fb_lanes = resident_lanes(k_fb_commit_cm<C, Fr>, 256);
     const size_t items = batch * width;
-    const size_t lanes = lanes_cache ? lanes_cache : 131072;
+    const size_t lanes = ctx->fb_lanes ? ctx->fb_lanes : 131072;
     const int W = t->fb_W;
     const int wpt = fb_wpt();
     const size_t WG = (size_t)(W + wpt - 1) / wpt;

@@ -165,6 +165,10 @@ struct vc_ctx {
     std::multimap<size_t, void*> pool_free;
     size_t pool_bytes = 0;
     bool timing = false;
+    // vc_ctx_set_option knobs (include/vc_msm.h VC_OPT_*)
+    int opt_shared_windows = 1;           // GLV MSMs over a whole table: one bucket set via Table::win
+    size_t opt_msm_chunk = size_t(1) << 27;  // MSMs above this many points run as summed chunks
+    uint32_t fb_lanes = 0;                // resident lanes of k_fb_commit_cm (cached per context)
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, long>> ktime;

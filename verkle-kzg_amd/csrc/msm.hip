@@ -912,7 +912,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     int top_shift = 0;
     int c = glv ? glv_window(nv) : choose_window(nv);
     if constexpr (std::is_same<C, BLS381G1>::value) {
-        static const bool shared_env = !(getenv("VKZG_MSM_SHARED") && atoi(getenv("VKZG_MSM_SHARED")) == 0);
+        const bool shared_env = ctx->opt_shared_windows != 0;  // vc_ctx_set_option(VC_OPT_MSM_SHARED_WINDOWS)
         const int cs = glv_window_shared(nv);
         const int Ws = (GLV_BITS + cs - 1) / cs;
         // top window: GLV_BITS - cs (Ws - 1) bits -> digits up to 2^tb; scaled to fill 2^(cs-1)
@@ -938,6 +938,9 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     // the slices' results add up to the whole MSM)
     const int wb = part * Wfull / parts, we = (part + 1) * Wfull / parts;
     const int W = we - wb;
+    // entry counts, offsets, scan counts and sorted positions are u32: nv * W must fit (msm_run
+    // cuts larger MSMs into chunks of ctx->opt_msm_chunk points, so this only guards misuse)
+    if ((uint64_t)nv * (uint64_t)Wfull >= 0xffffffffull) return VC_E_RANGE;
     if (W == 0) {
         Acc z = C::zero();
         memcpy(out_acc, &z, sizeof(Acc));
@@ -1235,15 +1238,37 @@ int msm_windows(int curve, size_t n, int* c, int* W, int* terms) {
     return VC_OK;
 }
 
+// MSMs of more than ctx->opt_msm_chunk points (default 2^27: nv * W then stays below 2^31 on
+// every curve, so the u32 entry space of the sort cannot wrap) run as consecutive point chunks
+// whose accumulators are added on the host; each chunk is an ordinary partial-table MSM.
+template <class C, class Fr>
+static int msm_run_chunked(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* sc, size_t n, int mont,
+                           int part, int parts, uint32_t* out_acc) {
+    using Acc = typename C::Acc;
+    const size_t chunk = std::max<size_t>(ctx->opt_msm_chunk, 1);
+    if (n <= chunk) return msm_run_t<C, Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
+    Acc res = C::zero();
+    for (size_t lo = 0; lo < n; lo += chunk) {
+        const size_t m = std::min(chunk, n - lo);
+        Acc r;
+        VK_TRY((msm_run_t<C, Fr>(ctx, t, offset + lo, sc + 8 * lo, m, mont, part, parts,
+                                 reinterpret_cast<uint32_t*>(&r))));
+        res = C::add(res, r);
+    }
+    memcpy(out_acc, &res, sizeof(Acc));
+    return VC_OK;
+}
+
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
             uint32_t* out_acc, int part, int parts) {
     const uint32_t* sc = reinterpret_cast<const uint32_t*>(d_scalars);
     switch (t->curve) {
-        case VC_CURVE_BN254: return msm_run_t<BN254G1, BN254Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
+        case VC_CURVE_BN254:
+            return msm_run_chunked<BN254G1, BN254Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
         case VC_CURVE_BLS12_381:
-            return msm_run_t<BLS381G1, BLS381Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
+            return msm_run_chunked<BLS381G1, BLS381Fr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
         case VC_CURVE_BANDERSNATCH:
-            return msm_run_t<Bandersnatch, BandFr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
+            return msm_run_chunked<Bandersnatch, BandFr>(ctx, t, offset, sc, n, mont, part, parts, out_acc);
     }
     return VC_E_INVALID;
 }

@@ -89,6 +89,21 @@ static std::vector<Fr> barycentric(size_t size, const Fr& point, const Fr& omega
     return res;
 }
 
+// compute_barycentric_coefficients divides by (point - w^i) for every i (precompute.rs:85,
+// ark-ff Div = inverse().unwrap()): a point that is a domain element w^i but not below `size`
+// as an integer (the one-hot branch, :75-79) makes the reference panic. host_batch_inv maps 1/0
+// to 0, which would give all-zero weights and let verify accept y = 0 for any commitment, so
+// the callers map this case to VC_E_DOMAIN instead (as the KZG B.4 panic).
+static bool barycentric_panics(size_t size, const Fr& point) {
+    Fr pc = fe_from_mont<F>(point);
+    bool small = true;
+    for (int i = 2; i < 8; i++) small &= pc.v[i] == 0;
+    uint64_t pv = (uint64_t)pc.v[0] | ((uint64_t)pc.v[1] << 32);
+    if (small && pv < size) return false;
+    // point^size == 1  <=>  point is one of the size-th roots of unity w^i
+    return fe_eq<F>(fe_pow_u64<F>(point, size), fe_one<F>());
+}
+
 static Fr inner(const Fr* a, const Fr* b, size_t n) {
     Fr s = fe_zero<F>();
     for (size_t i = 0; i < n; i++) s = fe_add<F>(s, fe_mul<F>(a[i], b[i]));
@@ -149,9 +164,11 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     while ((1ull << K) < N) K++;
     Fr omega = bn254_group_gen(N);
     std::vector<IpaState> st(B);
-    for (size_t p = 0; p < B; p++)
+    for (size_t p = 0; p < B; p++) {
         if (proofs[p].rounds < K || !proofs[p].l_xy || !proofs[p].r_xy || !proofs[p].l_inf || !proofs[p].r_inf)
             return VC_E_INVALID;
+        if (barycentric_panics(N, points[p])) return VC_E_DOMAIN;
+    }
     // the per-proof host work (barycentric weights, transcripts, scalar rows, folds: ~600 field
     // multiplies per proof per round) is independent across proofs: up to 16 host threads
     const unsigned T = B >= 16 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
@@ -246,6 +263,7 @@ int ipa_verify_impl(vc_ctx* ctx, Table* t, size_t N, const Acc& com, const Fr& p
     size_t K = pr->rounds;
     if ((1ull << K) != N) return VC_E_INVALID;  // gens = g[0..2^rounds], zip with points_coeffs
     Fr omega = bn254_group_gen(N);
+    if (barycentric_panics(N, point)) return VC_E_DOMAIN;
     std::vector<Fr> b = barycentric(N, point, omega);
     bool own = tr_in == nullptr;
     vc_transcript* tr = own ? vc_transcript_new("ipa") : tr_in;
@@ -884,8 +902,9 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
                          size_t first, const std::vector<uint32_t>& zval, void* d_S) {
     hipStream_t st = ctx->stream;
     const size_t Z = zval.size();
-    if (Qs == 0) {
+    if (Qs == 0) {  // an empty shard contributes zero sums (synchronous like every ABI call)
         VK_CHECK_HIP(hipMemsetAsync(d_S, 0, Z * N * 32, st));
+        VK_CHECK_HIP(hipStreamSynchronize(st));
         return VC_OK;
     }
     // row of each query: binary search in zval

@@ -23,6 +23,8 @@ SIGNATURES = {
     "vc_ctx_destroy": (None, [c_void_p]),
     "vc_ctx_curve": (c_int, [c_void_p]),
     "vc_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
+    "vc_ctx_set_option": (c_int, [c_void_p, c_int, ctypes.c_int64]),
+    "vc_ctx_get_option": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_int64)]),
     "vc_ctx_enable_timing": (c_int, [c_void_p, c_int]),
     "vc_ctx_kernel_time": (c_int, [c_void_p, c_char_p, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
     "vc_ctx_reset_timing": (c_int, [c_void_p]),

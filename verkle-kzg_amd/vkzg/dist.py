@@ -138,32 +138,35 @@ def kzg_open_sharded(engine, table, size, d_evals_ptr, max_items, point, rank, w
     return xy, inf, y
 
 
-def multiproof_prove_sharded(ipa, cxy, cinf, z, y, d_data_ptr, rank, world, device=None):
-    """IPA multiproof (multiproof.rs:99-176) over ranks: every rank runs the
-    host transcript over all queries (challenge r), accumulates the per-point sums S of its
-    query slice [lo, hi) = shard_range(Q) (d_data_ptr: that slice's evaluations, Qs x N
-    canonical u64x4 on this rank's device), the S matrices (rows x N x 32 B, <= 2 MiB at
-    N = 256) are all-gathered over RCCL -- the one exchange -- and every rank finishes
-    (quotients, D, E, inner proof) on the summed S."""
+def multiproof_prove_sharded(vc, cxy, cinf, z, y, d_data_ptr, rank, world, device=None):
+    """Multiproof (multiproof.rs:99-176) over ranks, IPA or KZG (`vc` is a
+    scheme.IPA or scheme.KZG): every rank runs the host transcript over all queries (challenge
+    r), accumulates the per-point sums S of its query slice [lo, hi) = shard_range(Q)
+    (d_data_ptr: that slice's evaluations, Qs x N canonical u64x4 on this rank's device), the S
+    matrices (rows x N x 32 B, <= 2 MiB at N = 256) are all-gathered over RCCL -- the one
+    exchange -- and every rank finishes (quotients, D, E, inner proof) on the summed S."""
     import torch
     import torch.distributed as dist
     from . import scheme
-    N = ipa.N
+    from ._lib import lib
+    N = vc.N if isinstance(vc, scheme.IPA) else vc.size
     tr, r, rows = scheme.multiproof_begin(N, cxy, cinf, z, y)
     lo, hi = shard_range(len(z), rank, world)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    S = torch.zeros((rows, N, 4), dtype=torch.int64, device=dev)
     try:
-        scheme.multiproof_accumulate(ipa.engine, N, z, lo, hi - lo, d_data_ptr, r, S.data_ptr())
-    except Exception:
-        from ._lib import lib
+        # every element of S is written by vc_multiproof_accumulate (on the engine's stream, which
+        # is synchronised before it returns): no fill on torch's stream that could race with it
+        S = torch.empty((rows, N, 4), dtype=torch.int64, device=dev)
+        torch.cuda.current_stream(dev).synchronize()
+        scheme.multiproof_accumulate(vc.engine, N, z, lo, hi - lo, d_data_ptr, r, S.data_ptr())
+        if world > 1:
+            outs = [torch.empty_like(S) for _ in range(world)]
+            dist.all_gather(outs, S)
+            parts = torch.stack(outs).contiguous()
+        else:
+            parts = S[None]
+        torch.cuda.current_stream(dev).synchronize()
+    except BaseException:
         lib().vc_transcript_free(tr)
         raise
-    if world > 1:
-        outs = [torch.empty_like(S) for _ in range(world)]
-        dist.all_gather(outs, S)
-        parts = torch.stack(outs).contiguous()
-    else:
-        parts = S[None]
-    torch.cuda.current_stream(dev).synchronize()
-    return scheme.multiproof_finish_ipa(ipa, z, parts.data_ptr(), world, tr)
+    return scheme.multiproof_finish(vc, z, parts.data_ptr(), world, tr)

@@ -20,7 +20,8 @@ SCALAR_R = {
 
 
 def _ptr(a):
-    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+    # the pointer object keeps `a` alive for the duration of the call (see scheme._p)
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
 def ints_to_limbs(vals, nl=4):
@@ -73,6 +74,46 @@ def random_scalars(curve, n, rng):
     return s
 
 
+SCALAR_BITS = {"bn254": 254, "bls12_381": 255, "bandersnatch": 253}
+
+
+def random_base_scalars(curve, seed, n):
+    """The discrete logs of vc_bases_random(seed, n): P_i = s_i * G with s_i from splitmix64 of
+    (seed, i) (bases.hip k_random) -- the host mirror of that derivation, so callers can check an
+    MSM over synthetic bases by linearity: sum k_i P_i = (sum k_i s_i mod r) * G. Returns (n, 4)
+    uint64 limbs."""
+    M1, M2, G = np.uint64(0xbf58476d1ce4e5b9), np.uint64(0x94d049bb133111eb), np.uint64(0x9e3779b97f4a7c15)
+    with np.errstate(over="ignore"):
+        st = np.uint64(seed) * np.uint64(0x100000001b3) + np.arange(n, dtype=np.uint64)
+        out = np.zeros((n, 4), dtype=np.uint64)
+        for k in range(4):
+            st = st + G
+            z = st.copy()
+            z = (z ^ (z >> np.uint64(30))) * M1
+            z = (z ^ (z >> np.uint64(27))) * M2
+            out[:, k] = z ^ (z >> np.uint64(31))
+    top = SCALAR_BITS[curve] - 2 - 192
+    out[:, 3] &= np.uint64((1 << top) - 1)
+    out[:, 0] |= np.uint64(1)
+    return out
+
+
+def limb_rows_to_ints(a):
+    """(n, k) uint64 limbs -> list of Python ints."""
+    a = np.ascontiguousarray(a, dtype="<u8")
+    k = a.shape[1]
+    b = a.tobytes()
+    return [int.from_bytes(b[8 * k * i:8 * k * (i + 1)], "little") for i in range(a.shape[0])]
+
+
+def dot_mod(a, b, r):
+    """sum a_i b_i mod r over two (n, 4) limb arrays (host, exact)."""
+    s = 0
+    for x, y in zip(limb_rows_to_ints(a), limb_rows_to_ints(b)):
+        s += x * y
+    return s % r
+
+
 def partials_sum(curve, accs):
     """vc_partials_sum: add projective accumulators on the host (no device needed)."""
     accs = np.ascontiguousarray(accs, dtype=np.uint32)
@@ -109,6 +150,18 @@ class Engine:
     # -------------------------------------------------------------- streams / timing
     def set_stream(self, stream_handle):
         check(lib().vc_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)), "vc_ctx_set_stream")
+
+    # vc_ctx_set_option knobs (include/vc_msm.h)
+    OPT_MSM_SHARED_WINDOWS = 1
+    OPT_MSM_CHUNK_POINTS = 2
+
+    def set_option(self, option, value):
+        check(lib().vc_ctx_set_option(self.h, option, int(value)), "vc_ctx_set_option")
+
+    def get_option(self, option):
+        v = ctypes.c_int64()
+        check(lib().vc_ctx_get_option(self.h, option, ctypes.byref(v)), "vc_ctx_get_option")
+        return v.value
 
     def enable_timing(self, on=True):
         check(lib().vc_ctx_enable_timing(self.h, 1 if on else 0), "vc_ctx_enable_timing")

@@ -20,7 +20,11 @@ _P = ctypes.c_void_p
 
 
 def _p(a):
-    return ctypes.c_void_p(a.ctypes.data)
+    # data_as keeps a reference to the array in the pointer object: callers pass temporaries
+    # (e.g. _p(_fr(point))), and a bare c_void_p(a.ctypes.data) let the array be freed before the
+    # foreign call read it -- harmless single-threaded by luck, garbage once another thread
+    # reused the memory (tests/test_gpu_threads.py found it)
+    return a.ctypes.data_as(ctypes.c_void_p)
 
 
 def _fr(x):
@@ -384,6 +388,26 @@ def multiproof_accumulate(engine, N, z, first, count, d_data_ptr, r, d_S_ptr):
     """Phase 2 (device): this shard's rows x N per-point sums into d_S (canonical u64 x 4)."""
     check(lib().vc_multiproof_accumulate(engine.h, N, len(z), _p(z), first, count, ctypes.c_void_p(d_data_ptr),
                                          _p(r), ctypes.c_void_p(d_S_ptr)), "multiproof_accumulate")
+
+
+def multiproof_finish(vc, z, d_S_parts_ptr, G, tr):
+    """Phase 3: sum the G shards' S, then D, t, E and the inner proof -- an IPA proof or the KZG
+    (proof, y) of prove_point at t (multiproof.rs:129-175). Frees `tr`."""
+    if isinstance(vc, IPA):
+        return multiproof_finish_ipa(vc, z, d_S_parts_ptr, G, tr)
+    N = vc.size
+    dxy = np.zeros(8, dtype=np.uint64)
+    dinf = np.zeros(1, dtype=np.uint8)
+    kxy = np.zeros(8, dtype=np.uint64)
+    kinf = np.zeros(1, dtype=np.uint8)
+    ky = np.zeros(4, dtype=np.uint64)
+    try:
+        check(lib().vc_multiproof_finish(vc.engine.h, 1, vc.table, N, len(z), _p(z), ctypes.c_void_p(d_S_parts_ptr),
+                                         G, tr, _p(dxy), _p(dinf), None, _p(kxy), _p(kinf), _p(ky)),
+              "multiproof_finish")
+    finally:
+        lib().vc_transcript_free(tr)
+    return {"proof": {"proof": _pt(kxy, kinf[0]), "y": limbs_to_int(ky)}, "d": _pt(dxy, dinf[0])}
 
 
 def multiproof_finish_ipa(ipa, z, d_S_parts_ptr, G, tr):

@@ -12,7 +12,7 @@ from .engine import limbs_to_int
 
 def _b(x):
     a = np.frombuffer(bytes(x), dtype=np.uint8).copy()
-    return a, ctypes.c_void_p(a.ctypes.data)
+    return a, a.ctypes.data_as(ctypes.c_void_p)
 
 
 class VerkleTree:
