@@ -45,6 +45,7 @@ extern "C" {
 #define VC_E_NOT_ON_CURVE (-6)/* an uploaded base is not on the curve              */
 #define VC_E_NO_DEVICE (-7)   /* no usable gfx950 device                           */
 #define VC_E_DOMAIN (-8)      /* evaluation point outside what the call supports   */
+#define VC_E_COMM (-9)        /* collective failed (vc_comm.h: RCCL or the callback) */
 
 typedef struct vc_ctx vc_ctx;
 

@@ -167,3 +167,51 @@ def test_multiproof_sums_exchange_gloo_world2():
     for p in procs:
         p.join(60)
     assert all(ok for _, ok in res), res
+
+
+def _comm_worker(rank, world, port, q):
+    """the C ABI's host-callback transport (vc_comm_init_host + vc_comm_allgather, include/
+    vc_comm.h) over a gloo group: what a non-RCCL caller of libvkzg.so plugs in."""
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd")]
+    import torch.distributed as dist
+    from vkzg import comm as vcomm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = vcomm.Comm.host(rank, world, vcomm.torch_allgather())
+    ok = c.rank == rank and c.world == world and not c.is_rccl
+    for size in (1, 13, 4096, 100_003):
+        send = bytes((rank * 31 + i) % 251 for i in range(size))
+        got = c.allgather(send)
+        want = b"".join(bytes((r * 31 + i) % 251 for i in range(size)) for r in range(world))
+        ok = ok and got == want
+    c.close()
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_comm_host_transport_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert sorted(res) == [(0, True), (1, True)]
+
+
+def test_comm_world_one_and_bad_args():
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd")]
+    import ctypes
+    from vkzg import comm as vcomm
+    from vkzg import lib
+    c = vcomm.Comm.host(0, 1, None)
+    assert c.allgather(b"xyz") == b"xyz" and c.world == 1
+    c.close()
+    h = ctypes.c_void_p()
+    assert lib().vc_comm_init_host(0, 2, ctypes.cast(None, vcomm.ALLGATHER_FN), None, ctypes.byref(h)) == -1
+    assert lib().vc_comm_init_host(2, 2, vcomm.ALLGATHER_FN(lambda *a: 0), None, ctypes.byref(h)) == -1

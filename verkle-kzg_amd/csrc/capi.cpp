@@ -163,6 +163,7 @@ const char* vc_strerror(int s) {
         case VC_E_NOT_ON_CURVE: return "base point not on the curve (or not canonical)";
         case VC_E_NO_DEVICE: return "no usable HIP device";
         case VC_E_DOMAIN: return "evaluation point outside the supported domain";
+        case VC_E_COMM: return "collective failed (RCCL or the all-gather callback)";
     }
     return "unknown status";
 }

@@ -1,0 +1,298 @@
+// Multi-GPU entry points (include/vc_comm.h): a vc_comm is one rank of a group with an
+// all-gather -- RCCL over xGMI (loaded at run time) or a caller-supplied host callback -- and
+// the sharded workloads run this rank's share on its vc_ctx, then ONE all-gather per exchange
+// step. The reference is single-process CPU code (utils.rs:16-19 and its
+// callers), so these have no reference counterpart beyond the per-rank work they split.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/vc_comm.h"
+#include "comm.hpp"
+#include "ctx.hpp"
+
+namespace {
+
+// RCCL entry points, resolved once with dlopen: the library stays optional (a host-callback
+// comm and every single-GPU call work without it), and a process that already loaded torch's
+// bundled RCCL does not get a second copy linked in at load time.
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* names[] = {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"};
+        void* h = nullptr;
+        for (const char* n : names)
+            if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL)) != nullptr) break;
+        if (!h) return;
+        r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        r.init_rank = reinterpret_cast<decltype(r.init_rank)>(dlsym(h, "ncclCommInitRank"));
+        r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
+        r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
+        r.ok = r.get_unique_id && r.init_rank && r.all_gather && r.destroy;
+    });
+    return r;
+}
+
+// grow-only device buffer of a comm (its own device, not a ctx pool: the comm outlives calls)
+struct Stage {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return VC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+        if (e != hipSuccess) {
+            vk::last_hip_error() = e;
+            p = nullptr;
+            return VC_E_OOM;
+        }
+        cap = bytes ? bytes : 16;
+        return VC_OK;
+    }
+    ~Stage() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+}  // namespace
+
+struct vc_comm {
+    int rank = 0, world = 1, device = -1;
+    ncclComm_t nccl = nullptr;
+    vc_allgather_fn fn = nullptr;
+    void* user = nullptr;
+    Stage send, recv, work;  // RCCL staging of host buffers; sharded-workload scratch
+    std::vector<uint8_t> hbuf;  // host staging of device all-gathers over a callback comm
+};
+
+namespace {
+
+int comm_allgather_dev(vc_comm* c, vc_ctx* ctx, const void* d_send, size_t bytes, void* d_recv);
+
+// host buffers -> host buffers
+int comm_allgather_host(vc_comm* c, vc_ctx* ctx, const void* send, size_t bytes, void* recv) {
+    if (!c->nccl && c->world == 1) {
+        if (bytes && recv != send) memcpy(recv, send, bytes);
+        return VC_OK;
+    }
+    if (!c->nccl) return c->fn(c->user, send, bytes, recv) == 0 ? VC_OK : VC_E_COMM;
+    if (!ctx) return VC_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    VK_TRY(c->send.ensure(bytes));
+    VK_TRY(c->recv.ensure(bytes * c->world));
+    VK_CHECK_HIP(hipMemcpyAsync(c->send.p, send, bytes, hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(comm_allgather_dev(c, ctx, c->send.p, bytes, c->recv.p));
+    VK_CHECK_HIP(hipMemcpyAsync(recv, c->recv.p, bytes * c->world, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+// device buffers (ctx's device) -> device buffers; synchronous
+int comm_allgather_dev(vc_comm* c, vc_ctx* ctx, const void* d_send, size_t bytes, void* d_recv) {
+    (void)hipSetDevice(ctx->device);
+    if (c->nccl) {
+        if (rccl().all_gather(d_send, d_recv, bytes, ncclUint8, c->nccl, ctx->stream) != ncclSuccess)
+            return VC_E_COMM;
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        return VC_OK;
+    }
+    if (c->world == 1) {
+        VK_CHECK_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        return VC_OK;
+    }
+    c->hbuf.resize(bytes * (c->world + 1));
+    uint8_t* hs = c->hbuf.data();
+    uint8_t* hr = hs + bytes;
+    VK_CHECK_HIP(hipMemcpyAsync(hs, d_send, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    if (c->fn(c->user, hs, bytes, hr) != 0) return VC_E_COMM;
+    VK_CHECK_HIP(hipMemcpyAsync(d_recv, hr, bytes * c->world, hipMemcpyHostToDevice, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+bool valid(const vc_comm* c, const vc_ctx* ctx) { return c && ctx && (!c->nccl || c->device == ctx->device); }
+
+}  // namespace
+
+extern "C" {
+
+int vc_comm_unique_id(uint8_t id[VC_COMM_ID_BYTES]) {
+    if (!id) return VC_E_INVALID;
+    const Rccl& r = rccl();
+    if (!r.ok) return VC_E_NO_DEVICE;
+    ncclUniqueId u;
+    if (r.get_unique_id(&u) != ncclSuccess) return VC_E_COMM;
+    static_assert(sizeof(u) == VC_COMM_ID_BYTES, "ncclUniqueId size");
+    memcpy(id, &u, VC_COMM_ID_BYTES);
+    return VC_OK;
+}
+
+int vc_comm_init_rccl(int device, int rank, int world, const uint8_t id[VC_COMM_ID_BYTES], vc_comm** out) {
+    if (!out || !id || world < 1 || rank < 0 || rank >= world) return VC_E_INVALID;
+    *out = nullptr;
+    const Rccl& r = rccl();
+    if (!r.ok) return VC_E_NO_DEVICE;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VC_E_NO_DEVICE;
+    if (device < 0 || device >= ndev) return VC_E_INVALID;
+    VK_CHECK_HIP(hipSetDevice(device));
+    ncclUniqueId u;
+    memcpy(&u, id, VC_COMM_ID_BYTES);
+    ncclComm_t nc = nullptr;
+    if (r.init_rank(&nc, world, u, rank) != ncclSuccess) return VC_E_COMM;
+    vc_comm* c = new vc_comm();
+    c->rank = rank;
+    c->world = world;
+    c->device = device;
+    c->nccl = nc;
+    *out = c;
+    return VC_OK;
+}
+
+int vc_comm_init_host(int rank, int world, vc_allgather_fn fn, void* user, vc_comm** out) {
+    if (!out || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return VC_E_INVALID;
+    vc_comm* c = new vc_comm();
+    c->rank = rank;
+    c->world = world;
+    c->fn = fn;
+    c->user = user;
+    *out = c;
+    return VC_OK;
+}
+
+void vc_comm_destroy(vc_comm* c) {
+    if (!c) return;
+    if (c->device >= 0) (void)hipSetDevice(c->device);
+    if (c->nccl) (void)rccl().destroy(c->nccl);
+    delete c;
+}
+
+int vc_comm_rank(const vc_comm* c) { return c ? c->rank : VC_E_INVALID; }
+int vc_comm_world(const vc_comm* c) { return c ? c->world : VC_E_INVALID; }
+int vc_comm_is_rccl(const vc_comm* c) { return c ? (c->nccl != nullptr) : VC_E_INVALID; }
+
+int vc_comm_allgather(vc_comm* c, vc_ctx* ctx, const void* send, size_t bytes, void* recv) {
+    if (!c || (bytes && (!send || !recv)) || (c->nccl && !valid(c, ctx))) return VC_E_INVALID;
+    return comm_allgather_host(c, ctx, send, bytes, recv);
+}
+
+// ---------------------------------------------------------------- sharded workloads
+
+int vc_msm_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t offset, const void* d_scalars, size_t n, int mont,
+                   uint64_t* out_xy, uint8_t* out_inf) {
+    if (!valid(comm, ctx) || !out_xy || !out_inf) return VC_E_INVALID;
+    const int words = vk::point_words(ctx->curve);
+    std::vector<uint32_t> part(words), parts((size_t)words * comm->world);
+    VK_TRY(vc_msm_device_window_part(ctx, table_id, offset, d_scalars, n, mont, comm->rank, comm->world, part.data()));
+    VK_TRY(comm_allgather_host(comm, ctx, part.data(), part.size() * 4, parts.data()));
+    return vc_partials_sum(ctx->curve, parts.data(), comm->world, out_xy, out_inf);
+}
+
+int vc_msm_batch_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t width, const void* d_scalars, size_t batch,
+                         int mont, uint64_t* out_xy, uint8_t* out_inf) {
+    if (!valid(comm, ctx) || width == 0 || (batch && (!d_scalars || !out_xy || !out_inf))) return VC_E_INVALID;
+    if (batch == 0) return VC_OK;
+    const size_t W2 = 2 * (size_t)vk::aff_limbs64(ctx->curve);  // u64 words of one affine point
+    size_t lo, hi;
+    vk::shard_range(batch, comm->rank, comm->world, &lo, &hi);
+    const size_t bmax = (batch + comm->world - 1) / comm->world, mine = hi - lo;
+    const size_t rec = W2 + 1;  // u64 words per record: x, y, inf
+    std::vector<uint64_t> send(bmax * rec, 0), recv(bmax * rec * comm->world);
+    if (mine > 0) {
+        (void)hipSetDevice(ctx->device);
+        VK_TRY(comm->work.ensure(mine * (W2 * 8 + 1)));
+        uint8_t* dxy = reinterpret_cast<uint8_t*>(comm->work.p);
+        uint8_t* dinf = dxy + mine * W2 * 8;
+        const uint8_t* sc = reinterpret_cast<const uint8_t*>(d_scalars) + lo * width * 32;
+        VK_TRY(vc_msm_batch_device(ctx, table_id, width, sc, mine, mont, dxy, dinf));
+        std::vector<uint64_t> hxy(mine * W2);
+        std::vector<uint8_t> hinf(mine);
+        VK_CHECK_HIP(hipMemcpy(hxy.data(), dxy, mine * W2 * 8, hipMemcpyDeviceToHost));
+        VK_CHECK_HIP(hipMemcpy(hinf.data(), dinf, mine, hipMemcpyDeviceToHost));
+        for (size_t b = 0; b < mine; b++) {
+            memcpy(&send[b * rec], &hxy[b * W2], W2 * 8);
+            send[b * rec + W2] = hinf[b];
+        }
+    }
+    VK_TRY(comm_allgather_host(comm, ctx, send.data(), send.size() * 8, recv.data()));
+    for (int k = 0; k < comm->world; k++) {
+        size_t a, e;
+        vk::shard_range(batch, k, comm->world, &a, &e);
+        const uint64_t* src = &recv[(size_t)k * bmax * rec];
+        for (size_t b = 0; b < e - a; b++) {
+            memcpy(&out_xy[(a + b) * W2], &src[b * rec], W2 * 8);
+            out_inf[a + b] = (uint8_t)src[b * rec + W2];
+        }
+    }
+    return VC_OK;
+}
+
+int vc_kzg_prove_sharded(vc_ctx* ctx, vc_comm* comm, int table, size_t size, const void* d_evals, size_t max,
+                         const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y) {
+    if (!valid(comm, ctx) || !point || !proof_xy || !proof_inf || !y) return VC_E_INVALID;
+    const int words = vk::point_words(ctx->curve);
+    std::vector<uint32_t> part(words), parts((size_t)words * comm->world);
+    VK_TRY(vc_kzg_prove_device_part(ctx, table, size, d_evals, max, point, comm->rank, comm->world, part.data(), y));
+    VK_TRY(comm_allgather_host(comm, ctx, part.data(), part.size() * 4, parts.data()));
+    return vc_partials_sum(ctx->curve, parts.data(), comm->world, proof_xy, proof_inf);
+}
+
+int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int table, size_t N, size_t Q,
+                                const void* d_data_slice, const uint64_t* com_xy, const uint8_t* com_inf,
+                                const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
+                                vc_ipa_proof* ipa_proof, uint64_t* kzg_proof_xy, uint8_t* kzg_proof_inf,
+                                uint64_t* kzg_y) {
+    if (!valid(comm, ctx) || !com_xy || !com_inf || !z || !y || !d_xy || !d_inf || Q == 0) return VC_E_INVALID;
+    if (scheme != 0 && scheme != 1) return VC_E_INVALID;
+    vc_transcript* tr = nullptr;
+    uint64_t r[4];
+    size_t rows = 0;
+    VK_TRY(vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows));
+    size_t lo, hi;
+    vk::shard_range(Q, comm->rank, comm->world, &lo, &hi);
+    const size_t sbytes = rows * N * 32;
+    int st = VC_OK;
+    do {
+        (void)hipSetDevice(ctx->device);
+        // [0, sbytes): this rank's S; [sbytes, ...): every rank's S in rank order
+        if ((st = comm->work.ensure(sbytes * (comm->world + 1))) != VC_OK) break;
+        uint8_t* dS = reinterpret_cast<uint8_t*>(comm->work.p);
+        if ((st = vc_multiproof_accumulate(ctx, N, Q, z, lo, hi - lo, d_data_slice, r, dS)) != VC_OK) break;
+        if ((st = comm_allgather_dev(comm, ctx, dS, sbytes, dS + sbytes)) != VC_OK) break;
+        st = vc_multiproof_finish(ctx, scheme, table, N, Q, z, dS + sbytes, comm->world, tr, d_xy, d_inf, ipa_proof,
+                                  kzg_proof_xy, kzg_proof_inf, kzg_y);
+    } while (false);
+    vc_transcript_free(tr);
+    return st;
+}
+
+int vc_verkle_commitment_sharded(vc_ctx* ctx, vc_comm* comm, int table, vc_verkle* tree, uint64_t* out_xy,
+                                 uint8_t* out_inf) {
+    if (!valid(comm, ctx) || !tree || !out_xy || !out_inf) return VC_E_INVALID;
+    vk::Shard sh;
+    sh.rank = comm->rank;
+    sh.world = comm->world;
+    sh.allgather = [&](const void* send, size_t bytes, void* recv) {
+        return comm_allgather_host(comm, ctx, send, bytes, recv);
+    };
+    return vk::verkle_commitment(ctx, table, tree, out_xy, out_inf, &sh);
+}
+
+}  // extern "C"

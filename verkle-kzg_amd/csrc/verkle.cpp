@@ -15,6 +15,7 @@
 #include "../../include/vc_scheme.h"
 #include "../../include/vc_verkle.h"
 #include "ctx.hpp"
+#include "comm.hpp"
 #include "host/fr.hpp"
 
 namespace {
@@ -260,8 +261,17 @@ int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, siz
     return VC_OK;
 }
 
-// gen_commitment (node.rs:205-277), level-batched.
+// gen_commitment (node.rs:205-277), level-batched. sh != nullptr: this rank's slices of every
+// level, one all-gather of the per-node records per level (vc_verkle_commitment_sharded).
 int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf) {
+    return vk::verkle_commitment(ctx, table, t, out_xy, out_inf, nullptr);
+}
+
+}  // extern "C"
+
+namespace vk {
+
+int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh) {
     if (!ctx || !t || !out_xy || !out_inf) return VC_E_INVALID;
     const int N = t->N;
     static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
@@ -273,7 +283,8 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
         tic = now;
     };
     // dirty nodes reachable from the root, with depth (clean subtrees are skipped: an insert
-    // clears every commitment on its path, so a clean node has clean descendants)
+    // clears every commitment on its path, so a clean node has clean descendants). Every rank
+    // holds the same tree, so every rank walks it to the same lists in the same order.
     std::vector<int> exts;
     std::vector<std::vector<int>> internals;  // by depth
     std::vector<std::pair<int, int>> stack{{0, 0}};
@@ -315,24 +326,25 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
             vals.insert(vals.end(), o.vals.begin(), o.vals.end());
         }
     };
-    // rows of items [0, count) built by fn(i, Rows&) on up to 16 host threads, in item order
-    // (the node walks are pointer-chasing std::map code: ~100-200 ns per node on one thread)
+    // rows of items [lo, hi) built by fn(i, Rows&) on up to 16 host threads, in item order
+    // (the node walks are pointer-chasing code: ~100-200 ns per node on one thread)
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    auto build_rows = [&](size_t count, size_t nnz_per, auto fn) {
+    auto build_rows = [&](size_t lo, size_t hi, size_t nnz_per, auto fn) {
         Rows out;
+        const size_t count = hi - lo;
         const unsigned T = count >= 4096 ? hw : 1;
         if (T == 1) {
             out.reserve(count, count * nnz_per);
-            for (size_t i = 0; i < count; i++) fn(i, out);
+            for (size_t i = lo; i < hi; i++) fn(i, out);
             return out;
         }
         std::vector<Rows> part(T);
         std::vector<std::thread> th;
         for (unsigned k = 0; k < T; k++)
             th.emplace_back([&, k] {
-                const size_t lo = count * k / T, hi = count * (k + 1) / T;
-                part[k].reserve(hi - lo, (hi - lo) * nnz_per);
-                for (size_t i = lo; i < hi; i++) fn(i, part[k]);
+                const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
+                part[k].reserve(b - a, (b - a) * nnz_per);
+                for (size_t i = a; i < b; i++) fn(i, part[k]);
             });
         for (auto& x : th) x.join();
         out.reserve(count, count * nnz_per);
@@ -368,14 +380,56 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
         lap("to_data_item");
         return st;
     };
+    // the nodes nodes[lo, hi) of a level got (xy, inf, items) here: store them; with a shard,
+    // first all-gather every rank's slice (records of 8 + 4 + 1 u64: xy, item, inf), so every
+    // rank stores the whole level
+    auto store_level = [&](const std::vector<int>& ids, size_t lo, size_t hi, const std::vector<uint64_t>& xy,
+                           const std::vector<uint8_t>& inf, const std::vector<uint64_t>& items) -> int {
+        auto put = [&](size_t i, const uint64_t* rxy, uint8_t rinf, const uint64_t* ritem) {
+            VNode& n = t->nodes[ids[i]];
+            memcpy(n.cxy, rxy, 64);
+            n.cinf = rinf;
+            memcpy(n.item, ritem, 32);
+            n.has_commit = true;
+        };
+        if (!sh) {
+            for_each(hi - lo, [&](size_t b) { put(lo + b, &xy[b * 8], inf[b], &items[b * 4]); });
+            return VC_OK;
+        }
+        constexpr size_t REC = 13;  // u64 words per record
+        const size_t B = ids.size(), bmax = (B + sh->world - 1) / sh->world;
+        std::vector<uint64_t> send(bmax * REC, 0), recv(bmax * REC * sh->world);
+        for (size_t b = 0; b < hi - lo; b++) {
+            memcpy(&send[b * REC], &xy[b * 8], 64);
+            memcpy(&send[b * REC + 8], &items[b * 4], 32);
+            send[b * REC + 12] = inf[b];
+        }
+        VK_TRY(sh->allgather(send.data(), send.size() * 8, recv.data()));
+        for (int k = 0; k < sh->world; k++) {
+            const size_t a = B * k / sh->world, e = B * (k + 1) / sh->world;
+            const uint64_t* src = &recv[(size_t)k * bmax * REC];
+            for_each(e - a, [&](size_t b) {
+                const uint64_t* rec = src + b * REC;
+                put(a + b, rec, (uint8_t)rec[12], rec + 8);
+            });
+        }
+        return VC_OK;
+    };
+    auto slice = [&](size_t B, size_t* lo, size_t* hi) {
+        *lo = sh ? B * sh->rank / sh->world : 0;
+        *hi = sh ? B * (sh->rank + 1) / sh->world : B;
+    };
     std::vector<uint64_t> xy, items, xy2, items2;
     std::vector<uint8_t> inf, inf2;
-    // extension nodes: c1, c2 (width N), then [1, stem, c1, c2] (width 4)
+    // extension nodes: c1, c2 (width N), then [1, stem, c1, c2] (width 4) -- both steps only need
+    // the node's own values, so a rank runs both on its slice and exchanges once
     if (!exts.empty()) {
         const size_t E = exts.size();
+        size_t lo, hi;
+        slice(E, &lo, &hi);
         // (position, value) writes of c1 / c2 in leaf order; a later write to the same
         // position overwrites, as c1_values[index] = ... does (node.rs:226-239)
-        Rows r12 = build_rows(E, (size_t)N, [&](size_t e, Rows& r) {
+        Rows r12 = build_rows(lo, hi, (size_t)N, [&](size_t e, Rows& r) {
             std::vector<std::pair<uint32_t, std::array<uint64_t, 4>>> half[2];
             auto put = [&](int h, uint32_t pos, const uint64_t* v) {
                 for (auto& pv : half[h])
@@ -390,12 +444,12 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
             const VNode& n = t->nodes[exts[e]];
             for (auto& kv : n.leaves) {
                 const size_t index = kv.first;
-                uint64_t lo[4], hi[4];
-                item_of_bytes(kv.second.data(), 16, lo);
-                item_of_bytes(kv.second.data() + 16, 16, hi);
+                uint64_t vlo[4], vhi[4];
+                item_of_bytes(kv.second.data(), 16, vlo);
+                item_of_bytes(kv.second.data() + 16, 16, vhi);
                 const int h = index < (size_t)(N / 2) ? 0 : 1;
-                put(h, (uint32_t)((2 * index) % N), lo);
-                put(h, (uint32_t)((2 * index + 1) % N), hi);
+                put(h, (uint32_t)((2 * index) % N), vlo);
+                put(h, (uint32_t)((2 * index + 1) % N), vhi);
             }
             for (int h = 0; h < 2; h++) {
                 for (auto& pv : half[h]) r.add(pv.first, pv.second.data());
@@ -403,44 +457,36 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
             }
         });
         VK_TRY(commit_rows(r12, xy, inf, items));
-        Rows rx = build_rows(E, 4, [&](size_t e, Rows& r) {
+        Rows rx = build_rows(lo, hi, 4, [&](size_t e, Rows& r) {
             const VNode& n = t->nodes[exts[e]];
             uint64_t one[4] = {1, 0, 0, 0}, stem_item[4];
             item_of_bytes(n.stem.data(), N, stem_item);  // bytes_to_item(stem.to_bytes())
             r.add(0, one);
             r.add(1, stem_item);
-            r.add(2, &items[(2 * e) * 4]);
-            r.add(3, &items[(2 * e + 1) * 4]);
+            r.add(2, &items[(2 * (e - lo)) * 4]);
+            r.add(3, &items[(2 * (e - lo) + 1) * 4]);
             r.end_row();
         });
         VK_TRY(commit_rows(rx, xy2, inf2, items2));
-        for_each(E, [&](size_t e) {
-            VNode& n = t->nodes[exts[e]];
-            memcpy(n.cxy, &xy2[e * 8], 64);
-            n.cinf = inf2[e];
-            memcpy(n.item, &items2[e * 4], 32);
-            n.has_commit = true;
-        });
+        VK_TRY(store_level(exts, lo, hi, xy2, inf2, items2));
     }
-    // internal nodes, deepest level first (HACK in the reference: width hard-coded 256)
+    // internal nodes, deepest level first (HACK in the reference: width hard-coded 256); a
+    // parent needs its children's items, so every depth is one exchange
     for (int depth = (int)internals.size() - 1; depth >= 0; depth--) {
         const std::vector<int>& lv = internals[depth];
-        Rows ri = build_rows(lv.size(), 4, [&](size_t b, Rows& r) {
+        size_t lo, hi;
+        slice(lv.size(), &lo, &hi);
+        Rows ri = build_rows(lo, hi, 4, [&](size_t b, Rows& r) {
             for (auto& kv : t->nodes[lv[b]].children) r.add(kv.first, t->nodes[kv.second].item);
             r.end_row();
         });
         VK_TRY(commit_rows(ri, xy, inf, items));
-        for_each(lv.size(), [&](size_t b) {
-            VNode& n = t->nodes[lv[b]];
-            memcpy(n.cxy, &xy[b * 8], 64);
-            n.cinf = inf[b];
-            memcpy(n.item, &items[b * 4], 32);
-            n.has_commit = true;
-        });
+        VK_TRY(store_level(lv, lo, hi, xy, inf, items));
     }
     memcpy(out_xy, t->nodes[0].cxy, 64);
     *out_inf = t->nodes[0].cinf;
     return VC_OK;
 }
 
-}  // extern "C"
+}  // namespace vk
+

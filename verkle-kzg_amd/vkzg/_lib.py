@@ -10,11 +10,14 @@ import re
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
 LIB_PATH = os.environ.get("VKZG_LIB") or os.path.join(ROOT, "lib", "libvkzg.so")
-HEADERS = [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("vc_msm.h", "vc_scheme.h", "vc_verkle.h")]
+HEADERS = [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("vc_msm.h", "vc_scheme.h", "vc_verkle.h",
+                                                                     "vc_comm.h")]
 
 c_void_p, c_int, c_size_t, c_uint64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
 c_double, c_long, c_char_p = ctypes.c_double, ctypes.c_long, ctypes.c_char_p
 P = ctypes.c_void_p
+# vc_allgather_fn (include/vc_comm.h): (user, send, bytes, recv) -> 0 on success
+ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
 
 SIGNATURES = {
     "vc_strerror": (c_char_p, [c_int]),
@@ -83,6 +86,21 @@ SIGNATURES = {
     "vc_multiproof_verify_ipa": (c_int, [c_void_p, c_int, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P,
                                          ctypes.POINTER(c_int)]),
     "vc_multiproof_kzg_claim": (c_int, [c_void_p, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P, P, P]),
+    # vc_comm.h
+    "vc_comm_unique_id": (c_int, [P]),
+    "vc_comm_init_rccl": (c_int, [c_int, c_int, c_int, P, ctypes.POINTER(c_void_p)]),
+    "vc_comm_init_host": (c_int, [c_int, c_int, ALLGATHER_FN, c_void_p, ctypes.POINTER(c_void_p)]),
+    "vc_comm_destroy": (None, [c_void_p]),
+    "vc_comm_rank": (c_int, [c_void_p]),
+    "vc_comm_world": (c_int, [c_void_p]),
+    "vc_comm_is_rccl": (c_int, [c_void_p]),
+    "vc_comm_allgather": (c_int, [c_void_p, c_void_p, P, c_size_t, P]),
+    "vc_msm_sharded": (c_int, [c_void_p, c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_msm_batch_sharded": (c_int, [c_void_p, c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_kzg_prove_sharded": (c_int, [c_void_p, c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
+    "vc_multiproof_prove_sharded": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P,
+                                            P, P, P, P, P]),
+    "vc_verkle_commitment_sharded": (c_int, [c_void_p, c_void_p, c_int, c_void_p, P, P]),
 }
 
 _lib = None
