@@ -64,10 +64,14 @@ def parse():
     ap.add_argument("--no-verkle", action="store_true", help="skip the verkle-tree commitment line (8(f) rank 1)")
     ap.add_argument("--no-ipa", action="store_true", help="skip the single IPA prove/verify line (benches/ipa.rs)")
     ap.add_argument("--verkle-keys", type=int, default=1 << 16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the Pippenger CPU baseline (0: min(16, cpu_count), one GPU's CPU share)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
     ap.add_argument("--no-variable-base", action="store_true",
                     help="skip the variable-base (no shared-window copies) MSM sub-line")
     ap.add_argument("--no-check", action="store_true", help="skip the one-time 2^20 result check")
+    ap.add_argument("--comm", choices=["capi", "torch"], default="capi",
+                    help="N > 1 exchange: vc_comm (C ABI, RCCL) or torch.distributed all-gather")
     return ap.parse_args()
 
 
@@ -104,6 +108,40 @@ def cpu_baseline(curve, n_full, sample):
             "sample": f"{sample} of {n_full} terms of the naive {curve} MSM (reference utils.rs:16-19 "
                       f"restated in C, oracle/c/ref_curve.c), 1 thread, {dt:.2f} s, extrapolated linearly",
             "ms_per_msm": per_msm_s * 1e3, "host_cpus": os.cpu_count()}
+
+
+def cpu_pippenger(curve, xy, inf, scalars, want, threads):
+    """The fair all-core CPU bound: the same 2^20 MSM by the bucket method in C
+    (oracle/c/ref_curve.c pip_msm: per-thread point chunks, signed windows, mixed bucket adds),
+    on `threads` host threads, the whole workload once (no extrapolation); its result is
+    checked against the GPU's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import cref  # CPU baseline leg only
+    t0 = time.perf_counter()
+    got = cref.pip_msm_arrays(curve, xy, inf, scalars, threads)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "MSM/s", "cores": threads, "kind": "pippenger",
+            "sample": f"the full {scalars.shape[0]}-term {curve} MSM of the bench (bases and scalars of the timed "
+                      f"step), Pippenger in C on {threads} threads (oracle/c/ref_curve.c pip_msm), {dt:.2f} s",
+            "ms_per_msm": dt * 1e3, "same_result_as_gpu": bool(got[1] == int(want[1]) and np.array_equal(got[0], np.asarray(want[0])))}
+
+
+def cpu_pippenger_commits(batch, threads):
+    """configs[2] on the CPU: `batch` width-256 Bandersnatch commits, one Pippenger per commit in C,
+    commits split over `threads` host threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import cref  # CPU baseline leg only
+    e = vkzg.Engine("bandersnatch", 0)
+    tid = e.random_bases(256, seed=3)
+    xy, inf = e.download_bases(tid)
+    e.close()
+    sc = vkzg.random_scalars("bandersnatch", 256 * batch, np.random.default_rng(9))
+    t0 = time.perf_counter()
+    cref.pip_msm_batch_arrays("bandersnatch", xy, inf, sc, 256, threads)
+    dt = time.perf_counter() - t0
+    return {"value": batch / dt, "unit": "commits/s", "cores": threads, "kind": "pippenger",
+            "sample": f"{batch} width-256 bandersnatch commits, Pippenger per commit in C "
+                      f"(oracle/c/ref_curve.c pip_msm_batch) on {threads} threads, {dt:.2f} s"}
 
 
 def cpu_commit_baselines(reps=8):
@@ -368,8 +406,30 @@ def main():
     scalars = vkzg.random_scalars(curve, n, rng)
     d_sc = torch.from_numpy(scalars.view(np.int64).copy()).to(dev)
 
+    # N > 1: the exchange goes through the C ABI (include/vc_comm.h: vc_msm_sharded over a
+    # vc_comm on RCCL, the path a Rust caller of libvkzg.so uses); the unique id travels over
+    # the torch.distributed group. --comm torch keeps the Python all-gather (vkzg.dist).
+    comm, comm_kind = None, "none" if world == 1 else a.comm
+    if world > 1 and a.comm == "capi":
+        from vkzg import comm as vcomm
+        obj = [vcomm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        try:
+            comm = vcomm.Comm.rccl(local, rank, world, obj[0])
+        except Exception as ex:  # no usable RCCL through the C ABI: torch's all-gather instead
+            print(f"[bench] vc_comm_init_rccl failed ({ex}); using the torch.distributed exchange",
+                  file=sys.stderr, flush=True)
+            comm_kind = "torch (vc_comm init failed)"
+        ok = torch.tensor([0 if comm is None else 1], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and comm is not None:  # every rank must take the same path
+            comm.close()
+            comm, comm_kind = None, "torch (vc_comm init failed on a peer)"
+
     def step():
-        # window-slice partial (HIP) -> RCCL all-gather of projective partials -> host sum
+        if comm is not None:  # window slice (HIP) -> vc_comm RCCL all-gather -> host sum, all in C
+            return comm.msm(eng, table, d_sc.data_ptr(), n)
+        # window-slice partial (HIP) -> torch RCCL all-gather of projective partials -> host sum
         return vdist.msm_sharded(eng, table, d_sc.data_ptr(), n, rank, world, dev if world > 1 else None,
                                  split="windows")
 
@@ -512,6 +572,7 @@ def main():
         "data": "synthetic (random subgroup bases s_i*G generated on device, uniform scalars < r)",
         "config": {"workload": f"single 2^{a.log_n}-point {curve} G1 Pippenger MSM (configs[1])",
                    "n_points": n, "curve": curve, "parallelism": f"Pippenger-window slices x{world}",
+                   "exchange": comm_kind,
                    "window_bits": c_bits, "windows": w_total,
                    "precomputed_bases": (f"{w_total} x 2n shifted window copies 2^(c w) P_i, 2^(c w) phi(P_i) "
                                          f"({w_total * 2 * n * 96 / 1e9:.2f} GB), built once per base table "
@@ -611,12 +672,25 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(curve, n, a.cpu_sample)
         out["cpu_baselines_other"] = cpu_commit_baselines()
+        # the all-core bound beside the 1-core naive port: the CPU share of one GPU on the box
+        thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+        bxy, binf = eng.download_bases(table)
+        out["cpu_baseline_pippenger"] = cpu_pippenger(curve, bxy, binf, scalars, res, thr)
+        del bxy, binf
+        out["cpu_baselines_other"]["C3_width256_commits_pippenger"] = cpu_pippenger_commits(a.commit_batch, thr)
         if "kzg" in out:  # configs[3] on the CPU: its two 2^20 MSMs alone (quotient not counted)
             out["cpu_baselines_other"]["C4_kzg_commit_open_lower_bound"] = {
                 "value": 2 * out["cpu_baseline"]["ms_per_msm"], "unit": "ms", "cores": 1, "kind": "port",
                 "sample": "2 x the naive 2^20 BLS12-381 MSM above (commit + proof MSM); the reference's "
                           "per-element inversions of the quotient are not counted, so this is a lower bound"}
+            pip = out["cpu_baseline_pippenger"]
+            out["cpu_baselines_other"]["C4_kzg_commit_open_lower_bound_pippenger"] = {
+                "value": 2 * pip["ms_per_msm"], "unit": "ms", "cores": pip["cores"], "kind": "pippenger",
+                "sample": "2 x the all-core Pippenger 2^20 BLS12-381 MSM above (commit + proof MSM); quotient "
+                          "not counted (lower bound)"}
 
+    if comm is not None:
+        comm.close()
     eng.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -273,6 +273,59 @@ static void pstore(u64* xy, uint8_t* inf, const pt* p) {
     from_mont(xy + NL, &y);
     *inf = 0;
 }
+/* mixed add, p Jacobian + (x2, y2) affine Montgomery (madd-2007-bl, 7M + 4S): the bucket add of
+ * the Pippenger baseline below (arkworks' buckets also add affine bases into projective sums) */
+static void pmadd(pt* r, const pt* p, const fe* x2, const fe* y2) {
+    if (piszero(p)) { r->x = *x2; r->y = *y2; r->z = ONE_; return; }
+    fe z1z1, u2, s2, t;
+    fmul(&z1z1, &p->z, &p->z);
+    fmul(&u2, x2, &z1z1);
+    fmul(&t, &p->z, &z1z1);
+    fmul(&s2, y2, &t);
+    if (feq(&u2, &p->x)) {
+        if (feq(&s2, &p->y)) { pdbl(r, p); return; }
+        pzero(r);
+        return;
+    }
+    fe h, hh, i, j, rr, v;
+    fsub(&h, &u2, &p->x);
+    fmul(&hh, &h, &h);
+    fadd(&i, &hh, &hh);
+    fadd(&i, &i, &i);
+    fmul(&j, &h, &i);
+    fsub(&rr, &s2, &p->y);
+    fadd(&rr, &rr, &rr);
+    fmul(&v, &p->x, &i);
+    pt o;
+    fmul(&o.x, &rr, &rr);
+    fsub(&o.x, &o.x, &j);
+    fsub(&o.x, &o.x, &v);
+    fsub(&o.x, &o.x, &v);
+    fsub(&t, &v, &o.x);
+    fmul(&t, &rr, &t);
+    fmul(&s2, &p->y, &j);
+    fadd(&s2, &s2, &s2);
+    fsub(&o.y, &t, &s2);
+    fadd(&t, &p->z, &h);
+    fmul(&t, &t, &t);
+    fsub(&t, &t, &z1z1);
+    fsub(&o.z, &t, &hh);
+    *r = o;
+}
+typedef struct { fe x, y; int inf; } aff;
+static void aload(aff* a, const u64* xy, int inf) {
+    a->inf = inf;
+    if (inf) return;
+    to_mont(&a->x, xy);
+    to_mont(&a->y, xy + NL);
+}
+static void aadd(pt* r, const pt* p, const aff* a, int neg) {
+    if (a->inf) { *r = *p; return; }
+    if (!neg) { pmadd(r, p, &a->x, &a->y); return; }
+    fe ny, z = {{0}};
+    fsub(&ny, &z, &a->y);
+    pmadd(r, p, &a->x, &ny);
+}
 #else
 /* ------------------------------------------------ twisted Edwards a=-5, extended (X,Y,T,Z) */
 typedef struct { fe x, y, t, z; } pt;
@@ -323,6 +376,23 @@ static void pstore(u64* xy, uint8_t* inf, const pt* p) {
     /* identity is (0, 1); y is canonical here */
     u64 one_c[NL] = {1};
     *inf = (fiszero(&x) && memcmp(xy + NL, one_c, sizeof one_c) == 0) ? 1 : 0;
+}
+#endif
+
+#if !SW
+typedef struct { pt p; int inf; } aff;  /* extended with Z = 1 (T = x y) */
+static void aload(aff* a, const u64* xy, int inf) {
+    a->inf = inf;
+    if (!inf) pload(&a->p, xy, 0);
+}
+static void aadd(pt* r, const pt* p, const aff* a, int neg) {
+    if (a->inf) { *r = *p; return; }
+    if (!neg) { padd(r, p, &a->p); return; }
+    pt q = a->p;
+    fe z = {{0}};
+    fsub(&q.x, &z, &q.x);
+    fsub(&q.t, &z, &q.t);
+    padd(r, p, &q);
 }
 #endif
 
@@ -393,6 +463,163 @@ int PFX(ref_msm)(const u64* bases, const uint8_t* inf, const u64* scalars, size_
     pstore(out_xy, out_inf, &acc);
     free(jobs);
     free(th);
+    return 0;
+}
+
+/* ------------------------------------------------ Pippenger baseline (SURVEY 8(d) "fair CPU bound")
+ * The same MSM by the bucket method on T threads: thread t runs a whole Pippenger over its point
+ * chunk [n t / T, n (t + 1) / T) -- signed c-bit digits (c ~ 0.69 log2(m) + 2, arkworks'
+ * ln_without_floats + 2), mixed bucket adds of affine bases, running-sum bucket reduction, Horner
+ * over windows -- and the T chunk sums are added. Exact group arithmetic: the affine result equals
+ * ref_msm's. Not a restatement of a reference line; it is the all-core CPU bound a fair
+ * comparison needs beside the 1-core naive port above. */
+static int pip_window(size_t m) {
+    int lg = 0;
+    while (((size_t)1 << (lg + 1)) <= m) lg++;
+    int c = lg * 69 / 100 + 2;
+    if (c < 2) c = 2;
+    if (c > 16) c = 16;
+    return c;
+}
+
+static void pip_chunk(const u64* bases, const uint8_t* inf, const u64* scalars, size_t lo, size_t hi, pt* out) {
+    pzero(out);
+    const size_t m = hi - lo;
+    if (m == 0) return;
+    const int c = pip_window(m);
+    const int W = (256 + 1 + c - 1) / c;  /* one spare bit absorbs the last carry */
+    const u64 mask = ((u64)1 << c) - 1;
+    const int64_t half = (int64_t)1 << (c - 1);
+    int32_t* dig = (int32_t*)malloc(sizeof(int32_t) * m * W);
+    aff* pts = (aff*)malloc(sizeof(aff) * m);
+    for (size_t i = 0; i < m; i++) {
+        aload(&pts[i], bases + (lo + i) * 2 * NL, inf ? inf[lo + i] : 0);
+        const u64* k = scalars + (lo + i) * 4;
+        int64_t carry = 0;
+        for (int w = 0; w < W; w++) {
+            const int b0 = w * c;
+            u64 raw = 0;
+            if (b0 < 256) {
+                const int q = b0 / 64, s = b0 % 64;
+                raw = k[q] >> s;
+                if (s && q + 1 < 4) raw |= k[q + 1] << (64 - s);
+            }
+            int64_t d = (int64_t)(raw & mask) + carry;
+            if (d > half) {
+                d -= (int64_t)1 << c;
+                carry = 1;
+            } else {
+                carry = 0;
+            }
+            dig[i * W + w] = (int32_t)d;
+        }
+    }
+    const size_t NB = (size_t)1 << (c - 1);
+    pt* bk = (pt*)malloc(sizeof(pt) * NB);
+    for (int w = W - 1; w >= 0; w--) {
+        for (int k = 0; k < c && w < W - 1; k++) pdbl(out, out);
+        for (size_t b = 0; b < NB; b++) pzero(&bk[b]);
+        for (size_t i = 0; i < m; i++) {
+            const int32_t d = dig[i * W + w];
+            if (d > 0) aadd(&bk[d - 1], &bk[d - 1], &pts[i], 0);
+            else if (d < 0) aadd(&bk[-d - 1], &bk[-d - 1], &pts[i], 1);
+        }
+        pt run, sum;
+        pzero(&run);
+        pzero(&sum);
+        for (size_t b = NB; b-- > 0;) {
+            padd(&run, &run, &bk[b]);
+            padd(&sum, &sum, &run);
+        }
+        padd(out, out, &sum);
+    }
+    free(bk);
+    free(pts);
+    free(dig);
+}
+
+typedef struct {
+    const u64* bases;
+    const uint8_t* inf;
+    const u64* scalars;
+    size_t lo, hi;     /* point chunk (pip_msm) or commit range (pip_msm_batch) */
+    size_t width;      /* 0: one chunk; else commits of `width` terms over bases[0, width) */
+    u64* out_xy;
+    uint8_t* out_inf;
+    pt acc;
+} pjob_t;
+
+static void* pip_job(void* arg) {
+    pjob_t* j = (pjob_t*)arg;
+    if (j->width == 0) {
+        pip_chunk(j->bases, j->inf, j->scalars, j->lo, j->hi, &j->acc);
+        return NULL;
+    }
+    for (size_t g = j->lo; g < j->hi; g++) {
+        pt r;
+        pip_chunk(j->bases, j->inf, j->scalars + g * j->width * 4, 0, j->width, &r);
+        pstore(j->out_xy + g * 2 * NL, j->out_inf + g, &r);
+    }
+    return NULL;
+}
+
+static void pip_run(pjob_t* jobs, int T) {
+    pthread_t* th = (pthread_t*)calloc(T, sizeof(pthread_t));
+    for (int t = 1; t < T; t++) pthread_create(&th[t], NULL, pip_job, &jobs[t]);
+    pip_job(&jobs[0]);
+    for (int t = 1; t < T; t++) pthread_join(th[t], NULL);
+    free(th);
+}
+
+int PFX(pip_msm)(const u64* bases, const uint8_t* inf, const u64* scalars, size_t n, int nthreads, u64* out_xy,
+                 uint8_t* out_inf) {
+    init();
+#if !SW
+    to_mont(&D_, D_CANON);
+#endif
+    int T = nthreads < 1 ? 1 : nthreads;
+    if ((size_t)T > n / 64) T = n / 64 ? (int)(n / 64) : 1;  /* at least 64 points per chunk */
+    pjob_t* jobs = (pjob_t*)calloc(T, sizeof(pjob_t));
+    for (int t = 0; t < T; t++) {
+        jobs[t].bases = bases;
+        jobs[t].inf = inf;
+        jobs[t].scalars = scalars;
+        jobs[t].lo = n * t / T;
+        jobs[t].hi = n * (t + 1) / T;
+    }
+    pip_run(jobs, T);
+    pt acc;
+    pzero(&acc);
+    for (int t = 0; t < T; t++) padd(&acc, &acc, &jobs[t].acc);
+    pstore(out_xy, out_inf, &acc);
+    free(jobs);
+    return 0;
+}
+
+/* `batch` commits of width terms each over bases[0, width) (scalars batch x width), commits split
+ * over T threads (the batched-commit baseline) */
+int PFX(pip_msm_batch)(const u64* bases, const uint8_t* inf, const u64* scalars, size_t width, size_t batch,
+                       int nthreads, u64* out_xy, uint8_t* out_inf) {
+    init();
+#if !SW
+    to_mont(&D_, D_CANON);
+#endif
+    if (width == 0) return -1;
+    int T = nthreads < 1 ? 1 : nthreads;
+    if ((size_t)T > batch) T = batch ? (int)batch : 1;
+    pjob_t* jobs = (pjob_t*)calloc(T, sizeof(pjob_t));
+    for (int t = 0; t < T; t++) {
+        jobs[t].bases = bases;
+        jobs[t].inf = inf;
+        jobs[t].scalars = scalars;
+        jobs[t].lo = batch * t / T;
+        jobs[t].hi = batch * (t + 1) / T;
+        jobs[t].width = width;
+        jobs[t].out_xy = out_xy;
+        jobs[t].out_inf = out_inf;
+    }
+    pip_run(jobs, T);
+    free(jobs);
     return 0;
 }
 

@@ -86,3 +86,45 @@ def on_curve(curve_name, bases):
     bases = np.ascontiguousarray(bases, dtype=np.uint64)
     fn = getattr(lib(), curve_name + "_ref_on_curve")
     return bool(fn(bases.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(bases.shape[0])))
+
+
+def pip_msm_arrays(curve_name, bases, inf, scalars, nthreads=1):
+    """Pippenger baseline (bucket method on `nthreads` threads, point chunks): same result as
+    msm_arrays. bases: (n, 2*NL) uint64 canonical; scalars: (n, 4) uint64 canonical."""
+    nl = NL[curve_name]
+    n = scalars.shape[0]
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    infp = None
+    if inf is not None:
+        inf = np.ascontiguousarray(inf, dtype=np.uint8)
+        infp = inf.ctypes.data_as(ctypes.c_void_p)
+    out = np.zeros(2 * nl, dtype=np.uint64)
+    oinf = np.zeros(1, dtype=np.uint8)
+    fn = getattr(lib(), curve_name + "_pip_msm")
+    fn.restype = ctypes.c_int
+    fn(bases.ctypes.data_as(ctypes.c_void_p), infp, scalars.ctypes.data_as(ctypes.c_void_p),
+       ctypes.c_size_t(n), ctypes.c_int(nthreads), out.ctypes.data_as(ctypes.c_void_p),
+       oinf.ctypes.data_as(ctypes.c_void_p))
+    return out, int(oinf[0])
+
+
+def pip_msm_batch_arrays(curve_name, bases, inf, scalars, width, nthreads=1):
+    """`batch` commits of `width` terms over bases[:width] (scalars (batch*width, 4)), commits
+    split over threads. Returns ((batch, 2*NL) xy, (batch,) inf)."""
+    nl = NL[curve_name]
+    batch = scalars.shape[0] // width
+    bases = np.ascontiguousarray(bases, dtype=np.uint64)
+    scalars = np.ascontiguousarray(scalars, dtype=np.uint64)
+    infp = None
+    if inf is not None:
+        inf = np.ascontiguousarray(inf, dtype=np.uint8)
+        infp = inf.ctypes.data_as(ctypes.c_void_p)
+    out = np.zeros((batch, 2 * nl), dtype=np.uint64)
+    oinf = np.zeros(batch, dtype=np.uint8)
+    fn = getattr(lib(), curve_name + "_pip_msm_batch")
+    fn.restype = ctypes.c_int
+    fn(bases.ctypes.data_as(ctypes.c_void_p), infp, scalars.ctypes.data_as(ctypes.c_void_p),
+       ctypes.c_size_t(width), ctypes.c_size_t(batch), ctypes.c_int(nthreads),
+       out.ctypes.data_as(ctypes.c_void_p), oinf.ctypes.data_as(ctypes.c_void_p))
+    return out, oinf

@@ -162,3 +162,43 @@ def test_golden_multiproof_verifies_and_tamper():
         vq2 = list(vq)
         vq2[0] = (vq[0][0], vq[0][1], (vq[0][2] + 1) % BN254.r)
         assert not protocol.verify_multiproof(vc, vq2, mp)
+
+
+@pytest.mark.parametrize("curve", ["bn254", "bls12_381", "bandersnatch"])
+def test_pippenger_baseline_matches_naive(oracle_c, curve):
+    """the all-core CPU Pippenger baseline (bench cpu_baseline leg) == the naive restatement of
+    utils.rs:16-19 on golden cases (identities, zero / r-1 scalars) and random sizes."""
+    import numpy as np
+    from pyoracle.curves import CURVES, random_points
+    C = CURVES[curve]
+    cases = [c for c in load("msm.json")["cases"] if c["curve"] == curve]
+    rng = random.Random(9)
+    for n in (64, 200, 1500):
+        pts = random_points(C, n, rng)
+        sc = [rng.randrange(C.r) for _ in pts]
+        sc[0], sc[1], sc[2] = 0, C.r - 1, 1
+        cases.append({"bases": pts, "scalars": sc})
+    for case in cases:
+        pts = [P(b) if isinstance(b, list) or b is None else b for b in case["bases"]]
+        if C.kind == "te":
+            pts = [(0, 1) if p is None else p for p in pts]
+        sc = [int(s, 16) if isinstance(s, str) else s for s in case["scalars"]]
+        arr, inf = oracle_c.points_to_array(curve, pts)
+        lim = oracle_c.ints_to_limbs(sc, 4)
+        want = oracle_c.msm_arrays(curve, arr, inf, lim, 2)
+        for T in (1, 3):
+            got = oracle_c.pip_msm_arrays(curve, arr, inf, lim, T)
+            assert got[1] == want[1] and np.array_equal(got[0], want[0]), (curve, len(pts), T)
+
+
+def test_pippenger_batch_baseline(oracle_c):
+    import numpy as np
+    from pyoracle.curves import BANDERSNATCH, random_points
+    rng = random.Random(4)
+    pts = random_points(BANDERSNATCH, 256, rng)
+    arr, inf = oracle_c.points_to_array("bandersnatch", pts)
+    sc = oracle_c.ints_to_limbs([rng.randrange(BANDERSNATCH.r) for _ in range(256 * 5)], 4)
+    xy, oinf = oracle_c.pip_msm_batch_arrays("bandersnatch", arr, inf, sc, 256, 3)
+    for j in range(5):
+        w = oracle_c.msm_arrays("bandersnatch", arr, inf, sc[j * 256:(j + 1) * 256], 2)
+        assert np.array_equal(xy[j], w[0]) and oinf[j] == w[1]
