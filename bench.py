@@ -294,10 +294,65 @@ def mp_line(a, rank, world, local, dev, stream):
     lib().vc_transcript_free(tr)
     meng.close()
     alg = Q * N * 32 + Q * 64 + Q * 40
-    return {"workload": f"IPA multiproof, Q = 2^{a.mp_log_q} width-256 queries, BN254 (configs[4]), query set "
-                        f"split over {world} rank(s)", "ms_per_multiproof": dt * 1e3,
-            "host_transcript_ms": t_begin * 1e3, "kernel_ms": kms, "algorithmic_bytes_per_unit": alg,
-            "achieved_GBps": alg / dt / 1e9, "d_inf": mp["d"] is None}
+    out = {"workload": f"IPA multiproof, Q = 2^{a.mp_log_q} width-256 queries, BN254 (configs[4]), query set "
+                       f"split over {world} rank(s)", "ms_per_multiproof": dt * 1e3,
+           "host_transcript_ms": t_begin * 1e3, "kernel_ms": kms, "algorithmic_bytes_per_unit": alg,
+           "achieved_GBps": alg / dt / 1e9, "d_inf": mp["d"] is None}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_multiproof(N, data, z, cxy, crs, a.cpu_threads or min(16, os.cpu_count() or 1))
+    return out
+
+
+def cpu_multiproof(N, data, z, cxy, crs, threads):
+    """configs[4] on the CPU, the reference's prove_multiproof (multiproof.rs:99-176) restated:
+    transcript bytes (Q x (C, z, y) records) hashed with SHA-256 (hashlib), the field phases in C
+    with the reference's thread structure (oracle/c/ref_multiproof.c: scaling par_iter over
+    queries, grouped quotients par_bridge over points, g and h serial) on `threads` threads, the
+    D and E commits by the naive inner_product in C (utils.rs:16-19, what IPA::commit runs), and
+    the inner IPA proof as its 8 rounds of L / R commits and generator folds (naive per-term
+    scalar multiplications of the same sizes). Challenges r, t are random field elements (their
+    values do not change the work)."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import cref  # CPU baseline leg only
+    from pyoracle import protocol
+    Q = z.shape[0]
+    r_mod = vkzg.SCALAR_R["bn254"]
+    rng = np.random.default_rng(5)
+    r, t = (int.from_bytes(rng.bytes(32), "little") % r_mod for _ in range(2))
+    crs_xy, crs_inf = cref.points_to_array("bn254", crs)
+    omega = protocol.group_gen(N)
+    t0 = time.perf_counter()
+    rec = np.zeros((Q, 75), dtype=np.uint8)           # "C" x[32] "z" z[8] "y" y[32]
+    rec[:, 0], rec[:, 33], rec[:, 42] = ord("C"), ord("z"), ord("y")
+    rec[:, 1:33] = np.ascontiguousarray(cxy[:, :4]).view(np.uint8).reshape(Q, 32)
+    rec[:, 34:42] = np.ascontiguousarray(z).view(np.uint8).reshape(Q, 8)
+    rec[:, 43:75] = np.ascontiguousarray(data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)]).view(
+        np.uint8).reshape(Q, 32)
+    hashlib.sha256(rec.tobytes()).digest()
+    t_tr = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    g, h = cref.mp_field_phases(N, data, z, r, t, omega, threads)
+    t_field = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cref.msm_arrays("bn254", crs_xy[:N], crs_inf[:N], g, 1)
+    cref.msm_arrays("bn254", crs_xy[:N], crs_inf[:N], h, 1)
+    t_commit = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    m = N
+    sc = np.asarray(g, dtype=np.uint64)
+    while m > 1:                                      # L, R and the fold of G each round
+        for _ in range(3):
+            cref.msm_arrays("bn254", crs_xy[:m // 2], crs_inf[:m // 2], sc[:m // 2], 1)
+        m //= 2
+    t_ipa = time.perf_counter() - t0
+    total = t_tr + t_field + t_commit + t_ipa
+    return {"value": 1.0 / total, "unit": "multiproofs/s", "ms_per_multiproof": total * 1e3, "cores": threads,
+            "kind": "port", "parts_ms": {"transcript_sha256": t_tr * 1e3, "field_phases": t_field * 1e3,
+                                         "d_e_commits_naive": t_commit * 1e3, "inner_ipa_naive": t_ipa * 1e3},
+            "sample": f"the full Q = {Q} x N = {N} workload once: field phases in C on {threads} threads with the "
+                      "reference's rayon structure (oracle/c/ref_multiproof.c), naive commits / IPA rounds in C "
+                      "(1 thread, as the reference's serial IPA), SHA-256 transcript via hashlib"}
 
 
 def ipa_line(local, stream, batch=256):

@@ -128,3 +128,24 @@ def pip_msm_batch_arrays(curve_name, bases, inf, scalars, width, nthreads=1):
        ctypes.c_size_t(width), ctypes.c_size_t(batch), ctypes.c_int(nthreads),
        out.ctypes.data_as(ctypes.c_void_p), oinf.ctypes.data_as(ctypes.c_void_p))
     return out, oinf
+
+
+def mp_field_phases(N, data, z, r, t, omega, nthreads=1):
+    """C restatement of prove_multiproof's field phases over BN254 Fr (oracle/c/ref_multiproof.c):
+    data (Q, N, 4) or (Q*N, 4) uint64 canonical, z (Q,) point indices, r / t / omega ints.
+    Returns (g, h): (N, 4) uint64 canonical each."""
+    data = np.ascontiguousarray(data, dtype=np.uint64)
+    z = np.ascontiguousarray(z, dtype=np.uint64)
+    Q = z.shape[0]
+    limbs = [ints_to_limbs([int(v)], 4)[0] for v in (r, t, omega)]
+    g = np.zeros((N, 4), dtype=np.uint64)
+    h = np.zeros((N, 4), dtype=np.uint64)
+    fn = lib().bn254fr_mp_field_phases
+    fn.restype = ctypes.c_int
+    st = fn(ctypes.c_size_t(N), ctypes.c_size_t(Q), data.ctypes.data_as(ctypes.c_void_p),
+            z.ctypes.data_as(ctypes.c_void_p), limbs[0].ctypes.data_as(ctypes.c_void_p),
+            limbs[1].ctypes.data_as(ctypes.c_void_p), limbs[2].ctypes.data_as(ctypes.c_void_p),
+            ctypes.c_int(nthreads), g.ctypes.data_as(ctypes.c_void_p), h.ctypes.data_as(ctypes.c_void_p))
+    if st != 0:
+        raise ValueError("bn254fr_mp_field_phases: bad argument")
+    return g, h

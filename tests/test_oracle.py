@@ -202,3 +202,36 @@ def test_pippenger_batch_baseline(oracle_c):
     for j in range(5):
         w = oracle_c.msm_arrays("bandersnatch", arr, inf, sc[j * 256:(j + 1) * 256], 2)
         assert np.array_equal(xy[j], w[0]) and oinf[j] == w[1]
+
+
+def test_multiproof_field_phases_c_vs_python(oracle_c):
+    """the C restatement of prove_multiproof's field phases (CPU baseline of configs[4]) == the
+    Python restatement's g and h (multiproof.rs:117-165) for arbitrary challenges r, t."""
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    r_mod = BN254.r
+    rng = random.Random(12)
+    N, Q = 32, 23
+    pre = protocol.PrecomputedLagrange(N)
+    datas = [[rng.randrange(r_mod) for _ in range(N)] for _ in range(Q)]
+    z = [rng.randrange(N) for _ in range(Q)]
+    z[3] = z[7] = z[11]                                     # repeated points are grouped
+    rr, t = rng.randrange(r_mod), rng.randrange(N, r_mod)
+    rp = protocol.powers_of(rr, Q, r_mod)
+    groups = {}
+    for i in range(Q):
+        groups.setdefault(z[i], []).append([v * rp[i] % r_mod for v in datas[i]])
+    g, h = [0] * N, [0] * N
+    invs = protocol.invert_domain_at(t, N, r_mod)
+    for zz, lst in groups.items():
+        total = [sum(col) % r_mod for col in zip(*lst)]
+        q = protocol.LagrangeBasis(total, N).divide_by_vanishing(pre, zz)
+        g = [(a + b) % r_mod for a, b in zip(g, q)]
+        for ev in lst:
+            h = [(a + b * invs[zz]) % r_mod for a, b in zip(h, ev)]
+    data = oracle_c.ints_to_limbs([v for d in datas for v in d], 4)
+    import numpy as np
+    for T in (1, 4):
+        cg, ch = oracle_c.mp_field_phases(N, data, np.array(z, dtype=np.uint64), rr, t, pre.omega, T)
+        assert [oracle_c.limbs_to_int(x) for x in cg] == g
+        assert [oracle_c.limbs_to_int(x) for x in ch] == h
