@@ -630,7 +630,7 @@ def main():
                    "exchange": comm_kind,
                    "window_bits": c_bits, "windows": w_total,
                    "precomputed_bases": (f"{w_total} x 2n shifted window copies 2^(c w) P_i, 2^(c w) phi(P_i) "
-                                         f"({w_total * 2 * n * 96 / 1e9:.2f} GB), built once per base table "
+                                         f"({w_total * 2 * n * 112 / 1e9:.2f} GB), built once per base table "
                                          "(a fixed CRS), untimed; `variable_base` is the same MSM without them")
                    if curve == "bls12_381" else None},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -699,7 +699,7 @@ def main():
             return {"window_bits": cw, "commits_per_s": B / cdt, "ms_per_batch": cdt * 1e3,
                     "fb_commit_kernel_ms": fb_ms / fb_n if fb_n else None,
                     "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
-                    "table_bytes": 256 * ((253 + 1 + cw - 1) // cw) * (1 << (cw - 1)) * 96}
+                    "table_bytes": 256 * ((253 + 1 + cw - 1) // cw) * (1 << (cw - 1)) * 108}  # FbE: 3 x 9 limbs
 
         big = ctime(a.commit_window)
         small = ctime(16) if a.commit_window != 16 else big

@@ -39,6 +39,17 @@ static void run(const char* name) {
         printf("{\"f\":\"%s\",\"op\":\"mul\",", name); pr("a", a); printf(","); pr("b", b); printf(","); pr("r", r); printf("}\n");
         f29<P> q = sqr29<P>(a);
         printf("{\"f\":\"%s\",\"op\":\"mul\",", name); pr("a", a); printf(","); pr("b", a); printf(","); pr("r", q); printf("}\n");
+        // products of carry-less sums (add29_raw): one raw operand at every L, two at L <= 9 (the
+        // Edwards mixed add's (X + Y)(x + y)); stress operands put every limb at 2^30 + 14
+        {
+            const f29<P> ra = add29_raw<P>(a, b), rb = add29_raw<P>(b, a);
+            const f29<P> r1 = mul29<P>(ra, b);
+            printf("{\"f\":\"%s\",\"op\":\"mul\",", name); pr("a", ra); printf(","); pr("b", b); printf(","); pr("r", r1); printf("}\n");
+            if constexpr (P::L <= 9) {
+                const f29<P> r2 = mul29<P>(ra, rb);
+                printf("{\"f\":\"%s\",\"op\":\"mul\",", name); pr("a", ra); printf(","); pr("b", rb); printf(","); pr("r", r2); printf("}\n");
+            }
+        }
         f29<P> s = add29<P>(a, b);
         printf("{\"f\":\"%s\",\"op\":\"add\",", name); pr("a", a); printf(","); pr("b", b); printf(","); pr("r", s); printf("}\n");
         // subtrahend below p (a mul output): sub2 / sub4 / sub16

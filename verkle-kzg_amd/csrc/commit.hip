@@ -23,13 +23,16 @@
 
 namespace vk {
 
-// Table entry (kept as a type so the layout can change in one place).
+// Table entry (kept as a type so the layout can change in one place): the radix-2^29 limbs the
+// mixed add consumes (ec29.hpp Aff, 4 B per 29-bit limb: 108 B for Bandersnatch's x, y, d x y),
+// so the loop reads operands with no unpacking (~53 of 2,250 instructions per Edwards add).
+// Padding the packed 96-B form to 128 B was measured slower (4.54 -> 4.93 ms at c = 16).
 template <class C>
-struct FbEntryNoPad {
-    typename C::Aff a;
+struct FbEntryLimbs {
+    typename Fast29<C>::type::Aff u;
 };
 template <class C>
-using FbE = FbEntryNoPad<C>;  // padding 96 -> 128 B measured slower (4.54 -> 4.93 ms at c = 16)
+using FbE = FbEntryLimbs<C>;
 
 // copy one window's normalised multiples into the table: tab[(i*W + w)*NBk + k] = aff[i*NBk + k],
 // in the packed-29 form the commit loops read
@@ -39,7 +42,10 @@ __global__ void k_fb_place(const typename C::Aff* __restrict__ aff, uint32_t n, 
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= (size_t)n * NBk) return;
     size_t i = j / NBk, k = j - i * NBk;
-    Fast29<C>::type::pack_aff(aff[j], &tab[(i * W + w) * NBk + k].a);  // packed-29 (ec29.hpp)
+    using FC = typename Fast29<C>::type;
+    typename C::Aff packed;
+    FC::pack_aff(aff[j], &packed);  // canonical x R'
+    tab[(i * W + w) * NBk + k].u = FC::load(&packed);
 }
 
 template <class Fr>
@@ -208,15 +214,15 @@ __global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>
             return carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
         };
         int32_t dn = next_digit();
-        typename C::Aff Pn = ti[dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0].a;
+        typename FC::Aff Pn = ti[dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0].u;
         for (int w = 0; w < W; w++) {
             const int32_t d = dn;
-            const typename C::Aff P = Pn;
+            const typename FC::Aff P = Pn;
             if (w + 1 < W) {
                 dn = next_digit();
-                Pn = ti[(size_t)(w + 1) * NBk + (dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0)].a;
+                Pn = ti[(size_t)(w + 1) * NBk + (dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0)].u;
             }
-            if (d != 0) acc = FC::madd(acc, FC::load(&P), d < 0);
+            if (d != 0) acc = FC::madd(acc, P, d < 0);
         }
     }
     piece[r] = acc;
@@ -260,7 +266,6 @@ __global__ void __launch_bounds__(64) k_fb_combine_wave(const typename Fast29<C>
     }
     if (lane == 0) out[g] = FC::store(v);
 }
-
 // ---- latency path for small batches (the IPA prover's L/R, multiproof D/E): every thread
 // adds the table points of WPT windows of one base, then a wave butterfly and an LDS step
 // fold the block to one partial; k_fb_combine_small adds a commit's few block partials.
@@ -314,7 +319,7 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
             carry = raw > half ? 1u : 0u;
             const int32_t d = carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
             if (w >= wb && d != 0)
-                fa = FC::madd(fa, FC::load(&ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].a), d < 0);
+                fa = FC::madd(fa, ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].u, d < 0);
         }
     }
     Acc acc = FC::store(fb_wave_sum29<FC>(fa));

@@ -87,6 +87,7 @@ struct Table {
     // window w ([w][2n] layout), so all windows share one set of buckets (msm.hip, "shared
     // windows"); built on first use for the window size c in win_c
     int win_ok = 0, win_c = 0, win_W = 0, win_ts = 0;
+    int win_limbs = 1;  // copies in radix-2^29 limbs (1) or packed-29 (0, VKZG_WIN_PACKED probe)
     DevBuf win;
 };
 

@@ -42,6 +42,8 @@ struct SW29 {
         a.y = unpack29<P>(p->y.v);
         return a;
     }
+    // a table point already in limbs (fixed-base tables, commit.hip FbE)
+    VK_HD static Aff load(const Aff* p) { return *p; }
     VK_HD static Acc dbl_aff(const f29<P>& x, const f29<P>& y) {
         const f29<P> U = add29<P>(y, y);
         const f29<P> V = sqr29<P>(U);
@@ -174,18 +176,25 @@ struct TE29 {
         a.kt = unpack29<P>(p->kt.v);
         return a;
     }
+    VK_HD static Aff load(const Aff* p) { return *p; }
     // unified mixed add (add-2008-hwcd, Z2 = 1, kt = d x2 y2): complete, no exceptions
     VK_HD static Acc madd(const Acc& p, const Aff& q, bool neg) {
         const f29<P> x2 = neg ? neg29<P, 2>(q.x) : q.x;
         const f29<P> kt = neg ? neg29<P, 2>(q.kt) : q.kt;
+        static_assert(P::L <= 9, "raw x raw operands of mul29 (add29_raw) need L <= 9");
         const f29<P> A = mul29<P>(p.X, x2);
         const f29<P> B = mul29<P>(p.Y, q.y);
         const f29<P> Cc = mul29<P>(p.T, kt);
-        const f29<P> E = sub2_29<P, 8>(mul29<P>(add29<P>(p.X, p.Y), add29<P>(x2, q.y)), A, B);
+        // sums that only feed products skip the carry pass (add29_raw): X + Y and x2 + y2 are both
+        // raw operands of one product, G = Z + C a raw operand of two
+        const f29<P> E = sub2_29<P, 8>(mul29<P>(add29_raw<P>(p.X, p.Y), add29_raw<P>(x2, q.y)), A, B);
         const f29<P> Fv = sub29<P, 4>(p.Z, Cc);
-        const f29<P> G = add29<P>(p.Z, Cc);
-        const f29<P> A2 = add29<P>(A, A);
-        const f29<P> H = add29<P>(B, add29<P>(add29<P>(A2, A2), A));  // B - a A, a = -5
+        const f29<P> G = add29_raw<P>(p.Z, Cc);
+        // H = B - a A = B + 5 A (a = -5): limb-wise < 2^31.6, one carry pass
+        f29<P> H;
+#pragma unroll
+        for (int j = 0; j < P::L; j++) H.v[j] = B.v[j] + 5u * A.v[j];
+        H = norm29<P>(H);
         Acc r;
         r.X = mul29<P>(E, Fv);
         r.Y = mul29<P>(G, H);

@@ -52,6 +52,19 @@ VK_HD f29<P> add29(const f29<P>& a, const f29<P>& b) {
     return norm29<P>(r);
 }
 
+// a + b without the carry pass: limbs <= 2^30 + 14 (inputs almost normalised). Only as a mul29
+// operand (or the subtrahend of sub29, whose subK limbs cover 2^30 + 8 -- not the sum of two
+// raw values), and only where the column bound holds: one raw operand keeps L products of
+// 2^59 + L of 2^58 below 2^63.4 up to L = 14; two raw operands (products < 2^60.01) need L <= 9
+// (9 x 2^60.01 + 9 x 2^58 < 2^63.5).
+template <class P>
+VK_HD f29<P> add29_raw(const f29<P>& a, const f29<P>& b) {
+    f29<P> r;
+#pragma unroll
+    for (int j = 0; j < P::L; j++) r.v[j] = a.v[j] + b.v[j];
+    return r;
+}
+
 // a - b + K p (K = 2..32, a constant of the generator): b's value must be below (K - 1) p
 // and its limbs (after an add) below 2^30 + 8
 template <class P, int K>

@@ -261,15 +261,17 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
 // the fix-up and the reduction (msm_tail.hip), which run the same arithmetic; converting them
 // to the ec.hpp form at the three store sites (4 multiplies each) put ~50 KB of rarely-run code
 // into the loop and cost 7 % of the kernel.
-template <class C>
+// BT: the base entry type -- packed-29 C::Aff (tables, window copies) or the limb form of the
+// fixed-base tables the sparse commits read (Fast29<C>::type::Aff, commit.hip FbE)
+template <class C, class BT = typename C::Aff>
 __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
-    const typename C::Aff* __restrict__ bases, const typename C::Aff* __restrict__ phi, uint32_t nphi,
+    const BT* __restrict__ bases, const BT* __restrict__ phi, uint32_t nphi,
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename Fast29<C>::type::Acc* __restrict__ buckets, typename Fast29<C>::type::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename Fast29<C>::type::Acc* __restrict__ owner_piece,
     uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max) {
     using FC = typename Fast29<C>::type;
-    using Aff = typename C::Aff;
+    using Aff = BT;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t L = offsets[NBtot];  // entry count, read on the device: no host round trip
     uint32_t k = t * M;                 // grid sized for the n*W upper bound
@@ -343,6 +345,18 @@ __global__ void __launch_bounds__(256) k_to_fast(const typename C::Aff* __restri
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fast29<C>::type::pack_aff(in[i], out + i);
+}
+// ... or straight to radix-2^29 limbs (the shared-window copies: the accumulate reads them with
+// no unpacking, 112 instead of 96 B per BLS12-381 point)
+template <class C>
+__global__ void __launch_bounds__(256) k_to_limbs(const typename C::Aff* __restrict__ in, size_t n,
+                                                 typename Fast29<C>::type::Aff* __restrict__ out) {
+    using FC = typename Fast29<C>::type;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    typename C::Aff packed;
+    FC::pack_aff(in[i], &packed);
+    out[i] = FC::load(&packed);
 }
 
 // ------------------------------------------------------------------ GLV endomorphism (BLS12-381 G1)
@@ -593,12 +607,17 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
     if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts) return VC_OK;
     const size_t n = t->n;
     t->win_ok = 0;
-    VK_TRY(t->win.ensure((size_t)W * 2 * n * sizeof(Aff)));
+    using FA = typename Fast29<C>::type::Aff;  // limb form (k_to_limbs)
+    // VKZG_WIN_PACKED=1 keeps the packed-29 form (A/B probe: unpacking costs the accumulate ~84 of
+    // 5,044 instructions per add, the limb form 16 B more per gather)
+    static const bool packed = getenv("VKZG_WIN_PACKED") != nullptr;
+    t->win_limbs = packed ? 0 : 1;
+    VK_TRY(t->win.ensure((size_t)W * 2 * n * (packed ? sizeof(Aff) : sizeof(FA))));
     Table cur;  // 2^(c w) P (affine, Montgomery): normalised by table_from_acc (commit.hip)
     DevBuf nxt, acc;
     VK_TRY(nxt.ensure(n * sizeof(Aff)));
     VK_TRY(acc.ensure(n * sizeof(Acc)));
-    Aff* win = t->win.as<Aff>();
+    FA* win = t->win.as<FA>();
     const unsigned g = (unsigned)((n + 255) / 256);
     for (int w = 0; w < W; w++) {
         const Aff* src = t->bases.as<Aff>();
@@ -609,9 +628,15 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
             VK_TRY(table_from_acc(ctx, &cur, acc.p, n));
             src = cur.bases.as<Aff>();
         }
-        VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, src, n, win + (size_t)w * 2 * n);
         VK_LAUNCH(ctx, "glv_phi", (k_glv_phi<C>), g, 256, 0, src, (uint32_t)n, bls_fq_mont(GLV_BETA), nxt.as<Aff>());
-        VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, nxt.as<Aff>(), n, win + (size_t)w * 2 * n + n);
+        if (packed) {
+            Aff* wp = t->win.as<Aff>();
+            VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, src, n, wp + (size_t)w * 2 * n);
+            VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, nxt.as<Aff>(), n, wp + (size_t)w * 2 * n + n);
+        } else {
+            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs<C>), g, 256, 0, src, n, win + (size_t)w * 2 * n);
+            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs<C>), g, 256, 0, nxt.as<Aff>(), n, win + (size_t)w * 2 * n + n);
+        }
     }
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // before the staging buffers are freed
     t->win_ok = 1;
@@ -720,9 +745,9 @@ struct MsmSlice {
     uint32_t Lmax = 0;
 };
 
-template <class C, class Src>
-static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const typename C::Aff* bases,
-                         const typename C::Aff* phi, uint32_t nphi, hipEvent_t acc_wait, hipEvent_t acc_done) {
+template <class C, class BT, class Src>
+static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const BT* bases, const BT* phi,
+                         uint32_t nphi, hipEvent_t acc_wait, hipEvent_t acc_done) {
     using Acc = typename C::Acc;
     using RAcc = FAcc<C>;  // raw radix-29 accumulators of the accumulate / fix-up / reduction
     const Lane L = sl.L;
@@ -819,7 +844,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W;
     // chain_max was cleared by k_sort_fine
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
-    VK_LAUNCH_ON(ctx, st, "msm_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi,
+    VK_LAUNCH_ON(ctx, st, "msm_accumulate", (k_msm_accumulate<C, BT>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi,
                  ws[WS_SORTED].as<uint32_t>(), sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
                  sl.owner_b, sl.chain_max);
     if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
@@ -918,7 +943,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         // top window: GLV_BITS - cs (Ws - 1) bits -> digits up to 2^tb; scaled to fill 2^(cs-1)
         const int tb = GLV_BITS - cs * (Ws - 1);
         const int ts = std::max(0, (cs - 1) - tb);
-        const size_t win_bytes = (size_t)Ws * 2 * t->n * sizeof(Aff);
+        const size_t win_bytes = (size_t)Ws * 2 * t->n * sizeof(typename Fast29<C>::type::Aff);
         if (glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
             const int st = win_tables<C>(ctx, t, cs, Ws, ts);
             if (st == VC_OK) {
@@ -975,16 +1000,24 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                 VK_CHECK_HIP(hipEventRecord(fork, ctx->stream));
                 VK_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, fork, 0));
             }
-            const Aff* win = t->win.as<Aff>();  // [w][2n]: entry w * 2n + i (sort_entries' stride)
+            // [w][2n] limb-form copies: entry w * 2n + i (sort_entries' stride)
+            const auto* win = t->win.as<typename Fast29<C>::type::Aff>();
             GlvDigits src{halves, inf, (uint32_t)n};
             if (shared && top_shift > 0) {
                 src.tw = Wfull - 1;
                 src.ts = top_shift;
             }
-            for (int k = 0; k < nsl; k++)
-                VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, shared ? win : bases,
-                                        shared ? win : dphi, shared ? 0xffffffffu : (uint32_t)n,
-                                        k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
+            for (int k = 0; k < nsl; k++) {
+                if (shared && !t->win_limbs)
+                    VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, t->win.as<Aff>(), t->win.as<Aff>(), 0xffffffffu,
+                                            k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
+                else if (shared)
+                    VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, win, win, 0xffffffffu, k == 1 ? acc0 : nullptr,
+                                            k == 0 ? acc0 : nullptr));
+                else
+                    VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, bases, dphi, (uint32_t)n, k == 1 ? acc0 : nullptr,
+                                            k == 0 ? acc0 : nullptr));
+            }
         }
     } else {
         if (nsl == 2) {
@@ -1102,7 +1135,6 @@ template <class C, class Fr>
 static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                               const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf) {
     using Acc = typename C::Acc;
-    using Aff = typename C::Aff;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
     for (size_t g = 0; g < batch; g++)
@@ -1187,7 +1219,9 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
                   d_cols.as<uint32_t>(), nnz, mont, c, W, d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
     VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, d_rp.as<uint64_t>(),
               d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
-    const Aff* tab = t->fb.as<Aff>();
+    // the fixed-base tables hold radix-2^29 limbs (commit.hip FbE): k_msm_accumulate<C, FA>
+    using FA = typename Fast29<C>::type::Aff;
+    const FA* tab = t->fb.as<FA>();
     if (Tmax > 0) {  // all-zero rows only: k_sparse_rows already set every chunk to the identity
         VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
         uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
@@ -1195,7 +1229,7 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         using RAcc = FAcc<C>;
         DevBuf& d_raw = ctx->ws[WS_RAW_B];
         VK_TRY(d_raw.ensure(nch * sizeof(RAcc)));
-        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
+        VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C, FA>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
                   d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
                   d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max);
         VK_TRY(msm_tail_fixup<C>(ctx, ctx->lane(0), Tmax, d_off.as<uint32_t>() + nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
