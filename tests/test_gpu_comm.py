@@ -232,3 +232,56 @@ def test_rccl_world_one():
     finally:
         c.close()
         eng.close()
+
+
+def _proc_rank(rank, world, port, q):
+    """one process per rank (as in deployment), each with its own vc_ctx on the one card, the
+    exchange through vc_comm_init_host over a gloo group (RCCL cannot put two ranks on one GPU)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "verkle-kzg_amd")]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import vkzg
+    from vkzg import comm as vcomm
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = vkzg.Engine("bls12_381", 0)
+        c = vcomm.Comm.host(rank, world, vcomm.torch_allgather())
+        n = 1 << 16
+        tab = eng.random_bases(n, seed=44)
+        sc = vkzg.random_scalars("bls12_381", n, np.random.default_rng(8))
+        d = torch.from_numpy(sc.view(np.int64).copy()).cuda()
+        torch.cuda.synchronize()
+        xy, inf = c.msm(eng, tab, d.data_ptr(), n)
+        wxy, winf = eng.msm(tab, sc)
+        q.put((rank, bool(inf == winf and np.array_equal(xy, wxy))))
+        c.close()
+        eng.close()
+    except Exception as ex:  # reported to the parent
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_msm_sharded_two_processes():
+    """vc_msm_sharded across two processes (one vc_ctx each, shared-window GLV MSM of 2^16 points,
+    window slices, gloo all-gather through the callback transport) == the single-process MSM."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_proc_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == [(0, True), (1, True)], res
