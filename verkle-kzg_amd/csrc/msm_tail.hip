@@ -220,6 +220,38 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
     if (lane == 0) out[sum] = A::store(v);
 }
 
+// the same on quads (SW curves): 16 logical lanes per wave, each a quad running the 4-lane
+// cooperative add (SW29::add_quad: ~3,100 instead of ~6,600 instructions per add). This stage is
+// latency-bound -- one wave per sum, W (J + 1) waves on 1024 SIMDs -- so the shorter add pays even
+// though a 52-partial sum then takes ceil(52 / 16) + 4 = 8 adds instead of 1 + 6 = 7.
+template <class C, class A>
+__global__ void __launch_bounds__(64) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial, uint32_t J,
+                                                     uint32_t nb1, uint32_t nb2, typename C::Acc* __restrict__ out) {
+    using Acc = typename A::Acc;
+    const uint32_t sum = blockIdx.x, lane = threadIdx.x, ql = lane >> 2, role = lane & 3;
+    const uint32_t w = sum / (J + 1), q = sum % (J + 1);
+    const uint32_t cnt = q < J ? nb1 : nb2;
+    const size_t start = (size_t)w * (J * nb1 + nb2) + (q < J ? q * nb1 : J * nb1);
+    uint32_t span = 1, lg = 0;
+    while (span < cnt && span < 16) {
+        span <<= 1;
+        lg++;
+    }
+    const uint32_t nk = (cnt + 15) / 16;
+    Acc v = A::zero();
+    for (uint32_t it = 0; it < nk + lg; it++) {  // one add call site
+        Acc o;
+        if (it < nk) {
+            const uint32_t k = ql + it * 16;
+            o = k < cnt ? partial[start + k] : A::zero();
+        } else {
+            o = shfl_acc<A>(v, 4u << (it - nk));  // quad to quad: xor of a multiple of 4
+        }
+        v = A::add_quad(v, o, role);
+    }
+    if (lane == 0) out[sum] = A::store(v);
+}
+
 // pointer-jumping rounds r0 <= r < r1 (span 2^r) for a host-known Lmax, or -- guarded -- rounds
 // whose kernels compare span with the device's chain_max: no host sync in the pipeline;
 // msm_tail_fixup_more finishes the rare longer chains afterwards. The carry pieces ping-pong
@@ -318,7 +350,10 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
     const uint32_t n_waves = (uint32_t)W * (J * nb1 + nb2);
     VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
               n_waves, live, partial);
-    VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
+    if constexpr (A::quad)
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
+    else
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
     return VC_OK;
 }
 

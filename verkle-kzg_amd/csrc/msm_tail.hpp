@@ -5,21 +5,25 @@
 #include "ec29.hpp"
 
 namespace vk {
-// items per lane of the bit-sum stage: the smallest K in [2, 16] whose busy waves (a wave per
-// 64 K items of each of the W (J + 1) sums) fit one wave per SIMD (1024): a wave costs K + 6
-// serial adds (its butterfly included) and a SIMD's second wave doubles its time, so fewer,
-// longer waves win until every SIMD has one (measured: 1192 busy waves at K = 7 took 2x the
-// 960 of K = 8 on a GLV 2^20 MSM)
-inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J) {
-    for (uint32_t k = 2; k < 16; k++) {
-        const uint64_t per = 64ull * k;
+// items per lane of the bit-sum stage: the smallest K in [2, 32] whose busy waves (a wave per
+// `lanes` K items of each of the W (J + 1) sums) fit one wave per SIMD (1024): a wave costs K +
+// log2(lanes) serial adds (its butterfly included) and a SIMD's second wave doubles its time, so
+// fewer, longer waves win until every SIMD has one (measured: 1192 busy waves at K = 7 took 2x the
+// 960 of K = 8 on a GLV 2^20 MSM). lanes = logical lanes per wave (64; 16 for quads of the
+// cooperative add, SW29::add_quad -- not used here: with every SIMD busy the stage is issue-bound,
+// and quads' 2.1x shorter adds lose to their 4x fewer lanes)
+inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J, uint32_t lanes = 64) {
+    for (uint32_t k = 2; k < 32; k++) {
+        const uint64_t per = (uint64_t)lanes * k;
         const uint64_t busy = (uint64_t)W * ((uint64_t)J * ((S / 2 + per - 1) / per) + (S + per - 1) / per);
         if (busy <= 1024) return k;
     }
-    return 16;
+    return 32;
 }
-// waves (= partial slots) of one bit-stage sum over `items` items (K per lane, 64 lanes)
-inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K) { return (items + 64 * K - 1) / (64 * K); }
+// waves (= partial slots) of one bit-stage sum over `items` items (K per logical lane)
+inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K, uint32_t lanes = 64) {
+    return (items + lanes * K - 1) / (lanes * K);
+}
 // guarded = 0: read the longest chain back (host sync) and run exactly the rounds it needs;
 // guarded = r > 0: r device-guarded rounds, no sync (chains up to 2^r threads; longer ones are
 // finished by msm_tail_fixup_more once the caller has read chain_max with its results)
