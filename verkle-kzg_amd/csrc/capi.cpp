@@ -217,6 +217,7 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         for (auto& b : ctx->pin) b.release();
         ctx->pin_io.release();
         ctx->pin_small.release();
+        ctx->pin_norm.release();
         for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
         ctx->pool_free.clear();
         for (auto& p : ctx->pending) {

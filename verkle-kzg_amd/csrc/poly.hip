@@ -47,16 +47,21 @@ __global__ void k_powers(fe<F> w, size_t n, fe<F>* __restrict__ out) {
 
 // out[k] = 1 / in[k] for k < n (zeros map to zero). Montgomery's trick at two levels: each
 // thread multiplies a chunk of CH, a workgroup scans its 256 chunk products (prefix and suffix,
-// LDS) and inverts their product once (binary Euclid, one lane), then every chunk's inverse is
+// LDS) and inverts their product, then every chunk's inverse is
 // inv(total) * prefix * suffix and the chunk is substituted backwards. One inversion per 256 CH
 // elements (per chunk before: 65,536 inversions for a 2^20 KZG quotient, 0.46 ms).
+// The workgroup products are inverted on the host (as commit.hip's split normalisation): a
+// per-workgroup lane inversion was ~130 us of serial binary Euclid on one GPU lane, the host
+// inverts all workgroup products with one inversion in a few us. k_binv_prep leaves the chunk
+// prefix products in out[], each chunk the product of its workgroup's OTHER chunk products, and
+// the workgroup product; k_binv_finish substitutes backwards.
 template <class F>
-__global__ void __launch_bounds__(256) k_batch_inv(const fe<F>* __restrict__ in, fe<F>* __restrict__ out, size_t n,
-                                                  int CH) {
+__global__ void __launch_bounds__(256) k_binv_prep(const fe<F>* __restrict__ in, fe<F>* __restrict__ out, size_t n,
+                                                  int CH, fe<F>* __restrict__ others, fe<F>* __restrict__ tot) {
     __shared__ fe<F> pre[256], suf[256];
-    __shared__ fe<F> tinv;
     const uint32_t t = threadIdx.x;
-    const size_t lo = ((size_t)blockIdx.x * 256 + t) * CH;
+    const size_t c = (size_t)blockIdx.x * 256 + t;
+    const size_t lo = c * CH;
     const size_t hi = lo + CH < n ? lo + CH : n;
     fe<F> acc = fe_one<F>();
     for (size_t k = lo; k < hi; k++) {
@@ -76,12 +81,22 @@ __global__ void __launch_bounds__(256) k_batch_inv(const fe<F>* __restrict__ in,
         suf[t] = q;
         __syncthreads();
     }
-    if (t == 0) tinv = fe_inv_bin<F>(pre[255]);
-    __syncthreads();
+    fe<F> o = fe_one<F>();
+    if (t > 0) o = pre[t - 1];
+    if (t < 255) o = t > 0 ? fe_mul<F>(o, suf[t + 1]) : suf[t + 1];
+    others[c] = o;
+    if (t == 0) tot[blockIdx.x] = pre[255];
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_binv_finish(const fe<F>* __restrict__ in, fe<F>* __restrict__ out, size_t n,
+                                                    int CH, const fe<F>* __restrict__ others,
+                                                    const fe<F>* __restrict__ binv) {
+    const size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t lo = c * CH;
     if (lo >= n) return;
-    fe<F> inv = tinv;  // 1 / (this chunk's product)
-    if (t > 0) inv = fe_mul<F>(inv, pre[t - 1]);
-    if (t < 255) inv = fe_mul<F>(inv, suf[t + 1]);
+    const size_t hi = lo + CH < n ? lo + CH : n;
+    fe<F> inv = fe_mul<F>(binv[blockIdx.x], others[c]);  // 1 / (this chunk's product)
     for (size_t k = hi; k-- > lo;) {
         fe<F> v = in[k];
         if (fe_is_zero<F>(v)) {
@@ -221,11 +236,36 @@ int domain_powers(vc_ctx* ctx, const fe<F>& w, size_t n, fe<F>* d_out) {
     return VC_OK;
 }
 
+// synchronises the stream once (the host inversion between the two kernels)
 template <class F>
 int batch_inverse(vc_ctx* ctx, const fe<F>* d_in, fe<F>* d_out, size_t n) {
+    if (n == 0) return VC_OK;
     const int CH = n >= (1u << 18) ? 16 : 4;
-    size_t chunks = (n + CH - 1) / CH;
-    VK_LAUNCH(ctx, "batch_inv", (k_batch_inv<F>), (chunks + 255) / 256, 256, 0, d_in, d_out, n, CH);
+    const size_t chunks = (n + CH - 1) / CH;
+    const size_t nblk = (chunks + 255) / 256;
+    DevBuf others(ctx), tot(ctx);
+    VK_TRY(others.ensure(nblk * 256 * sizeof(fe<F>)));
+    VK_TRY(tot.ensure(nblk * sizeof(fe<F>)));
+    VK_TRY(ctx->pin_norm.ensure(2 * nblk * sizeof(fe<F>)));
+    fe<F>* h = ctx->pin_norm.as<fe<F>>();
+    VK_LAUNCH(ctx, "binv_prep", (k_binv_prep<F>), nblk, 256, 0, d_in, d_out, n, CH, others.as<fe<F>>(),
+              tot.as<fe<F>>());
+    VK_CHECK_HIP(hipMemcpyAsync(h, tot.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    fe<F>* inv = h + nblk;  // Montgomery's trick over the workgroup products (never zero)
+    inv[0] = h[0];
+    for (size_t b = 1; b < nblk; b++) inv[b] = fe_mul<F>(inv[b - 1], h[b]);
+    fe<F> run = fe_inv_bin<F>(inv[nblk - 1]);
+    for (size_t b = nblk - 1; b > 0; b--) {
+        const fe<F> ib = fe_mul<F>(run, inv[b - 1]);
+        run = fe_mul<F>(run, h[b]);
+        inv[b] = ib;
+    }
+    inv[0] = run;
+    VK_CHECK_HIP(hipMemcpyAsync(tot.p, inv, nblk * sizeof(fe<F>), hipMemcpyHostToDevice, ctx->stream));
+    VK_LAUNCH(ctx, "binv_finish", (k_binv_finish<F>), nblk, 256, 0, d_in, d_out, n, CH, others.as<fe<F>>(),
+              tot.as<fe<F>>());
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // the pinned inverses are reused by the next call
     return VC_OK;
 }
 

@@ -37,7 +37,7 @@ for c in [int(x) for x in (sys.argv[1:] or ["16"])]:
     for _ in range(reps):
         e.msm_batch_device(tab, 256, dcs.data_ptr(), B, dxy.data_ptr(), dinf.data_ptr())
     torch.cuda.synchronize()
-    ks = {k: e.kernel_time(k) for k in ("fb_commit", "fb_combine", "fb_normalize_out")}
+    ks = {k: e.kernel_time(k) for k in ("fb_commit", "fb_combine", "fb_normalize_out", "norm_prep", "norm_finish")}
     e.enable_timing(False)
     print(f"c={c} B={B}: wall {wall:.3f} ms/batch ({B / wall * 1e3 / 1e6:.3f} M commits/s); " +
           ", ".join(f"{k} {ms / n:.3f} ms" for k, (ms, n) in ks.items() if n), flush=True)
