@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--no-variable-base", action="store_true",
                     help="skip the variable-base (no shared-window copies) MSM sub-line")
     ap.add_argument("--no-check", action="store_true", help="skip the one-time 2^20 result check")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="multi-rank rehearsal on a 1-GPU box: every rank on device 0, gloo process group, "
+                         "vc_comm host-callback exchange (RCCL refuses two ranks on one device); timings are "
+                         "not scaling numbers")
     ap.add_argument("--comm", choices=["capi", "torch"], default="capi",
                     help="N > 1 exchange: vc_comm (C ABI, RCCL) or torch.distributed all-gather")
     return ap.parse_args()
@@ -485,8 +489,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.rehearse_one_gpu:  # every rank on device 0, gloo + host-callback exchange (see --help)
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if a.rehearse_one_gpu else "nccl", init_method="env://")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev)
@@ -504,7 +510,10 @@ def main():
     # vc_comm on RCCL, the path a Rust caller of libvkzg.so uses); the unique id travels over
     # the torch.distributed group. --comm torch keeps the Python all-gather (vkzg.dist).
     comm, comm_kind = None, "none" if world == 1 else a.comm
-    if world > 1 and a.comm == "capi":
+    if world > 1 and a.rehearse_one_gpu:
+        from vkzg import comm as vcomm
+        comm, comm_kind = vcomm.Comm.host(rank, world, vcomm.torch_allgather()), "vc_comm host callback (gloo)"
+    elif world > 1 and a.comm == "capi":
         from vkzg import comm as vcomm
         obj = [vcomm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
