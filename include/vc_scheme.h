@@ -103,6 +103,23 @@ int vc_kzg_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals
  * the parts' accumulators sum (vc_partials_sum) to the proof */
 int vc_kzg_prove_device_part(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
                              const uint64_t* point, int part, int parts, uint32_t* out_acc, uint64_t* y);
+/* KZG::prove_all_points (kzg/mod.rs:200-235), the FK amortised opening -- private and never
+ * called in the reference (its test at :299 has no #[test]). table = the Lagrange SRS of domain
+ * `size`; evals = n_evals values (the data's own domain is next_pow2(n_evals), as
+ * LagrangeBasis::from_vec). Outputs *count points (out_xy, out_inf) and values (out_y = data[i]).
+ *   mode 0: the reference's computation exactly -- coefficients c of the data's interpolant of
+ *     degree d, c_hat = [c_d, 0^(d+1), c_0 .. c_{d-1}] cut to the domain D::new(2 d), g1 =
+ *     ifft(lagrange SRS) over the key domain, s_hat = reverse(g1[0..d]) || 0, h_hat =
+ *     ifft(fft(s_hat) .* fft(c_hat)); returns (h_hat[i], data[i]) for i < that domain.
+ *     VC_E_DOMAIN where the reference panics: all-zero data (coeffs[degree] of an empty
+ *     polynomial), a domain larger than the data (data[i] out of bounds), d > size.
+ *   mode 1: the opening proofs FK computes (what the reference's test expects): for every i <
+ *     size, pi_i = [q_i(s)]_1 with q_i = (f - f(w^i)) / (X - w^i) -- the Toeplitz product of the
+ *     coefficients with the monomial SRS fft(lagrange SRS) by a 2 size circulant, then an FFT.
+ *     Equal to vc_kzg_prove at index i; n_evals <= size (VC_E_RANGE otherwise).
+ * out_xy: count x 2 NL u64 (count <= size, or the mode-0 domain); out_y: count x 4 u64. */
+int vc_kzg_prove_all_points(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t n_evals, int mode,
+                            uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_y, size_t* count);
 /* the quotient alone (a5/a6), for parity tests: q (size x 4 u64) and y */
 int vc_kzg_quotient(vc_ctx* ctx, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
                     uint64_t* q_out, uint64_t* y);

@@ -393,6 +393,52 @@ class KZG:
         return self.verify_point(commitment, index, proof)
 
 
+def ark_fft(vals, n, r, omega, inverse=False):
+    """ark-poly Radix2EvaluationDomain fft / ifft of size n (fft_in_place first resizes the input
+    to n: truncates or zero-pads). O(n^2): small n only."""
+    a = (list(vals) + [0] * n)[:n]
+    w = pow(omega, -1, r) if inverse else omega
+    out = [sum(a[j] * pow(w, i * j, r) for j in range(n)) % r for i in range(n)]
+    if inverse:
+        ninv = pow(n, -1, r)
+        out = [x * ninv % r for x in out]
+    return out
+
+
+class ReferencePanic(Exception):
+    """where the reference panics (index out of bounds)"""
+
+
+def kzg_prove_all_points(kzg, data):
+    """KZG::prove_all_points (kzg/mod.rs:200-235) restated. Every point involved is a known multiple
+    of G (the SRS points are c_j G, kzg_lagrange_scalars), and the FFTs over G1 are linear, so the
+    computation runs on those scalars and each output is (scalar) G -- the same group elements.
+    Returns [(h_hat_i, data[i])]."""
+    C = kzg.curve
+    r = C.r
+    evals = list(data.evals)
+    m = domain_size(len(evals))                        # LagrangeBasis::from_vec's domain
+    coeffs = ark_fft(evals, m, r, group_gen(m, C), inverse=True)   # interpolate (:204)
+    while coeffs and coeffs[-1] == 0:                  # DensePolynomial trims trailing zeros
+        coeffs.pop()
+    if not coeffs:
+        raise ReferencePanic("coeffs[degree] of the zero polynomial")
+    d = len(coeffs) - 1                                # poly.degree()
+    D = domain_size(2 * d)                             # D::new(degree * 2)
+    chat = [coeffs[d]] + [0] * (d + 1) + coeffs[:d]
+    g1 = ark_fft(kzg.lagrange_scalars, kzg.size, r, kzg.pre.omega, inverse=True)
+    if d > len(g1):
+        raise ReferencePanic("g1[0..degree] out of bounds")
+    shat = list(reversed(g1[:d])) + [0] * (D - d)
+    y = ark_fft(chat, D, r, group_gen(D, C))
+    v = ark_fft(shat, D, r, group_gen(D, C))
+    u = [a * b % r for a, b in zip(v, y)]
+    h = ark_fft(u, D, r, group_gen(D, C), inverse=True)
+    if D > len(evals):
+        raise ReferencePanic("data[i] out of bounds")
+    return [(C.mul(C.g, hi), evals[i]) for i, hi in enumerate(h)]
+
+
 # ---------------------------------------------------------------- multiproof.rs
 def prove_multiproof(vc, queries):
     """multiproof.rs:99-176. queries: list of (data: LagrangeBasis, commit, z:int, y:int)."""

@@ -235,3 +235,45 @@ def test_multiproof_field_phases_c_vs_python(oracle_c):
         cg, ch = oracle_c.mp_field_phases(N, data, np.array(z, dtype=np.uint64), rr, t, pre.omega, T)
         assert [oracle_c.limbs_to_int(x) for x in cg] == g
         assert [oracle_c.limbs_to_int(x) for x in ch] == h
+
+
+def _pt_fft(C, pts, n, omega, inverse=False):
+    """ark-poly fft over points, O(n^2), straight from the definition (no scalar shortcut)"""
+    r = C.r
+    a = (list(pts) + [None] * n)[:n]
+    w = pow(omega, -1, r) if inverse else omega
+    out = []
+    for i in range(n):
+        acc = None
+        for j in range(n):
+            acc = C.add(acc, C.mul(a[j], pow(w, i * j, r))) if a[j] is not None else acc
+        out.append(C.mul(acc, pow(n, -1, r)) if (inverse and acc is not None) else acc)
+    return out
+
+
+def test_prove_all_points_oracle_scalar_shortcut():
+    """the oracle's kzg_prove_all_points works on the SRS scalars (L_j = c_j G); recompute one small
+    case from the points themselves (G1 FFTs by definition) and compare (kzg/mod.rs:200-235)."""
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    C, r = BN254, BN254.r
+    kz = protocol.KZG(8)
+    m = 4
+    w4 = protocol.group_gen(4)
+    coeffs = [5, 7]                                    # degree 1 -> domain D::new(2) = 2
+    evals = [sum(c * pow(w4, i * k, r) for k, c in enumerate(coeffs)) % r for i in range(m)]
+    data = protocol.LagrangeBasis(evals, 4)
+    got = protocol.kzg_prove_all_points(kz, data)
+    assert len(got) == 2
+    g1 = _pt_fft(C, kz.lagrange, 8, kz.pre.omega, inverse=True)
+    d, D = 1, 2
+    chat = [coeffs[d]] + [0] * (d + 1) + coeffs[:d]
+    shat = list(reversed(g1[:d])) + [None] * (D - d)
+    y = protocol.ark_fft(chat, D, r, protocol.group_gen(D))
+    v = _pt_fft(C, shat, D, protocol.group_gen(D))
+    u = [C.mul(p, k) if p is not None else None for p, k in zip(v, y)]
+    h = _pt_fft(C, u, D, protocol.group_gen(D), inverse=True)
+    assert [p for p, _ in got] == h
+    assert [yv for _, yv in got] == evals[:2]
+    with pytest.raises(protocol.ReferencePanic):
+        protocol.kzg_prove_all_points(kz, protocol.LagrangeBasis([0, 0, 0, 0], 4))

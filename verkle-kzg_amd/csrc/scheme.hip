@@ -385,6 +385,239 @@ static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals
     return VC_OK;
 }
 
+// ---------------------------------------------------------------- FK all-point openings (f4)
+// KZG::prove_all_points (kzg/mod.rs:200-235): radix-2 FFTs over G1 (a butterfly multiplies a
+// point by a twiddle: one double-and-add scalar multiplication) and over Fr, natural-order in and
+// out (bit reversal, then iterative Cooley-Tukey), as ark-poly's Radix2EvaluationDomain computes
+// them (fft: y_i = sum_j a_j w^(ij); ifft: a_j = n^-1 sum_i y_i w^(-ij)). Dead code in the
+// reference (no caller; its test at :299 has no #[test]); see DESIGN.md for both modes.
+template <class C, class Fr_>
+__device__ typename C::Acc pt_mul_fe(const typename C::Acc& p, const fe<Fr_>& k_mont) {
+    const fe<Fr_> k = fe_from_mont<Fr_>(k_mont);
+    typename C::Acc r = C::zero();
+    bool started = false;
+    for (int i = Fr_::N * 32 - 1; i >= 0; i--) {
+        const bool bit = (k.v[i >> 5] >> (i & 31)) & 1u;
+        if (started) r = C::dbl(r);
+        if (bit) {
+            r = started ? C::add(r, p) : p;
+            started = true;
+        }
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t bitrev32(uint32_t i, int lg) { return lg ? (__brev(i) >> (32 - lg)) : 0u; }
+
+template <class T>
+__global__ void k_bitrev(const T* __restrict__ in, T* __restrict__ out, uint32_t n, int lg) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[bitrev32(i, lg)] = in[i];
+}
+// one stage (blocks of 2 half): a[i0], a[i1] <- u + w v, u - w v with w = tw[j * step]
+template <class C, class Fr_>
+__global__ void k_pt_stage(typename C::Acc* __restrict__ a, uint32_t n, uint32_t half, const fe<Fr_>* __restrict__ tw,
+                           uint32_t step) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n / 2) return;
+    const uint32_t blk = g / half, j = g % half;
+    const uint32_t i0 = blk * 2 * half + j, i1 = i0 + half;
+    const typename C::Acc u = a[i0];
+    const typename C::Acc v = j == 0 ? a[i1] : pt_mul_fe<C, Fr_>(a[i1], tw[j * step]);
+    a[i0] = C::add(u, v);
+    a[i1] = C::add(u, C::neg(v));
+}
+template <class Fr_>
+__global__ void k_fr_stage(fe<Fr_>* __restrict__ a, uint32_t n, uint32_t half, const fe<Fr_>* __restrict__ tw,
+                           uint32_t step) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n / 2) return;
+    const uint32_t blk = g / half, j = g % half;
+    const uint32_t i0 = blk * 2 * half + j, i1 = i0 + half;
+    const fe<Fr_> u = a[i0], v = fe_mul<Fr_>(a[i1], tw[j * step]);
+    a[i0] = fe_add<Fr_>(u, v);
+    a[i1] = fe_sub<Fr_>(u, v);
+}
+// a[i] <- a[i] * (s ? s[i] : k)
+template <class C, class Fr_>
+__global__ void k_pt_scale(typename C::Acc* __restrict__ a, uint32_t n, const fe<Fr_>* __restrict__ s, fe<Fr_> k) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = pt_mul_fe<C, Fr_>(a[i], s ? s[i] : k);
+}
+template <class Fr_>
+__global__ void k_fr_scale(fe<Fr_>* __restrict__ a, uint32_t n, fe<Fr_> k) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = fe_mul<Fr_>(a[i], k);
+}
+template <class C>
+__global__ void k_aff_to_acc(const typename C::Aff* __restrict__ in, const uint8_t* __restrict__ inf, uint32_t n,
+                             typename C::Acc* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = inf[i] ? C::zero() : C::from_aff(in[i], false);
+}
+// out[i] = src[map(i)] or the identity: reversed prefix (mode 0's s_hat) / reversed shifted
+// prefix (mode 1's S') / a window (mode 1's h)
+template <class C>
+__global__ void k_pt_gather(const typename C::Acc* __restrict__ src, uint32_t n, int64_t base, int64_t dir,
+                            uint32_t valid, typename C::Acc* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = i < valid ? src[base + dir * (int64_t)i] : C::zero();
+}
+
+static int lg2_of(size_t n) {
+    int lg = 0;
+    while (((size_t)1 << lg) < n) lg++;
+    return lg;
+}
+// in-place FFT (inverse: iFFT incl. the 1/n) of n = 2^k points / field elements in a DevBuf
+template <class C, class Fr_>
+static int pt_fft(vc_ctx* ctx, DevBuf& a, size_t n, bool inverse) {
+    using Acc = typename C::Acc;
+    if (n <= 1) return VC_OK;
+    const int lg = lg2_of(n);
+    const fe<Fr_> w = group_gen_t<Fr_>(n, fr_generator<Fr_>());
+    DevBuf tw(ctx), tmp(ctx);
+    VK_TRY(tw.ensure(n / 2 * sizeof(fe<Fr_>)));
+    VK_TRY(tmp.ensure(n * sizeof(Acc)));
+    VK_TRY(domain_powers<Fr_>(ctx, inverse ? fe_inv_bin<Fr_>(w) : w, n / 2, tw.as<fe<Fr_>>()));
+    const unsigned g = (unsigned)((n + 255) / 256), g2 = (unsigned)((n / 2 + 255) / 256);
+    VK_LAUNCH(ctx, "fk_bitrev", (k_bitrev<Acc>), g, 256, 0, a.as<Acc>(), tmp.as<Acc>(), (uint32_t)n, lg);
+    for (uint32_t half = 1; half < n; half <<= 1)
+        VK_LAUNCH(ctx, "fk_pt_stage", (k_pt_stage<C, Fr_>), g2, 256, 0, tmp.as<Acc>(), (uint32_t)n, half,
+                  tw.as<fe<Fr_>>(), (uint32_t)(n / (2 * half)));
+    if (inverse)
+        VK_LAUNCH(ctx, "fk_pt_scale", (k_pt_scale<C, Fr_>), g, 256, 0, tmp.as<Acc>(), (uint32_t)n,
+                  (const fe<Fr_>*)nullptr, fe_inv_bin<Fr_>(mont_from_u64<Fr_>(n)));
+    VK_CHECK_HIP(hipMemcpyAsync(a.p, tmp.p, n * sizeof(Acc), hipMemcpyDeviceToDevice, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // tw / tmp go back to the pool
+    return VC_OK;
+}
+template <class Fr_>
+static int fr_fft(vc_ctx* ctx, DevBuf& a, size_t n, bool inverse) {
+    if (n <= 1) return VC_OK;
+    const int lg = lg2_of(n);
+    const fe<Fr_> w = group_gen_t<Fr_>(n, fr_generator<Fr_>());
+    DevBuf tw(ctx), tmp(ctx);
+    VK_TRY(tw.ensure(n / 2 * sizeof(fe<Fr_>)));
+    VK_TRY(tmp.ensure(n * sizeof(fe<Fr_>)));
+    VK_TRY(domain_powers<Fr_>(ctx, inverse ? fe_inv_bin<Fr_>(w) : w, n / 2, tw.as<fe<Fr_>>()));
+    const unsigned g = (unsigned)((n + 255) / 256), g2 = (unsigned)((n / 2 + 255) / 256);
+    VK_LAUNCH(ctx, "fk_bitrev", (k_bitrev<fe<Fr_>>), g, 256, 0, a.as<fe<Fr_>>(), tmp.as<fe<Fr_>>(), (uint32_t)n, lg);
+    for (uint32_t half = 1; half < n; half <<= 1)
+        VK_LAUNCH(ctx, "fk_fr_stage", (k_fr_stage<Fr_>), g2, 256, 0, tmp.as<fe<Fr_>>(), (uint32_t)n, half,
+                  tw.as<fe<Fr_>>(), (uint32_t)(n / (2 * half)));
+    if (inverse)
+        VK_LAUNCH(ctx, "fk_fr_scale", (k_fr_scale<Fr_>), g, 256, 0, tmp.as<fe<Fr_>>(), (uint32_t)n,
+                  fe_inv_bin<Fr_>(mont_from_u64<Fr_>(n)));
+    VK_CHECK_HIP(hipMemcpyAsync(a.p, tmp.p, n * sizeof(fe<Fr_>), hipMemcpyDeviceToDevice, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
+// mode 0: the reference's prove_all_points exactly; mode 1: the FK proofs it was meant to return
+template <class C, class Fr_>
+static int fk_all_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals, size_t ne, int mode,
+                    uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_y, size_t* count) {
+    using Acc = typename C::Acc;
+    if (!is_pow2(size) || t->n < size) return VC_E_INVALID;
+    if (ne == 0) return VC_E_DOMAIN;  // the reference: coeffs[degree] of the zero polynomial panics
+    const int NL = aff_limbs64(ctx->curve);
+    // the Lagrange SRS as projective points
+    DevBuf L(ctx);
+    VK_TRY(L.ensure(size * sizeof(Acc)));
+    VK_LAUNCH(ctx, "fk_aff_to_acc", (k_aff_to_acc<C>), (size + 255) / 256, 256, 0, t->bases.as<typename C::Aff>(),
+              t->inf.as<uint8_t>(), (uint32_t)size, L.as<Acc>());
+    auto upload_evals = [&](DevBuf& dst, size_t n) -> int {  // evals padded with zeros to n, Montgomery
+        DevBuf raw(ctx);
+        VK_TRY(dst.ensure(n * sizeof(fe<Fr_>)));
+        VK_TRY(raw.ensure(n * 32));
+        const size_t m = std::min(ne, n);
+        VK_CHECK_HIP(hipMemcpyAsync(raw.p, evals, m * 32, hipMemcpyHostToDevice, ctx->stream));
+        VK_TRY(canon_to_mont_dev<Fr_>(ctx, raw.p, n, m, dst.as<fe<Fr_>>()));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        return VC_OK;
+    };
+    DevBuf out(ctx);  // the D output points
+    size_t D = 0;
+    if (mode == 0) {
+        // data.interpolate() over the data's own domain (LagrangeBasis::from_vec: next_pow2(len))
+        size_t m = 1;
+        while (m < ne) m <<= 1;
+        DevBuf cf(ctx);
+        VK_TRY(upload_evals(cf, m));
+        VK_TRY(fr_fft<Fr_>(ctx, cf, m, true));
+        std::vector<fe<Fr_>> coeffs(m);
+        VK_CHECK_HIP(hipMemcpy(coeffs.data(), cf.p, m * sizeof(fe<Fr_>), hipMemcpyDeviceToHost));
+        size_t deg = m;
+        while (deg > 0 && fe_is_zero<Fr_>(coeffs[deg - 1])) deg--;
+        if (deg == 0) return VC_E_DOMAIN;  // zero polynomial: coeffs[degree] out of bounds
+        const size_t d = deg - 1;          // poly.degree()
+        D = 1;
+        while (D < 2 * d) D <<= 1;  // D::new(degree * 2)
+        if (D > ne || d > size) return VC_E_DOMAIN;  // data[i] / g1[0..degree] out of bounds
+        // c_hat = [c_d, 0^(d+1), c_0 .. c_{d-1}], resized to the domain by fft_in_place
+        std::vector<fe<Fr_>> chat(D, fe_zero<Fr_>());
+        std::vector<fe<Fr_>> full;
+        full.push_back(coeffs[d]);
+        full.insert(full.end(), d + 1, fe_zero<Fr_>());
+        full.insert(full.end(), coeffs.begin(), coeffs.begin() + d);
+        for (size_t i = 0; i < D && i < full.size(); i++) chat[i] = full[i];
+        DevBuf yv(ctx);
+        VK_TRY(yv.ensure(D * sizeof(fe<Fr_>)));
+        VK_CHECK_HIP(hipMemcpy(yv.p, chat.data(), D * sizeof(fe<Fr_>), hipMemcpyHostToDevice));
+        VK_TRY(fr_fft<Fr_>(ctx, yv, D, false));
+        // g1 = ifft(lagrange_commitments) over the key's domain; s_hat = reverse(g1[0..d]) || O
+        VK_TRY((pt_fft<C, Fr_>(ctx, L, size, true)));
+        VK_TRY(out.ensure(D * sizeof(Acc)));
+        VK_LAUNCH(ctx, "fk_gather", (k_pt_gather<C>), (D + 255) / 256, 256, 0, L.as<Acc>(), (uint32_t)D,
+                  (int64_t)d - 1, (int64_t)-1, (uint32_t)d, out.as<Acc>());
+        VK_TRY((pt_fft<C, Fr_>(ctx, out, D, false)));  // v
+        VK_LAUNCH(ctx, "fk_pt_scale", (k_pt_scale<C, Fr_>), (D + 255) / 256, 256, 0, out.as<Acc>(), (uint32_t)D,
+                  yv.as<fe<Fr_>>(), fe_zero<Fr_>());  // u = v .* y
+        VK_TRY((pt_fft<C, Fr_>(ctx, out, D, true)));    // h_hat
+    } else if (mode == 1) {
+        const size_t n = size;
+        D = n;
+        if (ne > n) return VC_E_RANGE;
+        DevBuf c2(ctx);
+        VK_TRY(upload_evals(c2, 2 * n));  // zero-padded to 2n; the first n entries are the data
+        // coefficients: iFFT over the key domain of the first n entries (the rest stays zero)
+        {
+            DevBuf cn(ctx);
+            VK_TRY(cn.ensure(n * sizeof(fe<Fr_>)));
+            VK_CHECK_HIP(hipMemcpyAsync(cn.p, c2.p, n * sizeof(fe<Fr_>), hipMemcpyDeviceToDevice, ctx->stream));
+            VK_TRY(fr_fft<Fr_>(ctx, cn, n, true));
+            VK_CHECK_HIP(hipMemcpyAsync(c2.p, cn.p, n * sizeof(fe<Fr_>), hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        VK_TRY(fr_fft<Fr_>(ctx, c2, 2 * n, false));
+        // monomial SRS S = fft(L) (setup made L = ifft(S)); S'[i] = S[n - 2 - i] for i <= n - 2
+        VK_TRY((pt_fft<C, Fr_>(ctx, L, n, false)));
+        DevBuf V(ctx);
+        VK_TRY(V.ensure(2 * n * sizeof(Acc)));
+        VK_LAUNCH(ctx, "fk_gather", (k_pt_gather<C>), (2 * n + 255) / 256, 256, 0, L.as<Acc>(), (uint32_t)(2 * n),
+                  (int64_t)n - 2, (int64_t)-1, (uint32_t)(n - 1), V.as<Acc>());
+        VK_TRY((pt_fft<C, Fr_>(ctx, V, 2 * n, false)));
+        VK_LAUNCH(ctx, "fk_pt_scale", (k_pt_scale<C, Fr_>), (2 * n + 255) / 256, 256, 0, V.as<Acc>(),
+                  (uint32_t)(2 * n), c2.as<fe<Fr_>>(), fe_zero<Fr_>());
+        VK_TRY((pt_fft<C, Fr_>(ctx, V, 2 * n, true)));  // the Toeplitz product, h_j at j + n - 1
+        VK_TRY(out.ensure(n * sizeof(Acc)));
+        VK_LAUNCH(ctx, "fk_gather", (k_pt_gather<C>), (n + 255) / 256, 256, 0, V.as<Acc>(), (uint32_t)n,
+                  (int64_t)n - 1, (int64_t)1, (uint32_t)n, out.as<Acc>());
+        VK_TRY((pt_fft<C, Fr_>(ctx, out, n, false)));  // proofs at w^i
+    } else {
+        return VC_E_INVALID;
+    }
+    DevBuf dxy(ctx), dinf(ctx);
+    VK_TRY(dxy.ensure(D * 2 * NL * 8));
+    VK_TRY(dinf.ensure(D));
+    VK_TRY(normalize_to_canon(ctx, ctx->curve, out.p, D, dxy.p, dinf.as<uint8_t>()));
+    VK_CHECK_HIP(hipMemcpy(out_xy, dxy.p, D * 2 * NL * 8, hipMemcpyDeviceToHost));
+    VK_CHECK_HIP(hipMemcpy(out_inf, dinf.p, D, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < D; i++)
+        for (int k = 0; k < 4; k++) out_y[4 * i + k] = i < ne ? evals[4 * i + k] : 0;
+    *count = D;
+    return VC_OK;
+}
+
 // ---------------------------------------------------------------- multiproof kernels
 // den[zi][k] = w^k - w^z (1 at k == z)
 __global__ void k_mp_den(const fe<F>* __restrict__ pw, const uint32_t* __restrict__ zval, size_t N, uint32_t Z,
@@ -759,6 +992,19 @@ int vc_kzg_prove_device_part(vc_ctx* ctx, int table, size_t size, const void* d_
     if (ctx->curve == VC_CURVE_BLS12_381)
         return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, ev, max, point, nullptr, nullptr, y, nullptr, true,
                                                part, parts, out_acc);
+    return VC_E_INVALID;
+}
+
+int vc_kzg_prove_all_points(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t n_evals, int mode,
+                            uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_y, size_t* count) {
+    if (!ctx || (n_evals && !evals) || !out_xy || !out_inf || !out_y || !count) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    if (ctx->curve == VC_CURVE_BN254)
+        return fk_all_t<BN254G1, BN254Fr>(ctx, t, size, evals, n_evals, mode, out_xy, out_inf, out_y, count);
+    if (ctx->curve == VC_CURVE_BLS12_381)
+        return fk_all_t<BLS381G1, BLS381Fr>(ctx, t, size, evals, n_evals, mode, out_xy, out_inf, out_y, count);
     return VC_E_INVALID;
 }
 

@@ -76,6 +76,8 @@ SIGNATURES = {
     "vc_ipa_verify_commitment_proof": (c_int, [c_void_p, c_int, P, ctypes.c_uint8, P, ctypes.POINTER(c_int)]),
     "vc_kzg_prove": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
     "vc_kzg_quotient": (c_int, [c_void_p, c_size_t, P, c_size_t, P, P, P]),
+    "vc_kzg_prove_all_points": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P, P,
+                                        ctypes.POINTER(c_size_t)]),
     "vc_kzg_prove_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
     "vc_kzg_prove_device_part": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, c_int, c_int, P, P]),
     "vc_multiproof_prove": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P, P, P, P, P, P]),

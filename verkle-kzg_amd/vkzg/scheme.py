@@ -312,6 +312,20 @@ class KZG:
     def prove(self, commitment, index, data):
         return self.prove_point(commitment, index, data)
 
+    def prove_all_points(self, data, mode=0):
+        """KZG::prove_all_points (kzg/mod.rs:200-235) -- mode 0: the reference's computation
+        exactly (its h_hat values, y = data[i]); mode 1: the FK opening proofs at every domain
+        point (== prove at each index). Returns a list of {"proof", "y"}."""
+        ev = data.limbs() if data.evals else np.zeros((0, 4), dtype=np.uint64)
+        n_out = self.size if mode == 1 else max(1, len(data.evals))
+        xy = np.zeros((n_out, 8), dtype=np.uint64)
+        inf = np.zeros(n_out, dtype=np.uint8)
+        ys = np.zeros((n_out, 4), dtype=np.uint64)
+        cnt = ctypes.c_size_t()
+        check(lib().vc_kzg_prove_all_points(self.engine.h, self.table, self.size, _p(ev), len(data.evals), mode,
+                                            _p(xy), _p(inf), _p(ys), ctypes.byref(cnt)), "kzg_prove_all_points")
+        return [{"proof": _pt(xy[i], inf[i]), "y": limbs_to_int(ys[i])} for i in range(cnt.value)]
+
     def quotient(self, point, data):
         ev = data.limbs()
         q = np.zeros((self.size, 4), dtype=np.uint64)
