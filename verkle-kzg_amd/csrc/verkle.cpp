@@ -7,8 +7,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <array>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -53,6 +56,63 @@ struct FlatMap {
         return it->second;
     }
 };
+
+// Persistent host workers for the commitment's parallel node loops. Spawning and joining 16
+// threads per loop cost ~0.3-0.8 ms and there are ~12 loops per commitment; the pool's threads
+// wait on a condition variable between loops (and are never joined: the pool lives until exit).
+class HostPool {
+public:
+    explicit HostPool(unsigned n) : n_(n) {
+        for (unsigned k = 1; k < n; k++) th_.emplace_back([this, k] { loop(k); });
+    }
+    unsigned size() const { return n_; }
+    // f(k) for every k < size(), k == 0 on the calling thread; one loop at a time
+    void run(const std::function<void(unsigned)>& f) {
+        std::lock_guard<std::mutex> one(run_mu_);
+        if (n_ == 1) {
+            f(0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            pending_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(unsigned k) {
+        unsigned seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)>* f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                f = job_;
+            }
+            (*f)(k);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    unsigned n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(unsigned)>* job_ = nullptr;
+    unsigned pending_ = 0, gen_ = 0;
+};
+static HostPool& host_pool() {
+    static HostPool* p = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    return *p;
+}
 
 struct VNode {
     bool ext = false;
@@ -285,21 +345,49 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     // dirty nodes reachable from the root, with depth (clean subtrees are skipped: an insert
     // clears every commitment on its path, so a clean node has clean descendants). Every rank
     // holds the same tree, so every rank walks it to the same lists in the same order.
+    // The walk of the root's subtrees is split over the host pool (contiguous ranges of the
+    // root's children; the per-worker lists are concatenated in worker order, so the lists --
+    // and a sharded run's slices -- are the same on every rank).
     std::vector<int> exts;
     std::vector<std::vector<int>> internals;  // by depth
-    std::vector<std::pair<int, int>> stack{{0, 0}};
-    while (!stack.empty()) {
-        auto [id, depth] = stack.back();
-        stack.pop_back();
-        const VNode& n = t->nodes[id];
-        if (n.has_commit) continue;
-        if (n.ext) {
-            exts.push_back(id);
-            continue;
+    auto walk = [&](int root, int depth0, std::vector<int>& ex, std::vector<std::vector<int>>& in) {
+        std::vector<std::pair<int, int>> stack{{root, depth0}};
+        while (!stack.empty()) {
+            auto [id, depth] = stack.back();
+            stack.pop_back();
+            const VNode& n = t->nodes[id];
+            if (n.has_commit) continue;
+            if (n.ext) {
+                ex.push_back(id);
+                continue;
+            }
+            if ((int)in.size() <= depth) in.resize(depth + 1);
+            in[depth].push_back(id);
+            for (auto& kv : n.children) stack.push_back({kv.second, depth + 1});
         }
-        if ((int)internals.size() <= depth) internals.resize(depth + 1);
-        internals[depth].push_back(id);
-        for (auto& kv : n.children) stack.push_back({kv.second, depth + 1});
+    };
+    {
+        const VNode& root = t->nodes[0];
+        HostPool& P = host_pool();
+        if (root.has_commit || root.ext || root.children.v.size() < 2 || t->nodes.size() < 4096 || P.size() == 1) {
+            walk(0, 0, exts, internals);
+        } else {
+            internals.resize(1);
+            internals[0].push_back(0);
+            const auto& ch = root.children.v;
+            const unsigned T = P.size();
+            std::vector<std::vector<int>> ex(T);
+            std::vector<std::vector<std::vector<int>>> in(T);
+            P.run([&](unsigned k) {
+                for (size_t c = ch.size() * k / T; c < ch.size() * (k + 1) / T; c++) walk(ch[c].second, 1, ex[k], in[k]);
+            });
+            for (unsigned k = 0; k < T; k++) {
+                exts.insert(exts.end(), ex[k].begin(), ex[k].end());
+                if (internals.size() < in[k].size()) internals.resize(in[k].size());
+                for (size_t d = 0; d < in[k].size(); d++)
+                    internals[d].insert(internals[d].end(), in[k][d].begin(), in[k][d].end());
+            }
+        }
     }
     // batched sparse commits (vc_msm_batch_sparse): rows of (column, value) non-zeros
     struct Rows {
@@ -318,52 +406,54 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         }
         void end_row() { ptr.push_back(cols.size()); }
         size_t n() const { return ptr.size() - 1; }
-        // append another builder's rows (row pointers shifted)
-        void append(const Rows& o) {
-            const uint64_t base = cols.size();
-            for (size_t i = 1; i < o.ptr.size(); i++) ptr.push_back(base + o.ptr[i]);
-            cols.insert(cols.end(), o.cols.begin(), o.cols.end());
-            vals.insert(vals.end(), o.vals.begin(), o.vals.end());
-        }
     };
-    // rows of items [lo, hi) built by fn(i, Rows&) on up to 16 host threads, in item order
-    // (the node walks are pointer-chasing code: ~100-200 ns per node on one thread)
-    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // rows of items [lo, hi) built by fn(i, Rows&) on the host pool, in item order (the node
+    // walks are pointer-chasing code: ~100-200 ns per node on one thread); every worker builds
+    // the rows of its item range, then copies them into place in parallel
+    HostPool& pool = host_pool();
     auto build_rows = [&](size_t lo, size_t hi, size_t nnz_per, auto fn) {
         Rows out;
         const size_t count = hi - lo;
-        const unsigned T = count >= 4096 ? hw : 1;
+        const unsigned T = count >= 4096 ? pool.size() : 1;
         if (T == 1) {
             out.reserve(count, count * nnz_per);
             for (size_t i = lo; i < hi; i++) fn(i, out);
             return out;
         }
         std::vector<Rows> part(T);
-        std::vector<std::thread> th;
-        for (unsigned k = 0; k < T; k++)
-            th.emplace_back([&, k] {
-                const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
-                part[k].reserve(b - a, (b - a) * nnz_per);
-                for (size_t i = a; i < b; i++) fn(i, part[k]);
-            });
-        for (auto& x : th) x.join();
-        out.reserve(count, count * nnz_per);
-        for (auto& r : part) out.append(r);
+        pool.run([&](unsigned k) {
+            const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
+            part[k].reserve(b - a, (b - a) * nnz_per);
+            for (size_t i = a; i < b; i++) fn(i, part[k]);
+        });
+        std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0);
+        for (unsigned k = 0; k < T; k++) {
+            roff[k + 1] = roff[k] + part[k].n();
+            noff[k + 1] = noff[k] + part[k].cols.size();
+        }
+        out.ptr.assign(roff[T] + 1, 0);
+        out.cols.resize(noff[T]);
+        out.vals.resize(4 * noff[T]);
+        pool.run([&](unsigned k) {
+            const Rows& r = part[k];
+            for (size_t i = 1; i < r.ptr.size(); i++) out.ptr[roff[k] + i] = noff[k] + r.ptr[i];
+            if (!r.cols.empty()) {
+                memcpy(&out.cols[noff[k]], r.cols.data(), r.cols.size() * 4);
+                memcpy(&out.vals[4 * noff[k]], r.vals.data(), r.vals.size() * 8);
+            }
+        });
         return out;
     };
-    // fn(i) for i in [0, count) on the same threads (independent per-item writes)
+    // fn(i) for i in [0, count) on the pool (independent per-item writes)
     auto for_each = [&](size_t count, auto fn) {
-        const unsigned T = count >= 4096 ? hw : 1;
+        const unsigned T = count >= 4096 ? pool.size() : 1;
         if (T == 1) {
             for (size_t i = 0; i < count; i++) fn(i);
             return;
         }
-        std::vector<std::thread> th;
-        for (unsigned k = 0; k < T; k++)
-            th.emplace_back([&, k] {
-                for (size_t i = count * k / T; i < count * (k + 1) / T; i++) fn(i);
-            });
-        for (auto& x : th) x.join();
+        pool.run([&](unsigned k) {
+            for (size_t i = count * k / T; i < count * (k + 1) / T; i++) fn(i);
+        });
     };
     lap("collect dirty");
     auto commit_rows = [&](const Rows& r, std::vector<uint64_t>& xy, std::vector<uint8_t>& inf,
@@ -430,16 +520,22 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         // (position, value) writes of c1 / c2 in leaf order; a later write to the same
         // position overwrites, as c1_values[index] = ... does (node.rs:226-239)
         Rows r12 = build_rows(lo, hi, (size_t)N, [&](size_t e, Rows& r) {
-            std::vector<std::pair<uint32_t, std::array<uint64_t, 4>>> half[2];
+            // positions (2 index) % N, (2 index + 1) % N < N <= 32: fixed slots, no allocation
+            struct PV {
+                uint32_t pos;
+                uint64_t v[4];
+            };
+            PV half[2][32];
+            int cnt[2] = {0, 0};
             auto put = [&](int h, uint32_t pos, const uint64_t* v) {
-                for (auto& pv : half[h])
-                    if (pv.first == pos) {
-                        memcpy(pv.second.data(), v, 32);
+                for (int k = 0; k < cnt[h]; k++)
+                    if (half[h][k].pos == pos) {
+                        memcpy(half[h][k].v, v, 32);
                         return;
                     }
-                std::array<uint64_t, 4> a;
-                memcpy(a.data(), v, 32);
-                half[h].push_back({pos, a});
+                half[h][cnt[h]].pos = pos;
+                memcpy(half[h][cnt[h]].v, v, 32);
+                cnt[h]++;
             };
             const VNode& n = t->nodes[exts[e]];
             for (auto& kv : n.leaves) {
@@ -452,7 +548,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                 put(h, (uint32_t)((2 * index + 1) % N), vhi);
             }
             for (int h = 0; h < 2; h++) {
-                for (auto& pv : half[h]) r.add(pv.first, pv.second.data());
+                for (int k = 0; k < cnt[h]; k++) r.add(half[h][k].pos, half[h][k].v);
                 r.end_row();
             }
         });

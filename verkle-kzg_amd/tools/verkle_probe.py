@@ -13,7 +13,7 @@ from vkzg import scheme  # noqa: E402
 from vkzg.verkle import VerkleTree  # noqa: E402
 
 NAMES = ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup", "sparse_store",
-         "sparse_combine", "normalize_out", "to_data_item", "fb_commit", "fb_combine", "fb_normalize_out",
+         "sparse_combine", "normalize_out", "norm_prep", "norm_finish", "to_data_item", "fb_commit", "fb_combine", "fb_normalize_out",
          "fb_commit_small")
 nk = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 eng = vkzg.Engine("bn254", 0)
