@@ -20,6 +20,7 @@
 #include "ec.hpp"
 #include "poly.hpp"
 #include "scheme_internal.hpp"
+#include "host/pool.hpp"
 
 namespace vk {
 
@@ -171,19 +172,7 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     }
     // the per-proof host work (barycentric weights, transcripts, scalar rows, folds: ~600 field
     // multiplies per proof per round) is independent across proofs: up to 16 host threads
-    const unsigned T = B >= 16 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
-    auto par_for = [&](auto fn) {
-        if (T == 1) {
-            for (size_t p = 0; p < B; p++) fn(p);
-            return;
-        }
-        std::vector<std::thread> th;
-        for (unsigned k = 0; k < T; k++)
-            th.emplace_back([&, k] {
-                for (size_t p = B * k / T; p < B * (k + 1) / T; p++) fn(p);
-            });
-        for (auto& x : th) x.join();
-    };
+    auto par_for = [&](auto fn) { pool_for(0, B, 16, fn); };  // the persistent host pool (host/pool.hpp)
     par_for([&](size_t p) {
         IpaState& s = st[p];
         s.a = data[p];
@@ -1050,13 +1039,11 @@ static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint
             memcpy(o + 43, y + 4 * i, 32);
         }
     };
-    const unsigned T = Q >= 8192 ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1;
-    if (T == 1) {
+    if (Q < 8192 || host_pool().size() == 1) {
         fill(0, Q);
     } else {
-        std::vector<std::thread> th;
-        for (unsigned k = 0; k < T; k++) th.emplace_back(fill, Q * k / T, Q * (k + 1) / T);
-        for (auto& x : th) x.join();
+        const unsigned T = host_pool().size();
+        host_pool().run([&](unsigned k) { fill(Q * k / T, Q * (k + 1) / T); });
     }
     return tr;
 }

@@ -7,11 +7,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <array>
-#include <condition_variable>
 #include <cstring>
-#include <functional>
 #include <map>
-#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -19,6 +16,7 @@
 #include "../../include/vc_verkle.h"
 #include "ctx.hpp"
 #include "comm.hpp"
+#include "host/pool.hpp"
 #include "host/fr.hpp"
 
 namespace {
@@ -56,63 +54,6 @@ struct FlatMap {
         return it->second;
     }
 };
-
-// Persistent host workers for the commitment's parallel node loops. Spawning and joining 16
-// threads per loop cost ~0.3-0.8 ms and there are ~12 loops per commitment; the pool's threads
-// wait on a condition variable between loops (and are never joined: the pool lives until exit).
-class HostPool {
-public:
-    explicit HostPool(unsigned n) : n_(n) {
-        for (unsigned k = 1; k < n; k++) th_.emplace_back([this, k] { loop(k); });
-    }
-    unsigned size() const { return n_; }
-    // f(k) for every k < size(), k == 0 on the calling thread; one loop at a time
-    void run(const std::function<void(unsigned)>& f) {
-        std::lock_guard<std::mutex> one(run_mu_);
-        if (n_ == 1) {
-            f(0);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            job_ = &f;
-            pending_ = n_ - 1;
-            gen_++;
-        }
-        cv_.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return pending_ == 0; });
-        job_ = nullptr;
-    }
-
-private:
-    void loop(unsigned k) {
-        unsigned seen = 0;
-        for (;;) {
-            const std::function<void(unsigned)>* f;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                f = job_;
-            }
-            (*f)(k);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_one();
-        }
-    }
-    unsigned n_;
-    std::vector<std::thread> th_;
-    std::mutex mu_, run_mu_;
-    std::condition_variable cv_, done_;
-    const std::function<void(unsigned)>* job_ = nullptr;
-    unsigned pending_ = 0, gen_ = 0;
-};
-static HostPool& host_pool() {
-    static HostPool* p = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-    return *p;
-}
 
 struct VNode {
     bool ext = false;
