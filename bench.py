@@ -530,6 +530,8 @@ def main():
             comm, comm_kind = None, "torch (vc_comm init failed on a peer)"
 
     def step():
+        if world == 1:  # one call: vc_msm_device (sort .. reduction, host fold, affine result)
+            return eng.msm_device(table, d_sc.data_ptr(), n)
         if comm is not None:  # window slice (HIP) -> vc_comm RCCL all-gather -> host sum, all in C
             return comm.msm(eng, table, d_sc.data_ptr(), n)
         # window-slice partial (HIP) -> torch RCCL all-gather of projective partials -> host sum

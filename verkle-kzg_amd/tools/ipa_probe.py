@@ -36,7 +36,7 @@ for name, f in (("commit", lambda: ipa.commit(data)), ("prove", lambda: ipa.prov
     e.enable_timing(False)
     names = ctypes.create_string_buffer(1 << 16)
     rows = []
-    for k in ("fb_commit", "fb_commit_small", "fb_combine", "fb_normalize", "fb_normalize_out", "normalize_out", "msm_accumulate",
+    for k in ("fb_commit", "fb_commit_small", "fb_combine", "fb_normalize", "fb_normalize_out", "normalize_out", "norm_prep", "norm_finish", "msm_accumulate",
               "msm_sort_hist", "msm_sort_coarse", "msm_sort_fine", "msm_fixup", "msm_bitsum", "msm_sumpart",
               "msm_segsum", "to_canon", "to_mont", "glv_split", "sparse", "fb_chunk"):
         ms, cnt = e.kernel_time(k)
@@ -61,7 +61,7 @@ e.reset_timing()
 ipa.prove_batch_points(coms, pts, datas)
 e.enable_timing(False)
 rows = []
-for k in ("fb_commit", "fb_commit_small", "fb_combine", "fb_normalize_out", "normalize_out", "fb_commit_cm"):
+for k in ("fb_commit", "fb_commit_small", "fb_combine", "fb_normalize_out", "normalize_out", "norm_prep", "norm_finish", "fb_commit_cm"):
     ms, cnt = e.kernel_time(k)
     if cnt:
         rows.append((k, ms, cnt))
