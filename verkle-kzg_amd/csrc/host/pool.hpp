@@ -5,9 +5,11 @@
 #pragma once
 #include <algorithm>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <utility>
 #include <vector>
 
 namespace vk {
@@ -18,27 +20,46 @@ public:
         for (unsigned k = 1; k < n; k++) th_.emplace_back([this, k] { loop(k); });
     }
     unsigned size() const { return n_; }
-    // f(k) for every k < size(), k == 0 on the calling thread; one loop at a time
+    // f(k) for every k < size(), k == 0 on the calling thread; one loop at a time. A loop
+    // started from inside a job (a worker, or the caller's own f(0)) runs serially on that thread
+    // instead of waiting for the pool it occupies. The first exception thrown by any f(k) is
+    // rethrown here once every worker has finished its part.
     void run(const std::function<void(unsigned)>& f) {
-        std::lock_guard<std::mutex> one(run_mu_);
-        if (n_ == 1) {
-            f(0);
+        if (n_ == 1 || in_job()) {
+            for (unsigned k = 0; k < n_; k++) f(k);
             return;
         }
+        std::lock_guard<std::mutex> one(run_mu_);
         {
             std::lock_guard<std::mutex> lk(mu_);
             job_ = &f;
             pending_ = n_ - 1;
+            err_ = nullptr;
             gen_++;
         }
         cv_.notify_all();
-        f(0);
+        call(f, 0);
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [&] { return pending_ == 0; });
         job_ = nullptr;
+        if (err_) std::rethrow_exception(std::exchange(err_, nullptr));
     }
 
 private:
+    static bool& in_job() {
+        static thread_local bool flag = false;
+        return flag;
+    }
+    void call(const std::function<void(unsigned)>& f, unsigned k) {
+        in_job() = true;
+        try {
+            f(k);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!err_) err_ = std::current_exception();
+        }
+        in_job() = false;
+    }
     void loop(unsigned k) {
         unsigned seen = 0;
         for (;;) {
@@ -49,7 +70,7 @@ private:
                 seen = gen_;
                 f = job_;
             }
-            (*f)(k);
+            call(*f, k);
             std::lock_guard<std::mutex> lk(mu_);
             if (--pending_ == 0) done_.notify_one();
         }
@@ -59,6 +80,7 @@ private:
     std::mutex mu_, run_mu_;
     std::condition_variable cv_, done_;
     const std::function<void(unsigned)>* job_ = nullptr;
+    std::exception_ptr err_;
     unsigned pending_ = 0, gen_ = 0;
 };
 inline HostPool& host_pool() {
