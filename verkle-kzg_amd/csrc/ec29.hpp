@@ -148,11 +148,16 @@ struct SW29 {
         for (int j = 0; j < P::L; j++) r.v[j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[j], K * 0x55, 0xf, 0xf, false);
         return r;
     }
+    // operand of this lane's role, by masks: a select of the values (role ? a.v[j] : b.v[j]) lets
+    // the compiler turn it into a load through a selected address, which pins the accumulators
+    // in scratch memory (572 B per lane, reloaded every add)
     __device__ static f29<P> sel4(uint32_t role, const f29<P>& a0, const f29<P>& a1, const f29<P>& a2,
                                   const f29<P>& a3) {
+        const uint32_t m0 = 0u - (uint32_t)(role == 0), m1 = 0u - (uint32_t)(role == 1);
+        const uint32_t m2 = 0u - (uint32_t)(role == 2), m3 = 0u - (uint32_t)(role == 3);
         f29<P> r;
 #pragma unroll
-        for (int j = 0; j < P::L; j++) r.v[j] = role == 0 ? a0.v[j] : role == 1 ? a1.v[j] : role == 2 ? a2.v[j] : a3.v[j];
+        for (int j = 0; j < P::L; j++) r.v[j] = (a0.v[j] & m0) | (a1.v[j] & m1) | (a2.v[j] & m2) | (a3.v[j] & m3);
         return r;
     }
     __device__ static Acc add_quad(const Acc& p, const Acc& q, uint32_t role) {

@@ -130,12 +130,29 @@ __global__ void __launch_bounds__(256) k_msm_segsum(const typename A::Acc* __res
             const size_t g = (size_t)w * NB + (hi - 1 - it / 2);
             y = offsets[g + 1] > offsets[g] ? buckets[g] : A::zero();
         }
-        const Acc r = A::add(second ? acc : R, y);
-        if (second) acc = r;
-        else R = r;
+        const Acc r = A::add(mask_select(second, acc, R), y);
+        acc = mask_select(second, r, acc);
+        R = mask_select(second, R, r);
     }
     accs[gid] = acc;
     Rs[gid] = R;
+}
+
+// c ? a : b word by word through masks: a plain select of two aggregates becomes a load through a
+// selected address, which keeps both in scratch memory for the whole loop
+template <class T>
+__device__ __forceinline__ T mask_select(bool c, const T& a, const T& b) {
+    static_assert(sizeof(T) % 4 == 0, "");
+    constexpr int NW = (int)(sizeof(T) / 4);
+    uint32_t wa[NW], wb[NW];
+    __builtin_memcpy(wa, &a, sizeof wa);
+    __builtin_memcpy(wb, &b, sizeof wb);
+    const uint32_t m = 0u - (uint32_t)c;
+#pragma unroll
+    for (int k = 0; k < NW; k++) wa[k] = (wa[k] & m) | (wb[k] & ~m);
+    T r;
+    __builtin_memcpy(&r, wa, sizeof wa);
+    return r;
 }
 
 template <class A>
@@ -222,34 +239,44 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
 
 // the same on quads (SW curves): 16 logical lanes per wave, each a quad running the 4-lane
 // cooperative add (SW29::add_quad: ~3,100 instead of ~6,600 instructions per add). This stage is
-// latency-bound -- one wave per sum, W (J + 1) waves on 1024 SIMDs -- so the shorter add pays even
-// though a 52-partial sum then takes ceil(52 / 16) + 4 = 8 adds instead of 1 + 6 = 7.
+// latency-bound -- a block per sum, W (J + 1) blocks on 1024 SIMDs -- so the shorter add pays.
+// A block of SUMPART_WAVES waves per sum (64 quads at 4): a 52-partial sum is one add per quad,
+// 4 butterfly levels inside each wave, then wave 0 folds the wave totals from LDS in 2 more --
+// 7 dependent adds (8 for the 103-partial A sum) instead of 8 (11) with one wave per sum.
+constexpr uint32_t SUMPART_WAVES = 4;
 template <class C, class A>
-__global__ void __launch_bounds__(64) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial, uint32_t J,
-                                                     uint32_t nb1, uint32_t nb2, typename C::Acc* __restrict__ out) {
+__global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial,
+                                                                     uint32_t J, uint32_t nb1, uint32_t nb2,
+                                                                     typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
-    const uint32_t sum = blockIdx.x, lane = threadIdx.x, ql = lane >> 2, role = lane & 3;
+    constexpr uint32_t QPB = 16 * SUMPART_WAVES, LGW = SUMPART_WAVES == 4 ? 2 : SUMPART_WAVES == 2 ? 1 : 0;
+    static_assert((1u << LGW) == SUMPART_WAVES, "SUMPART_WAVES: 1, 2 or 4");
+    __shared__ Acc wave_sum[SUMPART_WAVES];
+    const uint32_t sum = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, role = lane & 3;
     const uint32_t w = sum / (J + 1), q = sum % (J + 1);
     const uint32_t cnt = q < J ? nb1 : nb2;
     const size_t start = (size_t)w * (J * nb1 + nb2) + (q < J ? q * nb1 : J * nb1);
-    uint32_t span = 1, lg = 0;
-    while (span < cnt && span < 16) {
-        span <<= 1;
-        lg++;
-    }
-    const uint32_t nk = (cnt + 15) / 16;
+    const uint32_t nk = (cnt + QPB - 1) / QPB;
     Acc v = A::zero();
-    for (uint32_t it = 0; it < nk + lg; it++) {  // one add call site
+    for (uint32_t it = 0; it < nk + 4 + LGW; it++) {  // one add call site
         Acc o;
         if (it < nk) {
-            const uint32_t k = ql + it * 16;
+            const uint32_t k = (tid >> 2) + it * QPB;  // quad index within the block
             o = k < cnt ? partial[start + k] : A::zero();
+        } else if (it < nk + 4) {
+            o = shfl_acc<A>(v, 4u << (it - nk));  // quad to quad inside the wave: xor of a multiple of 4
         } else {
-            o = shfl_acc<A>(v, 4u << (it - nk));  // quad to quad: xor of a multiple of 4
+            if (it == nk + 4) {  // every quad of a wave holds the wave's total
+                if (lane == 0) wave_sum[wv] = v;
+                __syncthreads();
+                if (wv != 0) break;
+                v = (lane >> 2) < SUMPART_WAVES ? wave_sum[lane >> 2] : A::zero();
+            }
+            o = shfl_acc<A>(v, 4u << (it - nk - 4));
         }
         v = A::add_quad(v, o, role);
     }
-    if (lane == 0) out[sum] = A::store(v);
+    if (tid == 0) out[sum] = A::store(v);
 }
 
 // pointer-jumping rounds r0 <= r < r1 (span 2^r) for a host-known Lmax, or -- guarded -- rounds
@@ -351,7 +378,8 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
     VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
               n_waves, live, partial);
     if constexpr (A::quad)
-        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, nb1,
+                     nb2, out);
     else
         VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
     return VC_OK;
