@@ -311,6 +311,17 @@ __device__ __forceinline__ T shfl_xor_pod(const T& v, uint32_t m) {
     for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = __shfl_xor(src[k], m, 64);
     return o;
 }
+// v of lane `src` (word by word)
+template <class T>
+__device__ __forceinline__ T shfl_idx_pod(const T& v, uint32_t src_lane) {
+    static_assert(sizeof(T) % 4 == 0, "");
+    T o;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); k++) dst[k] = __shfl(src[k], (int)src_lane, 64);
+    return o;
+}
 #endif
 
 // curve of ec.hpp -> its radix-2^29 mixed-add engine
