@@ -136,10 +136,70 @@ static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_
     return VC_OK;
 }
 
+// Straus on the host pool for the verifiers' few-point MSMs (IPA verify: C and the 2K proof
+// points L_k / R_k, 17 at N = 256): on the GPU every term pays the Pippenger pipeline's fixed
+// latency (upload, sort, accumulate, fix-up, reductions: ~0.25 ms for 17 points); here each pool
+// thread takes a slice of the points -- 4-bit windows over 15 precomputed multiples, 252 shared
+// doublings -- and the slices are added (~0.1 ms). The points are checked as bases_fill checks
+// them (canonical coordinates, on the curve: VC_E_NOT_ON_CURVE).
+constexpr size_t HOST_MSM_MAX = 64;
+static int host_msm(const uint64_t* xy, const uint8_t* inf, const Fr* sc, size_t n, Acc* out) {
+    using Fq = BN254Fq;
+    std::vector<Acc> base(n, C::zero());
+    for (size_t i = 0; i < n; i++) {
+        if (inf[i]) continue;
+        fe<Fq> x, y;
+        memcpy(x.v, xy + 8 * i, 32);
+        memcpy(y.v, xy + 8 * i + 4, 32);
+        if (!fe_eq<Fq>(fe_reduce_once<Fq>(x), x) || !fe_eq<Fq>(fe_reduce_once<Fq>(y), y)) return VC_E_NOT_ON_CURVE;
+        x = fe_to_mont<Fq>(x);
+        y = fe_to_mont<Fq>(y);
+        fe<Fq> b = fe_zero<Fq>();
+        b.v[0] = (uint32_t)C::COEFF_B;
+        if (!fe_eq<Fq>(fe_add<Fq>(fe_mul<Fq>(fe_sqr<Fq>(x), x), fe_to_mont<Fq>(b)), fe_sqr<Fq>(y)))
+            return VC_E_NOT_ON_CURVE;
+        base[i].x = x;
+        base[i].y = y;
+        base[i].zz = fe_one<Fq>();
+        base[i].zzz = fe_one<Fq>();
+    }
+    HostPool& pool = host_pool();
+    const unsigned T = (unsigned)std::max<size_t>(1, std::min<size_t>(pool.size(), n));
+    std::vector<Acc> part(T, C::zero());
+    pool.run([&](unsigned k) {
+        if (k >= T) return;
+        const size_t lo = n * k / T, hi = n * (k + 1) / T;
+        std::vector<Acc> mult((hi - lo) * 16);
+        std::vector<Fr> can(hi - lo);
+        for (size_t i = lo; i < hi; i++) {
+            Acc* m = &mult[(i - lo) * 16];
+            m[1] = base[i];
+            m[2] = C::dbl(base[i]);
+            for (int j = 3; j < 16; j++) m[j] = C::add(m[j - 1], base[i]);
+            can[i - lo] = fe_from_mont<F>(sc[i]);
+        }
+        Acc acc = C::zero();
+        for (int w = 63; w >= 0; w--) {  // nibbles of the 256-bit canonical scalars, top first
+            if (!C::is_zero(acc))
+                for (int d = 0; d < 4; d++) acc = C::dbl(acc);
+            for (size_t i = lo; i < hi; i++) {
+                const uint32_t nib = (can[i - lo].v[w >> 3] >> (4 * (w & 7))) & 15u;
+                if (nib) acc = C::add(acc, mult[(i - lo) * 16 + nib]);
+            }
+        }
+        part[k] = acc;
+    });
+    Acc r = C::zero();
+    for (const Acc& p : part) r = C::add(r, p);
+    *out = r;
+    return VC_OK;
+}
+
 // variable-base MSM over host points (ctx scratch table) with Montgomery scalars -> Acc
 static int msm_points(vc_ctx* ctx, const std::vector<uint64_t>& xy, const std::vector<uint8_t>& inf,
                       const std::vector<Fr>& sc, Acc* out) {
     size_t n = sc.size();
+    if (n <= HOST_MSM_MAX) return host_msm(xy.data(), inf.data(), sc.data(), n, out);
     VK_TRY(bases_fill(ctx, &ctx->scratch, xy.data(), inf.data(), n));
     DevBuf d(ctx);
     VK_TRY(d.ensure(std::max<size_t>(n, 1) * 32));
