@@ -160,7 +160,7 @@ struct SW29 {
         for (int j = 0; j < P::L; j++) r.v[j] = (a0.v[j] & m0) | (a1.v[j] & m1) | (a2.v[j] & m2) | (a3.v[j] & m3);
         return r;
     }
-    __device__ static Acc add_quad(const Acc& p, const Acc& q, uint32_t role) {
+    __device__ __forceinline__ static Acc add_quad(const Acc& p, const Acc& q, uint32_t role) {
         if (p.inf) return q;
         if (q.inf) return p;
         // round 1: U1 = X1 ZZ2, U2 = X2 ZZ1, S1 = Y1 ZZZ2, S2 = Y2 ZZZ1

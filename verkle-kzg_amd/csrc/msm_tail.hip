@@ -95,6 +95,28 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk(typename A::Acc* __restr
     for (uint32_t u = t0 + 1; u <= t1; u++) acc = A::add(acc, carry[u]);
     buckets[b] = acc;
 }
+// the same with a quad per bucket (SW curves: SW29::add_quad, ~half the latency of an add): the
+// walk is bound by its longest chains -- the top window's hot buckets at the multi-GPU window
+// slices, up to 16 pieces -- and leaves most SIMDs idle with a lane per bucket
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_fixup_walk_q(typename A::Acc* __restrict__ buckets,
+                                                         const typename A::Acc* __restrict__ carry,
+                                                         const typename A::Acc* __restrict__ owner_piece,
+                                                         const uint32_t* __restrict__ offsets, uint32_t NBtot,
+                                                         uint32_t M, uint32_t limit) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, b = gid >> 2, role = gid & 3;
+    if (b >= NBtot) return;  // whole quads (NBtot * 4 threads)
+    const uint32_t lo = offsets[b], hi = offsets[b + 1];
+    if (hi <= lo) return;
+    const uint32_t t0 = lo / M, t1 = (hi - 1) / M;
+    if (t0 == t1 || t1 - t0 > limit) return;  // uniform over the quad
+    typename A::Acc acc = owner_piece[t0];
+    for (uint32_t u = t0 + 1; u <= t1; u++) {
+        const typename A::Acc o = carry[u];
+        acc = A::add_quad(acc, o, role);
+    }
+    if (role == 0) buckets[b] = acc;
+}
 
 // ------------------------------------------------------------------ bucket reduction
 // Window sum  V_w = sum_b (b + 1) B_b  over NB buckets, in two shallow GPU stages and a host pass:
@@ -189,6 +211,28 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
     const uint32_t base = wv * 64 * K;
     const Acc* src = (q < J ? Rs : accs) + (size_t)w * S;
     Acc v = A::zero();
+    if constexpr (A::quad) {
+        // K serial full adds per lane (every SIMD busy: issue-bound), then the wave's 64 lane sums
+        // on 4-lane cooperative adds: each quad first folds its own 4 lanes (3 rounds), then the
+        // 16 quads by xor (4) -- 7 adds of ~14.6k cycles instead of the 6-level butterfly of full
+        // adds (~30k cycles each)
+        for (uint32_t it = 0; it < K; it++) {
+            const uint32_t m = base + it * 64 + lane;
+            const uint32_t idx = q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m;
+            const size_t g = (size_t)w * S + idx;
+            const bool live = m < n_items && (!offsets || offsets[g + 1] > offsets[g]);
+            const Acc o = live ? src[idx] : A::zero();
+            v = A::add(v, o);
+        }
+        const uint32_t role = lane & 3, q0 = lane & ~3u;
+        Acc s = shfl_idx_pod(v, q0);
+        for (uint32_t it = 0; it < 7; it++) {
+            const Acc o = it < 3 ? shfl_idx_pod(v, q0 + it + 1) : shfl_acc<A>(s, 4u << (it - 3));
+            s = A::add_quad(s, o, role);
+        }
+        if (lane == 0) partial[gw] = s;
+        return;
+    }
     for (uint32_t it = 0; it < K + 6; it++) {
         Acc o;
         if (it < K) {
@@ -337,6 +381,17 @@ template <class C>
 int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t NBtot, uint32_t M, FAcc<C>* buckets,
                         const FAcc<C>* carry, const FAcc<C>* owner, uint32_t limit) {
     using A = typename Fast29<C>::type;
+    static const int quad_env = getenv("VKZG_FIXUP_QUAD") ? atoi(getenv("VKZG_FIXUP_QUAD")) : 1;  // A/B probe
+    // quads while their waves fit ~2 per SIMD (one bucket set: 2^15 buckets -> 2048 waves); with
+    // per-window bucket sets (8 x 2^15) every SIMD already has lane-per-bucket waves and the
+    // quads' ~2x instructions per add made the walk slower (0.08 -> 0.115 ms)
+    if constexpr (A::quad) {
+        if (quad_env && NBtot <= 65536) {
+            VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk_q<A>), (uint32_t)(((size_t)NBtot * 4 + 255) / 256), 256,
+                         0, buckets, carry, owner, offsets, NBtot, M, limit);
+            return VC_OK;
+        }
+    }
     VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk<A>), (NBtot + 255) / 256, 256, 0, buckets, carry, owner,
                  offsets, NBtot, M, limit);
     return VC_OK;
