@@ -14,6 +14,9 @@
 // Load balance does not depend on the scalar distribution: the accumulate work per
 // thread is fixed (M entries) even when every scalar hits one bucket.
 #include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -910,11 +913,21 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     return VC_OK;
 }
 
+// VKZG_HOST_TIMING=1: host-side phases of each MSM on stderr (probe; tools/msm_probe.py)
+static bool host_timing() {
+    static const bool on = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+    return on;
+}
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 template <class C, class Fr>
 static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc, size_t n,
                      int mont, int part, int parts, uint32_t* out_acc) {
     using Acc = typename C::Acc;
     using Aff = typename C::Aff;
+    const double t_entry = host_timing() ? now_us() : 0.0;
     if (n == 0) {
         Acc z = C::zero();
         memcpy(out_acc, &z, sizeof(Acc));
@@ -1030,12 +1043,18 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                                     k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
     }
     for (int k = 0; k < nsl; k++) VK_TRY(slice_fetch<C>(sl[k]));
+    const double t_enq = host_timing() ? now_us() : 0.0;
+    if (host_timing()) VK_CHECK_HIP(hipStreamSynchronize(sl[nsl - 1].L.st));
+    const double t_sync = host_timing() ? now_us() : 0.0;
     Acc res = C::zero();
     for (int k = 0; k < nsl; k++) {
         Acc r;
         VK_TRY(slice_finish<C>(ctx, sl[k], &r));
         res = C::add(res, r);
     }
+    if (host_timing())
+        fprintf(stderr, "msm_host n=%zu enqueue_us=%.1f wait_us=%.1f fold_us=%.1f\n", n, t_enq - t_entry,
+                t_sync - t_enq, now_us() - t_sync);
     if (nsl == 2) {  // later work on the context's stream stays ordered after lane 1
         join = ctx->get_event();
         VK_CHECK_HIP(hipEventRecord(join, ctx->side_stream));
