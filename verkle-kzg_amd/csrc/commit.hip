@@ -356,6 +356,30 @@ __global__ void __launch_bounds__(256) k_fb_combine_cm(const typename Fast29<C>:
     for (uint32_t k = 1; k < nch; k++) acc = FC::add(acc, piece[(size_t)k * batch + g]);
     out[g] = FC::store(acc);
 }
+// G = 2^lgG lanes per commit (consecutive lanes of one wave): each folds a strided share of the
+// nch pieces, then lgG xor levels -- ceil(nch / G) + lgG serial adds. G grows while the lanes
+// still fit one wave per SIMD: 10k width-256 commits (13 chunks) take 4 lanes each, 5 adds
+// instead of the 12 of a thread per commit on 157 waves
+template <class C>
+__global__ void __launch_bounds__(256) k_fb_combine_grp(const typename Fast29<C>::type::Acc* __restrict__ piece,
+                                                       uint32_t nch, uint32_t batch, uint32_t lgG,
+                                                       typename C::Acc* __restrict__ out) {
+    using FC = typename Fast29<C>::type;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, g = gid >> lgG, j = gid & ((1u << lgG) - 1);
+    const uint32_t G = 1u << lgG, nk = (nch + G - 1) / G;
+    typename FC::Acc v = FC::zero();
+    for (uint32_t it = 0; it < nk + lgG; it++) {  // one add call site; every lane runs the shuffles
+        typename FC::Acc o;
+        if (it < nk) {
+            const uint32_t k = j + it * G;
+            o = (g < batch && k < nch) ? piece[(size_t)k * batch + g] : FC::zero();
+        } else {
+            o = shfl_xor_pod(v, 1u << (it - nk));
+        }
+        v = FC::add(v, o);
+    }
+    if (g < batch && j == 0) out[g] = FC::store(v);
+}
 template <class C>
 __global__ void __launch_bounds__(64) k_fb_combine_wave(const typename Fast29<C>::type::Acc* __restrict__ piece,
                                                        uint32_t nch, uint32_t batch, typename C::Acc* __restrict__ out) {
@@ -605,7 +629,15 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     while ((1ull << lg) < std::min<size_t>(nch, 64)) lg++;
     const size_t cost_thread = nch * ((batch + 65535) / 65536);
     const size_t cost_wave = ((batch + 1023) / 1024) * ((nch + 63) / 64 + lg);
-    if (cost_thread <= cost_wave)
+    // lanes per commit: grow while there are pieces to split and the lanes fit a wave per SIMD
+    uint32_t lgG = 0;
+    while (lgG < 6 && (2ull << lgG) <= nch && batch * (2ull << lgG) <= 65536) lgG++;
+    static const int grp_env = getenv("VKZG_COMBINE_GROUP") ? atoi(getenv("VKZG_COMBINE_GROUP")) : 1;  // A/B probe
+    if (grp_env && lgG > 0 && lgG < 6)
+        VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_grp<C>), (uint32_t)(((batch << lgG) + 255) / 256), 256, 0,
+                  ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>(), (uint32_t)nch, (uint32_t)batch, lgG,
+                  ctx->ws[WS_OUT].as<Acc>());
+    else if (cost_thread <= cost_wave)
         VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_cm<C>), (batch + 255) / 256, 256, 0,
                   ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>(), (uint32_t)nch, (uint32_t)batch,
                   ctx->ws[WS_OUT].as<Acc>());
