@@ -304,6 +304,63 @@ static int acc_to_affine_t(const uint32_t* accw, uint64_t* out_xy, uint8_t* out_
     *out_inf = 0;
     return VC_OK;
 }
+// n accumulators -> canonical affine with ONE field inversion (Montgomery's trick over the
+// denominators: ZZZ for XYZZ, Z for extended Edwards); the same outputs as acc_to_affine_t
+template <class C>
+static int acc_to_affine_batch_t(const uint32_t* accw, size_t n, uint64_t* out_xy, uint8_t* out_inf) {
+    using F = typename C::F;
+    using Acc = typename C::Acc;
+    constexpr size_t AW = sizeof(Acc) / 4;
+    auto den = [](const Acc& a) {
+        if constexpr (C::is_te) return a.Z;
+        else return a.zzz;
+    };
+    std::vector<Acc> a(n);
+    std::vector<fe<F>> pre(n);
+    std::vector<uint8_t> live(n);
+    fe<F> run = fe_one<F>();
+    for (size_t i = 0; i < n; i++) {
+        memcpy(&a[i], accw + i * AW, sizeof(Acc));
+        bool z;
+        if constexpr (C::is_te) z = fe_is_zero<F>(a[i].Z);
+        else z = C::is_zero(a[i]);
+        live[i] = !z;
+        pre[i] = run;
+        if (live[i]) run = fe_mul<F>(run, den(a[i]));
+    }
+    fe<F> inv = fe_inv_bin<F>(run);
+    for (size_t i = n; i-- > 0;) {
+        uint64_t* xy = out_xy + i * F::N;  // 2 N 32-bit words = N u64 words per point
+        fe<F> x, y;
+        bool fin = false;
+        if (live[i]) {
+            const fe<F> id = fe_mul<F>(inv, pre[i]);  // 1 / den(a_i)
+            inv = fe_mul<F>(inv, den(a[i]));
+            if constexpr (C::is_te) {
+                x = fe_mul<F>(a[i].X, id);
+                y = fe_mul<F>(a[i].Y, id);
+                fin = !(fe_is_zero<F>(x) && fe_eq<F>(y, fe_one<F>()));
+            } else {
+                const fe<F> t = fe_mul<F>(id, a[i].zz);  // 1 / Z
+                x = fe_mul<F>(a[i].x, fe_sqr<F>(t));
+                y = fe_mul<F>(a[i].y, id);
+                fin = true;
+            }
+        }
+        if (!fin) {
+            memset(xy, 0, 2 * F::N * 4);
+            if (C::is_te) xy[0 + F::N / 2] = 1;  // y = 1
+            out_inf[i] = 1;
+            continue;
+        }
+        x = fe_from_mont<F>(x);
+        y = fe_from_mont<F>(y);
+        memcpy(xy, x.v, F::N * 4);
+        memcpy(reinterpret_cast<uint32_t*>(xy) + F::N, y.v, F::N * 4);
+        out_inf[i] = 0;
+    }
+    return VC_OK;
+}
 template <class C>
 static int acc_sum_t(const uint32_t* accs, size_t k, uint32_t* out) {
     typename C::Acc r = C::zero();
@@ -320,6 +377,14 @@ int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out
         case VC_CURVE_BN254: return acc_to_affine_t<BN254G1>(acc, out_xy, out_inf);
         case VC_CURVE_BLS12_381: return acc_to_affine_t<BLS381G1>(acc, out_xy, out_inf);
         case VC_CURVE_BANDERSNATCH: return acc_to_affine_t<Bandersnatch>(acc, out_xy, out_inf);
+    }
+    return VC_E_INVALID;
+}
+int acc_to_affine_batch(int curve, const uint32_t* accs, size_t n, uint64_t* out_xy, uint8_t* out_inf) {
+    switch (curve) {
+        case VC_CURVE_BN254: return acc_to_affine_batch_t<BN254G1>(accs, n, out_xy, out_inf);
+        case VC_CURVE_BLS12_381: return acc_to_affine_batch_t<BLS381G1>(accs, n, out_xy, out_inf);
+        case VC_CURVE_BANDERSNATCH: return acc_to_affine_batch_t<Bandersnatch>(accs, n, out_xy, out_inf);
     }
     return VC_E_INVALID;
 }

@@ -592,11 +592,15 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         std::vector<uint8_t> oinf(h_out_xy ? 0 : batch);
         uint64_t* rxy = h_out_xy ? h_out_xy : oxy.data();
         uint8_t* rinf = h_out_xy ? h_out_inf : oinf.data();
+        // the partials serially (the host pool's wake-up cost more than the ~23 us of adds of the
+        // IPA prover's 2 x 33 partials: prove 0.89 -> 1.07 ms), then one batched inversion
+        std::vector<Acc> sums(batch);
         for (size_t g = 0; g < batch; g++) {
             Acc a = parts[g * bpc];
             for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
-            VK_TRY(acc_to_affine(ctx->curve, reinterpret_cast<const uint32_t*>(&a), rxy + g * 2 * nl, rinf + g));
+            sums[g] = a;
         }
+        VK_TRY(acc_to_affine_batch(ctx->curve, reinterpret_cast<const uint32_t*>(sums.data()), batch, rxy, rinf));
         if (h_out_xy) {
             *on_host = true;
             return VC_OK;

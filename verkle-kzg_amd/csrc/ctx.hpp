@@ -215,6 +215,8 @@ int msm_windows(int curve, size_t n, int* c, int* W, int* terms);
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
             uint32_t* out_acc, int part = 0, int parts = 1);
 int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out_inf);
+// n accumulators with one field inversion (Montgomery's trick); same outputs as acc_to_affine
+int acc_to_affine_batch(int curve, const uint32_t* accs, size_t n, uint64_t* out_xy, uint8_t* out_inf);
 int acc_sum(int curve, const uint32_t* accs, size_t k, uint32_t* out);
 int point_words(int curve);
 int aff_limbs64(int curve);  // NL of the base field in u64 limbs
