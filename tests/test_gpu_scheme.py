@@ -353,3 +353,32 @@ def test_kzg_multiproof_sharded_golden(eng, G):
         mp = scheme.multiproof_finish(vc, z, parts.data_ptr(), G, tr)
     assert mp["d"] == P(g["d"])
     assert mp["proof"]["proof"] == P(g["proof"]["proof"]) and mp["proof"]["y"] == H(g["proof"]["y"])
+
+
+def test_multiproof_phases_reject_out_of_domain_z(eng):
+    """The sharded multiproof's accumulate / finish entry points take z from the caller again:
+    a query point outside the domain is VC_E_DOMAIN (the reference panics indexing the Lagrange
+    evaluations), an absurd domain size VC_E_INVALID -- validated before any allocation sized
+    by the values (multiproof.rs:119-144)."""
+    import ctypes
+    import numpy as np
+    import torch
+    import vkzg
+    from vkzg import scheme
+    from vkzg._lib import lib
+    N, Q = 256, 4
+    z = np.array([1, 5, 300, 7], dtype=np.uint64)  # 300 >= N
+    r = np.array([3, 0, 0, 0], dtype=np.uint64)
+    d_data = torch.zeros((Q, N, 4), dtype=torch.int64, device="cuda")
+    d_S = torch.zeros((Q, N, 4), dtype=torch.int64, device="cuda")
+    with pytest.raises(vkzg.VCError) as ex:
+        scheme.multiproof_accumulate(eng, N, z, 0, Q, d_data.data_ptr(), r, d_S.data_ptr())
+    assert ex.value.status == -8
+    zbig = np.array([1, 5, 1 << 62, 7], dtype=np.uint64)
+    with pytest.raises(vkzg.VCError) as ex:
+        scheme.multiproof_accumulate(eng, N, zbig, 0, Q, d_data.data_ptr(), r, d_S.data_ptr())
+    assert ex.value.status == -8
+    st = lib().vc_multiproof_accumulate(eng.h, 1 << 40, Q, z.ctypes.data_as(ctypes.c_void_p), 0, Q,
+                                        ctypes.c_void_p(d_data.data_ptr()), r.ctypes.data_as(ctypes.c_void_p),
+                                        ctypes.c_void_p(d_S.data_ptr()))
+    assert st == -1

@@ -1135,15 +1135,20 @@ static int mp_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* c
 }
 
 // distinct query points, sorted (the rows of S)
-static std::vector<uint32_t> mp_points(size_t Q, const uint64_t* z) {
-    uint64_t zmax = 0;
-    for (size_t i = 0; i < Q; i++) zmax = std::max(zmax, z[i]);
-    std::vector<uint8_t> seen(zmax + 1, 0);  // z < N (checked by the callers)
-    for (size_t i = 0; i < Q; i++) seen[z[i]] = 1;
-    std::vector<uint32_t> v;
-    for (uint64_t k = 0; k <= zmax; k++)
-        if (seen[k]) v.push_back((uint32_t)k);
-    return v;
+// distinct query points, sorted; VC_E_DOMAIN for a z outside the domain (the reference indexes
+// the Lagrange evaluations with it and panics). The accumulate / finish entry points take z
+// from the caller again, so every path validates here (a bitmap of N, not of max z).
+static int mp_points(size_t N, size_t Q, const uint64_t* z, std::vector<uint32_t>* out) {
+    if (N == 0 || N > (size_t(1) << 28)) return VC_E_INVALID;  // BN254 Fr has 2-adicity 28
+    std::vector<uint8_t> seen(N, 0);
+    for (size_t i = 0; i < Q; i++) {
+        if (z[i] >= N) return VC_E_DOMAIN;
+        seen[z[i]] = 1;
+    }
+    out->clear();
+    for (size_t k = 0; k < N; k++)
+        if (seen[k]) out->push_back((uint32_t)k);
+    return VC_OK;
 }
 
 // rp[i] = r^(first + i) (Montgomery)
@@ -1200,12 +1205,12 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
         VK_CHECK_HIP(hipStreamSynchronize(st));
         return VC_OK;
     }
-    // row of each query: binary search in zval
-    std::vector<uint32_t> row(Qs);
+    // row of each query: a table over the domain (z < N, checked by mp_points over all queries)
+    std::vector<uint32_t> row_of(N, 0xffffffffu), row(Qs);
+    for (size_t k = 0; k < Z; k++) row_of[zval[k]] = (uint32_t)k;
     for (size_t i = 0; i < Qs; i++) {
-        auto it = std::lower_bound(zval.begin(), zval.end(), (uint32_t)std::min<uint64_t>(z[i], 0xffffffffu));
-        if (z[i] >= N || it == zval.end() || *it != z[i]) return VC_E_DOMAIN;
-        row[i] = (uint32_t)(it - zval.begin());
+        if (z[i] >= N || row_of[z[i]] == 0xffffffffu) return VC_E_DOMAIN;
+        row[i] = row_of[z[i]];
     }
     // counting sort of the shard's queries by row, then chunks of <= MP_CHUNK queries
     std::vector<uint32_t> cnt(Z + 1, 0), order(Qs);
@@ -1330,7 +1335,8 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     vc_transcript* tr = nullptr;
     Fr r;
     VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
-    std::vector<uint32_t> zval = mp_points(Q, z);
+    std::vector<uint32_t> zval;
+    mp_points(N, Q, z, &zval);  // z validated by mp_begin
     DevBuf d_data(ctx), d_S(ctx);
     int st = d_data.ensure(Q * N * 32);
     if (st == VC_OK) st = d_S.ensure(zval.size() * N * 32);
@@ -1404,7 +1410,9 @@ int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_
     Fr r;
     VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
     canon_of(r, r_out);
-    *rows = mp_points(Q, z).size();
+    std::vector<uint32_t> zval;
+    mp_points(N, Q, z, &zval);  // z validated by mp_begin
+    *rows = zval.size();
     *tr_out = tr;
     return VC_OK;
 }
@@ -1415,7 +1423,9 @@ int vc_multiproof_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* z,
         return VC_E_INVALID;
     if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
     Guard g(ctx);
-    return mp_accumulate(ctx, N, Qs, d_data, z + first, fr_of(r), first, mp_points(Q, z), d_S);
+    std::vector<uint32_t> zval;
+    VK_TRY(mp_points(N, Q, z, &zval));
+    return mp_accumulate(ctx, N, Qs, d_data, z + first, fr_of(r), first, zval, d_S);
 }
 
 int vc_multiproof_finish(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* z,
@@ -1429,7 +1439,9 @@ int vc_multiproof_finish(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q,
     Guard g(ctx);
     Table* t = ctx->table(table);
     if (!t) return VC_E_TABLE;
-    return mp_finish(ctx, scheme, t, N, mp_points(Q, z), d_S_parts, G, tr, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf,
+    std::vector<uint32_t> zval;
+    VK_TRY(mp_points(N, Q, z, &zval));
+    return mp_finish(ctx, scheme, t, N, zval, d_S_parts, G, tr, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf,
                      kzg_y);
 }
 
