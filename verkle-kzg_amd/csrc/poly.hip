@@ -315,6 +315,29 @@ static int cached_inv1(vc_ctx* ctx, const fe<F>* pw, size_t n, fe<F>** out) {
     return VC_OK;
 }
 
+template <class F>
+int domain_tables(vc_ctx* ctx, const fe<F>& w, size_t n, const fe<F>** pw, const fe<F>** pwi, const fe<F>** inv1) {
+    fe<F>* a = nullptr;
+    VK_TRY(cached_powers<F>(ctx, w, n, &a));
+    *pw = a;
+    if (inv1) {
+        fe<F>* b = nullptr;
+        VK_TRY(cached_inv1<F>(ctx, a, n, &b));
+        *inv1 = b;
+    }
+    if (pwi) {
+        auto& slot = ctx->dcache[dkey<F>("pwi", n)];
+        if (!slot) {
+            auto b = std::make_unique<DevBuf>();
+            VK_TRY(b->ensure(n * sizeof(fe<F>)));
+            VK_TRY(domain_powers<F>(ctx, fe_inv_bin<F>(w), n, b->as<fe<F>>()));
+            slot = std::move(b);
+        }
+        *pwi = reinterpret_cast<const fe<F>*>(slot->p);
+    }
+    return VC_OK;
+}
+
 // q and y for KZG prove_point (device, Montgomery). point given in Montgomery form.
 template <class F>
 int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
@@ -418,6 +441,7 @@ int kzg_srs_dev(vc_ctx* ctx, size_t max_items, size_t n, const fe<Fr>& s_mont, c
 #define VK_INST_F(F)                                                                                   \
     template int domain_powers<F>(vc_ctx*, const fe<F>&, size_t, fe<F>*);                             \
     template int batch_inverse<F>(vc_ctx*, const fe<F>*, fe<F>*, size_t);                                           \
+    template int domain_tables<F>(vc_ctx*, const fe<F>&, size_t, const fe<F>**, const fe<F>**, const fe<F>**); \
     template int kzg_quotient_dev<F>(vc_ctx*, size_t, const fe<F>*, size_t, const fe<F>&, const fe<F>&, \
                                      fe<F>*, fe<F>*, DevBuf&, DevBuf&, DevBuf&);                       \
     template int canon_to_mont_dev<F>(vc_ctx*, const void*, size_t, size_t, fe<F>*);                  \

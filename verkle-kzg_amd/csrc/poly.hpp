@@ -8,6 +8,10 @@ template <class F>
 int domain_powers(vc_ctx* ctx, const fe<F>& w, size_t n, fe<F>* d_out);
 template <class F>
 int batch_inverse(vc_ctx* ctx, const fe<F>* d_in, fe<F>* d_out, size_t n);
+// per-ctx cached domain tables of size n (w = the n-th root of unity): pw[i] = w^i,
+// pwi[i] = w^-i, inv1[k] = 1/(w^k - 1) (k > 0; inv1[0] unused)
+template <class F>
+int domain_tables(vc_ctx* ctx, const fe<F>& w, size_t n, const fe<F>** pw, const fe<F>** pwi, const fe<F>** inv1);
 template <class F>
 int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
                      fe<F>* d_q, fe<F>* y_out, DevBuf& pw, DevBuf& tmp, DevBuf& part);

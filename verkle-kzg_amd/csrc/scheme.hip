@@ -668,19 +668,11 @@ static int fk_all_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals, s
 }
 
 // ---------------------------------------------------------------- multiproof kernels
-// den[zi][k] = w^k - w^z (1 at k == z)
-__global__ void k_mp_den(const fe<F>* __restrict__ pw, const uint32_t* __restrict__ zval, size_t N, uint32_t Z,
-                         fe<F>* __restrict__ den) {
-    size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= N * Z) return;
-    size_t zi = g / N, k = g % N;
-    uint32_t z = zval[zi];
-    den[g] = k == z ? fe_one<F>() : fe_sub<F>(pw[k], pw[z]);
-}
-
 // one block per z group: q_z[k] = (S_z[k] - S_z[z]) * inv[k] (k != z),
 // q_z[z] = -w^-z sum_{k != z} q_z[k] w^k   (divide_by_vanishing, lagrange_basis.rs:91-119)
-__global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, const fe<F>* __restrict__ inv,
+// 1/(w^k - w^z) = w^-z / (w^(k-z) - 1) = pw_inv[z] inv1[(k - z) mod N]: the per-domain cached
+// inv1 table replaces a Z x N denominator pass and its batch inversion (and host round trip)
+__global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, const fe<F>* __restrict__ inv1,
                                                 const fe<F>* __restrict__ pw, const fe<F>* __restrict__ pw_inv,
                                                 const uint32_t* __restrict__ zval, size_t N, fe<F>* __restrict__ Q) {
     __shared__ fe<F> sh[256];
@@ -688,11 +680,12 @@ __global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, co
     uint32_t z = zval[zi];
     const fe<F>* Sz = S + (size_t)zi * N;
     fe<F> fz = Sz[z];
+    const fe<F> wmz = pw_inv[z];
     fe<F> acc = fe_zero<F>();
     for (size_t k = threadIdx.x; k < N; k += 256) {
         fe<F> q = fe_zero<F>();
         if (k != z) {
-            q = fe_mul<F>(fe_sub<F>(Sz[k], fz), inv[(size_t)zi * N + k]);
+            q = fe_mul<F>(fe_mul<F>(fe_sub<F>(Sz[k], fz), wmz), inv1[(k + N - z) & (N - 1)]);
             acc = fe_add<F>(acc, fe_mul<F>(q, pw[k]));
         }
         Q[(size_t)zi * N + k] = q;
@@ -1265,28 +1258,20 @@ static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vec
     if (!is_pow2(N) || G < 1 || zval.empty()) return VC_E_INVALID;
     hipStream_t st = ctx->stream;
     const uint32_t Z = (uint32_t)zval.size();
-    DevBuf d_zv(ctx), d_S(ctx), d_den(ctx), d_inv(ctx), d_Q(ctx), d_pw(ctx), d_pwi(ctx), d_g(ctx), d_h(ctx), d_it(ctx);
+    DevBuf d_zv(ctx), d_S(ctx), d_Q(ctx), d_g(ctx), d_h(ctx), d_it(ctx);
     VK_TRY(d_zv.ensure(Z * 4));
     VK_TRY(d_S.ensure((size_t)Z * N * 32));
-    VK_TRY(d_den.ensure((size_t)Z * N * 32));
-    VK_TRY(d_inv.ensure((size_t)Z * N * 32));
     VK_TRY(d_Q.ensure((size_t)Z * N * 32));
-    VK_TRY(d_pw.ensure(N * 32));
-    VK_TRY(d_pwi.ensure(N * 32));
     VK_TRY(d_g.ensure(N * 32));
     VK_TRY(d_h.ensure(N * 32));
     VK_TRY(d_it.ensure(Z * 32));
     VK_CHECK_HIP(hipMemcpyAsync(d_zv.p, zval.data(), Z * 4, hipMemcpyHostToDevice, st));
     VK_LAUNCH(ctx, "mp_sum_parts", k_mp_sum_parts, ((size_t)Z * N + 255) / 256, 256, 0,
               reinterpret_cast<const Fr*>(d_S_parts), G, (size_t)Z * N, d_S.as<Fr>());
-    Fr omega = bn254_group_gen(N);
-    VK_TRY(domain_powers<F>(ctx, omega, N, d_pw.as<fe<F>>()));
-    VK_TRY(domain_powers<F>(ctx, fe_inv_bin<F>(omega), N, d_pwi.as<fe<F>>()));
-    VK_LAUNCH(ctx, "mp_den", k_mp_den, ((size_t)Z * N + 255) / 256, 256, 0, d_pw.as<fe<F>>(), d_zv.as<uint32_t>(), N,
-              Z, d_den.as<fe<F>>());
-    VK_TRY(batch_inverse<F>(ctx, d_den.as<fe<F>>(), d_inv.as<fe<F>>(), (size_t)Z * N));
-    VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, d_S.as<fe<F>>(), d_inv.as<fe<F>>(), d_pw.as<fe<F>>(),
-              d_pwi.as<fe<F>>(), d_zv.as<uint32_t>(), N, d_Q.as<fe<F>>());
+    const fe<F>*pw = nullptr, *pwi = nullptr, *inv1 = nullptr;
+    VK_TRY(domain_tables<F>(ctx, bn254_group_gen(N), N, &pw, &pwi, &inv1));
+    VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, d_S.as<fe<F>>(), inv1, pw, pwi, d_zv.as<uint32_t>(), N,
+              d_Q.as<fe<F>>());
     VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
               (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
     std::vector<Fr> g(N), h(N);
