@@ -382,3 +382,28 @@ def test_multiproof_phases_reject_out_of_domain_z(eng):
                                         ctypes.c_void_p(d_data.data_ptr()), r.ctypes.data_as(ctypes.c_void_p),
                                         ctypes.c_void_p(d_S.data_ptr()))
     assert st == -1
+
+
+def test_ipa_verify_proof_points_on_host_straus(eng, crs):
+    """IPA verify's C / L_k / R_k MSM (17 points at N = 32 + ...) runs as Straus on the host pool
+    (scheme.hip host_msm): swapped L / R and an identity L_k are rejected, an off-curve L_k is
+    VC_E_NOT_ON_CURVE exactly as the GPU upload reports it, and the verdicts match the oracle."""
+    import vkzg
+    from pyoracle import protocol
+    from vkzg import scheme
+    ipa = scheme.IPA(eng, 32, crs[:33])
+    oracle = protocol.IPA(32, points=crs[:33])
+    data = scheme.LagrangeBasis([(7 * i + 3) % 101 for i in range(32)])
+    com = ipa.commit(data)
+    pr = ipa.prove(com, 77, data)
+    assert ipa.verify(com, 77, pr) and oracle.verify(com, 77, pr.as_dict())
+    swapped = scheme.IPAProof(pr.r, pr.l, pr.tip, pr.y)
+    assert not ipa.verify(com, 77, swapped)
+    assert not oracle.verify(com, 77, swapped.as_dict())
+    ident = scheme.IPAProof([None] + list(pr.l[1:]), pr.r, pr.tip, pr.y)
+    assert not ipa.verify(com, 77, ident)
+    assert not oracle.verify(com, 77, ident.as_dict())
+    off = scheme.IPAProof([(1, 1)] + list(pr.l[1:]), pr.r, pr.tip, pr.y)
+    with pytest.raises(vkzg.VCError) as ex:
+        ipa.verify(com, 77, off)
+    assert ex.value.status == -6
