@@ -1321,7 +1321,11 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     Fr r;
     VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
     std::vector<uint32_t> zval;
-    mp_points(N, Q, z, &zval);  // z validated by mp_begin
+    int zst = mp_points(N, Q, z, &zval);  // z itself was validated by mp_begin
+    if (zst != VC_OK) {
+        vc_transcript_free(tr);
+        return zst;
+    }
     DevBuf d_data(ctx), d_S(ctx);
     int st = d_data.ensure(Q * N * 32);
     if (st == VC_OK) st = d_S.ensure(zval.size() * N * 32);
@@ -1338,6 +1342,7 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
 static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                     const uint64_t* y, const uint64_t* d_xy, uint8_t d_inf, Acc* claim, Fr* t_out,
                     vc_transcript** tr_out) {
+    if (!is_pow2(N) || N > (size_t(1) << 28)) return VC_E_INVALID;  // tables below are sized by N
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
     vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y);
@@ -1396,7 +1401,11 @@ int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_
     VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
     canon_of(r, r_out);
     std::vector<uint32_t> zval;
-    mp_points(N, Q, z, &zval);  // z validated by mp_begin
+    const int zst = mp_points(N, Q, z, &zval);  // z itself was validated by mp_begin
+    if (zst != VC_OK) {
+        vc_transcript_free(tr);
+        return zst;
+    }
     *rows = zval.size();
     *tr_out = tr;
     return VC_OK;
