@@ -724,9 +724,16 @@ def main():
             return dxy, dinf
 
         def ctime(cw):
+            fits = True
             try:
                 ceng.fixed_base_precompute(ctab, cw)
             except vkzg.VCError:  # table does not fit next to the rest
+                fits = False
+            if world > 1:  # every rank takes the same branch (a lone skip would hang the barriers)
+                ok = torch.tensor([1 if fits else 0], device=dev)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                fits = bool(int(ok.item()))
+            if not fits:
                 return None
             for _ in range(2):
                 cstep()
