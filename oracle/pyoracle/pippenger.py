@@ -90,3 +90,39 @@ def part_scalars(curve, scalars, part, parts, r):
             d = signed_digits(s, c, W)
             out.append(sum(d[w] << (c * w) for w in range(wb, we)) % r)
     return out
+
+
+# Radix-B shared windows (msm.hip k_glv_radix / radix_digits, the one-GPU whole-table GLV MSM):
+# B = 5 * 2^16, 7 windows (B^7 / 2 > 2^127), B / 2 = 5 * 2^15 buckets in one set.
+RADIX_MUL, RADIX_C0, RADIX_W = 5, 16, 7
+
+
+def radix_digits(k, mul=RADIX_MUL, c0=RADIX_C0, W=RADIX_W):
+    """W signed digits d_w in (-B/2, B/2] of 0 <= k < 2^127 with k = sum d_w B^w, B = mul 2^c0
+    (radix_digits: low c0 bits, then (k >> c0) mod mul, carry recoding as signed_digits)."""
+    B = mul << c0
+    out, carry = [], 0
+    for _ in range(W):
+        raw = (k % B) + carry
+        k //= B
+        if raw > B // 2:
+            out.append(raw - B)
+            carry = 1
+        else:
+            out.append(raw)
+            carry = 0
+    assert k == 0 and carry == 0, "scalar too wide for the radix"
+    return out
+
+
+def radix_bucket_sum(buckets, lseg):
+    """Host fold of the radix reduction (msm.hip slice_finish, msm_tail.hip segsum / bitsum):
+    V = sum_b (b + 1) B_b = A + lseg * sum_j 2^j T_j with segments of lseg buckets,
+    A = sum_s acc_s, acc_s = sum_k (k + 1) B_{s lseg + k}, T_j = sum_{s: bit j of s} R_s.
+    Works on any additive group given as numbers (integers mod anything)."""
+    S = len(buckets) // lseg
+    R = [sum(buckets[s * lseg:(s + 1) * lseg]) for s in range(S)]
+    A = sum((k + 1) * buckets[s * lseg + k] for s in range(S) for k in range(lseg))
+    J = max(1, (S - 1).bit_length())
+    T = [sum(R[s] for s in range(S) if (s >> j) & 1) for j in range(J)]
+    return A + lseg * sum(t << j for j, t in enumerate(T))

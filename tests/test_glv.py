@@ -81,3 +81,38 @@ def test_glv_curve_constants():
         assert _mulraw(C, P, C.r) is not None           # not in the r-torsion
         assert C.add((BETA * BETA * x % p, y), _mulraw(C, P, Z2)) is not None
         outside += 1
+
+
+def test_radix_digits_recombine_and_bound():
+    """k_glv_radix / radix_digits (msm.hip): the GLV halves in radix B = 5 * 2^16, 7 signed digits
+    |d_w| <= B/2 (bucket |d| - 1 < 5 * 2^15), the top digit never negative and never carrying."""
+    from pyoracle import pippenger
+    from pyoracle.curves import BLS12_381 as C
+    B = pippenger.RADIX_MUL << pippenger.RADIX_C0
+    assert B ** 7 // 2 > 1 << 127 and B ** 6 // 2 < 1 << 127
+    rng = random.Random(7)
+    ks = [0, 1, B // 2, B // 2 + 1, B - 1, B, (1 << 127) - 1, (1 << 126), B ** 6, B ** 6 - 1]
+    ks += [rng.randrange(1 << 127) for _ in range(2000)]
+    for k in ks:
+        d = pippenger.radix_digits(k)
+        assert sum(x * B ** w for w, x in enumerate(d)) == k
+        assert all(-B // 2 < x <= B // 2 for x in d)
+        assert d[-1] >= 0
+    # through the GLV split of edge scalars: both halves fit the radix
+    for k in _edge_scalars(C.r, pippenger.GLV_LAMBDA):
+        k1, k2 = pippenger.glv_split(k, C.r)
+        for h in (k1, k2):
+            d = pippenger.radix_digits(abs(h))
+            assert sum(x * B ** w for w, x in enumerate(d)) == abs(h)
+
+
+def test_radix_bucket_reduction_identity():
+    """the reduction of the 5 * 2^15 radix buckets (segments of Lseg = 5, bit sums over 2^15
+    segments, host fold A + 5 sum 2^j T_j) equals sum (b + 1) B_b -- checked over integers at a
+    reduced size with the same shape (segments of 5, power-of-two segment count)."""
+    from pyoracle import pippenger
+    rng = random.Random(11)
+    for S in (1, 2, 8, 64):
+        for lseg in (1, 4, 5):
+            b = [rng.randrange(1 << 64) for _ in range(S * lseg)]
+            assert pippenger.radix_bucket_sum(b, lseg) == sum((i + 1) * x for i, x in enumerate(b))

@@ -79,6 +79,55 @@ def test_msm_2e20_bls12_381(bls, path):
         e.set_option(e.OPT_MSM_CHUNK_POINTS, 1 << 27)
 
 
+@pytest.mark.parametrize("case", ["edges", "identity_bases", "all_equal", "half_zero"])
+def test_msm_radix_shared_edges(bls, case):
+    """the radix-B shared-window path (B = 5 * 2^16, 7 windows, 5 * 2^15 buckets; whole-table GLV
+    MSMs from 2^18 points) on edge inputs, pinned by linearity over P_i = s_i G: edge scalars (0,
+    1, r - 1, lambda, +-lambda/2, B^w boundaries), identity bases in the table, all-equal scalars
+    (one bucket per window holds every entry: the long-chain fix-up), half the scalars zero."""
+    import torch
+    import vkzg
+    from pyoracle import pippenger
+    from pyoracle.curves import BLS12_381 as C
+    n = 1 << 18
+    e = bls
+    tid = e.random_bases(n, seed=77)
+    s = vkzg.random_base_scalars("bls12_381", 77, n)
+    rng = np.random.default_rng(5)
+    k = vkzg.random_scalars("bls12_381", n, rng)
+    lam, B = pippenger.GLV_LAMBDA, pippenger.RADIX_MUL << pippenger.RADIX_C0
+    s_int = None
+    if case == "edges":
+        edge = [0, 1, 2, C.r - 1, C.r - 2, lam, lam + 1, lam >> 1, (lam >> 1) + 1, lam * ((lam >> 1) + 1),
+                B // 2, B // 2 + 1, B - 1, B, B ** 6, B ** 6 - 1, (1 << 127) - 1, C.r - lam]
+        pos = rng.choice(n, size=len(edge) * 50, replace=False)
+        kl = [vkzg.limbs_to_int(x) for x in k]
+        for j, p in enumerate(pos):
+            kl[p] = edge[j % len(edge)]
+        k = vkzg.ints_to_limbs(kl)
+    elif case == "identity_bases":
+        xy, inf = e.download_bases(tid)
+        idx = rng.choice(n, size=777, replace=False)
+        inf = inf.copy()
+        inf[idx] = 1
+        tid = e.upload_bases(xy, inf)
+        s_int = [0 if inf[i] else vkzg.limbs_to_int(s[i]) for i in range(n)]
+    elif case == "all_equal":
+        k = np.repeat(k[:1], n, axis=0)
+    elif case == "half_zero":
+        k = k.copy()
+        k[rng.choice(n, size=n // 2, replace=False)] = 0
+    if s_int is not None:
+        want = C.mul(C.g, sum(vkzg.limbs_to_int(a) * b for a, b in zip(k, s_int)) % C.r)
+    else:
+        want = C.mul(C.g, vkzg.dot_mod(k, s, C.r))
+    d_k = torch.from_numpy(np.ascontiguousarray(k).view(np.int64).copy()).cuda()
+    got = e.msm_device(tid, d_k.data_ptr(), n)
+    assert _pt("bls12_381", *got) == want
+    got = e.msm(tid, k)
+    assert _pt("bls12_381", *got) == want
+
+
 def test_msm_2e20_window_parts_sum(bls):
     """the 8-rank window split of the bench (vc_msm_device_window_part) at 2^20 adds up to the
     same linearity-pinned point."""

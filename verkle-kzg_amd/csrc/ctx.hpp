@@ -86,7 +86,7 @@ struct Table {
     // GLV MSMs over the whole table: packed-29 copies of 2^(c w) P and 2^(c w) phi(P) for every
     // window w ([w][2n] layout), so all windows share one set of buckets (msm.hip, "shared
     // windows"); built on first use for the window size c in win_c
-    int win_ok = 0, win_c = 0, win_W = 0, win_ts = 0;
+    int win_ok = 0, win_c = 0, win_W = 0, win_ts = 0, win_m = 1;  // win_m > 1: radix win_m 2^win_c
     int win_limbs = 1;  // copies in radix-2^29 limbs (1) or packed-29 (0, VKZG_WIN_PACKED probe)
     DevBuf win;
 };

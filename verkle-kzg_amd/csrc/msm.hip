@@ -127,6 +127,17 @@ struct GlvDigits {
     }
 };
 
+// Radix-B digits made by k_glv_radix ([W][nv] signed, zero for identity bases): entry i of the
+// (2n-term) MSM has digit dig[w * nv + i] in window w.
+struct RadixDigits {
+    const int32_t* dig;
+    uint32_t nv;
+    template <class Fn>
+    __device__ __forceinline__ void operator()(uint32_t i, int, int W, Fn&& f) const {
+        for (int w = 0; w < W; w++) f(w, dig[(size_t)w * nv + i]);
+    }
+};
+
 // Two-pass MSD counting sort of the n*W (window, bucket) keys, all in LDS -- no global atomics
 // (global atomics execute memory-side on CDNA4, ~26 G/s for scattered words, which made the
 // one-pass global-histogram sort cost 2.2 ms at 2^20 x 16 windows).
@@ -154,14 +165,14 @@ __device__ __forceinline__ uint32_t sort_slot(uint32_t b, uint32_t nblk) {
 }
 
 template <class Src>
-__global__ void __launch_bounds__(256) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
-                                                  uint32_t NBC, uint32_t nblk, uint32_t stride,
-                                                  uint32_t* __restrict__ counts) {
+__global__ void __launch_bounds__(1024) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
+                                                   uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t chunk,
+                                                   uint32_t* __restrict__ counts) {
     extern __shared__ uint32_t hist[];
     const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[k] = 0;
     __syncthreads();
-    const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
+    const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, n);
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb)
@@ -195,16 +206,16 @@ __device__ __forceinline__ uint32_t sort_entry_of(T x, uint32_t FB) {
 }
 
 template <class Src, class T>
-__global__ void __launch_bounds__(256) k_sort_coarse(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
-                                                    uint32_t NBC, uint32_t nblk, uint32_t stride,
-                                                    const uint32_t* __restrict__ base, T* __restrict__ tmp) {
+__global__ void __launch_bounds__(1024) k_sort_coarse(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
+                                                     uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t chunk,
+                                                     const uint32_t* __restrict__ base, T* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
     const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     const uint32_t slot = sort_slot(blockIdx.x, nblk);
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + slot];
     __syncthreads();
     const uint32_t fmask = (1u << FB) - 1;
-    const uint32_t lo = blockIdx.x * SORT_CHUNK, hi = min(lo + SORT_CHUNK, n);
+    const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, n);
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb) {
@@ -381,16 +392,8 @@ constexpr int GLV_BITS = 128;  // |k1|, |k2| < 2^127, plus the recoding's spare 
 
 typedef unsigned __int128 u128;
 
-template <class Fr>
-__global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ sc, uint32_t n, int mont, GlvK K,
-                                                  uint4* __restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fe<Fr> f = load_scalar<Fr>(sc, i);
-    if (mont) f = fe_from_mont<Fr>(f);
-    uint64_t s[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) s[k] = (uint64_t)f.v[2 * k] | ((uint64_t)f.v[2 * k + 1] << 32);
+// k = k1 + lambda k2 (k < 2^256, canonical or not): |k1| = rem (negative when nr), |k2| = q (nq)
+__device__ __forceinline__ void glv_decompose(uint64_t s[4], const GlvK& K, u128& rem, bool& nr, u128& q, bool& nq) {
     // s mod r (inputs are < 2^256 < 3r)
     for (int rep = 0; rep < 2; rep++) {
         bool ge = true;
@@ -421,7 +424,7 @@ __global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ 
         }
         p[a + 3] = carry;
     }
-    u128 q = ((u128)p[5] << 64) | p[4];
+    q = ((u128)p[5] << 64) | p[4];
     const u128 lam = ((u128)K.lam[1] << 64) | K.lam[0];
     // rem = s - q lambda (< 3 lambda: 3 limbs)
     uint64_t ql[4] = {0, 0, 0, 0};
@@ -456,12 +459,13 @@ __global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ 
         rm[1] = (uint64_t)(d >> 64);
         q += 1;
     }
-    u128 rem = ((u128)rm[1] << 64) | rm[0];
+    rem = ((u128)rm[1] << 64) | rm[0];
     // balance: k = rem + lambda q with rem in [0, lambda), q in [0, lambda + 1]
     //   q > lambda/2:   (rem - 1) + lambda (q - lambda - 1)   (= k - r)
     //   rem > lambda/2: (rem - lambda) + lambda (q + 1)
     const u128 half = lam >> 1;
-    bool nq = false, nr = false;
+    nq = false;
+    nr = false;
     if (q > half) {
         q = lam + 1 - q;  // magnitude of q - lambda - 1
         nq = true;
@@ -484,10 +488,88 @@ __global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ 
             q -= 1;
         }
     }
+}
+
+template <class Fr>
+__device__ __forceinline__ void glv_load(const uint32_t* __restrict__ sc, uint32_t i, int mont, uint64_t s[4]) {
+    fe<Fr> f = load_scalar<Fr>(sc, i);
+    if (mont) f = fe_from_mont<Fr>(f);
+#pragma unroll
+    for (int k = 0; k < 4; k++) s[k] = (uint64_t)f.v[2 * k] | ((uint64_t)f.v[2 * k + 1] << 32);
+}
+
+template <class Fr>
+__global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ sc, uint32_t n, int mont, GlvK K,
+                                                  uint4* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t s[4];
+    glv_load<Fr>(sc, i, mont, s);
+    u128 rem, q;
+    bool nr, nq;
+    glv_decompose(s, K, rem, nr, q, nq);
     out[i] = make_uint4((uint32_t)rem, (uint32_t)(rem >> 32), (uint32_t)(rem >> 64),
                         (uint32_t)(rem >> 96) | (nr ? 0x80000000u : 0u));
     out[n + i] = make_uint4((uint32_t)q, (uint32_t)(q >> 32), (uint32_t)(q >> 64),
                             (uint32_t)(q >> 96) | (nq ? 0x80000000u : 0u));
+}
+
+// Mixed-radix digits of a GLV half for the radix-B shared-window MSM (B = MUL 2^C0, not a power
+// of two): |k| < 2^127 = sum_w d_w B^w with signed d_w in (-B/2, B/2] (carry recoding as
+// for_each_digit), W digits (B^W / 2 > 2^127: the top digit is below B/2 and never carries).
+// k mod B = (k mod 2^C0) + 2^C0 ((k >> C0) mod MUL); the division by MUL runs over the four
+// 32-bit limbs from the top. A negative half negates every digit.
+template <uint32_t MUL, int C0>
+__device__ __forceinline__ void radix_digits(u128 k, bool neg, int W, int32_t* __restrict__ out, size_t stride) {
+    constexpr uint32_t B = MUL << C0, H = B / 2, LO = (1u << C0) - 1;
+    uint32_t x0 = (uint32_t)k, x1 = (uint32_t)(k >> 32), x2 = (uint32_t)(k >> 64), x3 = (uint32_t)(k >> 96);
+    uint32_t carry = 0;
+    for (int w = 0; w < W; w++) {
+        const uint32_t lo = x0 & LO;
+        x0 = (x0 >> C0) | (x1 << (32 - C0));
+        x1 = (x1 >> C0) | (x2 << (32 - C0));
+        x2 = (x2 >> C0) | (x3 << (32 - C0));
+        x3 >>= C0;
+        uint64_t cur = x3;
+        x3 = (uint32_t)(cur / MUL);
+        cur = ((cur % MUL) << 32) | x2;
+        x2 = (uint32_t)(cur / MUL);
+        cur = ((cur % MUL) << 32) | x1;
+        x1 = (uint32_t)(cur / MUL);
+        cur = ((cur % MUL) << 32) | x0;
+        x0 = (uint32_t)(cur / MUL);
+        const uint32_t raw = lo + ((uint32_t)(cur % MUL) << C0) + carry;
+        int32_t d;
+        if (raw > H) {
+            d = (int32_t)raw - (int32_t)B;
+            carry = 1;
+        } else {
+            d = (int32_t)raw;
+            carry = 0;
+        }
+        out[(size_t)w * stride] = neg ? -d : d;
+    }
+}
+
+// GLV split straight to radix-B digits: dig[w][i] (k1 of scalar i against P_i) and dig[w][n + i]
+// (k2 against phi(P_i)); identity bases get zero digits (no entries)
+template <class Fr, uint32_t MUL, int C0>
+__global__ void __launch_bounds__(256) k_glv_radix(const uint32_t* __restrict__ sc, const uint8_t* __restrict__ inf,
+                                                  uint32_t n, int mont, GlvK K, int W, int32_t* __restrict__ dig) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const size_t nv = 2 * (size_t)n;
+    if (inf != nullptr && inf[i]) {
+        for (int w = 0; w < W; w++) dig[(size_t)w * nv + i] = dig[(size_t)w * nv + n + i] = 0;
+        return;
+    }
+    uint64_t s[4];
+    glv_load<Fr>(sc, i, mont, s);
+    u128 rem, q;
+    bool nr, nq;
+    glv_decompose(s, K, rem, nr, q, nq);
+    radix_digits<MUL, C0>(rem, nr, W, dig + i, nv);
+    radix_digits<MUL, C0>(q, nq, W, dig + n + i, nv);
 }
 
 template <class C>
@@ -586,14 +668,21 @@ static int fast_tables(vc_ctx* ctx, Table* t, bool with_phi) {
     return VC_OK;
 }
 
-// out[i] = 2^c in[i] (identity bases stay the identity)
+// out[i] = mul 2^c in[i] (mul odd and small; identity bases stay the identity)
 template <class C>
 __global__ void __launch_bounds__(256) k_win_next(const typename C::Aff* __restrict__ in,
-                                                 const uint8_t* __restrict__ inf, uint32_t n, int c,
+                                                 const uint8_t* __restrict__ inf, uint32_t n, int c, uint32_t mul,
                                                  typename C::Acc* __restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     typename C::Acc a = inf[i] ? C::zero() : C::from_aff(in[i], false);
+    if (!inf[i] && mul > 1) {  // double-and-add; k P != +-P for 1 < k < r, so no exceptional add
+        const typename C::Aff p = in[i];
+        for (int b = 30 - __builtin_clz(mul); b >= 0; b--) {
+            a = C::dbl(a);
+            if ((mul >> b) & 1) a = C::madd(a, p, false);
+        }
+    }
     for (int k = 0; k < c; k++) a = C::dbl(a);
     out[i] = a;
 }
@@ -603,11 +692,12 @@ __global__ void __launch_bounds__(256) k_win_next(const typename C::Aff* __restr
 // window's digits to one set of 2^(c-1) buckets -- the same mixed adds, but one bucket reduction
 // instead of W and no doublings in the host fold. 2 W n points (1.6 GB at n = 2^20, c = 16),
 // built once per table and window size: W - 1 steps of c doublings + a batch normalisation.
+// mul > 1: radix B = mul 2^c (the radix-B shared windows): the copy of window w holds B^w P.
 template <class C>
-static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
+static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul = 1) {
     using Aff = typename C::Aff;
     using Acc = typename C::Acc;
-    if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts) return VC_OK;
+    if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts && t->win_m == (int)mul) return VC_OK;
     const size_t n = t->n;
     t->win_ok = 0;
     using FA = typename Fast29<C>::type::Aff;  // limb form (k_to_limbs)
@@ -627,7 +717,7 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
         if (w > 0) {
             // the top window's copy is 2^(c w - ts) P (its digits are scaled by 2^ts, GlvDigits)
             VK_LAUNCH(ctx, "win_next", (k_win_next<C>), g, 256, 0, w == 1 ? t->bases.as<Aff>() : cur.bases.as<Aff>(),
-                      t->inf.as<uint8_t>(), (uint32_t)n, w == W - 1 ? c - ts : c, acc.as<Acc>());
+                      t->inf.as<uint8_t>(), (uint32_t)n, w == W - 1 ? c - ts : c, mul, acc.as<Acc>());
             VK_TRY(table_from_acc(ctx, &cur, acc.p, n));
             src = cur.bases.as<Aff>();
         }
@@ -646,13 +736,14 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts) {
     t->win_c = c;
     t->win_W = W;
     t->win_ts = ts;
+    t->win_m = (int)mul;
     return VC_OK;
 }
 
 template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
-                        uint32_t NBC, uint32_t nblk, uint32_t stride, size_t ncnt, uint32_t* counts, uint32_t* base,
-                        void* tmp, uint32_t* offsets, uint32_t* sorted, uint32_t* zero_word) {
+                        uint32_t NBC, uint32_t nblk, uint32_t chunk, uint32_t stride, size_t ncnt, uint32_t* counts,
+                        uint32_t* base, void* tmp, uint32_t* offsets, uint32_t* sorted, uint32_t* zero_word) {
     hipStream_t st = L.st;
     const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
     const size_t lds = (size_t)bins * 4;
@@ -661,8 +752,12 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     // largest entry index e: i < nv, or w * stride + i with shared windows
     const uint64_t emax = stride ? (uint64_t)we * stride : (uint64_t)nv;
     const bool narrow = emax <= (1ull << (31 - FB));
-    VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, 256, lds, src, nv, c, wb, we, FB, NBC, nblk,
-                 stride, counts);
+    // scalars per hist / coarse block: runs of a block inside a coarse bin are chunk * W / bins
+    // entries long, so a big bucket set (many coarse bins) takes bigger blocks to keep the
+    // scatter's runs near a cache line
+    const uint32_t sblk = chunk >= 4096 ? 1024 : 256;
+    VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, sblk, lds, src, nv, c, wb, we, FB, NBC, nblk,
+                 stride, chunk, counts);
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
     VK_TRY(L.ws[WS_SCAN_TMP].ensure(tmp_bytes));
@@ -677,13 +772,13 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     const uint64_t total = stride ? (uint64_t)(we - wb) * stride : (uint64_t)nv * (uint32_t)(we - wb);
     const int fblk = fine_env == 256 || fine_env == 1024 ? fine_env : (total / bins >= (1u << 15) ? 1024 : 256);
     if (narrow) {
-        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, 256, lds, src, nv, c, wb, we, FB,
-                     NBC, nblk, stride, base, static_cast<uint32_t*>(tmp));
+        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, sblk, lds, src, nv, c, wb, we,
+                     FB, NBC, nblk, stride, chunk, base, static_cast<uint32_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, 0, static_cast<const uint32_t*>(tmp),
                      base, nblk, bins, FB, offsets, sorted, zero_word);
     } else {
-        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, 256, lds, src, nv, c, wb, we, FB,
-                     NBC, nblk, stride, base, static_cast<uint64_t*>(tmp));
+        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, sblk, lds, src, nv, c, wb, we,
+                     FB, NBC, nblk, stride, chunk, base, static_cast<uint64_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, fblk, 0, static_cast<const uint64_t*>(tmp),
                      base, nblk, bins, FB, offsets, sorted, zero_word);
     }
@@ -730,6 +825,7 @@ struct MsmSlice {
     Lane L{};
     int c = 0, wb = 0, we = 0, W = 0;
     bool shared = false;  // all windows into one bucket set (Table::win copies)
+    uint32_t m = 1;       // > 1: radix m 2^c digits (RadixDigits), m 2^(c-1) buckets
     int Wr = 0;           // bucket sets reduced: 1 shared, W otherwise
     uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
     uint32_t* offsets = nullptr;
@@ -757,7 +853,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     const int c = sl.c, W = sl.W;
     const int Wr = sl.shared ? 1 : W;
     sl.Wr = Wr;
-    const uint32_t NB = 1u << (c - 1);
+    const uint32_t NB = sl.m << (c - 1);
     const uint32_t NBtot = NB * (uint32_t)Wr;
     const size_t maxL = nv * (size_t)W;
     const size_t load = maxL / Wr;  // entries per bucket set
@@ -779,8 +875,9 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // windows, 2 for the 1-4 window slices of multi-GPU runs; 8 measured 0.1-0.15 ms slower)
     uint32_t Lseg = NB >= 64 ? 4 : (NB >= 4 ? 2 : 1);
     if (Lseg == 4 && (size_t)(NB / Lseg) * Wr < 65536) Lseg = 2;
-    // one bucket set: the bit sums straight over 2^15 buckets (measured), segments of 4 at 2^18
-    if (sl.shared) Lseg = NB >= (1u << 17) ? 4 : 1;
+    // one bucket set: the bit sums straight over 2^15 buckets (measured), segments of 4 at 2^18;
+    // radix m 2^c: segments of m buckets (S = 2^(c-1) segments)
+    if (sl.shared) Lseg = sl.m > 1 ? sl.m : (NB >= (1u << 17) ? 4 : 1);
     if (const char* el = getenv("VKZG_MSM_LSEG")) Lseg = (uint32_t)std::max(1, atoi(el));  // tuning probe
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
@@ -789,17 +886,29 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     hipStream_t st = L.st;
 
     // bucket sort geometry (k_sort_*): 2^FB fine buckets per coarse bin
-    uint32_t lgNB = (uint32_t)c - 1;
+    const uint32_t lgNB = (uint32_t)c - 1;  // NB = m 2^lgNB
     uint32_t FB = lgNB < 8 ? lgNB : 8;
+    uint32_t chunk = SORT_CHUNK;
+    if (sl.m > 1) {
+        // radix buckets (5 x 2^15 at 2^21 x 7 entries): FB = 7 keeps the coarse entries narrow
+        // (entry index < 7 x 2^21 < 2^24), i.e. 1280 coarse bins; blocks of 8192 scalars keep a
+        // block's runs ~45 entries long
+        FB = lgNB < 7 ? lgNB : 7;
+        chunk = 8192;
+    }
+    static const int chunk_env = getenv("VKZG_SORT_CHUNK") ? atoi(getenv("VKZG_SORT_CHUNK")) : 0;  // tuning probe
+    static const int fb_env = getenv("VKZG_SORT_FB") ? atoi(getenv("VKZG_SORT_FB")) : 0;           // tuning probe
+    if (chunk_env >= 256) chunk = (uint32_t)chunk_env;
     // shared windows: ~64K entries per coarse bin (one 1024-thread k_sort_fine block each) but at
     // least 256 bins (a fine block per CU). Measured at 2^21 x 8 entries (hist + coarse + fine):
     // 0.233 ms at 2^14 entries per bin (256-thread fine blocks), 0.222 at 2^15, 0.204 at 2^16,
     // 0.295 at 2^17 -- bigger bins shorten the scatter's partial-line writes
     static const int bin_lg = getenv("VKZG_SORT_BIN_LG") ? atoi(getenv("VKZG_SORT_BIN_LG")) : 16;  // tuning probe
-    while (sl.shared && FB > 1 && (load >> bin_lg) > (size_t)(NB >> FB)) FB--;
-    while (sl.shared && FB > 1 && (NB >> FB) < 256) FB--;
+    while (sl.shared && sl.m == 1 && FB > 1 && (load >> bin_lg) > (size_t)(NB >> FB)) FB--;
+    while (sl.shared && sl.m == 1 && FB > 1 && (NB >> FB) < 256) FB--;
+    if (fb_env >= 1 && fb_env <= (int)std::min<uint32_t>(lgNB, 8)) FB = (uint32_t)fb_env;
     const uint32_t NBC = NB >> FB;
-    const uint32_t nblk = (uint32_t)((nv + SORT_CHUNK - 1) / SORT_CHUNK);
+    const uint32_t nblk = (uint32_t)((nv + chunk - 1) / chunk);
     const size_t ncnt = (size_t)Wr * NBC * nblk + 1;
 
     DevBuf* ws = L.ws;
@@ -840,7 +949,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.bsum_part = ws[WS_WIN].as<RAcc>();
     sl.tail = ws[WS_TAIL].as<Acc>();
 
-    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, sl.shared ? (uint32_t)nv : 0u, ncnt,
+    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (uint32_t)nv : 0u, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
                         ws[WS_SORTED].as<uint32_t>(), sl.chain_max));
@@ -895,6 +1004,20 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     // slice = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host); with
     // shared windows the one bucket set already holds the 2^(c w) factors: A + Lseg sum_j 2^j T_j
     const uint32_t J = sl.J;
+    if (sl.shared && (sl.Lseg & (sl.Lseg - 1)) != 0) {  // radix buckets: Lseg = m is odd
+        Acc x = C::zero();
+        for (int j = (int)J - 1; j >= 0; j--) {
+            if (!C::is_zero(x)) x = C::dbl(x);
+            x = C::add(x, sl.ht[j]);
+        }
+        Acc r = C::zero();  // Lseg x by double-and-add
+        for (int b = 31 - __builtin_clz(sl.Lseg); b >= 0; b--) {
+            if (!C::is_zero(r)) r = C::dbl(r);
+            if ((sl.Lseg >> b) & 1) r = C::add(r, x);
+        }
+        *res = C::add(r, sl.ht[J]);
+        return VC_OK;
+    }
     int lg_seg = 0;
     while ((1u << lg_seg) < sl.Lseg) lg_seg++;
     const int maxpos = (sl.shared ? 0 : sl.c * (sl.we - 1)) + lg_seg + (int)J;
@@ -948,16 +1071,40 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     // 2^21 terms (7 windows instead of 8). VKZG_MSM_SHARED=0 keeps per-window buckets (probe).
     bool shared = false;
     int top_shift = 0;
+    uint32_t radix_m = 1;  // > 1: radix-B shared windows, B = radix_m 2^c
     int c = glv ? glv_window(nv) : choose_window(nv);
     if constexpr (std::is_same<C, BLS381G1>::value) {
         const bool shared_env = ctx->opt_shared_windows != 0;  // vc_ctx_set_option(VC_OPT_MSM_SHARED_WINDOWS)
+        // Radix-B shared windows (B = 5 x 2^16 ~ 2^18.3, one MSM on one GPU): 7 uniformly loaded
+        // windows instead of 8 (B^7 / 2 > 2^127, the GLV halves' bound) -- 12.5 % fewer mixed
+        // adds -- into 5 x 2^15 buckets. The power-of-two c = 19 (7 windows) left a 14-bit top
+        // window whose digits hit 1 bucket in 16 (chains in the fix-up) and 2^18 buckets to
+        // reduce. Window-sliced (multi-GPU) parts keep c = 16: a one-window slice would reduce
+        // the whole bucket set for 1/7 of the adds. VKZG_MSM_RADIX=1: power-of-two windows (probe).
+        static const int radix_env = getenv("VKZG_MSM_RADIX") ? atoi(getenv("VKZG_MSM_RADIX")) : 5;
+        if (glv && shared_env && offset == 0 && n == t->n && parts == 1 && nv >= (1u << 19) && radix_env == 5 &&
+            !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED")) {
+            const size_t win_bytes = (size_t)7 * 2 * t->n * sizeof(typename Fast29<C>::type::Aff);
+            if (win_bytes <= (8ull << 30)) {
+                const int st = win_tables<C>(ctx, t, 16, 7, 0, 5);
+                if (st == VC_OK) {
+                    shared = true;
+                    c = 16;
+                    radix_m = 5;
+                } else if (st != VC_E_OOM) {
+                    return st;
+                } else {
+                    t->win.release();
+                }
+            }
+        }
         const int cs = glv_window_shared(nv);
         const int Ws = (GLV_BITS + cs - 1) / cs;
         // top window: GLV_BITS - cs (Ws - 1) bits -> digits up to 2^tb; scaled to fill 2^(cs-1)
         const int tb = GLV_BITS - cs * (Ws - 1);
         const int ts = std::max(0, (cs - 1) - tb);
         const size_t win_bytes = (size_t)Ws * 2 * t->n * sizeof(typename Fast29<C>::type::Aff);
-        if (glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
+        if (!shared && glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
             const int st = win_tables<C>(ctx, t, cs, Ws, ts);
             if (st == VC_OK) {
                 shared = true;
@@ -971,7 +1118,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         }
     }
     // one spare bit absorbs the final carry of the signed recoding
-    const int Wfull = glv ? (GLV_BITS + c - 1) / c : (Fr::BITS + 1 + c - 1) / c;
+    const int Wfull = radix_m > 1 ? 7 : glv ? (GLV_BITS + c - 1) / c : (Fr::BITS + 1 + c - 1) / c;
     // window slice [wb, we) of this call (parts > 1: the MSM split by windows across GPUs;
     // the slices' results add up to the whole MSM)
     const int wb = part * Wfull / parts, we = (part + 1) * Wfull / parts;
@@ -998,16 +1145,21 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         sl[k].we = wb + (k + 1) * W / nsl;
         sl[k].W = sl[k].we - sl[k].wb;
         sl[k].shared = shared;
+        sl[k].m = radix_m;
     }
     hipEvent_t fork = nullptr, join = nullptr, acc0 = nullptr;
     if (nsl == 2) acc0 = ctx->get_event();
     if (glv) {
         if constexpr (std::is_same<C, BLS381G1>::value) {
-            VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 16));
+            VK_TRY(ctx->ws[WS_GLV_SC].ensure(radix_m > 1 ? nv * 4 * (size_t)Wfull : nv * 16));
             uint4* halves = ctx->ws[WS_GLV_SC].as<uint4>();
             const Aff* dphi = t->fast.as<Aff>() + t->n + offset;
-            VK_LAUNCH(ctx, "glv_split", (k_glv_split<Fr>), (n + 255) / 256, 256, 0, d_sc, (uint32_t)n, mont,
-                      glv_consts(), halves);
+            if (radix_m > 1)
+                VK_LAUNCH(ctx, "glv_split", (k_glv_radix<Fr, 5, 16>), (n + 255) / 256, 256, 0, d_sc, inf, (uint32_t)n,
+                          mont, glv_consts(), Wfull, ctx->ws[WS_GLV_SC].as<int32_t>());
+            else
+                VK_LAUNCH(ctx, "glv_split", (k_glv_split<Fr>), (n + 255) / 256, 256, 0, d_sc, (uint32_t)n, mont,
+                          glv_consts(), halves);
             if (nsl == 2) {
                 fork = ctx->get_event();
                 VK_CHECK_HIP(hipEventRecord(fork, ctx->stream));
@@ -1021,7 +1173,10 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                 src.ts = top_shift;
             }
             for (int k = 0; k < nsl; k++) {
-                if (shared && !t->win_limbs)
+                if (radix_m > 1)
+                    VK_TRY(slice_enqueue<C>(ctx, sl[k], RadixDigits{ctx->ws[WS_GLV_SC].as<int32_t>(), (uint32_t)nv}, nv,
+                                            win, win, 0xffffffffu, k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
+                else if (shared && !t->win_limbs)
                     VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, t->win.as<Aff>(), t->win.as<Aff>(), 0xffffffffu,
                                             k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
                 else if (shared)

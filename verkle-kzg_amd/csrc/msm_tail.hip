@@ -118,6 +118,23 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk_q(typename A::Acc* __res
     if (role == 0) buckets[b] = acc;
 }
 
+// c ? a : b word by word through masks: a plain select of two aggregates becomes a load through a
+// selected address, which keeps both in scratch memory for the whole loop
+template <class T>
+__device__ __forceinline__ T mask_select(bool c, const T& a, const T& b) {
+    static_assert(sizeof(T) % 4 == 0, "");
+    constexpr int NW = (int)(sizeof(T) / 4);
+    uint32_t wa[NW], wb[NW];
+    __builtin_memcpy(wa, &a, sizeof wa);
+    __builtin_memcpy(wb, &b, sizeof wb);
+    const uint32_t m = 0u - (uint32_t)c;
+#pragma unroll
+    for (int k = 0; k < NW; k++) wa[k] = (wa[k] & m) | (wb[k] & ~m);
+    T r;
+    __builtin_memcpy(&r, wa, sizeof wa);
+    return r;
+}
+
 // ------------------------------------------------------------------ bucket reduction
 // Window sum  V_w = sum_b (b + 1) B_b  over NB buckets, in two shallow GPU stages and a host pass:
 //  (1) k_msm_segsum: segment s of Lseg buckets -> acc_s = sum (b - lo + 1) B_b, R_s = sum B_b
@@ -160,21 +177,37 @@ __global__ void __launch_bounds__(256) k_msm_segsum(const typename A::Acc* __res
     Rs[gid] = R;
 }
 
-// c ? a : b word by word through masks: a plain select of two aggregates becomes a load through a
-// selected address, which keeps both in scratch memory for the whole loop
-template <class T>
-__device__ __forceinline__ T mask_select(bool c, const T& a, const T& b) {
-    static_assert(sizeof(T) % 4 == 0, "");
-    constexpr int NW = (int)(sizeof(T) / 4);
-    uint32_t wa[NW], wb[NW];
-    __builtin_memcpy(wa, &a, sizeof wa);
-    __builtin_memcpy(wb, &b, sizeof wb);
-    const uint32_t m = 0u - (uint32_t)c;
-#pragma unroll
-    for (int k = 0; k < NW; k++) wa[k] = (wa[k] & m) | (wb[k] & ~m);
-    T r;
-    __builtin_memcpy(&r, wa, sizeof wa);
-    return r;
+// the same on quads (SW curves, SW29::add_quad: about half the latency of an add): a segment
+// chain is 2 Lseg dependent adds and the 5 x 2^15 radix buckets give 2^15 segments, one wave per
+// SIMD on half the SIMDs with a lane each -- a quad each fills every SIMD twice
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_segsum_q(const typename A::Acc* __restrict__ buckets,
+                                                     const uint32_t* __restrict__ offsets, uint32_t NB, int W,
+                                                     uint32_t Lseg, uint32_t S, typename A::Acc* __restrict__ accs,
+                                                     typename A::Acc* __restrict__ Rs) {
+    using Acc = typename A::Acc;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, q = gid >> 2, role = gid & 3;
+    const uint32_t w = q / S, s = q % S;
+    if (w >= (uint32_t)W) return;  // whole quads
+    const uint32_t lo = s * Lseg, hi = min(lo + Lseg, NB);
+    Acc R = A::zero(), acc = A::zero();
+    for (uint32_t it = 0; it < 2 * (hi - lo); it++) {
+        const bool second = (it & 1) != 0;
+        Acc y;
+        if (second) {
+            y = R;
+        } else {
+            const size_t g = (size_t)w * NB + (hi - 1 - it / 2);
+            y = offsets[g + 1] > offsets[g] ? buckets[g] : A::zero();
+        }
+        const Acc r = A::add_quad(mask_select(second, acc, R), y, role);
+        acc = mask_select(second, r, acc);
+        R = mask_select(second, R, r);
+    }
+    if (role == 0) {
+        accs[q] = acc;
+        Rs[q] = R;
+    }
 }
 
 template <class A>
@@ -386,7 +419,7 @@ int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t N
     // per-window bucket sets (8 x 2^15) every SIMD already has lane-per-bucket waves and the
     // quads' ~2x instructions per add made the walk slower (0.08 -> 0.115 ms)
     if constexpr (A::quad) {
-        if (quad_env && NBtot <= 65536) {
+        if ((quad_env && NBtot <= 65536) || quad_env == 2) {
             VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk_q<A>), (uint32_t)(((size_t)NBtot * 4 + 255) / 256), 256,
                          0, buckets, carry, owner, offsets, NBtot, M, limit);
             return VC_OK;
@@ -423,8 +456,17 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
         accs = Rs = const_cast<FAcc<C>*>(buckets);
         live = offsets;
     } else {
-        VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segsum<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets, offsets, NB,
-                  W, Lseg, S, accs, Rs);
+        static const int segq_env = getenv("VKZG_SEGSUM_QUAD") ? atoi(getenv("VKZG_SEGSUM_QUAD")) : 1;  // A/B probe
+        bool quads = false;
+        if constexpr (A::quad) {
+            quads = segq_env != 0 && (size_t)S * W <= 65536;
+            if (quads)
+                VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segsum_q<A>), (S * (uint32_t)W * 4 + 255) / 256, 256, 0,
+                             buckets, offsets, NB, W, Lseg, S, accs, Rs);
+        }
+        if (!quads)
+            VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segsum<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets,
+                         offsets, NB, W, Lseg, S, accs, Rs);
     }
     const uint32_t sums = (uint32_t)W * (J + 1);
     const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);

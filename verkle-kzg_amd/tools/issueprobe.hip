@@ -41,6 +41,54 @@ __global__ void k_issue(uint32_t* out, long long* cyc, int iters) {
                             "v_add_u32 v16, %0, v26\n\t"
                             "v_add_u32 v17, %1, v27\n\t")
                          :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17");
+        } else if constexpr (KIND == 4) {
+            asm volatile(R8("v_lshrrev_b64 v[10:11], 29, v[20:21]\n\t"
+                            "v_lshrrev_b64 v[12:13], 29, v[22:23]\n\t"
+                            "v_lshrrev_b64 v[14:15], 29, v[24:25]\n\t"
+                            "v_lshrrev_b64 v[16:17], 29, v[26:27]\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17");
+        } else if constexpr (KIND == 5) {
+            asm volatile(R8("v_lshl_add_u64 v[10:11], v[20:21], 0, v[30:31]\n\t"
+                            "v_lshl_add_u64 v[12:13], v[22:23], 0, v[32:33]\n\t"
+                            "v_lshl_add_u64 v[14:15], v[24:25], 0, v[34:35]\n\t"
+                            "v_lshl_add_u64 v[16:17], v[26:27], 0, v[36:37]\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17");
+        } else if constexpr (KIND == 6) {
+            asm volatile(R8("v_alignbit_b32 v10, %0, v20, 29\n\t"
+                            "v_alignbit_b32 v11, %1, v21, 29\n\t"
+                            "v_alignbit_b32 v12, %0, v22, 29\n\t"
+                            "v_alignbit_b32 v13, %1, v23, 29\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13");
+        } else if constexpr (KIND == 7) {
+            asm volatile(R8("v_add3_u32 v10, %0, v20, v30\n\t"
+                            "v_add3_u32 v11, %1, v21, v31\n\t"
+                            "v_add3_u32 v12, %0, v22, v32\n\t"
+                            "v_add3_u32 v13, %1, v23, v33\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13");
+        } else if constexpr (KIND == 8) {
+            asm volatile(R8("v_mad_u32_u24 v10, %0, v20, v30\n\t"
+                            "v_mad_u32_u24 v11, %1, v21, v31\n\t"
+                            "v_mad_u32_u24 v12, %0, v22, v32\n\t"
+                            "v_mad_u32_u24 v13, %1, v23, v33\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13");
+        } else if constexpr (KIND == 9) {
+            asm volatile(R8("v_mul_hi_u32 v10, %0, v20\n\t"
+                            "v_mul_hi_u32 v11, %1, v21\n\t"
+                            "v_mul_hi_u32 v12, %0, v22\n\t"
+                            "v_mul_hi_u32 v13, %1, v23\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13");
+        } else if constexpr (KIND == 10) {
+            asm volatile(R8("v_fma_f64 v[10:11], v[20:21], v[22:23], v[24:25]\n\t"
+                            "v_fma_f64 v[12:13], v[20:21], v[22:23], v[26:27]\n\t"
+                            "v_fma_f64 v[14:15], v[20:21], v[22:23], v[28:29]\n\t"
+                            "v_fma_f64 v[16:17], v[20:21], v[22:23], v[30:31]\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17");
+        } else if constexpr (KIND == 11) {
+            asm volatile(R8("v_pk_mad_u16 v10, %0, v20, v30\n\t"
+                            "v_pk_mad_u16 v11, %1, v21, v31\n\t"
+                            "v_pk_mad_u16 v12, %0, v22, v32\n\t"
+                            "v_pk_mad_u16 v13, %1, v23, v33\n\t")
+                         :: "v"(a), "v"(b) : "v10", "v11", "v12", "v13");
         } else {
             asm volatile(R8("v_mul_lo_u32 v10, %0, v20\n\t"
                             "v_mul_lo_u32 v11, %1, v21\n\t"
@@ -78,7 +126,7 @@ void run(const char* name, int blocks, int threads) {
     (void)hipEventElapsedTime(&ms, e0, e1);
     long long c = 0;
     (void)hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-    const double inst = (double)iters * 64;  // per wave
+    const double inst = (double)iters * (KIND >= 4 && KIND != 12 ? 32 : 64);  // per wave
     const double waves_per_simd = (double)blocks * threads / 64 / 1024;
     printf("{\"probe\":\"%s\",\"waves_per_simd\":%.2f,\"cycles_per_inst_one_wave\":%.2f,"
            "\"simd_cycles_per_inst\":%.2f}\n",
@@ -89,12 +137,21 @@ void run(const char* name, int blocks, int threads) {
 
 int main() {
     const char* names[] = {"v_mad_u64_u32 x8 independent", "v_add_co/addc chain", "v_add_u32 independent",
-                           "v_mul_lo_u32 independent"};
+                           "v_mul_lo_u32 independent", "v_lshrrev_b64", "v_lshl_add_u64", "v_alignbit_b32",
+                           "v_add3_u32", "v_mad_u32_u24", "v_mul_hi_u32", "v_fma_f64", "v_pk_mad_u16"};
     for (int wps : {1, 2, 4}) {
         run<0>(names[0], 256 * wps, 256);
         run<1>(names[1], 256 * wps, 256);
         run<2>(names[2], 256 * wps, 256);
         run<3>(names[3], 256 * wps, 256);
+        run<4>(names[4], 256 * wps, 256);
+        run<5>(names[5], 256 * wps, 256);
+        run<6>(names[6], 256 * wps, 256);
+        run<7>(names[7], 256 * wps, 256);
+        run<8>(names[8], 256 * wps, 256);
+        run<9>(names[9], 256 * wps, 256);
+        run<10>(names[10], 256 * wps, 256);
+        run<11>(names[11], 256 * wps, 256);
     }
     return 0;
 }
