@@ -41,8 +41,8 @@ CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
 # (tools_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
-PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r02", "r01"))
-                    if os.path.exists(p)), os.path.join(ROOT, "profiles", "r02", "pmc_summary.json"))
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r03", "r02", "r01"))
+                    if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_summary.json"))
 
 
 def parse():
@@ -297,6 +297,7 @@ def mp_line(a, rank, world, local, dev, stream):
     from vkzg._lib import lib
     lib().vc_transcript_free(tr)
     pipe = mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, mp) if world == 1 else None
+    ref_shapes = mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev) if rank == 0 else None
     meng.close()
     alg = Q * N * 32 + Q * 64 + Q * 40
     out = {"workload": f"IPA multiproof, Q = 2^{a.mp_log_q} width-256 queries, BN254 (configs[4]), query set "
@@ -305,8 +306,58 @@ def mp_line(a, rank, world, local, dev, stream):
            "achieved_GBps": alg / dt / 1e9, "d_inf": mp["d"] is None}
     if pipe is not None:
         out["pipelined"] = pipe
+    if ref_shapes is not None:
+        out["reference_bench_shapes"] = ref_shapes
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_multiproof(N, data, z, cxy, crs, a.cpu_threads or min(16, os.cpu_count() or 1))
+    return out
+
+
+def mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, reps=5):
+    """The reference's multiproof benches (vector-commit/benches/ipa.rs:111-159): prove_multiproof
+    and verify_multiproof at Q = MAX_MULTIPROOF/8 x {1, 4, 8} = 4096, 16384, 32768 width-256 queries
+    (the first Q of this line's query set; evaluations device-resident). Prove = the three phases
+    (host transcript, per-point sums, finish with D, E and the inner IPA proof); verify =
+    vc_multiproof_verify_ipa (transcript, the e-coefficient MSM over the Q commitments -- 8(f) rank
+    2 -- and the inner IPA verification). Median of `reps` after a warm-up, each proof verified."""
+    import ctypes
+    from vkzg import scheme
+    from vkzg._lib import check, lib
+    out = {}
+    for q in (4096, 16384, 32768):
+        if q > z.shape[0]:
+            break
+        cq, ciq, zq, yq = (np.ascontiguousarray(v[:q]) for v in (cxy, cinf, z, y))
+
+        def prove():
+            tr, r, rows = scheme.multiproof_begin(N, cq, ciq, zq, yq)
+            S = torch.empty((rows, N, 4), dtype=torch.int64, device=dev)
+            torch.cuda.current_stream(dev).synchronize()
+            scheme.multiproof_accumulate(ipa.engine, N, zq, 0, q, d_all.data_ptr(), r, S.data_ptr())
+            return scheme.multiproof_finish(ipa, zq, S.data_ptr(), 1, tr)
+
+        def verify(mp):
+            b, _arrs = mp["proof"]._to()
+            dxy, dinf = scheme._pt_arrays([mp["d"]])
+            res = ctypes.c_int()
+            check(lib().vc_multiproof_verify_ipa(ipa.engine.h, ipa.table, N, q, scheme._p(cq), scheme._p(ciq),
+                                                 scheme._p(zq), scheme._p(yq), scheme._p(dxy), int(dinf[0]),
+                                                 ctypes.byref(b), ctypes.byref(res)), "multiproof_verify")
+            return bool(res.value)
+
+        mp = prove()
+        ok = verify(mp)
+        tp, tv = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            mp = prove()
+            tp.append((time.perf_counter() - t0) * 1e3)
+            t0 = time.perf_counter()
+            ok = verify(mp) and ok
+            tv.append((time.perf_counter() - t0) * 1e3)
+        out[str(q)] = {"prove_ms_median": float(np.median(tp)), "verify_ms_median": float(np.median(tv)),
+                       "prove_ms": [round(x, 3) for x in tp], "verify_ms": [round(x, 3) for x in tv],
+                       "verified": ok}
     return out
 
 
@@ -465,11 +516,14 @@ def verkle_line(a, local, stream):
     t.commitment(veng, kzg.table)
     t_full = time.perf_counter() - t0
     kms = {}
-    for k in ("fb_commit", "fb_combine", "fb_normalize_out", "fb_commit_small", "to_data_item"):
+    for k in ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup_init", "msm_fixup_jump",
+              "msm_fixup", "sparse_store", "sparse_combine", "norm_prep", "norm_finish", "fb_normalize",
+              "fb_commit", "fb_combine", "fb_commit_small", "to_data_item"):
         ms, cnt = veng.kernel_time(k)
         if cnt:
             kms[k] = round(ms, 3)
     veng.enable_timing(False)
+    gpu_ms = sum(kms.values())
     upd = max(1, nk // 100)
     for i in rng.integers(0, nk, size=upd):
         t.insert_single(keys[i].tobytes(), rng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
@@ -480,8 +534,9 @@ def verkle_line(a, local, stream):
     veng.close()
     return {"workload": f"verkle tree, {nk} random 32-unit keys, KZG(256) BN254 (8(f) rank 1)",
             "nodes": st, "insert_s": t_ins, "full_commitment_ms": t_full * 1e3,
-            "nodes_per_s_full": st["dirty"] / t_full, "full_kernel_ms_total": kms, "updated_keys": upd, "dirty_nodes": dirty,
-            "update_commitment_ms": t_upd * 1e3}
+            "nodes_per_s_full": st["dirty"] / t_full, "full_kernel_ms_total": kms,
+            "full_split_ms": {"gpu_kernels": gpu_ms, "host_and_transfers": t_full * 1e3 - gpu_ms},
+            "updated_keys": upd, "dirty_nodes": dirty, "update_commitment_ms": t_upd * 1e3}
 
 
 def main():
@@ -546,18 +601,25 @@ def main():
     torch.cuda.synchronize(dev)
     eng.enable_timing(True)
     eng.reset_timing()
+    step_ms = []  # every step returns its host result (the call is synchronous): per-step times
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        ts = time.perf_counter()
         res = step()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     eng.enable_timing(False)
+    plan = eng.msm_last_plan()  # the geometry the timed MSMs ran (before the 1-term result check)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+        tm = torch.tensor(step_ms, dtype=torch.float64, device=dev)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)  # per-step max over ranks
+        step_ms = tm.cpu().tolist()
     ms_per_step = dt / a.steps * 1e3
 
     # dominant kernel (bucket accumulation) device time, HIP events on the launch stream
@@ -636,8 +698,7 @@ def main():
     # wave-level, from the committed profile of this same command) x 64 lanes / its live time,
     # against the live issue peak of 4-cycle VALU work (v_mad_u64_u32; VCC adds issue the same,
     # plain 32-bit adds in half: tools/issueprobe.hip), i.e. lanes x SIMDs x clock / 4
-    from vkzg.dist import window_count
-    c_bits, w_total, terms = window_count(curve, n, with_terms=True)
+    c_bits, w_total, terms = plan["window_bits"], plan["windows"], plan["terms_per_point"]
     w_rank = (rank + 1) * w_total // world - rank * w_total // world
     madds = terms * n * w_rank
     mad_peak = eng.device_mad_rate()
@@ -674,6 +735,8 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
+        "ms_per_step_median": float(np.median(step_ms)),
+        "ms_per_step_min": float(np.min(step_ms)),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -682,11 +745,13 @@ def main():
         "config": {"workload": f"single 2^{a.log_n}-point {curve} G1 Pippenger MSM (configs[1])",
                    "n_points": n, "curve": curve, "parallelism": f"Pippenger-window slices x{world}",
                    "exchange": comm_kind,
-                   "window_bits": c_bits, "windows": w_total,
-                   "precomputed_bases": (f"{w_total} x 2n shifted window copies 2^(c w) P_i, 2^(c w) phi(P_i) "
-                                         f"({w_total * 2 * n * 112 / 1e9:.2f} GB), built once per base table "
+                   "window_bits": c_bits, "windows": w_total, "radix": plan["radix_mul"] << c_bits,
+                   "radix_form": f"{plan['radix_mul']} * 2^{c_bits}", "terms_per_point": terms,
+                   "precomputed_bases": (f"{w_total} x 2n window copies B^w P_i, B^w phi(P_i) with B = "
+                                         f"{plan['radix_mul']} * 2^{c_bits}, each x, y, -y in radix-2^29 limbs "
+                                         f"({w_total * 2 * n * 168 / 1e9:.2f} GB), built once per base table "
                                          "(a fixed CRS), untimed; `variable_base` is the same MSM without them")
-                   if curve == "bls12_381" else None},
+                   if plan["shared_windows"] else None},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -806,6 +871,8 @@ def main():
         thr = a.cpu_threads or min(16, os.cpu_count() or 1)
         bxy, binf = eng.download_bases(table)
         out["cpu_baseline_pippenger"] = cpu_pippenger(curve, bxy, binf, scalars, res, thr)
+        # and on every host core the box reports ("Pippenger on all host cores")
+        out["cpu_baseline_pippenger_allcores"] = cpu_pippenger(curve, bxy, binf, scalars, res, os.cpu_count() or 1)
         del bxy, binf
         out["cpu_baselines_other"]["C3_width256_commits_pippenger"] = cpu_pippenger_commits(a.commit_batch, thr)
         if "kzg" in out:  # configs[3] on the CPU: its two 2^20 MSMs alone (quotient not counted)

@@ -17,6 +17,13 @@
  * The collective order is the same on every rank (SPMD): every rank calls the same sequence of
  * sharded entry points with the same group-wide arguments. A vc_comm is used by one host thread
  * at a time. Status codes as in vc_msm.h.
+ *
+ * Failures are group-wide: a rank whose share fails (out of memory, a HIP error, a bad table)
+ * still enters every exchange of the step, carrying its status with its records (or in a 4-byte
+ * status exchange ahead of a device all-gather), so no peer is left waiting in RCCL. Every rank
+ * then returns an error: the failing rank its own status, the others VC_E_PEER. Host exchanges
+ * over RCCL are staged through buffers allocated once by vc_comm_init_rccl and move in fixed
+ * 1 MiB pieces, so no exchange allocates on the way in.
  */
 #ifndef VC_COMM_H
 #define VC_COMM_H

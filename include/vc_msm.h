@@ -46,6 +46,7 @@ extern "C" {
 #define VC_E_NO_DEVICE (-7)   /* no usable gfx950 device                           */
 #define VC_E_DOMAIN (-8)      /* evaluation point outside what the call supports   */
 #define VC_E_COMM (-9)        /* collective failed (vc_comm.h: RCCL or the callback) */
+#define VC_E_PEER (-10)       /* another rank of the vc_comm failed this step (vc_comm.h) */
 
 typedef struct vc_ctx vc_ctx;
 
@@ -111,6 +112,12 @@ int vc_msm_device_partial(vc_ctx* ctx, int table_id, size_t offset, const void* 
  * split by the GLV endomorphism (BLS12-381, n >= 4096, tables of subgroup points: 2n terms of
  * 127-bit scalars over P_i and phi(P_i), W windows of those), else 1 */
 int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows, int* terms_per_point);
+/* Geometry the last MSM on this context actually ran (any vc_msm* entry point): windows of radix
+ * radix_mul * 2^window_bits (radix_mul > 1: the mixed-radix shared windows of a one-GPU
+ * whole-table GLV MSM, e.g. 5 * 2^16 with 7 windows), terms per point, and whether all windows
+ * shared one bucket set through the table's window copies. Any out pointer may be NULL. */
+int vc_msm_last_plan(const vc_ctx* ctx, int* window_bits, int* windows, int* terms_per_point, int* radix_mul,
+                     int* shared_windows);
 int vc_msm_device_window_part(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars, size_t n,
                               int mont, int part, int parts, uint32_t* out_acc);
 /* Sum k partial accumulators (host) and normalise to canonical affine. */

@@ -68,3 +68,18 @@ def test_partials_sum_host_path():
             want = C.add(want, p)
         got = (vkzg.limbs_to_int(out[:nl]), vkzg.limbs_to_int(out[nl:]))
         assert got == want and oinf[0] == 0
+
+
+def test_hot_kernels_keep_two_waves_per_simd():
+    """the VALU-bound loops (k_msm_accumulate, k_fb_commit_cm) must fit 256 VGPRs + AGPRs without
+    spills: two waves per SIMD. A mixed-add variant at 268 VGPRs ran at one wave per SIMD and made
+    the 2^20 accumulate 15 % slower (profiles/r03: 2.24 -> 2.56 ms)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "verkle-kzg_amd", "tools"))
+    import kernel_regs
+    lib = os.path.join(root, "verkle-kzg_amd", "lib", "libvkzg.so")
+    rows = kernel_regs.kernel_regs(lib, "k_msm_accumulate") + kernel_regs.kernel_regs(lib, "k_fb_commit_cm")
+    assert len(rows) >= 10
+    for name, vgpr, agpr, spill in rows:
+        assert vgpr + agpr <= 256 and spill == 0, (name, vgpr, agpr, spill)

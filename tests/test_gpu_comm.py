@@ -196,6 +196,57 @@ def test_verkle_commitment_sharded():
         assert all(r == want for r in res)
 
 
+@pytest.mark.parametrize("what", ["msm", "msm_batch", "kzg", "verkle"])
+def test_sharded_failure_is_group_wide(what):
+    """SPMD failure (include/vc_comm.h): rank 1's share fails (an unknown table id), yet it enters
+    the step's exchange with its status, so no rank waits forever; the failing rank returns its own
+    error (VC_E_TABLE) and its peers VC_E_PEER."""
+    import torch
+    import vkzg
+    from vkzg import scheme
+    from vkzg.verkle import VerkleTree
+    curve = {"msm": "bls12_381", "msm_batch": "bandersnatch", "kzg": "bn254", "verkle": "bn254"}[what]
+    n = 5000
+
+    def body(k, comm, e):
+        try:
+            if what == "msm":
+                tab = e.random_bases(n, seed=3)
+                d = torch.from_numpy(vkzg.random_scalars(curve, n, np.random.default_rng(1)).view(np.int64).copy()).cuda()
+                torch.cuda.synchronize()
+                comm.msm(e, 999 if k == 1 else tab, d.data_ptr(), n)
+            elif what == "msm_batch":
+                tab = e.random_bases(256, seed=3)
+                d = torch.from_numpy(vkzg.random_scalars(curve, 256 * 30, np.random.default_rng(1)).view(np.int64).copy()).cuda()
+                torch.cuda.synchronize()
+                comm.msm_batch(e, 999 if k == 1 else tab, 256, d.data_ptr(), 30)
+            elif what == "kzg":
+                kz = scheme.KZG(e, 256)
+                if k == 1:
+                    kz.table = 999
+                data = scheme.LagrangeBasis(list(range(1, 257)), 256)
+                d = torch.from_numpy(data.limbs(256).view(np.int64).copy()).cuda()
+                torch.cuda.synchronize()
+                comm.kzg_prove(kz, d.data_ptr(), 256, 7)
+            else:
+                kz = scheme.KZG(e, 256)
+                t = VerkleTree(4)
+                rng = random.Random(2)
+                for _ in range(300):
+                    try:
+                        t.insert_single(tuple(rng.randrange(12) for _ in range(4)), bytes(32))
+                    except Exception:
+                        pass
+                comm.verkle_commitment(t, e, 999 if k == 1 else kz.table)
+            return 0
+        except vkzg.VCError as ex:
+            return ex.status
+
+    for G in (2, 3):
+        st = run_ranks(G, curve, body)
+        assert st[1] == -4 and all(s == -10 for i, s in enumerate(st) if i != 1), st
+
+
 def test_rccl_world_one():
     """RCCL transport (dlopen'd librccl) at world 1: unique id, init, the host all-gather and the
     device exchange inside the sharded multiproof, and a sharded MSM == the plain calls."""

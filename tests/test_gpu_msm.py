@@ -257,6 +257,37 @@ def test_batch_commit(engines, oracle_c, curve):
                 assert np.array_equal(got_xy[j], want[0]), j
 
 
+def test_batch_commit_edwards_identity(engines, oracle_c):
+    """Bandersnatch commits that sum to the identity through P + (-P) (Edwards identity (0 : Z : Z)
+    with Z != 1): the device normalisation (large batches, k_norm_prep / k_norm_finish) must divide
+    by Z like the host path of small batches and report the identity, (0, 1) with inf = 1."""
+    import vkzg
+    from pyoracle.curves import CURVES as OC
+    C = OC["bandersnatch"]
+    e = engines["bandersnatch"]
+    xy, _ = e.download_bases(e.random_bases(2, seed=3))
+    xy = np.array(xy, dtype=np.uint64)
+    x0 = vkzg.limbs_to_int(xy[0][:4])
+    xy[1][:4] = vkzg.ints_to_limbs([(C.p - x0) % C.p])[0]   # -P = (-x, y)
+    xy[1][4:] = xy[0][4:]
+    inf = np.zeros(2, dtype=np.uint8)
+    tid = e.upload_bases(xy, inf)
+    e.fixed_base_precompute(tid, 8)
+    rng = np.random.default_rng(8)
+    ident_xy = np.array([0, 0, 0, 0, 1, 0, 0, 0], dtype=np.uint64)
+    for batch in (3, 100):                               # host latency path, device normalisation
+        sc = vkzg.random_scalars("bandersnatch", 2 * batch, rng)
+        for j in range(0, batch, 2):
+            sc[2 * j + 1] = sc[2 * j]                    # a P + a (-P) = O
+        got_xy, got_inf = e.msm_batch(tid, sc, 2)
+        for j in range(batch):
+            if j % 2 == 0:
+                assert got_inf[j] == 1 and np.array_equal(np.asarray(got_xy[j], dtype=np.uint64), ident_xy), (batch, j)
+            else:
+                want = _oracle(oracle_c, "bandersnatch", xy, inf, sc[2 * j:2 * j + 2])
+                assert got_inf[j] == want[1] and np.array_equal(got_xy[j], want[0]), (batch, j)
+
+
 @pytest.mark.parametrize("curve", CURVES)
 def test_batch_commit_sparse(engines, oracle_c, curve):
     """vc_msm_batch_sparse (CSR rows) vs the oracle: empty rows, single non-zeros, long rows

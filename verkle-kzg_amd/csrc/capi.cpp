@@ -164,6 +164,7 @@ const char* vc_strerror(int s) {
         case VC_E_NO_DEVICE: return "no usable HIP device";
         case VC_E_DOMAIN: return "evaluation point outside the supported domain";
         case VC_E_COMM: return "collective failed (RCCL or the all-gather callback)";
+        case VC_E_PEER: return "another rank of the group failed this step";
     }
     return "unknown status";
 }
@@ -337,6 +338,17 @@ static int msm_device_acc(vc_ctx* ctx, int id, size_t offset, const void* d_sc, 
 int vc_msm_windows(int curve, size_t n, int* window_bits, int* windows, int* terms_per_point) {
     if (!valid_curve(curve) || !window_bits || !windows) return VC_E_INVALID;
     return vk::msm_windows(curve, n, window_bits, windows, terms_per_point);
+}
+
+int vc_msm_last_plan(const vc_ctx* ctx, int* window_bits, int* windows, int* terms_per_point, int* radix_mul,
+                     int* shared_windows) {
+    if (!ctx) return VC_E_INVALID;
+    if (window_bits) *window_bits = ctx->plan.c;
+    if (windows) *windows = ctx->plan.W;
+    if (terms_per_point) *terms_per_point = ctx->plan.terms;
+    if (radix_mul) *radix_mul = ctx->plan.m;
+    if (shared_windows) *shared_windows = ctx->plan.shared;
+    return VC_OK;
 }
 
 int vc_msm_device_window_part(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n, int mont, int part,

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -84,6 +85,10 @@ namespace {
 
 int comm_allgather_dev(vc_comm* c, vc_ctx* ctx, const void* d_send, size_t bytes, void* d_recv);
 
+// RCCL staging of host exchanges: fixed pieces through buffers allocated once at init, so an
+// exchange never allocates (a rank that failed to grow a buffer could not enter the collective)
+constexpr size_t HOST_PIECE = size_t(1) << 20;
+
 // host buffers -> host buffers
 int comm_allgather_host(vc_comm* c, vc_ctx* ctx, const void* send, size_t bytes, void* recv) {
     if (!c->nccl && c->world == 1) {
@@ -93,12 +98,41 @@ int comm_allgather_host(vc_comm* c, vc_ctx* ctx, const void* send, size_t bytes,
     if (!c->nccl) return c->fn(c->user, send, bytes, recv) == 0 ? VC_OK : VC_E_COMM;
     if (!ctx) return VC_E_INVALID;
     (void)hipSetDevice(ctx->device);
-    VK_TRY(c->send.ensure(bytes));
-    VK_TRY(c->recv.ensure(bytes * c->world));
-    VK_CHECK_HIP(hipMemcpyAsync(c->send.p, send, bytes, hipMemcpyHostToDevice, ctx->stream));
-    VK_TRY(comm_allgather_dev(c, ctx, c->send.p, bytes, c->recv.p));
-    VK_CHECK_HIP(hipMemcpyAsync(recv, c->recv.p, bytes * c->world, hipMemcpyDeviceToHost, ctx->stream));
-    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    const uint8_t* s = static_cast<const uint8_t*>(send);
+    uint8_t* r = static_cast<uint8_t*>(recv);
+    for (size_t off = 0; off < bytes; off += HOST_PIECE) {  // same piece sequence on every rank
+        const size_t m = std::min(HOST_PIECE, bytes - off);
+        VK_CHECK_HIP(hipMemcpyAsync(c->send.p, s + off, m, hipMemcpyHostToDevice, ctx->stream));
+        VK_TRY(comm_allgather_dev(c, ctx, c->send.p, m, c->recv.p));
+        for (int k = 0; k < c->world; k++)
+            VK_CHECK_HIP(hipMemcpyAsync(r + (size_t)k * bytes + off, static_cast<uint8_t*>(c->recv.p) + (size_t)k * m, m,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return VC_OK;
+}
+
+// the group's statuses of one step (a 4-byte exchange): every rank learns whether all shares
+// succeeded. Returns own status if it failed, VC_E_PEER if only a peer failed, else VC_OK (or
+// the exchange's own error).
+int agree(vc_comm* c, vc_ctx* ctx, int st) {
+    std::vector<int32_t> all(c->world);
+    const int32_t mine = st;
+    const int cs = comm_allgather_host(c, ctx, &mine, 4, all.data());
+    if (cs != VC_OK) return cs;
+    if (st != VC_OK) return st;
+    for (int k = 0; k < c->world; k++)
+        if (all[k] != VC_OK) return VC_E_PEER;
+    return VC_OK;
+}
+// the same for statuses already gathered inside the records (stride bytes apart, status first)
+int agree_in(const vc_comm* c, int st, const uint8_t* recs, size_t stride) {
+    if (st != VC_OK) return st;
+    for (int k = 0; k < c->world; k++) {
+        int32_t v;
+        memcpy(&v, recs + (size_t)k * stride, 4);
+        if (v != VC_OK) return VC_E_PEER;
+    }
     return VC_OK;
 }
 
@@ -125,6 +159,23 @@ int comm_allgather_dev(vc_comm* c, vc_ctx* ctx, const void* d_send, size_t bytes
     VK_CHECK_HIP(hipMemcpyAsync(d_recv, hr, bytes * c->world, hipMemcpyHostToDevice, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     return VC_OK;
+}
+
+// one exchange of projective partials: record = status word + the partial (zero on failure);
+// every rank sums the partials or returns the group's error
+template <class Fn>
+int partial_step(vc_ctx* ctx, vc_comm* comm, Fn&& compute, uint64_t* out_xy, uint8_t* out_inf) {
+    const int words = vk::point_words(ctx->curve);
+    const size_t rec = (size_t)words + 1;
+    std::vector<uint32_t> part(rec, 0), parts(rec * comm->world);
+    const int st = compute(part.data() + 1);
+    if (st != VC_OK) std::fill(part.begin(), part.end(), 0u);
+    part[0] = (uint32_t)st;
+    VK_TRY(comm_allgather_host(comm, ctx, part.data(), rec * 4, parts.data()));
+    VK_TRY(agree_in(comm, st, reinterpret_cast<const uint8_t*>(parts.data()), rec * 4));
+    std::vector<uint32_t> acc((size_t)words * comm->world);
+    for (int k = 0; k < comm->world; k++) memcpy(&acc[(size_t)k * words], &parts[k * rec + 1], (size_t)words * 4);
+    return vc_partials_sum(ctx->curve, acc.data(), comm->world, out_xy, out_inf);
 }
 
 bool valid(const vc_comm* c, const vc_ctx* ctx) { return c && ctx && (!c->nccl || c->device == ctx->device); }
@@ -162,6 +213,11 @@ int vc_comm_init_rccl(int device, int rank, int world, const uint8_t id[VC_COMM_
     c->world = world;
     c->device = device;
     c->nccl = nc;
+    // host-exchange staging, once (comm_allgather_host moves fixed pieces through it)
+    if (c->send.ensure(HOST_PIECE) != VC_OK || c->recv.ensure(HOST_PIECE * world) != VC_OK) {
+        vc_comm_destroy(c);
+        return VC_E_OOM;
+    }
     *out = c;
     return VC_OK;
 }
@@ -195,14 +251,14 @@ int vc_comm_allgather(vc_comm* c, vc_ctx* ctx, const void* send, size_t bytes, v
 
 // ---------------------------------------------------------------- sharded workloads
 
+
+
 int vc_msm_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t offset, const void* d_scalars, size_t n, int mont,
                    uint64_t* out_xy, uint8_t* out_inf) {
     if (!valid(comm, ctx) || !out_xy || !out_inf) return VC_E_INVALID;
-    const int words = vk::point_words(ctx->curve);
-    std::vector<uint32_t> part(words), parts((size_t)words * comm->world);
-    VK_TRY(vc_msm_device_window_part(ctx, table_id, offset, d_scalars, n, mont, comm->rank, comm->world, part.data()));
-    VK_TRY(comm_allgather_host(comm, ctx, part.data(), part.size() * 4, parts.data()));
-    return vc_partials_sum(ctx->curve, parts.data(), comm->world, out_xy, out_inf);
+    return partial_step(ctx, comm, [&](uint32_t* part) {
+        return vc_msm_device_window_part(ctx, table_id, offset, d_scalars, n, mont, comm->rank, comm->world, part);
+    }, out_xy, out_inf);
 }
 
 int vc_msm_batch_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t width, const void* d_scalars, size_t batch,
@@ -214,28 +270,36 @@ int vc_msm_batch_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t width,
     vk::shard_range(batch, comm->rank, comm->world, &lo, &hi);
     const size_t bmax = (batch + comm->world - 1) / comm->world, mine = hi - lo;
     const size_t rec = W2 + 1;  // u64 words per record: x, y, inf
-    std::vector<uint64_t> send(bmax * rec, 0), recv(bmax * rec * comm->world);
+    const size_t slot = 1 + bmax * rec;  // a rank's status word, then its records
+    std::vector<uint64_t> send(slot, 0), recv(slot * comm->world);
+    int st = VC_OK;
     if (mine > 0) {
-        (void)hipSetDevice(ctx->device);
-        VK_TRY(comm->work.ensure(mine * (W2 * 8 + 1)));
-        uint8_t* dxy = reinterpret_cast<uint8_t*>(comm->work.p);
-        uint8_t* dinf = dxy + mine * W2 * 8;
-        const uint8_t* sc = reinterpret_cast<const uint8_t*>(d_scalars) + lo * width * 32;
-        VK_TRY(vc_msm_batch_device(ctx, table_id, width, sc, mine, mont, dxy, dinf));
-        std::vector<uint64_t> hxy(mine * W2);
-        std::vector<uint8_t> hinf(mine);
-        VK_CHECK_HIP(hipMemcpy(hxy.data(), dxy, mine * W2 * 8, hipMemcpyDeviceToHost));
-        VK_CHECK_HIP(hipMemcpy(hinf.data(), dinf, mine, hipMemcpyDeviceToHost));
-        for (size_t b = 0; b < mine; b++) {
-            memcpy(&send[b * rec], &hxy[b * W2], W2 * 8);
-            send[b * rec + W2] = hinf[b];
-        }
+        auto share = [&]() -> int {
+            (void)hipSetDevice(ctx->device);
+            VK_TRY(comm->work.ensure(mine * (W2 * 8 + 1)));
+            uint8_t* dxy = reinterpret_cast<uint8_t*>(comm->work.p);
+            uint8_t* dinf = dxy + mine * W2 * 8;
+            const uint8_t* sc = reinterpret_cast<const uint8_t*>(d_scalars) + lo * width * 32;
+            VK_TRY(vc_msm_batch_device(ctx, table_id, width, sc, mine, mont, dxy, dinf));
+            std::vector<uint64_t> hxy(mine * W2);
+            std::vector<uint8_t> hinf(mine);
+            VK_CHECK_HIP(hipMemcpy(hxy.data(), dxy, mine * W2 * 8, hipMemcpyDeviceToHost));
+            VK_CHECK_HIP(hipMemcpy(hinf.data(), dinf, mine, hipMemcpyDeviceToHost));
+            for (size_t b = 0; b < mine; b++) {
+                memcpy(&send[1 + b * rec], &hxy[b * W2], W2 * 8);
+                send[1 + b * rec + W2] = hinf[b];
+            }
+            return VC_OK;
+        };
+        st = share();  // a failed share still enters the exchange (vc_comm.h)
     }
+    send[0] = (uint64_t)(uint32_t)st;
     VK_TRY(comm_allgather_host(comm, ctx, send.data(), send.size() * 8, recv.data()));
+    VK_TRY(agree_in(comm, st, reinterpret_cast<const uint8_t*>(recv.data()), slot * 8));
     for (int k = 0; k < comm->world; k++) {
         size_t a, e;
         vk::shard_range(batch, k, comm->world, &a, &e);
-        const uint64_t* src = &recv[(size_t)k * bmax * rec];
+        const uint64_t* src = &recv[(size_t)k * slot + 1];
         for (size_t b = 0; b < e - a; b++) {
             memcpy(&out_xy[(a + b) * W2], &src[b * rec], W2 * 8);
             out_inf[a + b] = (uint8_t)src[b * rec + W2];
@@ -247,11 +311,9 @@ int vc_msm_batch_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t width,
 int vc_kzg_prove_sharded(vc_ctx* ctx, vc_comm* comm, int table, size_t size, const void* d_evals, size_t max,
                          const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y) {
     if (!valid(comm, ctx) || !point || !proof_xy || !proof_inf || !y) return VC_E_INVALID;
-    const int words = vk::point_words(ctx->curve);
-    std::vector<uint32_t> part(words), parts((size_t)words * comm->world);
-    VK_TRY(vc_kzg_prove_device_part(ctx, table, size, d_evals, max, point, comm->rank, comm->world, part.data(), y));
-    VK_TRY(comm_allgather_host(comm, ctx, part.data(), part.size() * 4, parts.data()));
-    return vc_partials_sum(ctx->curve, parts.data(), comm->world, proof_xy, proof_inf);
+    return partial_step(ctx, comm, [&](uint32_t* part) {
+        return vc_kzg_prove_device_part(ctx, table, size, d_evals, max, point, comm->rank, comm->world, part, y);
+    }, proof_xy, proof_inf);
 }
 
 int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int table, size_t N, size_t Q,
@@ -264,22 +326,28 @@ int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int tabl
     vc_transcript* tr = nullptr;
     uint64_t r[4];
     size_t rows = 0;
-    VK_TRY(vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows));
     size_t lo, hi;
     vk::shard_range(Q, comm->rank, comm->world, &lo, &hi);
+    // this rank's share up to the exchange; its status is agreed on before the device all-gather
+    // (a rank without its S buffer cannot enter that collective)
+    int st = vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows);
     const size_t sbytes = rows * N * 32;
-    int st = VC_OK;
-    do {
+    uint8_t* dS = nullptr;
+    if (st == VC_OK) {
         (void)hipSetDevice(ctx->device);
         // [0, sbytes): this rank's S; [sbytes, ...): every rank's S in rank order
-        if ((st = comm->work.ensure(sbytes * (comm->world + 1))) != VC_OK) break;
-        uint8_t* dS = reinterpret_cast<uint8_t*>(comm->work.p);
-        if ((st = vc_multiproof_accumulate(ctx, N, Q, z, lo, hi - lo, d_data_slice, r, dS)) != VC_OK) break;
-        if ((st = comm_allgather_dev(comm, ctx, dS, sbytes, dS + sbytes)) != VC_OK) break;
+        st = comm->work.ensure(sbytes * (comm->world + 1));
+        if (st == VC_OK) {
+            dS = reinterpret_cast<uint8_t*>(comm->work.p);
+            st = vc_multiproof_accumulate(ctx, N, Q, z, lo, hi - lo, d_data_slice, r, dS);
+        }
+    }
+    st = agree(comm, ctx, st);
+    if (st == VC_OK) st = comm_allgather_dev(comm, ctx, dS, sbytes, dS + sbytes);
+    if (st == VC_OK)
         st = vc_multiproof_finish(ctx, scheme, table, N, Q, z, dS + sbytes, comm->world, tr, d_xy, d_inf, ipa_proof,
                                   kzg_proof_xy, kzg_proof_inf, kzg_y);
-    } while (false);
-    vc_transcript_free(tr);
+    if (tr) vc_transcript_free(tr);
     return st;
 }
 

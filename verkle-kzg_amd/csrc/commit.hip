@@ -112,6 +112,15 @@ __device__ __forceinline__ fe<typename C::F> denom(const typename C::Acc& a) {
     else return a.zzz;
 }
 
+// accumulators that take denominator 1 in the batch inversion: the SW identity (Z = 0, nothing
+// to invert). An Edwards point always has Z != 0 -- its identity (0 : Z : Z) included, which must
+// be divided by Z like any other point (it was counted as 1 and came out as (0, Z), not (0, 1))
+template <class C>
+__device__ __forceinline__ bool norm_as_one(const typename C::Acc& a) {
+    if constexpr (C::is_te) return false;
+    else return C::is_zero(a);
+}
+
 template <class C>
 __global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __restrict__ in, size_t count,
                                                   typename C::Aff* __restrict__ out_aff,
@@ -124,10 +133,7 @@ __global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __rest
     uint32_t tid = threadIdx.x;
     typename C::Acc a = j < count ? in[j] : C::zero();
     bool ident = C::is_zero(a);
-    fe<F> z = (j < count && !ident) ? denom<C>(a) : fe_one<F>();
-    if constexpr (!C::is_te) {
-        if (ident) z = fe_one<F>();
-    }
+    fe<F> z = (j < count && !norm_as_one<C>(a)) ? denom<C>(a) : fe_one<F>();
     pre[tid] = z;
     suf[tid] = z;
     __syncthreads();
@@ -195,7 +201,7 @@ __global__ void __launch_bounds__(256) k_norm_prep(const typename C::Acc* __rest
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t tid = threadIdx.x;
     const typename C::Acc a = j < count ? in[j] : C::zero();
-    fe<F> z = (j < count && !C::is_zero(a)) ? denom<C>(a) : fe_one<F>();
+    fe<F> z = (j < count && !norm_as_one<C>(a)) ? denom<C>(a) : fe_one<F>();
     pre[tid] = z;
     suf[tid] = z;
     __syncthreads();

@@ -171,6 +171,11 @@ struct vc_ctx {
     int opt_shared_windows = 1;           // GLV MSMs over a whole table: one bucket set via Table::win
     size_t opt_msm_chunk = size_t(1) << 27;  // MSMs above this many points run as summed chunks
     uint32_t fb_lanes = 0;                // resident lanes of k_fb_commit_cm (cached per context)
+    // geometry of the last MSM (vc_msm_last_plan): window bits c, windows W (of the whole MSM),
+    // terms per point (2 with the GLV split), radix multiplier m (radix m 2^c; 1 = 2^c), shared
+    struct {
+        int c, W, terms, m, shared;
+    } plan = {0, 0, 0, 0, 0};
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, long>> ktime;

@@ -25,6 +25,11 @@ struct SW29 {
     struct Aff {
         f29<P> x, y;
     };
+    // a base with both signs of y (the shared-window copies): the accumulate picks y or -y by
+    // the entry's sign through the load address, so the mixed add has no negation in it
+    struct AffN {
+        f29<P> x, y, ny;
+    };
     struct Acc {
         f29<P> x, y, zz, zzz;
         bool inf;
@@ -79,13 +84,23 @@ struct SW29 {
         const f29<P> PPP = mul29<P>(Pd, PP);
         const f29<P> Q = mul29<P>(p.x, PP);
         Acc r;
-        r.x = sub2_29<P, 8>(sqr29<P>(R), PPP, add29<P>(Q, Q));
+        // X3 = R^2 - PPP - 2Q in one pass: 8p - (PPP + 2Q) per limb (product outputs: limbs < 2^29,
+        // so the subtrahend's limbs stay below 3 * 2^29 < subK's 2^31 - 4), one carry pass
+        {
+            const f29<P> RR = sqr29<P>(R);
+            f29<P> x3;
+#pragma unroll
+            for (int j = 0; j < P::L; j++) x3.v[j] = RR.v[j] + subk<P, 8>(j) - (PPP.v[j] + Q.v[j] + Q.v[j]);
+            r.x = norm29<P>(x3);
+        }
         // Y3 = R (Q - X3) + Y1 (4p - PPP) with one reduction (mul2sum29)
         r.y = mul2sum29<P>(R, sub29<P, 16>(Q, r.x), p.y, neg29<P, 4>(PPP));
         r.zz = mul29<P>(p.zz, PP);
         r.zzz = mul29<P>(p.zzz, PPP);
         r.inf = false;
-        if (is_zero_mo29<P>(r.zz)) {  // P == 0 mod p: q = +-acc (rare)
+        // P == 0 mod p (q = +-acc, rare). (A filter on ZZ3's lowest limb first kept more values live
+        // across the branch: 268 VGPRs, one wave per SIMD, 2.24 -> 2.56 ms -- the full check stays.)
+        if (is_zero_mo29<P>(r.zz)) {
             if (is_zero_mo29<P>(mul29<P>(R, one29<P>()))) return dbl_aff(q.x, y2);
             return zero();
         }

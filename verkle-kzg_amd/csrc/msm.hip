@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -275,8 +276,14 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
 // the fix-up and the reduction (msm_tail.hip), which run the same arithmetic; converting them
 // to the ec.hpp form at the three store sites (4 multiplies each) put ~50 KB of rarely-run code
 // into the loop and cost 7 % of the kernel.
-// BT: the base entry type -- packed-29 C::Aff (tables, window copies) or the limb form of the
-// fixed-base tables the sparse commits read (Fast29<C>::type::Aff, commit.hip FbE)
+// BT: the base entry type -- packed-29 C::Aff (tables), the limb form of the fixed-base tables
+// the sparse commits read (Fast29<C>::type::Aff, commit.hip FbE), or the signed limb form of the
+// shared-window copies (SW29::AffN: x, y, -y -- the entry's sign picks the y to load)
+template <class FC, class BT, class = void>
+struct is_affn : std::false_type {};
+template <class FC, class BT>
+struct is_affn<FC, BT, std::void_t<typename FC::AffN>> : std::is_same<BT, typename FC::AffN> {};
+
 template <class C, class BT = typename C::Aff>
 __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     const BT* __restrict__ bases, const BT* __restrict__ phi, uint32_t nphi,
@@ -306,16 +313,33 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     typename FC::Acc acc = FC::zero();
     // entry j < nphi: bases[j]; j >= nphi: phi[j - nphi] (the GLV endomorphism images)
     auto base_of = [&](uint32_t j) -> const Aff* { return j < nphi ? bases + j : phi + (j - nphi); };
+    constexpr bool SN = is_affn<FC, BT>::value;
+    using Pre = std::conditional_t<SN, typename FC::Aff, Aff>;  // the prefetched entry
+    auto fetch = [&](uint32_t id) -> Pre {
+        const Aff* b = base_of(id & 0x7fffffffu);
+        if constexpr (SN) {
+            typename FC::Aff a;
+            a.x = b->x;
+            // y or -y through the address (a select of values would load both)
+            a.y = *reinterpret_cast<const decltype(a.y)*>(reinterpret_cast<const char*>(&b->y) +
+                                                          ((id >> 31) ? sizeof(a.y) : 0u));
+            return a;
+        } else {
+            return *b;
+        }
+    };
     uint32_t idx = sorted[k];
-    Aff P = *base_of(idx & 0x7fffffffu);
+    Pre P = fetch(idx);
     while (true) {
         uint32_t cur = idx;
-        const typename FC::Aff Q = FC::load(&P);
+        typename FC::Aff Q;
+        if constexpr (SN) Q = P;
+        else Q = FC::load(&P);
         if (k + 1 < e) {  // prefetch next base
             idx = sorted[k + 1];
-            P = *base_of(idx & 0x7fffffffu);
+            P = fetch(idx);
         }
-        acc = FC::madd(acc, Q, (cur >> 31) != 0);
+        acc = FC::madd(acc, Q, !SN && (cur >> 31) != 0);
         k++;
         if (k == bend || k == e) {
             bool right_open = (k == e) && (bend > e);
@@ -371,6 +395,25 @@ __global__ void __launch_bounds__(256) k_to_limbs(const typename C::Aff* __restr
     typename C::Aff packed;
     FC::pack_aff(in[i], &packed);
     out[i] = FC::load(&packed);
+}
+
+// ... and to the signed limb form (x, y, -y) of the shared-window copies
+template <class C>
+__global__ void __launch_bounds__(256) k_to_limbs_n(const typename C::Aff* __restrict__ in, size_t n,
+                                                   typename Fast29<C>::type::AffN* __restrict__ out) {
+    using FC = typename Fast29<C>::type;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    typename C::Aff a = in[i], packed;
+    FC::pack_aff(a, &packed);
+    const typename FC::Aff l = FC::load(&packed);
+    a.y = fe_neg<typename C::F>(a.y);
+    FC::pack_aff(a, &packed);
+    typename FC::AffN o;
+    o.x = l.x;
+    o.y = l.y;
+    o.ny = FC::load(&packed).y;
+    out[i] = o;
 }
 
 // ------------------------------------------------------------------ GLV endomorphism (BLS12-381 G1)
@@ -519,6 +562,20 @@ __global__ void __launch_bounds__(256) k_glv_split(const uint32_t* __restrict__ 
 // for_each_digit), W digits (B^W / 2 > 2^127: the top digit is below B/2 and never carries).
 // k mod B = (k mod 2^C0) + 2^C0 ((k >> C0) mod MUL); the division by MUL runs over the four
 // 32-bit limbs from the top. A negative half negates every digit.
+// (rem 2^32 + x) / MUL for rem < MUL, in 32-bit steps (2^32 = MUL Q + 1 for MUL | 2^32 - 1):
+// x = MUL q0 + x0 with q0 by a multiply-high, then rem + x0 < 2 MUL carries at most one
+template <uint32_t MUL>
+__device__ __forceinline__ uint32_t div_step(uint32_t x, uint32_t& rem) {
+    static_assert(MUL == 5 || MUL == 3, "2^32 = 1 mod MUL");
+    constexpr uint32_t Q = (uint32_t)(0xffffffffull / MUL);  // (2^32 - 1) / MUL
+    const uint32_t q0 = MUL == 5 ? __umulhi(x, 0xCCCCCCCDu) >> 2 : __umulhi(x, 0xAAAAAAABu) >> 1;
+    const uint32_t t = rem + (x - q0 * MUL);
+    const uint32_t ge = t >= MUL ? 1u : 0u;
+    const uint32_t q = rem * Q + q0 + ge;
+    rem = t - ge * MUL;
+    return q;
+}
+
 template <uint32_t MUL, int C0>
 __device__ __forceinline__ void radix_digits(u128 k, bool neg, int W, int32_t* __restrict__ out, size_t stride) {
     constexpr uint32_t B = MUL << C0, H = B / 2, LO = (1u << C0) - 1;
@@ -530,15 +587,12 @@ __device__ __forceinline__ void radix_digits(u128 k, bool neg, int W, int32_t* _
         x1 = (x1 >> C0) | (x2 << (32 - C0));
         x2 = (x2 >> C0) | (x3 << (32 - C0));
         x3 >>= C0;
-        uint64_t cur = x3;
-        x3 = (uint32_t)(cur / MUL);
-        cur = ((cur % MUL) << 32) | x2;
-        x2 = (uint32_t)(cur / MUL);
-        cur = ((cur % MUL) << 32) | x1;
-        x1 = (uint32_t)(cur / MUL);
-        cur = ((cur % MUL) << 32) | x0;
-        x0 = (uint32_t)(cur / MUL);
-        const uint32_t raw = lo + ((uint32_t)(cur % MUL) << C0) + carry;
+        uint32_t rem = 0;
+        x3 = div_step<MUL>(x3, rem);
+        x2 = div_step<MUL>(x2, rem);
+        x1 = div_step<MUL>(x1, rem);
+        x0 = div_step<MUL>(x0, rem);
+        const uint32_t raw = lo + (rem << C0) + carry;
         int32_t d;
         if (raw > H) {
             d = (int32_t)raw - (int32_t)B;
@@ -700,9 +754,10 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul 
     if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts && t->win_m == (int)mul) return VC_OK;
     const size_t n = t->n;
     t->win_ok = 0;
-    using FA = typename Fast29<C>::type::Aff;  // limb form (k_to_limbs)
+    using FA = typename Fast29<C>::type::AffN;  // signed limb form (k_to_limbs_n)
     // VKZG_WIN_PACKED=1 keeps the packed-29 form (A/B probe: unpacking costs the accumulate ~84 of
-    // 5,044 instructions per add, the limb form 16 B more per gather)
+    // 5,044 instructions per add, the limb form 16 B more per gather); the limb form holds
+    // x, y and -y (168 B) so the accumulate never negates
     static const bool packed = getenv("VKZG_WIN_PACKED") != nullptr;
     t->win_limbs = packed ? 0 : 1;
     VK_TRY(t->win.ensure((size_t)W * 2 * n * (packed ? sizeof(Aff) : sizeof(FA))));
@@ -727,8 +782,8 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul 
             VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, src, n, wp + (size_t)w * 2 * n);
             VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, nxt.as<Aff>(), n, wp + (size_t)w * 2 * n + n);
         } else {
-            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs<C>), g, 256, 0, src, n, win + (size_t)w * 2 * n);
-            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs<C>), g, 256, 0, nxt.as<Aff>(), n, win + (size_t)w * 2 * n + n);
+            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs_n<C>), g, 256, 0, src, n, win + (size_t)w * 2 * n);
+            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs_n<C>), g, 256, 0, nxt.as<Aff>(), n, win + (size_t)w * 2 * n + n);
         }
     }
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));  // before the staging buffers are freed
@@ -1084,7 +1139,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         static const int radix_env = getenv("VKZG_MSM_RADIX") ? atoi(getenv("VKZG_MSM_RADIX")) : 5;
         if (glv && shared_env && offset == 0 && n == t->n && parts == 1 && nv >= (1u << 19) && radix_env == 5 &&
             !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED")) {
-            const size_t win_bytes = (size_t)7 * 2 * t->n * sizeof(typename Fast29<C>::type::Aff);
+            const size_t win_bytes = (size_t)7 * 2 * t->n * sizeof(typename Fast29<C>::type::AffN);
             if (win_bytes <= (8ull << 30)) {
                 const int st = win_tables<C>(ctx, t, 16, 7, 0, 5);
                 if (st == VC_OK) {
@@ -1103,7 +1158,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         // top window: GLV_BITS - cs (Ws - 1) bits -> digits up to 2^tb; scaled to fill 2^(cs-1)
         const int tb = GLV_BITS - cs * (Ws - 1);
         const int ts = std::max(0, (cs - 1) - tb);
-        const size_t win_bytes = (size_t)Ws * 2 * t->n * sizeof(typename Fast29<C>::type::Aff);
+        const size_t win_bytes = (size_t)Ws * 2 * t->n * sizeof(typename Fast29<C>::type::AffN);
         if (!shared && glv && shared_env && offset == 0 && n == t->n && win_bytes <= (8ull << 30)) {
             const int st = win_tables<C>(ctx, t, cs, Ws, ts);
             if (st == VC_OK) {
@@ -1119,6 +1174,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     }
     // one spare bit absorbs the final carry of the signed recoding
     const int Wfull = radix_m > 1 ? 7 : glv ? (GLV_BITS + c - 1) / c : (Fr::BITS + 1 + c - 1) / c;
+    ctx->plan = {c, Wfull, glv ? 2 : 1, (int)radix_m, shared ? 1 : 0};  // vc_msm_last_plan
     // window slice [wb, we) of this call (parts > 1: the MSM split by windows across GPUs;
     // the slices' results add up to the whole MSM)
     const int wb = part * Wfull / parts, we = (part + 1) * Wfull / parts;
@@ -1166,7 +1222,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                 VK_CHECK_HIP(hipStreamWaitEvent(ctx->side_stream, fork, 0));
             }
             // [w][2n] limb-form copies: entry w * 2n + i (sort_entries' stride)
-            const auto* win = t->win.as<typename Fast29<C>::type::Aff>();
+            const auto* win = t->win.as<typename Fast29<C>::type::AffN>();
             GlvDigits src{halves, inf, (uint32_t)n};
             if (shared && top_shift > 0) {
                 src.tw = Wfull - 1;

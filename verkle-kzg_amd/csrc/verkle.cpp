@@ -310,7 +310,10 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     {
         const VNode& root = t->nodes[0];
         HostPool& P = host_pool();
-        if (root.has_commit || root.ext || root.children.v.size() < 2 || t->nodes.size() < 4096 || P.size() == 1) {
+        // (the branch depends only on the tree, never on this host's core count: ranks of a
+        // sharded run with different pool sizes must produce the same lists; a one-thread pool
+        // runs the same per-child walk serially)
+        if (root.has_commit || root.ext || root.children.v.size() < 2 || t->nodes.size() < 4096) {
             walk(0, 0, exts, internals);
         } else {
             internals.resize(1);
@@ -319,9 +322,11 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             const unsigned T = P.size();
             std::vector<std::vector<int>> ex(T);
             std::vector<std::vector<std::vector<int>>> in(T);
-            P.run([&](unsigned k) {
+            auto part = [&](unsigned k) {
                 for (size_t c = ch.size() * k / T; c < ch.size() * (k + 1) / T; c++) walk(ch[c].second, 1, ex[k], in[k]);
-            });
+            };
+            if (T == 1) part(0);
+            else P.run(part);
             for (unsigned k = 0; k < T; k++) {
                 exts.insert(exts.end(), ex[k].begin(), ex[k].end());
                 if (internals.size() < in[k].size()) internals.resize(in[k].size());
@@ -414,8 +419,10 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     // the nodes nodes[lo, hi) of a level got (xy, inf, items) here: store them; with a shard,
     // first all-gather every rank's slice (records of 8 + 4 + 1 u64: xy, item, inf), so every
     // rank stores the whole level
+    // st: this rank's status for the level -- a failed share still enters the exchange with it
+    // (include/vc_comm.h), so every rank stops at the same level with an error
     auto store_level = [&](const std::vector<int>& ids, size_t lo, size_t hi, const std::vector<uint64_t>& xy,
-                           const std::vector<uint8_t>& inf, const std::vector<uint64_t>& items) -> int {
+                           const std::vector<uint8_t>& inf, const std::vector<uint64_t>& items, int st) -> int {
         auto put = [&](size_t i, const uint64_t* rxy, uint8_t rinf, const uint64_t* ritem) {
             VNode& n = t->nodes[ids[i]];
             memcpy(n.cxy, rxy, 64);
@@ -424,21 +431,26 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             n.has_commit = true;
         };
         if (!sh) {
+            if (st != VC_OK) return st;
             for_each(hi - lo, [&](size_t b) { put(lo + b, &xy[b * 8], inf[b], &items[b * 4]); });
             return VC_OK;
         }
         constexpr size_t REC = 13;  // u64 words per record
-        const size_t B = ids.size(), bmax = (B + sh->world - 1) / sh->world;
-        std::vector<uint64_t> send(bmax * REC, 0), recv(bmax * REC * sh->world);
-        for (size_t b = 0; b < hi - lo; b++) {
-            memcpy(&send[b * REC], &xy[b * 8], 64);
-            memcpy(&send[b * REC + 8], &items[b * 4], 32);
-            send[b * REC + 12] = inf[b];
+        const size_t B = ids.size(), bmax = (B + sh->world - 1) / sh->world, slot = 1 + bmax * REC;
+        std::vector<uint64_t> send(slot, 0), recv(slot * sh->world);
+        send[0] = (uint64_t)(uint32_t)st;
+        for (size_t b = 0; st == VC_OK && b < hi - lo; b++) {
+            memcpy(&send[1 + b * REC], &xy[b * 8], 64);
+            memcpy(&send[1 + b * REC + 8], &items[b * 4], 32);
+            send[1 + b * REC + 12] = inf[b];
         }
         VK_TRY(sh->allgather(send.data(), send.size() * 8, recv.data()));
+        if (st != VC_OK) return st;
+        for (int k = 0; k < sh->world; k++)
+            if ((int32_t)(uint32_t)recv[(size_t)k * slot] != VC_OK) return VC_E_PEER;
         for (int k = 0; k < sh->world; k++) {
             const size_t a = B * k / sh->world, e = B * (k + 1) / sh->world;
-            const uint64_t* src = &recv[(size_t)k * bmax * REC];
+            const uint64_t* src = &recv[(size_t)k * slot + 1];
             for_each(e - a, [&](size_t b) {
                 const uint64_t* rec = src + b * REC;
                 put(a + b, rec, (uint8_t)rec[12], rec + 8);
@@ -493,8 +505,9 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                 r.end_row();
             }
         });
-        VK_TRY(commit_rows(r12, xy, inf, items));
-        Rows rx = build_rows(lo, hi, 4, [&](size_t e, Rows& r) {
+        int st = commit_rows(r12, xy, inf, items);
+        Rows rx;
+        if (st == VC_OK) rx = build_rows(lo, hi, 4, [&](size_t e, Rows& r) {
             const VNode& n = t->nodes[exts[e]];
             uint64_t one[4] = {1, 0, 0, 0}, stem_item[4];
             item_of_bytes(n.stem.data(), N, stem_item);  // bytes_to_item(stem.to_bytes())
@@ -504,8 +517,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             r.add(3, &items[(2 * (e - lo) + 1) * 4]);
             r.end_row();
         });
-        VK_TRY(commit_rows(rx, xy2, inf2, items2));
-        VK_TRY(store_level(exts, lo, hi, xy2, inf2, items2));
+        if (st == VC_OK) st = commit_rows(rx, xy2, inf2, items2);
+        VK_TRY(store_level(exts, lo, hi, xy2, inf2, items2, st));
     }
     // internal nodes, deepest level first (HACK in the reference: width hard-coded 256); a
     // parent needs its children's items, so every depth is one exchange
@@ -517,8 +530,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             for (auto& kv : t->nodes[lv[b]].children) r.add(kv.first, t->nodes[kv.second].item);
             r.end_row();
         });
-        VK_TRY(commit_rows(ri, xy, inf, items));
-        VK_TRY(store_level(lv, lo, hi, xy, inf, items));
+        const int st = commit_rows(ri, xy, inf, items);
+        VK_TRY(store_level(lv, lo, hi, xy, inf, items, st));
     }
     memcpy(out_xy, t->nodes[0].cxy, 64);
     *out_inf = t->nodes[0].cinf;

@@ -250,6 +250,15 @@ class Engine:
                                           1 if mont else 0, _ptr(acc)), "vc_msm_device_partial")
         return acc
 
+    def msm_last_plan(self):
+        """geometry of the last MSM on this engine (vc_msm_last_plan): window bits, windows, terms
+        per point, radix multiplier (radix = mul * 2^bits), shared windows"""
+        v = [ctypes.c_int() for _ in range(5)]
+        check(lib().vc_msm_last_plan(self.h, *[ctypes.byref(x) for x in v]), "vc_msm_last_plan")
+        c, W, terms, mul, shared = (x.value for x in v)
+        return {"window_bits": c, "windows": W, "terms_per_point": terms, "radix_mul": mul,
+                "shared_windows": bool(shared)}
+
     def msm_device_window_part(self, table, d_scalars_ptr, n, part, parts, offset=0, mont=False):
         """Accumulator of Pippenger windows [part*W/parts, (part+1)*W/parts) of the whole MSM."""
         acc = np.zeros(self.point_words(), dtype=np.uint32)
