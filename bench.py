@@ -45,6 +45,12 @@ PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.j
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_summary.json"))
 
 
+def progress(msg):
+    """one stderr line per finished bench stage (rank 0): long runs show they are alive"""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,7 +239,7 @@ def kzg_line(a, rank, world, local, dev, stream):
             "achieved_GBps_in_domain": fused_bytes / (res["in_domain"]["ms_per_commit_open"] * 1e-3) / 1e9}
 
 
-def mp_line(a, rank, world, local, dev, stream):
+def mp_line(a, rank, world, local, dev, stream, comm=None):
     """configs[4]: IPA multiproof (multiproof.rs:99-176) over Q = 2^mp_log_q width-256 queries
     on BN254 (the reference's curve), the query set sharded over the ranks (vkzg.dist
     .multiproof_prove_sharded: host transcript on every rank, per-point sums of the local
@@ -297,6 +303,8 @@ def mp_line(a, rank, world, local, dev, stream):
     from vkzg._lib import lib
     lib().vc_transcript_free(tr)
     pipe = mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, mp) if world == 1 else None
+    par = mp_proof_parallel(ipa, N, cxy, cinf, z, y, d_all, dev, rank, world, comm, mp) \
+        if (world == 1 or comm is not None) else {"skipped": "no vc_comm for the proof exchange"}
     ref_shapes = mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev) if rank == 0 else None
     meng.close()
     alg = Q * N * 32 + Q * 64 + Q * 40
@@ -308,6 +316,10 @@ def mp_line(a, rank, world, local, dev, stream):
         out["pipelined"] = pipe
     if ref_shapes is not None:
         out["reference_bench_shapes"] = ref_shapes
+    out["proof_parallel"] = par
+    out["sliced_bound"] = ("the query-sliced single multiproof repeats the host transcript "
+                           f"({t_begin * 1e3:.2f} ms) and the finish on every rank: at most ~1.15x on 8 GPUs "
+                           "(DESIGN.md 6); proof_parallel scales with the ranks")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_multiproof(N, data, z, cxy, crs, a.cpu_threads or min(16, os.cpu_count() or 1))
     return out
@@ -359,6 +371,50 @@ def mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, reps=5):
                        "prove_ms": [round(x, 3) for x in tp], "verify_ms": [round(x, 3) for x in tv],
                        "verified": ok}
     return out
+
+
+def mp_proof_parallel(ipa, N, cxy, cinf, z, y, d_all, dev, rank, world, comm, want, per_rank=4, reps=3):
+    """Proof-parallel multiproofs (the throughput mode of configs[4] on N GPUs): P = per_rank x N
+    independent multiproofs of the line's Q queries; rank k proves its shard_range(P) proofs end
+    to end (vc_multiproof_prove_many: transcripts on host threads beside the GPU sums, D / E commits
+    and inner IPA proofs batched over its proofs) and one all-gather of the finished proofs
+    (vc_multiproof_prove_many_sharded) gives every rank all P. Every proof is the same query set
+    (the cost does not depend on the values); each is checked against the single-proof result."""
+    from vkzg import scheme
+    P = per_rank * world
+    lo, hi = vdist.shard_range(P, rank, world)
+    mine = hi - lo
+    tile = lambda a: np.ascontiguousarray(np.broadcast_to(a, (P,) + a.shape))  # noqa: E731
+    cx, ci, zz, yy = tile(cxy), tile(cinf), tile(z), tile(y)
+    d_mine = d_all.repeat(mine, 1) if mine > 0 else None
+    torch.cuda.synchronize(dev)
+
+    def step():
+        if world == 1:
+            return scheme.prove_multiproof_many(ipa, cx, ci, zz, yy, d_mine.data_ptr())
+        return comm.multiproof_many(ipa, cx, ci, zz, yy, d_mine.data_ptr() if d_mine is not None else 0)
+
+    first = step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / reps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    same = len(got) == P and all(g["d"] == want["d"] and g["proof"].as_dict() == want["proof"].as_dict()
+                                 for g in got + first)
+    del d_mine
+    return {"proofs": P, "proofs_per_rank": per_rank, "ms_per_batch": dt * 1e3, "multiproofs_per_s": P / dt,
+            "ms_per_multiproof_amortised": dt / P * 1e3, "same_proofs_as_single": same,
+            "exchange": "vc_multiproof_prove_many_sharded (vc_comm all-gather of finished proofs)" if world > 1
+            else "one GPU: vc_multiproof_prove_many"}
 
 
 def mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, want, P=6):
@@ -641,6 +697,7 @@ def main():
         if not ok:
             raise SystemExit(f"bench: 2^{a.log_n} MSM result check FAILED: {res} vs {want}")
 
+    progress(f"headline: {ms_per_step:.3f} ms per MSM")
     # variable-base sub-line: the same MSM without the per-table shifted window copies
     # (VC_OPT_MSM_SHARED_WINDOWS = 0): plain Pippenger, W bucket sets, no precomputation
     variable = None
@@ -703,8 +760,11 @@ def main():
     madds = terms * n * w_rank
     mad_peak = eng.device_mad_rate()
     pmc = json.load(open(PMC_SUMMARY)) if os.path.exists(PMC_SUMMARY) else None
+    # the committed counters count only if they were taken on this geometry (same n, windows, radix)
+    pmc_match = bool(pmc) and all(pmc.get("config", {}).get(k) == v for k, v in
+                                  (("log_n", a.log_n), ("windows", w_total), ("radix", plan["radix_mul"] << c_bits)))
     insts = None
-    if pmc and world == 1 and pmc.get("config", {}).get("log_n") == a.log_n:
+    if pmc_match and world == 1:
         # the headline's instantiation: limb-form shared-window copies (BT = SW29<..>::Aff)
         key = [k for k in pmc["kernels"] if k.startswith("vk::k_msm_accumulate") and CURVE_TAG[curve] in k]
         key = sorted(key, key=lambda k: "SW29" not in k)
@@ -719,11 +779,10 @@ def main():
             "peak_source": "vc_device_mad_rate: v_mad_u64_u32 issue rate measured live on this GPU",
             "insts_source": os.path.relpath(PMC_SUMMARY, ROOT) if insts else None}
     traffic, traffic_src = None, None
-    if world == 1 and os.path.exists(PMC_SUMMARY):
-        pmc = json.load(open(PMC_SUMMARY))
+    if world == 1 and pmc_match:
         key = sorted([k for k in pmc.get("kernels", {}) if "k_msm_accumulate<vk::SWCurve<vk::BLS381Fq" in k],
                      key=lambda k: "SW29" not in k)
-        if key and pmc.get("config", {}).get("log_n") == a.log_n and curve == "bls12_381":
+        if key and curve == "bls12_381":
             traffic = pmc["kernels"][key[0]].get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
 
@@ -769,6 +828,7 @@ def main():
         "host_scalars": host_line,
     }
 
+    progress("variable-base / host-scalar lines done")
     if not a.no_secondary:
         # config 3: batched width-256 commits (fixed-base tables), batch split across ranks; timed
         # on the c = commit_window table (167 GB at c = 20) and on the deployable c = 16 one (12.9 GB)
@@ -852,20 +912,26 @@ def main():
             }
         cstate["eng"].close()
 
+    progress("commit lines done")
     if not a.no_kzg:
         out["kzg"] = kzg_line(a, rank, world, local, dev, stream)
+        progress("kzg line done")
 
     if not a.no_mp:
-        out["multiproof"] = mp_line(a, rank, world, local, dev, stream)
+        out["multiproof"] = mp_line(a, rank, world, local, dev, stream, comm)
+        progress("multiproof line done")
 
     if rank == 0 and not a.no_ipa:
         out["ipa"] = ipa_line(local, stream)
+        progress("ipa line done")
 
     if rank == 0 and not a.no_verkle:
         out["verkle"] = verkle_line(a, local, stream)
+        progress("verkle line done")
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(curve, n, a.cpu_sample)
+        progress("cpu naive baseline done")
         out["cpu_baselines_other"] = cpu_commit_baselines()
         # the all-core bound beside the 1-core naive port: the CPU share of one GPU on the box
         thr = a.cpu_threads or min(16, os.cpu_count() or 1)

@@ -85,6 +85,23 @@ int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int tabl
                                 const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
                                 vc_ipa_proof* ipa_proof, uint64_t* kzg_proof_xy, uint8_t* kzg_proof_inf,
                                 uint64_t* kzg_y);
+/* Proof-parallel multiproofs over all ranks (the 8-GPU throughput mode of configs[4]): P
+ * independent multiproofs of Q queries each; rank k proves proofs shard_range(P, k, G) end to end
+ * (vc_multiproof_prove_many) and one all-gather of the finished proofs gives every rank all P.
+ * com_xy / com_inf / z / y: all P proofs' queries (host, layouts of vc_multiproof_prove_many);
+ * d_data_mine: this rank's proofs' evaluations [P_k][Q][N] (device); outputs: all P. The
+ * query-sliced single multiproof (vc_multiproof_prove_sharded) is bounded near one GPU's time by
+ * the transcript and finish every rank repeats (at most ~1.15x on 8 GPUs); this mode is not. */
+int vc_multiproof_prove_many_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int table, size_t N, size_t Q, size_t P,
+                                     const void* d_data_mine, const uint64_t* com_xy, const uint8_t* com_inf,
+                                     const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
+                                     vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y);
+/* Its exchange alone: this rank holds proofs shard_range(P, k, G) (at their global positions in
+ * the outputs) and its share's status; afterwards every rank holds all P, or every rank returns
+ * an error (its own status, or VC_E_PEER). ctx may be NULL over a host-callback comm. */
+int vc_multiproof_gather(vc_comm* comm, vc_ctx* ctx, int status, int scheme, size_t N, size_t P, uint64_t* d_xy,
+                         uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf,
+                         uint64_t* kzg_y);
 /* Node::gen_commitment (node.rs:205-277) level by level over all ranks: every rank holds the same
  * tree (the same inserts); the dirty extension nodes and each depth's dirty internal nodes are cut
  * into contiguous rank slices, each rank commits its slice, and one all-gather per level gives

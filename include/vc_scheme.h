@@ -148,6 +148,17 @@ int vc_multiproof_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* z,
 int vc_multiproof_finish(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* z,
                          const void* d_S_parts, int G, vc_transcript* transcript, uint64_t* d_xy, uint8_t* d_inf,
                          vc_ipa_proof* ipa_proof, uint64_t* kzg_proof_xy, uint8_t* kzg_proof_inf, uint64_t* kzg_y);
+/* Proof-parallel: P independent multiproofs of Q queries each on one GPU (a caller proving
+ * several blocks). Per proof the result is vc_multiproof_prove's; the host transcripts run on
+ * worker threads beside the GPU's per-point sums, and the D / E commits and (IPA) the inner
+ * proofs run once for all P proofs (batched). Layouts: com_xy [P][Q][8], com_inf [P][Q],
+ * z [P][Q], y [P][Q][4] (host); d_data [P][Q][N] x 4 u64 canonical (device); outputs d_xy [P][8],
+ * d_inf [P], and ipa_proofs[P] (scheme 0, each with caller-owned round arrays) or
+ * kzg_xy [P][8], kzg_inf [P], kzg_y [P][4] (scheme 1). */
+int vc_multiproof_prove_many(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, size_t P, const void* d_data,
+                             const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                             uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy,
+                             uint8_t* kzg_inf, uint64_t* kzg_y);
 /* IPA-scheme verification (verify_multiproof :178-215 + low_level_verify_ipa) */
 int vc_multiproof_verify_ipa(vc_ctx* ctx, int table, size_t N, size_t Q, const uint64_t* com_xy,
                              const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,

@@ -215,3 +215,81 @@ def test_comm_world_one_and_bad_args():
     h = ctypes.c_void_p()
     assert lib().vc_comm_init_host(0, 2, ctypes.cast(None, vcomm.ALLGATHER_FN), None, ctypes.byref(h)) == -1
     assert lib().vc_comm_init_host(2, 2, vcomm.ALLGATHER_FN(lambda *a: 0), None, ctypes.byref(h)) == -1
+
+
+def _mp_gather_worker(rank, world, port, q):
+    """vc_multiproof_gather (the proof-parallel multiproof exchange, include/vc_comm.h) over the
+    host-callback transport on a gloo group: every rank fills its shard_range(P) proofs, all ranks
+    end with all P; a failed share makes every rank fail (its status / VC_E_PEER)."""
+    import sys
+    sys.path[:0] = [os.path.join(ROOT, "verkle-kzg_amd")]
+    import numpy as np
+    import torch.distributed as dist
+    import vkzg
+    from vkzg import comm as vcomm
+    from vkzg import dist as vdist
+    from vkzg import scheme
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = vcomm.Comm.host(rank, world, vcomm.torch_allgather())
+    ok = True
+    N, P = 8, 5
+
+    def fill(out, p, rng):
+        out.d_xy[p] = rng.integers(0, 1 << 63, size=8, dtype=np.uint64)
+        out.d_inf[p] = p % 2
+        if out.scheme == 0:
+            a = out.arrs[p]
+            a["lxy"][:] = rng.integers(0, 1 << 63, size=a["lxy"].shape, dtype=np.uint64)
+            a["rxy"][:] = rng.integers(0, 1 << 63, size=a["rxy"].shape, dtype=np.uint64)
+            a["linf"][:] = rng.integers(0, 2, size=a["linf"].shape, dtype=np.uint8)
+            a["rinf"][:] = rng.integers(0, 2, size=a["rinf"].shape, dtype=np.uint8)
+            out.bufs[p].tip[:] = [int(v) for v in rng.integers(0, 1 << 63, size=4, dtype=np.uint64)]
+            out.bufs[p].y[:] = [int(v) for v in rng.integers(0, 1 << 63, size=4, dtype=np.uint64)]
+        else:
+            out.kxy[p] = rng.integers(0, 1 << 63, size=8, dtype=np.uint64)
+            out.kinf[p] = 1 - p % 2
+            out.ky[p] = rng.integers(0, 1 << 63, size=4, dtype=np.uint64)
+
+    def snapshot(out, p):
+        s = [out.d_xy[p].tolist(), int(out.d_inf[p])]
+        if out.scheme == 0:
+            a = out.arrs[p]
+            s += [a["lxy"].tolist(), a["rxy"].tolist(), a["linf"].tolist(), a["rinf"].tolist(),
+                  list(out.bufs[p].tip), list(out.bufs[p].y)]
+        else:
+            s += [out.kxy[p].tolist(), int(out.kinf[p]), out.ky[p].tolist()]
+        return s
+
+    for sid in (0, 1):
+        want = scheme.MultiproofSet(sid, N, P)
+        for p in range(P):
+            fill(want, p, np.random.default_rng(100 * sid + p))
+        out = scheme.MultiproofSet(sid, N, P)
+        lo, hi = vdist.shard_range(P, rank, world)
+        for p in range(lo, hi):
+            fill(out, p, np.random.default_rng(100 * sid + p))
+        c.multiproof_gather(out)
+        ok = ok and all(snapshot(out, p) == snapshot(want, p) for p in range(P))
+        # rank 1's share failed (VC_E_OOM): it returns that, its peer VC_E_PEER -- nobody hangs
+        try:
+            c.multiproof_gather(scheme.MultiproofSet(sid, N, P), status=-3 if rank == 1 else 0)
+            ok = False
+        except vkzg.VCError as ex:
+            ok = ok and ex.status == (-3 if rank == 1 else -10)
+    c.close()
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_multiproof_gather_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(60)
+    assert sorted(res) == [(0, True), (1, True)]

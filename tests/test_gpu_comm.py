@@ -196,6 +196,71 @@ def test_verkle_commitment_sharded():
         assert all(r == want for r in res)
 
 
+def _many_queries(vc, N, P, Q, seed):
+    """P query sets of Q random width-N datasets: [P][Q] host arrays, the [P][Q][N] evaluations
+    and the per-proof query lists of scheme.prove_multiproof"""
+    from vkzg import scheme
+    rng = random.Random(seed)
+    sets, data = [], []
+    for p in range(P):
+        qs = []
+        for _ in range(Q):
+            d = scheme.LagrangeBasis([rng.randrange(scheme.R_BN254) for _ in range(N)])
+            zq = rng.randrange(N)
+            qs.append((d, vc.commit(d), zq, d.evals[zq]))
+        sets.append(qs)
+    arrs = [scheme._queries(qs, N) for qs in sets]
+    cxy = np.stack([a[2] for a in arrs])
+    cinf = np.stack([a[3] for a in arrs])
+    z = np.stack([a[4] for a in arrs])
+    y = np.stack([a[5] for a in arrs])
+    data = np.concatenate([a[1] for a in arrs])
+    return sets, cxy, cinf, z, y, data
+
+
+@pytest.mark.parametrize("name", ["ipa", "kzg"])
+def test_multiproof_many_and_proof_parallel_ranks(name):
+    """vc_multiproof_prove_many (P proofs, batched D / E commits and inner proofs) == P separate
+    vc_multiproof_prove calls; vc_multiproof_prove_many_sharded over G = 2, 3 thread-ranks (each
+    proving its shard_range(P) proofs, one all-gather of the proofs) == the same proofs."""
+    import torch
+    import vkzg
+    from vkzg import dist as vdist
+    from vkzg import scheme
+    crs = [P(h) for h in _golden("ipa_crs_bn254.json")["points"]]
+    N, NP, Q = 32, 5, 24
+
+    def make(e):
+        return scheme.IPA(e, N, crs[:N + 1]) if name == "ipa" else scheme.KZG(e, N)
+
+    def norm(mp):
+        pr = mp["proof"]
+        return (mp["d"], pr.as_dict() if name == "ipa" else pr)
+
+    e = vkzg.Engine("bn254")
+    try:
+        vc = make(e)
+        sets, cxy, cinf, z, y, data = _many_queries(vc, N, NP, Q, 9)
+        want = [norm(scheme.prove_multiproof(vc, qs)) for qs in sets]
+        d = torch.from_numpy(data.view(np.int64).copy()).cuda()
+        torch.cuda.synchronize()
+        got = [norm(mp) for mp in scheme.prove_multiproof_many(vc, cxy, cinf, z, y, d.data_ptr())]
+        assert got == want
+    finally:
+        e.close()
+
+    def body(k, comm, eng):
+        v = make(eng)
+        lo, hi = vdist.shard_range(NP, comm.rank, comm.world)
+        dm = torch.from_numpy(data[lo * Q * N:hi * Q * N].view(np.int64).copy()).cuda() if hi > lo else None
+        torch.cuda.synchronize()
+        return [norm(mp) for mp in comm.multiproof_many(v, cxy, cinf, z, y, dm.data_ptr() if dm is not None else 0)]
+
+    for G in (2, 3):
+        for res in run_ranks(G, "bn254", body):
+            assert res == want
+
+
 @pytest.mark.parametrize("what", ["msm", "msm_batch", "kzg", "verkle"])
 def test_sharded_failure_is_group_wide(what):
     """SPMD failure (include/vc_comm.h): rank 1's share fails (an unknown table id), yet it enters

@@ -351,6 +351,96 @@ int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int tabl
     return st;
 }
 
+// ---- proof-parallel multiproofs: rank k proves proofs shard_range(P, k, G) end to end
+// (vc_multiproof_prove_many), one all-gather of the finished proofs (D, and the IPA proof or the
+// KZG (proof, y)) gives every rank all P. The query-sliced single multiproof above cannot go
+// much below one GPU's time: every rank repeats the serial host transcript (~2.7 ms at Q = 2^16)
+// and the finish (~1.8 ms), so it scales at most ~1.15x on 8 GPUs; independent proofs scale with
+// the ranks.
+int vc_multiproof_gather(vc_comm* comm, vc_ctx* ctx, int status, int scheme, size_t N, size_t P, uint64_t* d_xy,
+                         uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf,
+                         uint64_t* kzg_y) {
+    if (!comm || (comm->nccl && !valid(comm, ctx)) || (scheme != 0 && scheme != 1) || N == 0 || (N & (N - 1)))
+        return VC_E_INVALID;
+    if (P && (!d_xy || !d_inf || (scheme == 0 && !ipa_proofs) || (scheme == 1 && (!kzg_xy || !kzg_inf || !kzg_y))))
+        return VC_E_INVALID;
+    size_t K = 0;
+    while ((size_t(1) << K) < N) K++;
+    const size_t rec = scheme == 0 ? 9 + 18 * K + 8 : 9 + 13;  // u64 words per proof
+    size_t lo, hi;
+    vk::shard_range(P, comm->rank, comm->world, &lo, &hi);
+    const size_t bmax = (P + comm->world - 1) / comm->world, slot = 1 + bmax * rec;
+    std::vector<uint64_t> send(slot, 0), recv(slot * comm->world);
+    send[0] = (uint64_t)(uint32_t)status;
+    for (size_t p = lo; status == VC_OK && p < hi; p++) {
+        uint64_t* r = &send[1 + (p - lo) * rec];
+        memcpy(r, d_xy + p * 8, 64);
+        r[8] = d_inf[p];
+        if (scheme == 0) {
+            const vc_ipa_proof& pr = ipa_proofs[p];
+            for (size_t k = 0; k < K; k++) {
+                memcpy(r + 9 + 18 * k, pr.l_xy + 8 * k, 64);
+                r[9 + 18 * k + 8] = pr.l_inf[k];
+                memcpy(r + 9 + 18 * k + 9, pr.r_xy + 8 * k, 64);
+                r[9 + 18 * k + 17] = pr.r_inf[k];
+            }
+            memcpy(r + 9 + 18 * K, pr.tip, 32);
+            memcpy(r + 9 + 18 * K + 4, pr.y, 32);
+        } else {
+            memcpy(r + 9, kzg_xy + p * 8, 64);
+            r[17] = kzg_inf[p];
+            memcpy(r + 18, kzg_y + p * 4, 32);
+        }
+    }
+    VK_TRY(comm_allgather_host(comm, ctx, send.data(), send.size() * 8, recv.data()));
+    VK_TRY(agree_in(comm, status, reinterpret_cast<const uint8_t*>(recv.data()), slot * 8));
+    for (int k = 0; k < comm->world; k++) {
+        size_t a, e;
+        vk::shard_range(P, k, comm->world, &a, &e);
+        for (size_t p = a; p < e; p++) {
+            const uint64_t* r = &recv[(size_t)k * slot + 1 + (p - a) * rec];
+            memcpy(d_xy + p * 8, r, 64);
+            d_inf[p] = (uint8_t)r[8];
+            if (scheme == 0) {
+                vc_ipa_proof& pr = ipa_proofs[p];
+                if (pr.rounds < K || !pr.l_xy || !pr.r_xy || !pr.l_inf || !pr.r_inf) return VC_E_INVALID;
+                pr.rounds = K;
+                for (size_t j = 0; j < K; j++) {
+                    memcpy(pr.l_xy + 8 * j, r + 9 + 18 * j, 64);
+                    pr.l_inf[j] = (uint8_t)r[9 + 18 * j + 8];
+                    memcpy(pr.r_xy + 8 * j, r + 9 + 18 * j + 9, 64);
+                    pr.r_inf[j] = (uint8_t)r[9 + 18 * j + 17];
+                }
+                memcpy(pr.tip, r + 9 + 18 * K, 32);
+                memcpy(pr.y, r + 9 + 18 * K + 4, 32);
+            } else {
+                memcpy(kzg_xy + p * 8, r + 9, 64);
+                kzg_inf[p] = (uint8_t)r[17];
+                memcpy(kzg_y + p * 4, r + 18, 32);
+            }
+        }
+    }
+    return VC_OK;
+}
+
+int vc_multiproof_prove_many_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int table, size_t N, size_t Q, size_t P,
+                                     const void* d_data_mine, const uint64_t* com_xy, const uint8_t* com_inf,
+                                     const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
+                                     vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!valid(comm, ctx)) return VC_E_INVALID;
+    size_t lo, hi;
+    vk::shard_range(P, comm->rank, comm->world, &lo, &hi);
+    const int st = hi > lo ? vc_multiproof_prove_many(ctx, scheme, table, N, Q, hi - lo, d_data_mine,
+                                                      com_xy ? com_xy + lo * Q * 8 : nullptr,
+                                                      com_inf ? com_inf + lo * Q : nullptr, z ? z + lo * Q : nullptr,
+                                                      y ? y + lo * Q * 4 : nullptr, d_xy ? d_xy + lo * 8 : nullptr,
+                                                      d_inf ? d_inf + lo : nullptr, ipa_proofs ? ipa_proofs + lo : nullptr,
+                                                      kzg_xy ? kzg_xy + lo * 8 : nullptr, kzg_inf ? kzg_inf + lo : nullptr,
+                                                      kzg_y ? kzg_y + lo * 4 : nullptr)
+                           : VC_OK;
+    return vc_multiproof_gather(comm, ctx, st, scheme, N, P, d_xy, d_inf, ipa_proofs, kzg_xy, kzg_inf, kzg_y);
+}
+
 int vc_verkle_commitment_sharded(vc_ctx* ctx, vc_comm* comm, int table, vc_verkle* tree, uint64_t* out_xy,
                                  uint8_t* out_inf) {
     if (!valid(comm, ctx) || !tree || !out_xy || !out_inf) return VC_E_INVALID;

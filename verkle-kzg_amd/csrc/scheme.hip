@@ -12,7 +12,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -1338,6 +1342,156 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
     return st;
 }
 
+// P independent multiproofs of Q queries each (same N, one CRS / SRS) on one GPU, proof-parallel:
+// the host transcripts (records + serial SHA-256, the part that bounds one proof) run on worker
+// threads while the GPU accumulates every proof whose challenge r is ready; each later stage then
+// runs ONCE for all P proofs -- one batched D commit, one batched E commit and, for IPA, one
+// batched inner proof (its 8 latency-bound rounds shared by the P proofs) -- instead of P times.
+// Each proof is the one mp_prove gives for its queries. Arrays are [P][Q] (com_xy [P][Q][8],
+// y [P][Q][4]); d_data [P][Q][N] canonical on the device; outputs [P].
+static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, size_t P, const uint8_t* d_data,
+                         const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                         uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy,
+                         uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
+    if (P == 0) return VC_OK;
+    struct Begun {
+        vc_transcript* tr = nullptr;
+        Fr r;
+        std::vector<uint32_t> zval;
+        int st = VC_E_INVALID;
+        bool done = false;
+    };
+    std::vector<Begun> B(P);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<size_t> next{0};
+    const unsigned T = (unsigned)std::min<size_t>(P, std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)));
+    std::vector<std::thread> workers;
+    for (unsigned k = 0; k < T; k++)
+        workers.emplace_back([&] {
+            for (size_t p; (p = next.fetch_add(1)) < P;) {
+                Begun b;
+                b.st = mp_begin(N, Q, com_xy + p * Q * 8, com_inf + p * Q, z + p * Q, y + p * Q * 4, &b.tr, &b.r);
+                if (b.st == VC_OK) b.st = mp_points(N, Q, z + p * Q, &b.zval);
+                std::lock_guard<std::mutex> lk(mu);
+                B[p] = std::move(b);
+                B[p].done = true;
+                cv.notify_all();
+            }
+        });
+    auto free_all = [&] {
+        for (auto& w : workers) w.join();
+        workers.clear();
+        for (auto& b : B)
+            if (b.tr) vc_transcript_free(b.tr);
+    };
+    // phase 2: per-point sums of each proof as soon as its transcript is done (GPU, in order)
+    std::vector<std::unique_ptr<DevBuf>> S(P);
+    int st = VC_OK;
+    for (size_t p = 0; p < P && st == VC_OK; p++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return B[p].done; });
+        }
+        if ((st = B[p].st) != VC_OK) break;
+        S[p] = std::make_unique<DevBuf>(ctx);
+        st = S[p]->ensure(B[p].zval.size() * N * 32);
+        if (st == VC_OK)
+            st = mp_accumulate(ctx, N, Q, d_data + p * Q * N * 32, z + p * Q, B[p].r, 0, B[p].zval, S[p]->p);
+    }
+    for (auto& w : workers) w.join();
+    workers.clear();
+    if (st != VC_OK) {
+        free_all();
+        return st;
+    }
+    // phase 3: quotients and g of every proof, then D for all P in one batched commit
+    hipStream_t hs = ctx->stream;
+    const fe<F>*pw = nullptr, *pwi = nullptr, *inv1 = nullptr;
+    st = domain_tables<F>(ctx, bn254_group_gen(N), N, &pw, &pwi, &inv1);
+    std::vector<std::unique_ptr<DevBuf>> Sm(P), Qb(P), zv(P), it(P);
+    DevBuf d_g(ctx), d_h(ctx);
+    if (st == VC_OK) st = d_g.ensure(P * N * 32);
+    if (st == VC_OK) st = d_h.ensure(P * N * 32);
+    for (size_t p = 0; p < P && st == VC_OK; p++) {
+        const uint32_t Z = (uint32_t)B[p].zval.size();
+        Sm[p] = std::make_unique<DevBuf>(ctx);
+        Qb[p] = std::make_unique<DevBuf>(ctx);
+        zv[p] = std::make_unique<DevBuf>(ctx);
+        it[p] = std::make_unique<DevBuf>(ctx);
+        if ((st = Sm[p]->ensure((size_t)Z * N * 32)) != VC_OK || (st = Qb[p]->ensure((size_t)Z * N * 32)) != VC_OK ||
+            (st = zv[p]->ensure(Z * 4)) != VC_OK || (st = it[p]->ensure(Z * 32)) != VC_OK)
+            break;
+        auto launch = [&]() -> int {
+            VK_CHECK_HIP(hipMemcpyAsync(zv[p]->p, B[p].zval.data(), Z * 4, hipMemcpyHostToDevice, hs));
+            VK_LAUNCH(ctx, "mp_sum_parts", k_mp_sum_parts, ((size_t)Z * N + 255) / 256, 256, 0, S[p]->as<Fr>(), 1,
+                      (size_t)Z * N, Sm[p]->as<Fr>());
+            VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, Sm[p]->as<fe<F>>(), inv1, pw, pwi, zv[p]->as<uint32_t>(), N,
+                      Qb[p]->as<fe<F>>());
+            VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
+                      (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N);
+            return VC_OK;
+        };
+        st = launch();
+    }
+    std::vector<Fr> g(P * N), h(P * N);
+    std::vector<uint64_t> dxy(P * 8), exy(P * 8);
+    std::vector<uint8_t> dinf(P), einf(P);
+    std::vector<Fr> tt(P);
+    if (st == VC_OK && hipMemcpyAsync(g.data(), d_g.p, P * N * 32, hipMemcpyDeviceToHost, hs) != hipSuccess) st = VC_E_HIP;
+    if (st == VC_OK && hipStreamSynchronize(hs) != hipSuccess) st = VC_E_HIP;
+    if (st == VC_OK) st = commit_batch(ctx, t, N, g.data(), P, dxy.data(), dinf.data());
+    // t of every proof, then h and E for all P
+    for (size_t p = 0; p < P && st == VC_OK; p++) {
+        transcript_append_point(B[p].tr, &dxy[p * 8], dinf[p], "D");
+        tt[p] = transcript_digest(B[p].tr, "t");
+        const std::vector<Fr> invs = invert_domain_at(tt[p], N);  // 1/(t - z), z an integer (utils.rs:57-62)
+        const uint32_t Z = (uint32_t)B[p].zval.size();
+        std::vector<Fr> invz(Z);
+        for (uint32_t k = 0; k < Z; k++) invz[k] = invs[B[p].zval[k]];
+        if (hipMemcpyAsync(it[p]->p, invz.data(), Z * 32, hipMemcpyHostToDevice, hs) != hipSuccess) {
+            st = VC_E_HIP;
+            break;
+        }
+        auto launch = [&]() -> int {
+            VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
+                      it[p]->as<fe<F>>(), N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N);
+            return VC_OK;
+        };
+        st = launch();
+        if (st == VC_OK && hipStreamSynchronize(hs) != hipSuccess) st = VC_E_HIP;  // invz dies here
+    }
+    if (st == VC_OK && hipMemcpyAsync(h.data(), d_h.p, P * N * 32, hipMemcpyDeviceToHost, hs) != hipSuccess) st = VC_E_HIP;
+    if (st == VC_OK && hipStreamSynchronize(hs) != hipSuccess) st = VC_E_HIP;
+    if (st == VC_OK) st = commit_batch(ctx, t, N, h.data(), P, exy.data(), einf.data());
+    std::vector<std::vector<Fr>> hmg(P, std::vector<Fr>(N));
+    std::vector<Acc> mc(P);
+    for (size_t p = 0; p < P && st == VC_OK; p++) {
+        transcript_append_point(B[p].tr, &exy[p * 8], einf[p], "E");
+        for (size_t k = 0; k < N; k++) hmg[p][k] = fe_sub<F>(h[p * N + k], g[p * N + k]);
+        mc[p] = C::add(acc_of(&exy[p * 8], einf[p]), C::neg(acc_of(&dxy[p * 8], dinf[p])));
+        memcpy(d_xy + p * 8, &dxy[p * 8], 64);
+        d_inf[p] = dinf[p];
+    }
+    // the inner proofs: one batched IPA (each proof with its own transcript), or P KZG openings
+    if (st == VC_OK && scheme == 0) {
+        std::vector<vc_transcript*> trs(P);
+        for (size_t p = 0; p < P; p++) trs[p] = B[p].tr;
+        st = ipa_prove_impl(ctx, t, N, hmg, mc, tt, trs.data(), ipa_proofs);
+    }
+    for (size_t p = 0; st == VC_OK && scheme == 1 && p < P; p++) {
+        std::vector<uint64_t> ev(N * 4);
+        for (size_t k = 0; k < N; k++) canon_of(hmg[p][k], &ev[4 * k]);
+        uint64_t tc[4];
+        canon_of(tt[p], tc);
+        st = kzg_prove_t<BN254G1, BN254Fr>(ctx, t, N, ev.data(), N, tc, kzg_xy + p * 8, kzg_inf + p, kzg_y + p * 4,
+                                          nullptr);
+    }
+    free_all();
+    return st;
+}
+
 // E - D and t of verify_multiproof (:178-215); tr returned positioned after "E"
 static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                     const uint64_t* y, const uint64_t* d_xy, uint8_t d_inf, Acc* claim, Fr* t_out,
@@ -1391,6 +1545,23 @@ int vc_multiproof_prove(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, 
     Table* t = ctx->table(table);
     if (!t) return VC_E_TABLE;
     return mp_prove(ctx, scheme, t, N, Q, data, com_xy, com_inf, z, y, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf, kzg_y);
+}
+
+int vc_multiproof_prove_many(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, size_t P, const void* d_data,
+                             const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                             uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy,
+                             uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!ctx || (P && (!d_data || !com_xy || !com_inf || !z || !y || !d_xy || !d_inf)) ||
+        ctx->curve != VC_CURVE_BN254 || (scheme != 0 && scheme != 1))
+        return VC_E_INVALID;
+    for (size_t p = 0; scheme == 0 && p < P; p++)
+        if (!ipa_proofs || !proof_ok(&ipa_proofs[p])) return VC_E_INVALID;
+    if (scheme == 1 && P && (!kzg_xy || !kzg_inf || !kzg_y)) return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    return mp_prove_many(ctx, scheme, t, N, Q, P, static_cast<const uint8_t*>(d_data), com_xy, com_inf, z, y, d_xy,
+                         d_inf, ipa_proofs, kzg_xy, kzg_inf, kzg_y);
 }
 
 int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,

@@ -50,7 +50,9 @@ def main(d, out):
         lines = [ln for ln in open(f"{d}/bench_trace.json") if ln.startswith("{")]
         bench = json.loads(lines[-1])
         npts = bench["config"]["n_points"]
-        config = {"log_n": npts.bit_length() - 1, "curve": bench["config"]["curve"], "n_gpus": bench["n_gpus"]}
+        config = {"log_n": npts.bit_length() - 1, "curve": bench["config"]["curve"], "n_gpus": bench["n_gpus"],
+                  "windows": bench["config"].get("windows"), "radix": bench["config"].get("radix"),
+                  "terms_per_point": bench["config"].get("terms_per_point")}
     except (OSError, IndexError, KeyError, ValueError):
         pass
     with open(out, "w") as f:

@@ -83,6 +83,8 @@ SIGNATURES = {
     "vc_kzg_prove_device_part": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, c_int, c_int, P, P]),
     "vc_multiproof_prove": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P, P, P, P, P, P]),
     "vc_multiproof_begin": (c_int, [c_size_t, c_size_t, P, P, P, P, P, P, P]),
+    "vc_multiproof_prove_many": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, c_size_t, c_void_p, P, P, P, P,
+                                         P, P, P, P, P, P]),
     "vc_multiproof_accumulate": (c_int, [c_void_p, c_size_t, c_size_t, P, c_size_t, c_size_t, P, P, P]),
     "vc_multiproof_finish": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, c_int, c_void_p, P, P, P, P,
                                      P, P]),
@@ -104,6 +106,9 @@ SIGNATURES = {
     "vc_multiproof_prove_sharded": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P,
                                             P, P, P, P, P]),
     "vc_verkle_commitment_sharded": (c_int, [c_void_p, c_void_p, c_int, c_void_p, P, P]),
+    "vc_multiproof_prove_many_sharded": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, c_size_t,
+                                                 c_void_p, P, P, P, P, P, P, P, P, P, P]),
+    "vc_multiproof_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P]),
 }
 
 _lib = None

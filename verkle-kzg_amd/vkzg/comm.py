@@ -160,6 +160,28 @@ class Comm:
               "vc_multiproof_prove_sharded")
         return {"proof": {"proof": scheme._pt(kxy, kinf[0]), "y": limbs_to_int(ky)}, "d": scheme._pt(dxy, dinf[0])}
 
+    def multiproof_many(self, vc, cxy, cinf, z, y, d_data_mine_ptr):
+        """proof-parallel multiproofs over the ranks (vc_multiproof_prove_many_sharded): all P
+        proofs' queries on the host ([P][Q] layouts), this rank's proofs' evaluations at
+        d_data_mine_ptr ([P_k][Q][N], device); every rank returns all P proofs."""
+        from . import scheme
+        ipa = isinstance(vc, scheme.IPA)
+        N = vc.N if ipa else vc.size
+        P, Q = z.shape
+        out = scheme.MultiproofSet(0 if ipa else 1, N, P)
+        cxy, cinf, z, y = (np.ascontiguousarray(a) for a in (cxy, cinf, z, y))
+        check(lib().vc_multiproof_prove_many_sharded(vc.engine.h, self.h, out.scheme, vc.table, N, Q, P,
+                                                     ctypes.c_void_p(d_data_mine_ptr), _p(cxy), _p(cinf), _p(z),
+                                                     _p(y), *out.args()), "vc_multiproof_prove_many_sharded")
+        return out.proofs()
+
+    def multiproof_gather(self, out, status=0, engine=None):
+        """the proof-parallel exchange alone (vc_multiproof_gather) on a scheme.MultiproofSet whose
+        shard_range(P, rank, world) entries this rank filled; status = this rank's share's status"""
+        check(lib().vc_multiproof_gather(self.h, engine.h if engine is not None else None, status, out.scheme, out.N,
+                                         out.P, *out.args()), "vc_multiproof_gather")
+        return out
+
     def verkle_commitment(self, tree, engine, table):
         """root commitment of a verkle tree every rank holds identically; each level's dirty
         nodes are cut into rank slices and all-gathered."""

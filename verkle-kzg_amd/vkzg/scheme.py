@@ -386,6 +386,58 @@ def verify_multiproof(vc, vqueries, mp):
     return {"commitment": _pt(oxy, oinf[0]), "t": limbs_to_int(t)}
 
 
+class MultiproofSet:
+    """Output buffers of P multiproofs (vc_multiproof_prove_many / _sharded / _gather): D points,
+    and P IPA proofs (scheme 0) or P KZG (proof, y) pairs (scheme 1)."""
+
+    def __init__(self, scheme_id, N, P):
+        self.scheme, self.N, self.P = scheme_id, N, P
+        self.d_xy = np.zeros((max(P, 1), 8), dtype=np.uint64)
+        self.d_inf = np.zeros(max(P, 1), dtype=np.uint8)
+        self.bufs, self.arrs = None, []
+        self.kxy = self.kinf = self.ky = None
+        if scheme_id == 0:
+            self.bufs = (_ProofBuf * max(P, 1))()
+            for p in range(P):
+                b, arrs = IPAProof._alloc(_log2(N))
+                self.bufs[p] = b
+                self.arrs.append(arrs)
+        else:
+            self.kxy = np.zeros((max(P, 1), 8), dtype=np.uint64)
+            self.kinf = np.zeros(max(P, 1), dtype=np.uint8)
+            self.ky = np.zeros((max(P, 1), 4), dtype=np.uint64)
+
+    def args(self):
+        """(d_xy, d_inf, ipa_proofs, kzg_xy, kzg_inf, kzg_y) pointers of the C ABI"""
+        if self.scheme == 0:
+            return _p(self.d_xy), _p(self.d_inf), ctypes.cast(self.bufs, ctypes.c_void_p), None, None, None
+        return _p(self.d_xy), _p(self.d_inf), None, _p(self.kxy), _p(self.kinf), _p(self.ky)
+
+    def proofs(self):
+        out = []
+        for p in range(self.P):
+            if self.scheme == 0:
+                pr = IPAProof._from(self.bufs[p], self.arrs[p])
+            else:
+                pr = {"proof": _pt(self.kxy[p], self.kinf[p]), "y": limbs_to_int(self.ky[p])}
+            out.append({"proof": pr, "d": _pt(self.d_xy[p], self.d_inf[p])})
+        return out
+
+
+def prove_multiproof_many(vc, cxy, cinf, z, y, d_data_ptr):
+    """P independent multiproofs at once on one GPU (vc_multiproof_prove_many): cxy [P][Q][8],
+    cinf [P][Q], z [P][Q], y [P][Q][4] host arrays; d_data_ptr -> [P][Q][N] canonical evaluations
+    on the device. Returns P {"proof", "d"} as prove_multiproof does."""
+    ipa = isinstance(vc, IPA)
+    N = vc.N if ipa else vc.size
+    P, Q = z.shape
+    out = MultiproofSet(0 if ipa else 1, N, P)
+    cxy, cinf, z, y = (np.ascontiguousarray(a) for a in (cxy, cinf, z, y))
+    check(lib().vc_multiproof_prove_many(vc.engine.h, out.scheme, vc.table, N, Q, P, ctypes.c_void_p(d_data_ptr),
+                                         _p(cxy), _p(cinf), _p(z), _p(y), *out.args()), "multiproof_prove_many")
+    return out.proofs()
+
+
 # ---------------------------------------------------------------- sharded multiproof (SURVEY 8(e) C5)
 def multiproof_begin(N, cxy, cinf, z, y):
     """Phase 1 (host, every rank): transcript over all queries -> (transcript handle, r limbs, rows)."""
