@@ -231,6 +231,26 @@ def kzg_line(a, rank, world, local, dev, stream):
             if cnt:
                 qk[k] = round(ms / cnt, 4)
         res[name] = {"ms_per_commit_open": dt * 1e3, "quotient_kernels_ms": qk}
+        if world == 1:  # commit + open as one call: both SRS MSMs in one batched pipeline
+            pt = vkzg.ints_to_limbs([point])[0].copy()
+            bufs = [np.zeros(12, dtype=np.uint64), np.zeros(1, dtype=np.uint8), np.zeros(12, dtype=np.uint64),
+                    np.zeros(1, dtype=np.uint8), np.zeros(4, dtype=np.uint64)]
+            P = lambda x: ctypes.c_void_p(x.ctypes.data)  # noqa: E731
+
+            def fused():
+                check(lib().vc_kzg_commit_prove_device(keng.h, tid, d, ctypes.c_void_p(d_ev.data_ptr()), d, P(pt),
+                                                       *[P(b) for b in bufs]), "vc_kzg_commit_prove_device")
+            fused()
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                fused()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            com_s, prf_s = step(point)
+            same = (vkzg.arrays_to_points("bls12_381", bufs[0][None, :], bufs[1])[0] ==
+                    vkzg.arrays_to_points("bls12_381", np.asarray(com_s[0])[None, :], np.array([com_s[1]], np.uint8))[0])
+            res[name]["fused_ms_median"] = float(np.median(ts))
+            res[name]["fused_same_commitment"] = bool(same)
     keng.close()
     fused_bytes = d * (96 + 32) + 2 * 96  # SURVEY 8(d) C4 fused minimum
     return {"workload": f"KZG commit + open, d = 2^{a.kzg_log_d}, BLS12-381 (configs[3]), MSMs window-split "

@@ -98,6 +98,13 @@ int vc_msm(vc_ctx* ctx, int table_id, size_t offset, const uint64_t* scalars, si
 /* Same with scalars already resident in device memory (4 u64 per scalar). */
 int vc_msm_device(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars, size_t n,
                   int mont, uint64_t* out_xy, uint8_t* out_inf);
+/* `count` MSMs over one base table (the first n bases, n <= its size): scalar set k at d_scalars[k]
+ * (device, 4 u64 each; mont[k] as vc_msm's flag) -> out_xy[k], out_inf[k] (canonical affine).
+ * Same results as count vc_msm_device calls; when they cover a whole BLS12-381 table of >= 2^18
+ * points they run as ONE pipeline (one sort into count bucket sets, one accumulate, one
+ * reduction), so the latency-bound tail is paid once. */
+int vc_msm_device_many(vc_ctx* ctx, int table_id, const void* const* d_scalars, const int* mont, size_t n,
+                       size_t count, uint64_t* out_xy, uint8_t* out_inf);
 /* Partial MSM for sharding across GPUs: returns the un-normalised accumulator (projective,
  * curve-specific words, see vc_point_words) so ranks can all-gather and add. */
 int vc_point_words(int curve);

@@ -98,6 +98,12 @@ int vc_kzg_prove(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, siz
 /* same with the evaluations already in device memory (canonical, 4 u64 each) */
 int vc_kzg_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
                         const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y);
+/* commit + prove_point in one call (configs[3]'s unit): C = commit(evals) (kzg/mod.rs:126-134) and
+ * the proof at `point` as vc_kzg_prove_device; both MSMs over the SRS run as one batched
+ * pipeline (vc_msm_device_many). */
+int vc_kzg_commit_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
+                               const uint64_t* point, uint64_t* com_xy, uint8_t* com_inf, uint64_t* proof_xy,
+                               uint8_t* proof_inf, uint64_t* y);
 /* multi-GPU open: the quotient (every part computes it; it is elementwise and ~10 % of the
  * MSM) and window slice `part` of `parts` of the proof MSM as an un-normalised accumulator;
  * the parts' accumulators sum (vc_partials_sum) to the proof */

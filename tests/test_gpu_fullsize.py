@@ -254,6 +254,49 @@ def test_kzg_commit_open_2e20_trapdoor(where):
             assert yv == vkzg.limbs_to_int(ev[m])
         proof = _pt("bls12_381", pxy, pinf[0])
         assert C.mul(proof, (100 - zval) % C.r) == C.add(com, C.neg(C.mul(C.g, yv)))
+        # the fused commit + open (both MSMs in one batched pipeline) gives the same C, pi, y
+        cxy = np.zeros(12, dtype=np.uint64)
+        cinf = np.zeros(1, dtype=np.uint8)
+        pxy2 = np.zeros(12, dtype=np.uint64)
+        pinf2 = np.zeros(1, dtype=np.uint8)
+        y2 = np.zeros(4, dtype=np.uint64)
+        check(lib().vc_kzg_commit_prove_device(e.h, tid, d, ctypes.c_void_p(d_ev.data_ptr()), d, P(pt), P(cxy),
+                                               P(cinf), P(pxy2), P(pinf2), P(y2)), "vc_kzg_commit_prove_device")
+        assert _pt("bls12_381", cxy, cinf[0]) == com
+        assert _pt("bls12_381", pxy2, pinf2[0]) == proof and vkzg.limbs_to_int(y2) == yv
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("curve,n", [("bls12_381", 1 << 18), ("bls12_381", 5000), ("bn254", 1 << 12)])
+def test_msm_device_many(curve, n):
+    """vc_msm_device_many == separate vc_msm_device calls: K = 3 scalar sets (one batched pipeline
+    into 3 bucket sets on the BLS12-381 radix geometry, a loop elsewhere), one set Montgomery, one
+    all-equal (the long-chain fix-up inside the batch), by linearity on P_i = s_i G at 2^18."""
+    import torch
+    import vkzg
+    from pyoracle.curves import CURVES
+    C = CURVES[curve]
+    e = vkzg.Engine(curve)
+    try:
+        tid = e.random_bases(n, seed=31)
+        rng = np.random.default_rng(32)
+        sets = [vkzg.random_scalars(curve, n, rng) for _ in range(3)]
+        sets[2] = np.repeat(sets[2][:1], n, axis=0)
+        d = [torch.from_numpy(s.view(np.int64).copy()).cuda() for s in sets]
+        # set 1 in arkworks Montgomery form: x R mod r (R = 2^256)
+        R = (1 << 256) % C.r
+        mont1 = vkzg.ints_to_limbs([vkzg.limbs_to_int(x) * R % C.r for x in sets[1]])
+        d[1] = torch.from_numpy(np.ascontiguousarray(mont1).view(np.int64).copy()).cuda()
+        torch.cuda.synchronize()
+        got = e.msm_device_many(tid, [x.data_ptr() for x in d], n, mont=[False, True, False])
+        for k in range(3):
+            want = e.msm_device(tid, d[k].data_ptr(), n, mont=(k == 1))
+            assert got[k][1] == want[1] and np.array_equal(got[k][0], want[0]), k
+        if n == 1 << 18:
+            assert e.msm_last_plan()["radix_mul"] == 5
+            s = vkzg.random_base_scalars(curve, 31, n)
+            assert _pt(curve, *got[0]) == C.mul(C.g, vkzg.dot_mod(sets[0], s, C.r))
     finally:
         e.close()
 

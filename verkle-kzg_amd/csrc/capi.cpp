@@ -374,6 +374,25 @@ int vc_msm_device(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n
     return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
 }
 
+int vc_msm_device_many(vc_ctx* ctx, int id, const void* const* d_scalars, const int* mont, size_t n, size_t count,
+                       uint64_t* out_xy, uint8_t* out_inf) {
+    if (!ctx || (count && (!d_scalars || !mont || !out_xy || !out_inf))) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    if (n > t->n) return VC_E_RANGE;
+    for (size_t k = 0; k < count; k++)
+        if (n > 0 && !d_scalars[k]) return VC_E_INVALID;
+    if (count == 0) return VC_OK;
+    const int words = vk::point_words(ctx->curve);
+    std::vector<uint32_t> acc((size_t)words * count);
+    VK_TRY(vk::msm_run_many(ctx, t, d_scalars, mont, n, count, acc.data()));
+    const int NL = vk::aff_limbs64(ctx->curve);
+    for (size_t k = 0; k < count; k++)
+        VK_TRY(vk::acc_to_affine(ctx->curve, acc.data() + k * words, out_xy + k * 2 * NL, out_inf + k));
+    return VC_OK;
+}
+
 int vc_msm(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n, int mont,
            uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || !out_xy || !out_inf || (n > 0 && !scalars)) return VC_E_INVALID;

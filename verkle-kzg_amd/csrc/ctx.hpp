@@ -219,6 +219,10 @@ int device_mad_rate(vc_ctx* ctx, double* tera_per_s);
 int msm_windows(int curve, size_t n, int* c, int* W, int* terms);
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
             uint32_t* out_acc, int part = 0, int parts = 1);
+// K MSMs over the whole table t (scalar set k at d_scalars[k], Montgomery flag mont[k]) -> K
+// accumulators; one batched pipeline where the geometry allows (msm.hip msm_run_many_t)
+int msm_run_many(vc_ctx* ctx, Table* t, const void* const* d_scalars, const int* mont, size_t n, size_t K,
+                 uint32_t* out_accs);
 int acc_to_affine(int curve, const uint32_t* acc, uint64_t* out_xy, uint8_t* out_inf);
 // n accumulators with one field inversion (Montgomery's trick); same outputs as acc_to_affine
 int acc_to_affine_batch(int curve, const uint32_t* accs, size_t n, uint64_t* out_xy, uint8_t* out_inf);

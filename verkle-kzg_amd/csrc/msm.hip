@@ -167,17 +167,19 @@ __device__ __forceinline__ uint32_t sort_slot(uint32_t b, uint32_t nblk) {
 
 template <class Src>
 __global__ void __launch_bounds__(1024) k_sort_hist(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
-                                                   uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t chunk,
-                                                   uint32_t* __restrict__ counts) {
+                                                   uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t wps,
+                                                   uint32_t chunk, uint32_t* __restrict__ counts) {
     extern __shared__ uint32_t hist[];
-    const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
+    // shared windows: windows [s wps, (s + 1) wps) fill bucket set s (several MSMs over one table)
+    const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, n);
     for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb)
-                atomicAdd(&hist[(stride ? 0u : (uint32_t)(w - wb)) * NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)],
+                atomicAdd(&hist[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC +
+                                (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)],
                           1u);
         });
     }
@@ -208,10 +210,11 @@ __device__ __forceinline__ uint32_t sort_entry_of(T x, uint32_t FB) {
 
 template <class Src, class T>
 __global__ void __launch_bounds__(1024) k_sort_coarse(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
-                                                     uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t chunk,
-                                                     const uint32_t* __restrict__ base, T* __restrict__ tmp) {
+                                                     uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t wps,
+                                                     uint32_t chunk, const uint32_t* __restrict__ base,
+                                                     T* __restrict__ tmp) {
     extern __shared__ uint32_t cur[];
-    const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
+    const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
     const uint32_t slot = sort_slot(blockIdx.x, nblk);
     for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) cur[k] = base[(size_t)k * nblk + slot];
     __syncthreads();
@@ -221,8 +224,8 @@ __global__ void __launch_bounds__(1024) k_sort_coarse(Src src, uint32_t n, int c
         src(i, c, we, [&](int w, int32_t d) {
             if (d != 0 && w >= wb) {
                 uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-                uint32_t pos = atomicAdd(&cur[(stride ? 0u : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
-                const uint32_t e = stride ? i + (uint32_t)w * stride : i;
+                uint32_t pos = atomicAdd(&cur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
+                const uint32_t e = stride ? i + ((uint32_t)w % wps) * stride : i;
                 tmp[pos] = sort_pack<T>(b & fmask, e, d < 0, FB);
             }
         });
@@ -797,22 +800,24 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul 
 
 template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
-                        uint32_t NBC, uint32_t nblk, uint32_t chunk, uint32_t stride, size_t ncnt, uint32_t* counts,
-                        uint32_t* base, void* tmp, uint32_t* offsets, uint32_t* sorted, uint32_t* zero_word) {
+                        uint32_t NBC, uint32_t nblk, uint32_t chunk, uint32_t stride, uint32_t wps, size_t ncnt,
+                        uint32_t* counts, uint32_t* base, void* tmp, uint32_t* offsets, uint32_t* sorted,
+                        uint32_t* zero_word) {
     hipStream_t st = L.st;
-    const uint32_t bins = (stride ? 1u : (uint32_t)(we - wb)) * NBC;
+    if (stride && wps == 0) return VC_E_INVALID;
+    const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
     const size_t lds = (size_t)bins * 4;
     if (lds > 64 * 1024) return VC_E_INVALID;  // c <= 16 keeps bins <= W * 128
     if (ncnt != (size_t)bins * nblk + 1) return VC_E_INVALID;
     // largest entry index e: i < nv, or w * stride + i with shared windows
-    const uint64_t emax = stride ? (uint64_t)we * stride : (uint64_t)nv;
+    const uint64_t emax = stride ? (uint64_t)std::min<uint32_t>((uint32_t)we, wps) * stride : (uint64_t)nv;
     const bool narrow = emax <= (1ull << (31 - FB));
     // scalars per hist / coarse block: runs of a block inside a coarse bin are chunk * W / bins
     // entries long, so a big bucket set (many coarse bins) takes bigger blocks to keep the
     // scatter's runs near a cache line
     const uint32_t sblk = chunk >= 4096 ? 1024 : 256;
     VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, sblk, lds, src, nv, c, wb, we, FB, NBC, nblk,
-                 stride, chunk, counts);
+                 stride, wps, chunk, counts);
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
     VK_TRY(L.ws[WS_SCAN_TMP].ensure(tmp_bytes));
@@ -828,12 +833,12 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     const int fblk = fine_env == 256 || fine_env == 1024 ? fine_env : (total / bins >= (1u << 15) ? 1024 : 256);
     if (narrow) {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, sblk, lds, src, nv, c, wb, we,
-                     FB, NBC, nblk, stride, chunk, base, static_cast<uint32_t*>(tmp));
+                     FB, NBC, nblk, stride, wps, chunk, base, static_cast<uint32_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, 0, static_cast<const uint32_t*>(tmp),
                      base, nblk, bins, FB, offsets, sorted, zero_word);
     } else {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, sblk, lds, src, nv, c, wb, we,
-                     FB, NBC, nblk, stride, chunk, base, static_cast<uint64_t*>(tmp));
+                     FB, NBC, nblk, stride, wps, chunk, base, static_cast<uint64_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, fblk, 0, static_cast<const uint64_t*>(tmp),
                      base, nblk, bins, FB, offsets, sorted, zero_word);
     }
@@ -881,7 +886,9 @@ struct MsmSlice {
     int c = 0, wb = 0, we = 0, W = 0;
     bool shared = false;  // all windows into one bucket set (Table::win copies)
     uint32_t m = 1;       // > 1: radix m 2^c digits (RadixDigits), m 2^(c-1) buckets
-    int Wr = 0;           // bucket sets reduced: 1 shared, W otherwise
+    int sets = 1;         // shared windows: bucket sets = MSMs over the table in this slice
+    uint32_t wps = 0;     // shared windows: windows per set (the window copies' count)
+    int Wr = 0;           // bucket sets reduced: `sets` shared, W otherwise
     uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
     uint32_t* offsets = nullptr;
     uint32_t* chain_max = nullptr;  // in the WS_TAIL buffer, tail_bytes after the tail points
@@ -905,8 +912,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     using Acc = typename C::Acc;
     using RAcc = FAcc<C>;  // raw radix-29 accumulators of the accumulate / fix-up / reduction
     const Lane L = sl.L;
-    const int c = sl.c, W = sl.W;
-    const int Wr = sl.shared ? 1 : W;
+    const int c = sl.c, W = sl.W;  // shared: W = sets x windows per set
+    const int Wr = sl.shared ? sl.sets : W;
     sl.Wr = Wr;
     const uint32_t NB = sl.m << (c - 1);
     const uint32_t NBtot = NB * (uint32_t)Wr;
@@ -1004,7 +1011,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.bsum_part = ws[WS_WIN].as<RAcc>();
     sl.tail = ws[WS_TAIL].as<Acc>();
 
-    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (uint32_t)nv : 0u, ncnt,
+    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (uint32_t)nv : 0u,
+                        sl.wps, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
                         ws[WS_SORTED].as<uint32_t>(), sl.chain_max));
@@ -1042,6 +1050,28 @@ static int slice_fetch(MsmSlice<C>& sl) {
 }
 
 template <class C>
+static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res);
+
+// the reduced points of bucket set `set` (shared windows: one MSM each) -> its sum
+template <class C>
+static typename C::Acc shared_set_sum(const MsmSlice<C>& sl, int set) {
+    using Acc = typename C::Acc;
+    const uint32_t J = sl.J;
+    const Acc* ht = sl.ht.data() + (size_t)set * (J + 1);
+    Acc x = C::zero();  // sum_j 2^j T_j
+    for (int j = (int)J - 1; j >= 0; j--) {
+        if (!C::is_zero(x)) x = C::dbl(x);
+        x = C::add(x, ht[j]);
+    }
+    Acc r = C::zero();  // Lseg x by double-and-add (Lseg = m for the radix buckets)
+    for (int b = 31 - __builtin_clz(sl.Lseg); b >= 0; b--) {
+        if (!C::is_zero(r)) r = C::dbl(r);
+        if ((sl.Lseg >> b) & 1) r = C::add(r, x);
+    }
+    return C::add(r, ht[J]);
+}
+
+template <class C>
 static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     using Acc = typename C::Acc;
     VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
@@ -1059,18 +1089,12 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     // slice = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host); with
     // shared windows the one bucket set already holds the 2^(c w) factors: A + Lseg sum_j 2^j T_j
     const uint32_t J = sl.J;
+    if (sl.shared && sl.sets > 1) {  // several MSMs: res[k] = set k's sum
+        for (int k = 0; k < sl.sets; k++) res[k] = shared_set_sum<C>(sl, k);
+        return VC_OK;
+    }
     if (sl.shared && (sl.Lseg & (sl.Lseg - 1)) != 0) {  // radix buckets: Lseg = m is odd
-        Acc x = C::zero();
-        for (int j = (int)J - 1; j >= 0; j--) {
-            if (!C::is_zero(x)) x = C::dbl(x);
-            x = C::add(x, sl.ht[j]);
-        }
-        Acc r = C::zero();  // Lseg x by double-and-add
-        for (int b = 31 - __builtin_clz(sl.Lseg); b >= 0; b--) {
-            if (!C::is_zero(r)) r = C::dbl(r);
-            if ((sl.Lseg >> b) & 1) r = C::add(r, x);
-        }
-        *res = C::add(r, sl.ht[J]);
+        *res = shared_set_sum<C>(sl, 0);
         return VC_OK;
     }
     int lg_seg = 0;
@@ -1202,6 +1226,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         sl[k].W = sl[k].we - sl[k].wb;
         sl[k].shared = shared;
         sl[k].m = radix_m;
+        sl[k].wps = (uint32_t)Wfull;
     }
     hipEvent_t fork = nullptr, join = nullptr, acc0 = nullptr;
     if (nsl == 2) acc0 = ctx->get_event();
@@ -1276,6 +1301,76 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     }
     memcpy(out_acc, &res, sizeof(Acc));
     return VC_OK;
+}
+
+// K MSMs over one whole table (e.g. a KZG commitment and its opening proof over the Lagrange
+// SRS): one pipeline for all K -- the radix digits of every scalar set, ONE sort into K bucket
+// sets (bucket set k of entry (k, w, i) names the same window copy B^w P_i), one accumulate
+// launch, one fix-up and one reduction over the K sets -- so the latency-bound tail and the
+// launch gaps are paid once, not K times. Only the radix shared-window geometry (BLS12-381, GLV,
+// whole table from 2^18 points) batches; other tables run the K MSMs one by one.
+template <class C, class Fr>
+static int msm_run_many_t(vc_ctx* ctx, Table* t, const void* const* d_sc, const int* mont, size_t n, size_t K,
+                          uint32_t* out_accs) {
+    using Acc = typename C::Acc;
+    bool batched = false;
+    if constexpr (std::is_same<C, BLS381G1>::value) {
+        bool glv = false;
+        if (K > 1 && n == t->n && n >= (1u << 18) && n < (1u << 30) && ctx->opt_shared_windows != 0 &&
+            !getenv("VKZG_MSM_RADIX") && !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED") &&
+            (uint64_t)2 * n * 7 * K < 0xffffffffull)
+            VK_TRY(glv_table_ok(ctx, t, &glv));
+        if (glv) {
+            VK_TRY(fast_tables<C>(ctx, t, true));
+            const int st = win_tables<C>(ctx, t, 16, 7, 0, 5);
+            if (st == VC_E_OOM) t->win.release();
+            else if (st != VC_OK) return st;
+            batched = st == VC_OK;
+        }
+        if (batched) {
+            const size_t nv = 2 * n;
+            const int Ws = 7;
+            VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 4 * (size_t)Ws * K));
+            int32_t* dig = ctx->ws[WS_GLV_SC].as<int32_t>();
+            for (size_t k = 0; k < K; k++)
+                VK_LAUNCH(ctx, "glv_split", (k_glv_radix<Fr, 5, 16>), (n + 255) / 256, 256, 0,
+                          static_cast<const uint32_t*>(d_sc[k]), t->inf.as<uint8_t>(), (uint32_t)n, mont[k], glv_consts(),
+                          Ws, dig + k * (size_t)Ws * nv);
+            MsmSlice<C> sl;
+            sl.L = ctx->lane(0);
+            sl.c = 16;
+            sl.m = 5;
+            sl.shared = true;
+            sl.sets = (int)K;
+            sl.wps = (uint32_t)Ws;
+            sl.wb = 0;
+            sl.we = Ws * (int)K;
+            sl.W = sl.we;
+            const auto* win = t->win.as<typename Fast29<C>::type::AffN>();
+            VK_TRY(slice_enqueue<C>(ctx, sl, RadixDigits{dig, (uint32_t)nv}, nv, win, win, 0xffffffffu, nullptr, nullptr));
+            VK_TRY(slice_fetch<C>(sl));
+            std::vector<Acc> res(K);
+            VK_TRY(slice_finish<C>(ctx, sl, res.data()));
+            memcpy(out_accs, res.data(), K * sizeof(Acc));
+            ctx->plan = {16, Ws, 2, 5, 1};
+            return VC_OK;
+        }
+    }
+    for (size_t k = 0; k < K; k++)
+        VK_TRY(msm_run(ctx, t, 0, d_sc[k], n, mont[k], out_accs + k * (sizeof(Acc) / 4)));
+    return VC_OK;
+}
+
+int msm_run_many(vc_ctx* ctx, Table* t, const void* const* d_sc, const int* mont, size_t n, size_t K, uint32_t* out) {
+    switch (t->curve) {
+        case VC_CURVE_BN254:
+            return msm_run_many_t<BN254G1, BN254Fr>(ctx, t, d_sc, mont, n, K, out);
+        case VC_CURVE_BLS12_381:
+            return msm_run_many_t<BLS381G1, BLS381Fr>(ctx, t, d_sc, mont, n, K, out);
+        case VC_CURVE_BANDERSNATCH:
+            return msm_run_many_t<Bandersnatch, BandFr>(ctx, t, d_sc, mont, n, K, out);
+    }
+    return VC_E_INVALID;
 }
 
 // ------------------------------------------------------------------ sparse batched commits

@@ -406,7 +406,8 @@ uint32_t fr_generator<BLS381Fr>() { return 7; }
 template <class C_, class Fr_>
 static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
                        uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y_out, uint64_t* q_out, bool d_evals = false,
-                       int part = 0, int parts = 1, uint32_t* out_acc = nullptr) {
+                       int part = 0, int parts = 1, uint32_t* out_acc = nullptr, uint64_t* com_xy = nullptr,
+                       uint8_t* com_inf = nullptr) {
     if (!is_pow2(size) || max > size) return VC_E_INVALID;
     if (t && t->n < size) return VC_E_RANGE;
     DevBuf d_f(ctx), d_q(ctx), pw(ctx), tmp(ctx), part_buf(ctx);
@@ -428,7 +429,15 @@ static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals
         VK_CHECK_HIP(hipMemcpyAsync(q_out, tmp.p, size * 32, hipMemcpyDeviceToHost, ctx->stream));
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     }
-    if (t && out_acc) {
+    if (t && com_xy) {  // commitment + proof: the two MSMs over the SRS as one batched pipeline
+        const void* sc[2] = {d_f.p, d_q.p};
+        const int mt[2] = {1, 1};
+        const int words = point_words(ctx->curve);
+        std::vector<uint32_t> acc(2 * (size_t)words);
+        VK_TRY(msm_run_many(ctx, t, sc, mt, size, 2, acc.data()));
+        VK_TRY(acc_to_affine(ctx->curve, acc.data(), com_xy, com_inf));
+        VK_TRY(acc_to_affine(ctx->curve, acc.data() + words, proof_xy, proof_inf));
+    } else if (t && out_acc) {
         VK_TRY(msm_run(ctx, t, 0, d_q.p, size, 1, out_acc, part, parts));
     } else if (t) {
         std::vector<uint32_t> acc(point_words(ctx->curve));
@@ -1021,6 +1030,24 @@ int vc_kzg_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals
         return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, size, ev, max, point, proof_xy, proof_inf, y, nullptr, true);
     if (ctx->curve == VC_CURVE_BLS12_381)
         return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, ev, max, point, proof_xy, proof_inf, y, nullptr, true);
+    return VC_E_INVALID;
+}
+
+int vc_kzg_commit_prove_device(vc_ctx* ctx, int table, size_t size, const void* d_evals, size_t max,
+                               const uint64_t* point, uint64_t* com_xy, uint8_t* com_inf, uint64_t* proof_xy,
+                               uint8_t* proof_inf, uint64_t* y) {
+    if (!ctx || (max && !d_evals) || !point || !com_xy || !com_inf || !proof_xy || !proof_inf || !y)
+        return VC_E_INVALID;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    const uint64_t* ev = reinterpret_cast<const uint64_t*>(d_evals);
+    if (ctx->curve == VC_CURVE_BN254)
+        return kzg_prove_t<BN254G1, BN254Fr>(ctx, t, size, ev, max, point, proof_xy, proof_inf, y, nullptr, true, 0, 1,
+                                             nullptr, com_xy, com_inf);
+    if (ctx->curve == VC_CURVE_BLS12_381)
+        return kzg_prove_t<BLS381G1, BLS381Fr>(ctx, t, size, ev, max, point, proof_xy, proof_inf, y, nullptr, true, 0,
+                                               1, nullptr, com_xy, com_inf);
     return VC_E_INVALID;
 }
 

@@ -51,6 +51,8 @@ SIGNATURES = {
     "vc_transcript_reserve": (None, [c_void_p, c_size_t]),
     "vc_msm_windows": (c_int, [c_int, c_size_t, P, P, P]),
     "vc_msm_last_plan": (c_int, [c_void_p, P, P, P, P, P]),
+    "vc_msm_device_many": (c_int, [c_void_p, c_int, c_void_p, P, c_size_t, c_size_t, P, P]),
+    "vc_kzg_commit_prove_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P, P, P]),
     "vc_msm_device_window_part": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, c_int, c_int, P]),
     "vc_partials_sum": (c_int, [c_int, P, c_size_t, P, P]),
     "vc_msm_batch": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),

@@ -235,6 +235,18 @@ class Engine:
                                   1 if mont else 0, _ptr(out), _ptr(oinf)), "vc_msm_device")
         return out, int(oinf[0])
 
+    def msm_device_many(self, table, d_scalars_ptrs, n, mont=None):
+        """len(d_scalars_ptrs) MSMs over one table (vc_msm_device_many): one batched pipeline on
+        the radix shared-window geometry -> list of (xy, inf)"""
+        K = len(d_scalars_ptrs)
+        ptrs = (ctypes.c_void_p * max(K, 1))(*[ctypes.c_void_p(p) for p in d_scalars_ptrs])
+        mt = np.array([1 if (mont and mont[k]) else 0 for k in range(K)] or [0], dtype=np.int32)
+        out = np.zeros((max(K, 1), 2 * self.nl), dtype=np.uint64)
+        oinf = np.zeros(max(K, 1), dtype=np.uint8)
+        check(lib().vc_msm_device_many(self.h, table, ptrs, _ptr(mt), n, K, _ptr(out), _ptr(oinf)),
+              "vc_msm_device_many")
+        return [(out[k], int(oinf[k])) for k in range(K)]
+
     def device_mad_rate(self):
         """Measured v_mad_u64_u32 throughput of this device (tera-ops/s)."""
         v = ctypes.c_double(0)
