@@ -877,11 +877,11 @@ def main():
                 return vdist.all_gather_commitments(dxy[:Bl], dinf[:Bl], B, world)
             return dxy, dinf
 
-        def ctime(cw):
+        def ctime(cw, windows=0):
             ceng, ctab = cstate["eng"], cstate["tab"]
             fits = True
             try:
-                ceng.fixed_base_precompute(ctab, cw)
+                ceng.fixed_base_precompute(ctab, cw, windows)
             except vkzg.VCError:  # table does not fit next to the rest
                 fits = False
             if world > 1:  # every rank takes the same branch (a lone skip would hang the barriers)
@@ -912,13 +912,17 @@ def main():
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                 cdt = float(tt.item())
             fb_ms, fb_n = ceng.kernel_time("fb_commit")
-            return {"window_bits": cw, "commits_per_s": B / cdt, "ms_per_batch": cdt * 1e3,
+            gc, gw, gbig = ceng.fixed_base_geometry(ctab)
+            return {"window_bits": cw, "windows": gw, "wide_windows": gbig, "commits_per_s": B / cdt,
+                    "ms_per_batch": cdt * 1e3,
                     "fb_commit_kernel_ms": fb_ms / fb_n if fb_n else None,
                     "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
-                    "table_bytes": 256 * ((253 + 1 + cw - 1) // cw) * (1 << (cw - 1)) * 108}  # FbE: 3 x 9 limbs
+                    "table_bytes": 256 * (gw + gbig) * (1 << (gc - 1)) * 108}  # FbE: 3 x 9 limbs
 
         big = ctime(a.commit_window)
         small = ctime(16) if a.commit_window != 16 else big
+        # the <= 60 GB table: 14 windows (12 of 18 bits, 2 of 19), 58 GB
+        mixed = ctime(18, 14)
         head = big or small
         if head is None:  # neither table fits beside the rest on every rank
             out["secondary"] = {"workload": f"{B} batched width-256 Bandersnatch commits (configs[2])",
@@ -929,6 +933,7 @@ def main():
                             f"c={head['window_bits']}, batch split over {world} rank(s)",
                 **head,
                 "c16": small,
+                "mixed_c18_w14": mixed,
             }
         cstate["eng"].close()
 

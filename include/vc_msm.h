@@ -145,6 +145,15 @@ int vc_msm_batch_sparse(vc_ctx* ctx, int table_id, size_t batch, const uint64_t*
 /* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 20]
  * (n x ceil(bits/c) x 2^(c-1) affine points: 167 GB for 256 Bandersnatch bases at c = 20). */
 int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
+/* The same with `windows` signed-digit windows of window_bits or window_bits + 1 bits (the
+ * last bits + 1 - window_bits * windows windows are the wider ones; window_bits in [4, 19]).
+ * Sizes a table between two uniform ones: Bandersnatch window_bits 18, windows 14 is 58 GB
+ * for 256 bases with the 14 windows per scalar of the 101 GB c = 19 table. windows = 0, or at
+ * least the uniform count, is vc_fixed_base_precompute. VC_E_INVALID when the windows cannot
+ * cover the scalar with at most one extra bit each. */
+int vc_fixed_base_precompute_windows(vc_ctx* ctx, int table_id, int window_bits, int windows);
+/* Geometry of a table's fixed-base tables (0s if none yet): window bits c, windows, wide windows */
+int vc_fixed_base_geometry(vc_ctx* ctx, int table_id, int* window_bits, int* windows, int* wide_windows);
 
 #ifdef __cplusplus
 }

@@ -215,6 +215,32 @@ def test_commit_10k_width256_c20(oracle_c):
         e.close()
 
 
+def test_commit_10k_width256_mixed_c18_w14(oracle_c):
+    """configs[2] on the deployable mixed table: 14 windows (12 of 18 bits, 2 of 19), 58 GB for
+    256 Bandersnatch bases; 8 sampled commits against the oracle."""
+    import torch
+    import vkzg
+    e = vkzg.Engine("bandersnatch")
+    try:
+        tab = e.random_bases(256, seed=3)
+        xy, inf = e.download_bases(tab)
+        e.fixed_base_precompute(tab, 18, 14)
+        assert e.fixed_base_geometry(tab) == (18, 14, 2)
+        B = 10_000
+        sc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(15))
+        d_sc = torch.from_numpy(sc.view(np.int64).copy()).cuda()
+        d_xy = torch.zeros((B, 8), dtype=torch.int64, device="cuda")
+        d_inf = torch.zeros(B, dtype=torch.uint8, device="cuda")
+        e.msm_batch_device(tab, 256, d_sc.data_ptr(), B, d_xy.data_ptr(), d_inf.data_ptr())
+        got_xy = d_xy.cpu().numpy().view(np.uint64)
+        got_inf = d_inf.cpu().numpy()
+        for j in list(np.random.default_rng(16).choice(B, 6, replace=False)) + [0, B - 1]:
+            want = oracle_c.msm_arrays("bandersnatch", xy, inf, sc[j * 256:(j + 1) * 256], 1)
+            assert got_inf[j] == want[1] and np.array_equal(got_xy[j], want[0]), j
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("where", ["in_domain", "outside"])
 def test_kzg_commit_open_2e20_trapdoor(where):
     """configs[3]: commit + open at d = 2^20 on BLS12-381 (the bench's workload), checked by the

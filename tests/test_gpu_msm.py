@@ -257,6 +257,49 @@ def test_batch_commit(engines, oracle_c, curve):
                 assert np.array_equal(got_xy[j], want[0]), j
 
 
+@pytest.mark.parametrize("curve", CURVES)
+@pytest.mark.parametrize("c,windows", [(8, 30), (12, 20), (5, 43)])
+def test_batch_commit_mixed_windows(engines, oracle_c, curve, c, windows):
+    """fixed-base tables with windows of c and c + 1 bits (vc_fixed_base_precompute_windows): the
+    latency path (small batch), the chunk-major path (large batch) and the sparse CSR commits read
+    the same mixed schedule; sampled commits vs the oracle, and the reported geometry"""
+    import vkzg
+    e = engines[curve]
+    bits = {"bn254": 254, "bls12_381": 255, "bandersnatch": 253}[curve]
+    rng = np.random.default_rng(77 + c)
+    width = 40
+    tid = e.random_bases(width, seed=c + windows)
+    xy, inf = e.download_bases(tid)
+    e.fixed_base_precompute(tid, c, windows)
+    assert e.fixed_base_geometry(tid) == (c, windows, bits + 1 - c * windows)
+    for batch in (4, 900):
+        sc = vkzg.random_scalars(curve, width * batch, rng)
+        sc[width:2 * width] = 0
+        got_xy, got_inf = e.msm_batch(tid, sc, width)
+        for j in sorted({0, 1, batch - 1} | set(rng.integers(0, batch, 4).tolist())):
+            want = _oracle(oracle_c, curve, xy, inf, sc[j * width:(j + 1) * width])
+            assert got_inf[j] == want[1], (batch, j)
+            if not want[1]:
+                assert np.array_equal(got_xy[j], want[0]), (batch, j)
+    # sparse rows (3 non-zeros each) read the same schedule
+    from pyoracle.curves import CURVES as OC
+    pts = vkzg.arrays_to_points(curve, xy, inf)
+    rows = 50
+    cols = [int(v) for v in rng.integers(0, width, size=3 * rows)]
+    vals = [int.from_bytes(rng.bytes(32), "little") % OC[curve].r for _ in range(3 * rows)]
+    ptr = list(range(0, 3 * rows + 1, 3))
+    got_xy, got_inf = e.msm_batch_sparse(tid, ptr, cols, vkzg.ints_to_limbs(vals))
+    for g in (0, 7, rows - 1):
+        want = oracle_c.msm(curve, [pts[k] for k in cols[3 * g:3 * g + 3]], vals[3 * g:3 * g + 3], 4)
+        if curve == "bandersnatch" and want == (0, 1):
+            want = None
+        got = None if got_inf[g] else vkzg.arrays_to_points(curve, got_xy[g:g + 1], got_inf[g:g + 1])[0]
+        assert got == want, g
+    # a schedule that needs windows wider than c + 1
+    with pytest.raises(vkzg.VCError):
+        e.fixed_base_precompute(tid, 8, 10)
+
+
 def test_batch_commit_edwards_identity(engines, oracle_c):
     """Bandersnatch commits that sum to the identity through P + (-P) (Edwards identity (0 : Z : Z)
     with Z != 1): the device normalisation (large batches, k_norm_prep / k_norm_finish) must divide

@@ -422,6 +422,26 @@ int vc_fixed_base_precompute(vc_ctx* ctx, int id, int window_bits) {
     return vk::fixed_base_precompute(ctx, t, window_bits);
 }
 
+int vc_fixed_base_precompute_windows(vc_ctx* ctx, int id, int window_bits, int windows) {
+    if (!ctx || windows < 0) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    return vk::fixed_base_precompute(ctx, t, window_bits, windows);
+}
+
+int vc_fixed_base_geometry(vc_ctx* ctx, int id, int* window_bits, int* windows, int* wide_windows) {
+    if (!ctx) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    const bool built = t->fb_c != 0 && t->fb.p;
+    if (window_bits) *window_bits = built ? t->fb_c : 0;
+    if (windows) *windows = built ? t->fb_W : 0;
+    if (wide_windows) *wide_windows = built ? t->fb_big : 0;
+    return VC_OK;
+}
+
 int vc_msm_batch_device(vc_ctx* ctx, int id, size_t width, const void* d_sc, size_t batch, int mont,
                         void* d_out_xy, uint8_t* d_out_inf) {
     if (!ctx || (batch > 0 && (!d_sc || !d_out_xy || !d_out_inf)) || width == 0) return VC_E_INVALID;

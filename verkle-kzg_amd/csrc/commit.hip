@@ -34,19 +34,35 @@ struct FbEntryLimbs {
 template <class C>
 using FbE = FbEntryLimbs<C>;
 
-// copy one window's normalised multiples into the table: tab[(i*W + w)*NBk + k] = aff[i*NBk + k],
-// in the packed-29 form the commit loops read
+// copy one window's NBw normalised multiples into the table: tab[i*stride + off(w) + k] =
+// aff[i*NBw + k], in the packed-29 form the commit loops read
 template <class C>
-__global__ void k_fb_place(const typename C::Aff* __restrict__ aff, uint32_t n, uint32_t NBk, int W, int w,
+__global__ void k_fb_place(const typename C::Aff* __restrict__ aff, uint32_t n, uint32_t NBw, FbGeom g, int w,
                            FbE<C>* __restrict__ tab) {
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= (size_t)n * NBk) return;
-    size_t i = j / NBk, k = j - i * NBk;
+    if (j >= (size_t)n * NBw) return;
+    size_t i = j / NBw, k = j - i * NBw;
     using FC = typename Fast29<C>::type;
     typename C::Aff packed;
     FC::pack_aff(aff[j], &packed);  // canonical x R'
-    tab[(i * W + w) * NBk + k].u = FC::load(&packed);
+    tab[i * g.stride() + g.off(w) + k].u = FC::load(&packed);
 }
+
+// signed digits of a scalar over the table's windows (widths g.width(w)): d in (-2^(cw-1), 2^(cw-1)]
+template <class Fr>
+struct FbDigits {
+    fe<Fr> s;
+    uint32_t carry = 0;
+    __device__ __forceinline__ int32_t next(int cw) {
+        const uint32_t mask = (1u << cw) - 1, half = 1u << (cw - 1);
+        const uint32_t raw = (s.v[0] & mask) + carry;
+#pragma unroll
+        for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> cw) | (s.v[k + 1] << (32 - cw));
+        s.v[7] >>= cw;
+        carry = raw > half ? 1u : 0u;
+        return carry ? (int32_t)raw - (int32_t)(1u << cw) : (int32_t)raw;
+    }
+};
 
 template <class Fr>
 __device__ __forceinline__ fe<Fr> load_scalar_fb(const uint32_t* __restrict__ sc, size_t i) {
@@ -308,39 +324,30 @@ static int normalize_split(vc_ctx* ctx, const typename C::Acc* d_in, size_t coun
 template <class C, class Fr>
 __global__ void __launch_bounds__(256) VK_COMMIT_OCC k_fb_commit_cm(const FbE<C>* __restrict__ tab,
                                                      const uint8_t* __restrict__ inf, uint32_t width,
-                                                     int c, int W, const uint32_t* __restrict__ sc,
+                                                     FbGeom fg, const uint32_t* __restrict__ sc,
                                                      uint32_t batch, int mont, uint32_t K, uint32_t nruns,
                                                      typename Fast29<C>::type::Acc* __restrict__ piece) {
     using FC = typename Fast29<C>::type;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nruns) return;
     const uint32_t chunk = r / batch, g = r - chunk * batch;
-    const uint32_t NBk = 1u << (c - 1);
-    const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
+    const int W = fg.W;
     const uint32_t i0 = chunk * K, i1 = min(i0 + K, width);
     typename FC::Acc acc = FC::zero();
     for (uint32_t i = i0; i < i1; i++) {
         if (inf[i]) continue;
-        fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
-        if (mont) s = fe_from_mont<Fr>(s);
-        const FbE<C>* ti = tab + (size_t)i * W * NBk;
-        uint32_t carry = 0;
-        auto next_digit = [&]() -> int32_t {
-            uint32_t raw = (s.v[0] & mask) + carry;
-#pragma unroll
-            for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
-            s.v[7] >>= c;
-            carry = raw > half ? 1u : 0u;
-            return carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
-        };
-        int32_t dn = next_digit();
+        FbDigits<Fr> dg;
+        dg.s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
+        if (mont) dg.s = fe_from_mont<Fr>(dg.s);
+        const FbE<C>* ti = tab + (size_t)i * fg.stride();
+        int32_t dn = dg.next(fg.width(0));
         typename FC::Aff Pn = ti[dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0].u;
         for (int w = 0; w < W; w++) {
             const int32_t d = dn;
             const typename FC::Aff P = Pn;
             if (w + 1 < W) {
-                dn = next_digit();
-                Pn = ti[(size_t)(w + 1) * NBk + (dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0)].u;
+                dn = dg.next(fg.width(w + 1));
+                Pn = ti[fg.off(w + 1) + (dn != 0 ? (uint32_t)(dn < 0 ? -dn : dn) - 1 : 0)].u;
             }
             if (d != 0) acc = FC::madd(acc, P, d < 0);
         }
@@ -436,34 +443,27 @@ __device__ __forceinline__ typename FC::Acc fb_wave_sum29(typename FC::Acc v) {
 
 template <class C, class Fr>
 __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
-                                                        const uint8_t* __restrict__ inf, uint32_t width, int c,
-                                                        int W, const uint32_t* __restrict__ sc, int mont,
+                                                        const uint8_t* __restrict__ inf, uint32_t width, FbGeom fg,
+                                                        const uint32_t* __restrict__ sc, int mont,
                                                         uint32_t bpc, int wpt, typename C::Acc* __restrict__ part) {
     using Acc = typename C::Acc;
     using FC = typename Fast29<C>::type;
     __shared__ Acc wsum[4];
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
+    const int W = fg.W;
     const uint32_t WG = (uint32_t)(W + wpt - 1) / wpt;
     const uint32_t j = blk * 256 + threadIdx.x;
     const uint32_t i = j / WG, wg = j % WG;
-    const uint32_t NBk = 1u << (c - 1);
-    const uint32_t mask = (1u << c) - 1, half = 1u << (c - 1);
     typename FC::Acc fa = FC::zero();
     if (i < width && !inf[i]) {
-        fe<Fr> s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
-        if (mont) s = fe_from_mont<Fr>(s);
-        const FbE<C>* ti = tab + (size_t)i * W * NBk;
+        FbDigits<Fr> dg;
+        dg.s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
+        if (mont) dg.s = fe_from_mont<Fr>(dg.s);
+        const FbE<C>* ti = tab + (size_t)i * fg.stride();
         const int wb = (int)wg * wpt, we = min(W, wb + wpt);
-        uint32_t carry = 0;
         for (int w = 0; w < we; w++) {
-            uint32_t raw = (s.v[0] & mask) + carry;
-#pragma unroll
-            for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
-            s.v[7] >>= c;
-            carry = raw > half ? 1u : 0u;
-            const int32_t d = carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw;
-            if (w >= wb && d != 0)
-                fa = FC::madd(fa, ti[(size_t)w * NBk + (uint32_t)(d < 0 ? -d : d) - 1].u, d < 0);
+            const int32_t d = dg.next(fg.width(w));
+            if (w >= wb && d != 0) fa = FC::madd(fa, ti[fg.off(w) + (uint32_t)(d < 0 ? -d : d) - 1].u, d < 0);
         }
     }
     if constexpr (FC::quad) {
@@ -525,41 +525,56 @@ static uint32_t resident_lanes(Kern k, int block) {
 }
 
 // ------------------------------------------------------------------ host drivers
+// scalar bits of the curve's group order (signed digits need windows covering bits + 1)
 template <class C>
-static int fb_precompute_t(vc_ctx* ctx, Table* t, int c) {
+using FrOf = typename std::conditional<std::is_same<C, BN254G1>::value, BN254Fr,
+                                       typename std::conditional<std::is_same<C, BLS381G1>::value, BLS381Fr,
+                                                                 BandFr>::type>::type;
+
+// windows = 0: uniform c-bit windows; otherwise `windows` windows of c or c + 1 bits (the last
+// bits + 1 - c windows wide), which must cover the scalar's bits + 1
+template <class C>
+static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
     using Acc = typename C::Acc;
     using Aff = typename C::Aff;
-    using Fr = typename std::conditional<std::is_same<C, BN254G1>::value, BN254Fr,
-                                         typename std::conditional<std::is_same<C, BLS381G1>::value, BLS381Fr,
-                                                                   BandFr>::type>::type;
-    if (c < 4 || c > 20) return VC_E_INVALID;
+    using Fr = FrOf<C>;
+    if (c < 4 || c > 20 || windows < 0) return VC_E_INVALID;
     const uint32_t n = (uint32_t)t->n;
-    const int W = (Fr::BITS + 1 + c - 1) / c;
-    const uint32_t NBk = 1u << (c - 1);
-    if (t->fb_c == c && t->fb.p) return VC_OK;
+    int W = (Fr::BITS + 1 + c - 1) / c, big = 0;
+    if (windows > 0 && windows < W) {
+        big = Fr::BITS + 1 - c * windows;
+        if (big > windows || c == 20) return VC_E_INVALID;  // needs wider windows than c + 1
+        W = windows;
+    }
+    const FbGeom g{c, W, big};
+    const uint32_t NBk = 1u << (c - 1), NBmax = big ? 2 * NBk : NBk;
+    if (t->fb_c == c && t->fb_W == W && t->fb_big == big && t->fb.p) return VC_OK;
     t->fb.release();
-    VK_TRY(t->fb.ensure(std::max<size_t>((size_t)n * W * NBk, 1) * sizeof(FbE<C>)));
+    t->fb_c = 0;
+    VK_TRY(t->fb.ensure(std::max<size_t>((size_t)n * g.stride(), 1) * sizeof(FbE<C>)));
     DevBuf Q, tmp, aff_w;
     VK_TRY(Q.ensure(std::max<uint32_t>(n, 1) * sizeof(Acc)));
-    VK_TRY(tmp.ensure(std::max<size_t>((size_t)n * NBk, 1) * sizeof(Acc)));
-    VK_TRY(aff_w.ensure(std::max<size_t>((size_t)n * NBk, 1) * sizeof(Aff)));
-    const uint32_t CH = NBk >= 64 ? 64 : NBk;
-    const uint32_t nch = (NBk + CH - 1) / CH;
+    VK_TRY(tmp.ensure(std::max<size_t>((size_t)n * NBmax, 1) * sizeof(Acc)));
+    VK_TRY(aff_w.ensure(std::max<size_t>((size_t)n * NBmax, 1) * sizeof(Aff)));
     for (int w = 0; w < W; w++) {
+        const uint32_t NBw = 1u << (g.width(w) - 1);
+        const uint32_t CH = NBw >= 64 ? 64 : NBw;
+        const uint32_t nch = (NBw + CH - 1) / CH;
+        // Q = 2^(bits below window w) G: the previous window's width more doublings
         VK_LAUNCH(ctx, "fb_shift", (k_fb_shift<C>), (n + 255) / 256, 256, 0, Q.as<Acc>(),
-                  t->bases.as<Aff>(), n, c, w == 0 ? 1 : 0);
+                  t->bases.as<Aff>(), n, w == 0 ? 0 : g.width(w - 1), w == 0 ? 1 : 0);
         VK_LAUNCH(ctx, "fb_fill", (k_fb_fill<C>), ((size_t)n * nch + 127) / 128, 128, 0, Q.as<Acc>(), n,
-                  NBk, CH, tmp.as<Acc>());
-        size_t cnt = (size_t)n * NBk;
+                  NBw, CH, tmp.as<Acc>());
+        size_t cnt = (size_t)n * NBw;
         VK_LAUNCH(ctx, "fb_normalize", (k_normalize<C>), (cnt + 255) / 256, 256, 0, tmp.as<Acc>(), cnt,
                   aff_w.as<Aff>(), (uint32_t*)nullptr, (uint8_t*)nullptr);
-        // place window w into T[i][w][k]
-        VK_LAUNCH(ctx, "fb_place", (k_fb_place<C>), (cnt + 255) / 256, 256, 0, aff_w.as<Aff>(), n, NBk, W, w,
+        VK_LAUNCH(ctx, "fb_place", (k_fb_place<C>), (cnt + 255) / 256, 256, 0, aff_w.as<Aff>(), n, NBw, g, w,
                   t->fb.as<FbE<C>>());
     }
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     t->fb_c = c;
     t->fb_W = W;
+    t->fb_big = big;
     return VC_OK;
 }
 
@@ -568,21 +583,22 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host) {
     using Acc = typename C::Acc;
     if (width > t->n) return VC_E_RANGE;
-    if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8));
+    if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8, 0));
     if (batch == 0) return VC_OK;
     VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
     // resident lanes of this context's device (cached per ctx: the Guard's mutex serialises it)
     if (!ctx->fb_lanes) ctx->fb_lanes = resident_lanes(k_fb_commit_cm<C, Fr>, 256);
     const size_t items = batch * width;
     const size_t lanes = ctx->fb_lanes ? ctx->fb_lanes : 131072;
-    const int W = t->fb_W;
+    const FbGeom fg = t->fb_geom();
+    const int W = fg.W;
     const int wpt = fb_wpt();
     const size_t WG = (size_t)(W + wpt - 1) / wpt;
     if (items * WG <= lanes && batch <= 64) {  // small batch: latency path
         const uint32_t bpc = (uint32_t)((width * WG + 255) / 256);
         VK_TRY(ctx->ws[WS_PIECE].ensure((size_t)batch * bpc * sizeof(Acc)));
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
-                  t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, W, reinterpret_cast<const uint32_t*>(d_sc), mont,
+                  t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
                   bpc, wpt, ctx->ws[WS_PIECE].as<Acc>());
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
@@ -630,7 +646,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (nruns >= (1ull << 31)) return VC_E_RANGE;
     VK_TRY(ctx->ws[WS_PIECE].ensure(nruns * sizeof(typename Fast29<C>::type::Acc)));
     VK_LAUNCH(ctx, "fb_commit", (k_fb_commit_cm<C, Fr>), (nruns + 255) / 256, 256, 0,
-              t->fb.as<FbE<C>>(), t->inf.as<uint8_t>(), (uint32_t)width, t->fb_c, t->fb_W,
+              t->fb.as<FbE<C>>(), t->inf.as<uint8_t>(), (uint32_t)width, fg,
               reinterpret_cast<const uint32_t*>(d_sc), (uint32_t)batch, mont, (uint32_t)K, (uint32_t)nruns,
               ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>());
     // serial adds per SIMD: a thread per commit (nch adds, batch / 64 waves) vs a wave per commit
@@ -664,7 +680,7 @@ template <class C>
 static int table_from_acc_t(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) {
     t->curve = ctx->curve;
     t->n = n;
-    t->fb_c = t->fb_W = 0;
+    t->fb_c = t->fb_W = t->fb_big = 0;
     t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(typename C::Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
@@ -699,11 +715,11 @@ int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void
     return VC_E_INVALID;
 }
 
-int fixed_base_precompute(vc_ctx* ctx, Table* t, int c) {
+int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows) {
     switch (t->curve) {
-        case VC_CURVE_BN254: return fb_precompute_t<BN254G1>(ctx, t, c);
-        case VC_CURVE_BLS12_381: return fb_precompute_t<BLS381G1>(ctx, t, c);
-        case VC_CURVE_BANDERSNATCH: return fb_precompute_t<Bandersnatch>(ctx, t, c);
+        case VC_CURVE_BN254: return fb_precompute_t<BN254G1>(ctx, t, c, windows);
+        case VC_CURVE_BLS12_381: return fb_precompute_t<BLS381G1>(ctx, t, c, windows);
+        case VC_CURVE_BANDERSNATCH: return fb_precompute_t<Bandersnatch>(ctx, t, c, windows);
     }
     return VC_E_INVALID;
 }

@@ -68,14 +68,29 @@ struct PinBuf {
     PinBuf& operator=(const PinBuf&) = delete;
 };
 
+// window schedule of a fixed-base table (commit.hip): W signed-digit windows, the last `big` of
+// them c + 1 bits wide and the rest c, so a scalar of B bits needs c W + big >= B + 1. Base i's
+// block holds stride() entries; window w's 2^(width(w) - 1) multiples start at off(w). Mixed
+// widths put a table between two uniform sizes: Bandersnatch c = 18, W = 14, big = 2 is 58 GB
+// with the 14 windows of the 101 GB c = 19 table (15 at c = 18).
+struct FbGeom {
+    int c, W, big;
+    __host__ __device__ __forceinline__ int width(int w) const { return c + (w >= W - big ? 1 : 0); }
+    __host__ __device__ __forceinline__ size_t off(int w) const {
+        return (size_t)(w + (w > W - big ? w - (W - big) : 0)) << (c - 1);
+    }
+    __host__ __device__ __forceinline__ size_t stride() const { return (size_t)(W + big) << (c - 1); }
+};
+
 struct Table {
     int curve = 0;
     size_t n = 0;
     DevBuf bases;  // n x Aff (Montgomery)
     DevBuf inf;    // n x u8
     // fixed-base window tables for batched commits
-    int fb_c = 0, fb_W = 0;
+    int fb_c = 0, fb_W = 0, fb_big = 0;
     DevBuf fb;
+    FbGeom fb_geom() const { return FbGeom{fb_c, fb_W, fb_big}; }
     // 1: every base lies in the prime-order subgroup (the GLV endomorphism acts as lambda, so
     // msm.hip may split scalars), 0: some base does not, -1: not checked yet
     int subgroup = -1;
@@ -233,7 +248,7 @@ int bases_upload(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, 
 int bases_fill(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf, size_t n);
 int bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id);
 int bases_download(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf);
-int fixed_base_precompute(vc_ctx* ctx, Table* t, int c);
+int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows = 0);
 int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void* d_out_xy, uint8_t* d_out_inf);
 int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                      const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);

@@ -1381,32 +1381,46 @@ int msm_run_many(vc_ctx* ctx, Table* t, const void* const* d_sc, const int* mont
 // entries per thread, rows straddling threads merged by the fix-up) sums them. For verkle
 // nodes (~5 non-zeros of 256 per internal node, 2 of N per extension row) this replaces
 // dense width-256 rows.
+// the signed digits of a scalar over a fixed-base table's windows (widths g.width(w), ctx.hpp)
+template <class Fr, class Fn>
+__device__ __forceinline__ void for_each_digit_fb(fe<Fr> s, const FbGeom& g, Fn&& f) {
+    uint32_t carry = 0;
+    for (int w = 0; w < g.W; w++) {
+        const int c = g.width(w);
+        const uint32_t raw = (s.v[0] & ((1u << c) - 1)) + carry;
+#pragma unroll
+        for (int k = 0; k < 7; k++) s.v[k] = (s.v[k] >> c) | (s.v[k + 1] << (32 - c));
+        s.v[7] >>= c;
+        carry = raw > (1u << (c - 1)) ? 1u : 0u;
+        f(w, carry ? (int32_t)raw - (int32_t)(1u << c) : (int32_t)raw);
+    }
+}
+
 template <class Fr>
-__global__ void k_sparse_count(const uint32_t* __restrict__ sc, size_t nnz, int mont, int c, int W,
+__global__ void k_sparse_count(const uint32_t* __restrict__ sc, size_t nnz, int mont, FbGeom g,
                                uint32_t* __restrict__ cnt) {
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nnz) return;
     fe<Fr> s = load_scalar<Fr>(sc, j);
     if (mont) s = fe_from_mont<Fr>(s);
     uint32_t k = 0;
-    for_each_digit<Fr>(s, c, W, [&](int, int32_t d) { k += d != 0; });
+    for_each_digit_fb<Fr>(s, g, [&](int, int32_t d) { k += d != 0; });
     cnt[j] = k;
 }
 
 template <class Fr>
 __global__ void k_sparse_expand(const uint32_t* __restrict__ sc, const uint32_t* __restrict__ cols, size_t nnz,
-                                int mont, int c, int W, const uint32_t* __restrict__ eoff,
+                                int mont, FbGeom g, const uint32_t* __restrict__ eoff,
                                 uint32_t* __restrict__ entries) {
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nnz) return;
     fe<Fr> s = load_scalar<Fr>(sc, j);
     if (mont) s = fe_from_mont<Fr>(s);
-    const uint32_t NBk = 1u << (c - 1), i = cols[j];
+    const uint32_t base = cols[j] * (uint32_t)g.stride();
     uint32_t pos = eoff[j];
-    for_each_digit<Fr>(s, c, W, [&](int w, int32_t d) {
+    for_each_digit_fb<Fr>(s, g, [&](int w, int32_t d) {
         if (d != 0)
-            entries[pos++] = (((uint32_t)i * (uint32_t)W + (uint32_t)w) * NBk + (uint32_t)(d < 0 ? -d : d) - 1) |
-                             (d < 0 ? 0x80000000u : 0u);
+            entries[pos++] = (base + (uint32_t)g.off(w) + (uint32_t)(d < 0 ? -d : d) - 1) | (d < 0 ? 0x80000000u : 0u);
     });
 }
 
@@ -1467,7 +1481,8 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     for (size_t j = 0; j < nnz; j++)
         if (cols[j] >= t->n) return VC_E_RANGE;
     if (t->fb_c == 0) VK_TRY(fixed_base_precompute(ctx, t, 8));
-    const int c = t->fb_c, W = t->fb_W;
+    const FbGeom fg = t->fb_geom();
+    const int W = fg.W;
     // rows are cut into chunks of <= CHNZ non-zeros (the accumulate's buckets), so a long row
     // (e.g. a verkle root: 256 children x W windows) does not become one bucket straddling
     // hundreds of threads -- whose pieces the fix-up would add serially; chunk sums are folded
@@ -1482,7 +1497,7 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     }
     rc[batch] = (uint32_t)(cptr.size() - 1);
     const size_t nch = cptr.size() - 1;
-    if ((uint64_t)t->n * W << (c - 1) >= (1ull << 31)) return VC_E_RANGE;  // entry index + sign bit
+    if ((uint64_t)t->n * fg.stride() >= (1ull << 31)) return VC_E_RANGE;  // entry index + sign bit
     const size_t maxL = nnz * (size_t)W;
     if (maxL >= 0xffffffffull) return VC_E_RANGE;
     hipStream_t st = ctx->stream;
@@ -1532,7 +1547,7 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_CHECK_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + nnz, 0, 4, st));
     if (nnz)
         VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(), nnz, mont,
-                  c, W, d_cnt.as<uint32_t>());
+                  fg, d_cnt.as<uint32_t>());
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
                                                   nnz + 1, st));
@@ -1541,7 +1556,7 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
                                                   nnz + 1, st));
     if (nnz)
         VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(),
-                  d_cols.as<uint32_t>(), nnz, mont, c, W, d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
+                  d_cols.as<uint32_t>(), nnz, mont, fg, d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
     VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, d_rp.as<uint64_t>(),
               d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
     // the fixed-base tables hold radix-2^29 limbs (commit.hip FbE): k_msm_accumulate<C, FA>

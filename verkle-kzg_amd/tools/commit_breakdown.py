@@ -1,5 +1,6 @@
 """C3 probe: per-kernel times of one 10k x width-256 Bandersnatch batched commit (fixed-base
-table at window c): fb_commit (chunk-major main kernel), fb_combine, fb_normalize_out."""
+table at window c, or "c:W" for W mixed windows of c / c + 1 bits): fb_commit (chunk-major main
+kernel), fb_combine, fb_normalize_out."""
 import os
 import sys
 import time
@@ -19,9 +20,11 @@ sc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(5))
 dcs = torch.from_numpy(sc.view(np.int64)).to(dev)
 dxy = torch.zeros((B, 8), dtype=torch.int64, device=dev)
 dinf = torch.zeros(B, dtype=torch.uint8, device=dev)
-for c in [int(x) for x in (sys.argv[1:] or ["16"])]:
+for arg in sys.argv[1:] or ["16"]:
+    c, W = (int(v) for v in arg.split(":")) if ":" in arg else (int(arg), 0)
     t0 = time.time()
-    e.fixed_base_precompute(tab, c)
+    e.fixed_base_precompute(tab, c, W)
+    c = f"{c} W={e.fixed_base_geometry(tab)[1]} wide={e.fixed_base_geometry(tab)[2]}"
     torch.cuda.synchronize()
     print(f"precompute c={c}: {time.time() - t0:.2f} s", flush=True)
     e.msm_batch_device(tab, 256, dcs.data_ptr(), B, dxy.data_ptr(), dinf.data_ptr())

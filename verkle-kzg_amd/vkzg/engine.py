@@ -209,8 +209,20 @@ class Engine:
         check(lib().vc_bases_download(self.h, table, _ptr(xy), _ptr(inf)), "vc_bases_download")
         return xy, inf
 
-    def fixed_base_precompute(self, table, window_bits=8):
-        check(lib().vc_fixed_base_precompute(self.h, table, window_bits), "vc_fixed_base_precompute")
+    def fixed_base_precompute(self, table, window_bits=8, windows=0):
+        """Fixed-base window tables; windows > 0 mixes window_bits / window_bits + 1 bit windows."""
+        if windows:
+            check(lib().vc_fixed_base_precompute_windows(self.h, table, window_bits, windows),
+                  "vc_fixed_base_precompute_windows")
+        else:
+            check(lib().vc_fixed_base_precompute(self.h, table, window_bits), "vc_fixed_base_precompute")
+
+    def fixed_base_geometry(self, table):
+        """(window_bits, windows, wide_windows) of the table's fixed-base tables (0s if none)."""
+        c, w, b = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().vc_fixed_base_geometry(self.h, table, ctypes.byref(c), ctypes.byref(w), ctypes.byref(b)),
+              "vc_fixed_base_geometry")
+        return c.value, w.value, b.value
 
     # -------------------------------------------------------------- MSM
     def msm(self, table, scalars, offset=0, mont=False):
