@@ -70,3 +70,46 @@ def test_shared_ctx_eight_threads():
                     assert r[2] is True
     finally:
         eng.close()
+
+
+def test_context_per_thread():
+    """The overlap pattern for rayon-style callers: one vc_ctx per worker
+    thread, each with its own stream and its own copy of the CRS, so latency-bound calls (the IPA
+    prover's dependent rounds) from different threads run on the GPU at the same time instead of
+    queueing on one context's mutex. Proofs must equal the single-context ones."""
+    import vkzg
+    from vkzg import scheme
+    N, T, per = 256, 4, 6
+    crs = scheme.ipa_crs(N + 1, max_=512)
+    rng = np.random.default_rng(12)
+    jobs = [(scheme.LagrangeBasis([int(v) for v in rng.integers(0, 1 << 62, size=N)]), int(rng.integers(0, 4 * N)))
+            for _ in range(T * per)]
+    engs = [vkzg.Engine("bn254") for _ in range(T)]
+    try:
+        ipas = [scheme.IPA(e, N, crs) for e in engs]
+        want = []
+        for data, pt in jobs:
+            com = ipas[0].commit(data)
+            want.append((com, str(ipas[0].prove_point(com, pt, data).as_dict())))
+        got = [None] * len(jobs)
+        errors = []
+
+        def worker(k):
+            try:
+                for i in range(k, len(jobs), T):
+                    data, pt = jobs[i]
+                    com = ipas[k].commit(data)
+                    got[i] = (com, str(ipas[k].prove_point(com, pt, data).as_dict()))
+            except Exception as ex:  # surfaced below
+                errors.append(ex)
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(T)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errors, errors
+        assert got == want
+    finally:
+        for e in engs:
+            e.close()
