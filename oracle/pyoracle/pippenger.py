@@ -126,3 +126,21 @@ def radix_bucket_sum(buckets, lseg):
     J = max(1, (S - 1).bit_length())
     T = [sum(R[s] for s in range(S) if (s >> j) & 1) for j in range(J)]
     return A + lseg * sum(t << j for j, t in enumerate(T))
+
+
+def radix_bucket_sum_residue(buckets, lseg):
+    """The residue form of the same reduction (msm_tail.hip k_msm_segr + the U sums of
+    k_msm_bitsum, msm.hip shared_set_sum): with b = lseg s + r,
+    V = lseg * sum_j 2^j T_j + sum_r (r + 1) U_r,  U_r = sum_s B_{lseg s + r},
+    and sum_r (r + 1) U_r taken as the host does it, by suffix sums."""
+    S = len(buckets) // lseg
+    R = [sum(buckets[s * lseg:(s + 1) * lseg]) for s in range(S)]
+    U = [sum(buckets[s * lseg + r] for s in range(S)) for r in range(lseg)]
+    J = max(1, (S - 1).bit_length())
+    T = [sum(R[s] for s in range(S) if (s >> j) & 1) for j in range(J)]
+    v = lseg * sum(t << j for j, t in enumerate(T))
+    suf = 0
+    for r in range(lseg - 1, -1, -1):
+        suf += U[r]
+        v += suf
+    return v

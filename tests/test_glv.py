@@ -116,3 +116,4 @@ def test_radix_bucket_reduction_identity():
         for lseg in (1, 4, 5):
             b = [rng.randrange(1 << 64) for _ in range(S * lseg)]
             assert pippenger.radix_bucket_sum(b, lseg) == sum((i + 1) * x for i, x in enumerate(b))
+            assert pippenger.radix_bucket_sum_residue(b, lseg) == sum((i + 1) * x for i, x in enumerate(b))

@@ -890,6 +890,7 @@ struct MsmSlice {
     uint32_t wps = 0;     // shared windows: windows per set (the window copies' count)
     int Wr = 0;           // bucket sets reduced: `sets` shared, W otherwise
     uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
+    uint32_t nU = 1;  // sums per set after the J bit sums: A (1), or the Lseg residue sums U_r
     uint32_t* offsets = nullptr;
     uint32_t* chain_max = nullptr;  // in the WS_TAIL buffer, tail_bytes after the tail points
     size_t tail_bytes = 0;
@@ -944,6 +945,9 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     const uint32_t S = NB / Lseg;  // power of two
     uint32_t J = 0;
     while ((1u << J) < S) J++;
+    // shared windows with segments: the residue form of the reduction (msm_tail.hip k_msm_segr)
+    static const int resid_env = getenv("VKZG_TAIL_RESIDUE") ? atoi(getenv("VKZG_TAIL_RESIDUE")) : 1;  // A/B probe
+    const uint32_t nU = (sl.shared && Lseg > 1 && resid_env) ? Lseg : 1;
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     hipStream_t st = L.st;
 
@@ -986,9 +990,10 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     VK_TRY(ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(ws[WS_SEG].ensure((size_t)S * Wr * sizeof(RAcc)));
     VK_TRY(ws[WS_TREE].ensure((size_t)S * Wr * sizeof(RAcc)));
-    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * (J + 1) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)Wr, J)) * sizeof(RAcc)));
+    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * (J + nU) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)Wr, J, 64, nU)) *
+                             sizeof(RAcc)));
     // tail points, then the chain_max word: one read-back
-    const size_t tail_bytes = ((size_t)Wr * (J + 1) * sizeof(Acc) + 15) & ~(size_t)15;
+    const size_t tail_bytes = ((size_t)Wr * (J + nU) * sizeof(Acc) + 15) & ~(size_t)15;
     VK_TRY(ws[WS_TAIL].ensure(tail_bytes + 16));
 
     sl.NB = NB;
@@ -998,6 +1003,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.Lseg = Lseg;
     sl.S = S;
     sl.J = J;
+    sl.nU = nU;
     sl.offsets = ws[WS_OFFSETS].as<uint32_t>();
     sl.tail_bytes = tail_bytes;
     sl.chain_max = reinterpret_cast<uint32_t*>(ws[WS_TAIL].as<uint8_t>() + tail_bytes);
@@ -1036,14 +1042,14 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     else
         VK_TRY(msm_tail_fixup_walk<C>(ctx, L, sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.owner, 1u << sl.guard));
     VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, Wr, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
-                              sl.tail));
+                              sl.tail, nU > 1));
     return VC_OK;
 }
 
 // read back (after every slice has been enqueued: a copy into pageable memory may block the host)
 template <class C>
 static int slice_fetch(MsmSlice<C>& sl) {
-    sl.ht.resize((size_t)sl.Wr * (sl.J + 1));
+    sl.ht.resize((size_t)sl.Wr * (sl.J + sl.nU));
     VK_TRY(sl.L.pin->ensure(sl.tail_bytes + 16));
     VK_CHECK_HIP(hipMemcpyAsync(sl.L.pin->p, sl.tail, sl.tail_bytes + 4, hipMemcpyDeviceToHost, sl.L.st));
     return VC_OK;
@@ -1053,11 +1059,12 @@ template <class C>
 static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res);
 
 // the reduced points of bucket set `set` (shared windows: one MSM each) -> its sum
+//   Lseg sum_j 2^j T_j + A,  A = sum_r (r + 1) U_r = sum_k (U_k + ... + U_{nU-1}) (suffix sums)
 template <class C>
 static typename C::Acc shared_set_sum(const MsmSlice<C>& sl, int set) {
     using Acc = typename C::Acc;
     const uint32_t J = sl.J;
-    const Acc* ht = sl.ht.data() + (size_t)set * (J + 1);
+    const Acc* ht = sl.ht.data() + (size_t)set * (J + sl.nU);
     Acc x = C::zero();  // sum_j 2^j T_j
     for (int j = (int)J - 1; j >= 0; j--) {
         if (!C::is_zero(x)) x = C::dbl(x);
@@ -1068,7 +1075,12 @@ static typename C::Acc shared_set_sum(const MsmSlice<C>& sl, int set) {
         if (!C::is_zero(r)) r = C::dbl(r);
         if ((sl.Lseg >> b) & 1) r = C::add(r, x);
     }
-    return C::add(r, ht[J]);
+    Acc suf = C::zero();
+    for (int k = (int)sl.nU - 1; k >= 0; k--) {
+        suf = C::add(suf, ht[J + k]);
+        r = C::add(r, suf);
+    }
+    return r;
 }
 
 template <class C>
@@ -1081,7 +1093,7 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
         VK_TRY(msm_tail_fixup<C>(ctx, sl.L, sl.Tmax, sl.offsets + sl.NBtot, sl.M, sl.buckets, sl.carry, sl.through,
                                  sl.owner, sl.owner_b, sl.chain_max, 0));
         VK_TRY(msm_tail_reduce<C>(ctx, sl.L, sl.buckets, sl.offsets, sl.NB, sl.Wr, sl.Lseg, sl.S, sl.J, sl.seg,
-                                  sl.rs, sl.bsum_part, sl.tail));
+                                  sl.rs, sl.bsum_part, sl.tail, sl.nU > 1));
         VK_CHECK_HIP(hipMemcpyAsync(sl.ht.data(), sl.tail, sl.ht.size() * sizeof(Acc), hipMemcpyDeviceToHost,
                                     sl.L.st));
         VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
@@ -1093,7 +1105,7 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
         for (int k = 0; k < sl.sets; k++) res[k] = shared_set_sum<C>(sl, k);
         return VC_OK;
     }
-    if (sl.shared && (sl.Lseg & (sl.Lseg - 1)) != 0) {  // radix buckets: Lseg = m is odd
+    if (sl.shared) {  // one bucket set: Lseg x (radix buckets: Lseg = m is odd) and the U_r weights
         *res = shared_set_sum<C>(sl, 0);
         return VC_OK;
     }

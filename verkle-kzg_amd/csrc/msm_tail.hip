@@ -210,6 +210,46 @@ __global__ void __launch_bounds__(256) k_msm_segsum_q(const typename A::Acc* __r
     }
 }
 
+// Residue form of the reduction (the radix shared-window MSM, Lseg = m = 5): with b = Lseg s + r,
+//   V = sum_b (b + 1) B_b = Lseg sum_s s R_s + sum_r (r + 1) U_r,   U_r = sum_s B_{Lseg s + r},
+// so the segment stage only needs R_s = sum_r B_{Lseg s + r} (Lseg - 1 dependent adds instead of
+// the 2 Lseg of acc_s and R_s), and the bit stage adds the Lseg sums U_r (bucket columns of S
+// items) beside its J sums T_j; the host weighs U_r by r + 1 (shared_set_sum).
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_segr(const typename A::Acc* __restrict__ buckets,
+                                                 const uint32_t* __restrict__ offsets, uint32_t NB, int W,
+                                                 uint32_t Lseg, uint32_t S, typename A::Acc* __restrict__ Rs) {
+    using Acc = typename A::Acc;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t w = gid / S, s = gid % S;
+    if (w >= (uint32_t)W) return;
+    const size_t g0 = (size_t)w * NB + (size_t)s * Lseg;
+    Acc R = A::zero();
+    for (uint32_t r = 0; r < Lseg; r++) {
+        const size_t g = g0 + r;
+        const Acc y = offsets[g + 1] > offsets[g] ? buckets[g] : A::zero();
+        R = A::add(R, y);
+    }
+    Rs[gid] = R;
+}
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_segr_q(const typename A::Acc* __restrict__ buckets,
+                                                   const uint32_t* __restrict__ offsets, uint32_t NB, int W,
+                                                   uint32_t Lseg, uint32_t S, typename A::Acc* __restrict__ Rs) {
+    using Acc = typename A::Acc;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, q = gid >> 2, role = gid & 3;
+    const uint32_t w = q / S, s = q % S;
+    if (w >= (uint32_t)W) return;  // whole quads
+    const size_t g0 = (size_t)w * NB + (size_t)s * Lseg;
+    Acc R = A::zero();
+    for (uint32_t r = 0; r < Lseg; r++) {
+        const size_t g = g0 + r;
+        const Acc y = offsets[g + 1] > offsets[g] ? buckets[g] : A::zero();
+        R = A::add_quad(R, y, role);
+    }
+    if (role == 0) Rs[q] = R;
+}
+
 template <class A>
 __device__ __forceinline__ typename A::Acc shfl_acc(const typename A::Acc& v, uint32_t m) {
     static_assert(sizeof(typename A::Acc) % 4 == 0, "");
@@ -223,26 +263,39 @@ __device__ __forceinline__ typename A::Acc shfl_acc(const typename A::Acc& v, ui
 
 // stage 1: lane sums K (msm_bitsum_k) selected items of one (w, q) sum serially, then the wave
 // folds its 64 lane sums (xor butterfly) -- K + 6 iterations of one add:
-//   q < J: R_s over s with bit q set (S/2 items, nb1 waves);  q == J: acc_s (S items, nb2 waves).
+//   q < J: T_q = R_s over s with bit q set (S/2 items of tsrc, nb1 waves);
+//   q = J + u (u < nU): U_u = item nU m + u of usrc over m < S (S items, nb2 waves) -- nU = 1 with
+//   usrc = acc_s is the sum A = sum_s acc_s, nU = Lseg with usrc = the buckets the residue sums.
+// tsrc / usrc item liveness from toff / uoff (bucket offsets: an empty bucket was never written)
+// when they are buckets, none otherwise.
 // Waves are laid out compactly (window by window: J x nb1 bit-sum waves, then nb2), so the grid
 // holds only busy waves and every CU gets at most one block (a grid with idle waves let the
 // dispatcher stack two busy blocks on some CUs: their SIMDs ran two waves, twice as long).
 template <class A>
-__global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __restrict__ accs,
-                                                   const typename A::Acc* __restrict__ Rs, uint32_t S, uint32_t J,
-                                                   uint32_t K, uint32_t nb1, uint32_t nb2, uint32_t n_waves,
-                                                   const uint32_t* __restrict__ offsets,
+__global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __restrict__ usrc,
+                                                   const typename A::Acc* __restrict__ tsrc, uint32_t S, uint32_t J,
+                                                   uint32_t nU, uint32_t K, uint32_t nb1, uint32_t nb2,
+                                                   uint32_t n_waves, const uint32_t* __restrict__ toff,
+                                                   const uint32_t* __restrict__ uoff,
                                                    typename A::Acc* __restrict__ partial) {
     using Acc = typename A::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
-    const uint32_t per_w = J * nb1 + nb2;
+    const uint32_t per_w = J * nb1 + nU * nb2;
     const uint32_t w = gw / per_w, r = gw % per_w;
-    const uint32_t q = r < J * nb1 ? r / nb1 : J;
-    const uint32_t wv = r < J * nb1 ? r % nb1 : r - J * nb1;
+    const uint32_t q = r < J * nb1 ? r / nb1 : J + (r - J * nb1) / nb2;
+    const uint32_t wv = r < J * nb1 ? r % nb1 : (r - J * nb1) % nb2;
     const uint32_t n_items = q < J ? S / 2 : S;
     const uint32_t base = wv * 64 * K;
-    const Acc* src = (q < J ? Rs : accs) + (size_t)w * S;
+    const uint32_t u = q - J;  // q >= J: the column of the U sum
+    const size_t set0 = q < J ? (size_t)w * S : (size_t)w * S * nU;
+    const Acc* src = (q < J ? tsrc : usrc) + set0;
+    const uint32_t* off = (q < J ? toff : uoff);
+    if (off) off += set0;
+    // item m of this sum -> its index in src (T_q: the m-th s with bit q set; U_u: nU m + u)
+    auto item = [&](uint32_t m) -> uint32_t {
+        return q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m * nU + u;
+    };
     Acc v = A::zero();
     if constexpr (A::quad) {
         // K serial full adds per lane (every SIMD busy: issue-bound), then the wave's 64 lane sums
@@ -251,9 +304,8 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
         // adds (~30k cycles each)
         for (uint32_t it = 0; it < K; it++) {
             const uint32_t m = base + it * 64 + lane;
-            const uint32_t idx = q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m;
-            const size_t g = (size_t)w * S + idx;
-            const bool live = m < n_items && (!offsets || offsets[g + 1] > offsets[g]);
+            const uint32_t idx = item(m);
+            const bool live = m < n_items && (!off || off[idx + 1] > off[idx]);
             const Acc o = live ? src[idx] : A::zero();
             v = A::add(v, o);
         }
@@ -270,11 +322,8 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
         Acc o;
         if (it < K) {
             const uint32_t m = base + it * 64 + lane;  // lane-interleaved rows
-            const uint32_t idx = q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m;
-            // Lseg = 1 (no segment stage): the items are the buckets themselves (offsets != null),
-            // an empty bucket was never written
-            const size_t g = (size_t)w * S + idx;
-            const bool live = m < n_items && (!offsets || offsets[g + 1] > offsets[g]);
+            const uint32_t idx = item(m);
+            const bool live = m < n_items && (!off || off[idx + 1] > off[idx]);
             o = live ? src[idx] : A::zero();
         } else {
             o = shfl_acc<A>(v, 1u << (it - K));
@@ -288,12 +337,13 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
 // the butterfly)
 template <class C, class A>
 __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __restrict__ partial, uint32_t J,
-                                                   uint32_t nb1, uint32_t nb2, typename C::Acc* __restrict__ out) {
+                                                   uint32_t nU, uint32_t nb1, uint32_t nb2,
+                                                   typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
-    const uint32_t w = sum / (J + 1), q = sum % (J + 1);
+    const uint32_t w = sum / (J + nU), q = sum % (J + nU);
     const uint32_t cnt = q < J ? nb1 : nb2;
-    const size_t start = (size_t)w * (J * nb1 + nb2) + (q < J ? q * nb1 : J * nb1);
+    const size_t start = (size_t)w * (J * nb1 + nU * nb2) + (q < J ? q * nb1 : J * nb1 + (q - J) * nb2);
     uint32_t span = 1, lg = 0;
     while (span < cnt && span < 64) {
         span <<= 1;
@@ -323,16 +373,16 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
 constexpr uint32_t SUMPART_WAVES = 4;
 template <class C, class A>
 __global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial,
-                                                                     uint32_t J, uint32_t nb1, uint32_t nb2,
-                                                                     typename C::Acc* __restrict__ out) {
+                                                                     uint32_t J, uint32_t nU, uint32_t nb1,
+                                                                     uint32_t nb2, typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
     constexpr uint32_t QPB = 16 * SUMPART_WAVES, LGW = SUMPART_WAVES == 4 ? 2 : SUMPART_WAVES == 2 ? 1 : 0;
     static_assert((1u << LGW) == SUMPART_WAVES, "SUMPART_WAVES: 1, 2 or 4");
     __shared__ Acc wave_sum[SUMPART_WAVES];
     const uint32_t sum = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, role = lane & 3;
-    const uint32_t w = sum / (J + 1), q = sum % (J + 1);
+    const uint32_t w = sum / (J + nU), q = sum % (J + nU);
     const uint32_t cnt = q < J ? nb1 : nb2;
-    const size_t start = (size_t)w * (J * nb1 + nb2) + (q < J ? q * nb1 : J * nb1);
+    const size_t start = (size_t)w * (J * nb1 + nU * nb2) + (q < J ? q * nb1 : J * nb1 + (q - J) * nb2);
     const uint32_t nk = (cnt + QPB - 1) / QPB;
     Acc v = A::zero();
     for (uint32_t it = 0; it < nk + 4 + LGW; it++) {  // one add call site
@@ -445,16 +495,36 @@ int msm_tail_fixup_more(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uin
     return VC_OK;
 }
 
-// outputs W x (J + 1) points in ec.hpp form: [w][q] = T_wq (q < J), A_w (q == J)
+// outputs W x (J + nU) points in ec.hpp form: [w][q] = T_wq (q < J), then A_w (nU = 1) or the
+// residue sums U_w,u (nU = Lseg, `residue`)
 template <class C>
 int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
-                    typename C::Acc* out) {
+                    typename C::Acc* out, bool residue) {
     using A = typename Fast29<C>::type;
-    const uint32_t* live = nullptr;
+    const uint32_t* toff = nullptr;
+    const uint32_t* uoff = nullptr;
+    const FAcc<C>* usrc = accs;
+    uint32_t nU = 1;
     if (Lseg == 1) {  // segments of one bucket: R_s = acc_s = B_s, read in place
         accs = Rs = const_cast<FAcc<C>*>(buckets);
-        live = offsets;
+        usrc = buckets;
+        toff = uoff = offsets;
+    } else if (residue) {
+        nU = Lseg;
+        usrc = buckets;
+        uoff = offsets;
+        static const int segrq_env = getenv("VKZG_SEGR_QUAD") ? atoi(getenv("VKZG_SEGR_QUAD")) : 1;  // A/B probe
+        bool quads = false;
+        if constexpr (A::quad) {
+            quads = segrq_env != 0 && (size_t)S * W <= 65536;
+            if (quads)
+                VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segr_q<A>), (S * (uint32_t)W * 4 + 255) / 256, 256, 0,
+                             buckets, offsets, NB, W, Lseg, S, Rs);
+        }
+        if (!quads)
+            VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segr<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets,
+                         offsets, NB, W, Lseg, S, Rs);
     } else {
         static const int segq_env = getenv("VKZG_SEGSUM_QUAD") ? atoi(getenv("VKZG_SEGSUM_QUAD")) : 1;  // A/B probe
         bool quads = false;
@@ -468,17 +538,17 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
             VK_LAUNCH_ON(ctx, L.st, "msm_segsum", (k_msm_segsum<A>), (S * (uint32_t)W + 255) / 256, 256, 0, buckets,
                          offsets, NB, W, Lseg, S, accs, Rs);
     }
-    const uint32_t sums = (uint32_t)W * (J + 1);
-    const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J);
+    const uint32_t sums = (uint32_t)W * (J + nU);
+    const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J, 64, nU);
     const uint32_t nb1 = msm_bitsum_pw(S / 2, K), nb2 = msm_bitsum_pw(S, K);
-    const uint32_t n_waves = (uint32_t)W * (J * nb1 + nb2);
-    VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, accs, Rs, S, J, K, nb1, nb2,
-              n_waves, live, partial);
+    const uint32_t n_waves = (uint32_t)W * (J * nb1 + nU * nb2);
+    VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, usrc, Rs, S, J, nU, K,
+                 nb1, nb2, n_waves, toff, uoff, partial);
     if constexpr (A::quad)
-        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, nb1,
-                     nb2, out);
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, nU,
+                     nb1, nb2, out);
     else
-        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nb1, nb2, out);
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nU, nb1, nb2, out);
     return VC_OK;
 }
 
@@ -490,7 +560,7 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
     template int msm_tail_fixup_walk<C>(vc_ctx*, Lane, const uint32_t*, uint32_t, uint32_t, FAcc<C>*, const FAcc<C>*, \
                                         const FAcc<C>*, uint32_t);                                             \
     template int msm_tail_reduce<C>(vc_ctx*, Lane, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
-                                    uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*);
+                                    uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*, bool);
 VK_INST_TAIL(BN254G1)
 VK_INST_TAIL(BLS381G1)
 VK_INST_TAIL(Bandersnatch)

@@ -12,10 +12,10 @@ namespace vk {
 // 960 of K = 8 on a GLV 2^20 MSM). lanes = logical lanes per wave (64; 16 for quads of the
 // cooperative add, SW29::add_quad -- not used here: with every SIMD busy the stage is issue-bound,
 // and quads' 2.1x shorter adds lose to their 4x fewer lanes)
-inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J, uint32_t lanes = 64) {
+inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J, uint32_t lanes = 64, uint32_t nU = 1) {
     for (uint32_t k = 2; k < 32; k++) {
         const uint64_t per = (uint64_t)lanes * k;
-        const uint64_t busy = (uint64_t)W * ((uint64_t)J * ((S / 2 + per - 1) / per) + (S + per - 1) / per);
+        const uint64_t busy = (uint64_t)W * ((uint64_t)J * ((S / 2 + per - 1) / per) + nU * ((S + per - 1) / per));
         if (busy <= 1024) return k;
     }
     return 32;
@@ -52,5 +52,5 @@ inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {
 template <class C>
 int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
-                    typename C::Acc* out);
+                    typename C::Acc* out, bool residue = false);
 }  // namespace vk
