@@ -13,4 +13,4 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 echo smoke-done
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
 echo bench-done
-bash $R/tools_profile.sh $TAG
+[ "${2:-}" = "noprof" ] || bash $R/tools_profile.sh $TAG
