@@ -1040,7 +1040,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
         VK_TRY(msm_tail_fixup<C>(ctx, L, Tmax, sl.offsets + NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
                                  sl.owner_b, sl.chain_max, sl.guard));
     else
-        VK_TRY(msm_tail_fixup_walk<C>(ctx, L, sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.owner, 1u << sl.guard));
+        VK_TRY(msm_tail_fixup_walk<C>(ctx, L, sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.owner, 1u << sl.guard,
+                                      sl.owner_b, sl.through, Tmax));
     VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, Wr, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
                               sl.tail, nU > 1));
     return VC_OK;

@@ -118,6 +118,36 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk_q(typename A::Acc* __res
     if (role == 0) buckets[b] = acc;
 }
 
+// The same walk with a lane per accumulate THREAD: the owner thread t of a straddling bucket
+// (owner_bucket[t] != NONE) adds the carry pieces of t + 1 .. u1 (through == 2 continues, 1 ends).
+// Denser than a lane per bucket when there are fewer threads than buckets -- the radix
+// shared-window MSM has ~90 entries per bucket and 112 per thread: 131K lanes, every one an
+// owner, two waves per SIMD in one round, where the 164K lanes per bucket took 2.5 waves per
+// SIMD, i.e. two rounds. Chains longer than `limit` are left to the host path, as above.
+template <class A>
+__global__ void __launch_bounds__(256) k_msm_fixup_own(typename A::Acc* __restrict__ buckets,
+                                                      const typename A::Acc* __restrict__ carry,
+                                                      const typename A::Acc* __restrict__ owner_piece,
+                                                      const uint32_t* __restrict__ owner_bucket,
+                                                      const uint8_t* __restrict__ through, uint32_t Tmax,
+                                                      const uint32_t* __restrict__ Lp, uint32_t M, uint32_t limit) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t T = (*Lp + M - 1) / M;
+    if (t >= T || t >= Tmax) return;
+    const uint32_t b = owner_bucket[t];
+    if (b == NONE_T) return;
+    // an owner piece exists only when the bucket continues into t + 1, so the chain ends in a
+    // thread u1 < T with through[u1] == 1
+    uint32_t u1 = t + 1;
+    while (through[u1] == 2) {
+        if (u1 - t >= limit) return;  // longer than the walk takes: host path
+        u1++;
+    }
+    typename A::Acc acc = owner_piece[t];
+    for (uint32_t u = t + 1; u <= u1; u++) acc = A::add(acc, carry[u]);
+    buckets[b] = acc;
+}
+
 // c ? a : b word by word through masks: a plain select of two aggregates becomes a load through a
 // selected address, which keeps both in scratch memory for the whole loop
 template <class T>
@@ -462,9 +492,17 @@ int msm_tail_fixup(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uint32_t
 // the serial walk of every owner over at most `limit` carry pieces (see k_msm_fixup_walk)
 template <class C>
 int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t NBtot, uint32_t M, FAcc<C>* buckets,
-                        const FAcc<C>* carry, const FAcc<C>* owner, uint32_t limit) {
+                        const FAcc<C>* carry, const FAcc<C>* owner, uint32_t limit, const uint32_t* owner_b,
+                        const uint8_t* through, uint32_t Tmax) {
     using A = typename Fast29<C>::type;
     static const int quad_env = getenv("VKZG_FIXUP_QUAD") ? atoi(getenv("VKZG_FIXUP_QUAD")) : 1;  // A/B probe
+    static const int own_env = getenv("VKZG_FIXUP_OWN") ? atoi(getenv("VKZG_FIXUP_OWN")) : 1;     // A/B probe
+    // fewer accumulate threads than buckets: a lane per owner thread (k_msm_fixup_own)
+    if (own_env && owner_b && Tmax <= NBtot) {
+        VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_own<A>), (Tmax + 255) / 256, 256, 0, buckets, carry, owner,
+                     owner_b, through, Tmax, offsets + NBtot, M, limit);
+        return VC_OK;
+    }
     // quads while their waves fit ~2 per SIMD (one bucket set: 2^15 buckets -> 2048 waves); with
     // per-window bucket sets (8 x 2^15) every SIMD already has lane-per-bucket waves and the
     // quads' ~2x instructions per add made the walk slower (0.08 -> 0.115 ms)
@@ -558,7 +596,7 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
     template int msm_tail_fixup_more<C>(vc_ctx*, Lane, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,      \
                                         const uint8_t*, const FAcc<C>*, const uint32_t*, uint32_t, uint32_t);   \
     template int msm_tail_fixup_walk<C>(vc_ctx*, Lane, const uint32_t*, uint32_t, uint32_t, FAcc<C>*, const FAcc<C>*, \
-                                        const FAcc<C>*, uint32_t);                                             \
+                                        const FAcc<C>*, uint32_t, const uint32_t*, const uint8_t*, uint32_t);                                             \
     template int msm_tail_reduce<C>(vc_ctx*, Lane, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
                                     uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*, bool);
 VK_INST_TAIL(BN254G1)

@@ -40,7 +40,8 @@ int msm_tail_fixup_more(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uin
                         uint32_t guarded, uint32_t Lmax);
 template <class C>
 int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t NBtot, uint32_t M, FAcc<C>* buckets,
-                        const FAcc<C>* carry, const FAcc<C>* owner, uint32_t limit);
+                        const FAcc<C>* carry, const FAcc<C>* owner, uint32_t limit, const uint32_t* owner_b = nullptr,
+                        const uint8_t* through = nullptr, uint32_t Tmax = 0);
 // guarded rounds for nv entries over NB buckets per window at M entries per thread: covers a
 // bucket of 4x the mean load (the top window of a GLV split uses half its buckets: 2x)
 inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {

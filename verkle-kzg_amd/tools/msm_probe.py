@@ -18,6 +18,8 @@ curve = sys.argv[1] if len(sys.argv) > 1 else "bls12_381"
 n = 1 << (int(sys.argv[2]) if len(sys.argv) > 2 else 20)
 e = vkzg.Engine(curve, 0)
 e.set_stream(torch.cuda.current_stream().cuda_stream)
+if os.environ.get("VKZG_MSM_SHARED") == "0":  # per-window buckets, no window copies (variable base)
+    e.set_option(e.OPT_MSM_SHARED_WINDOWS, 0)
 tid = e.random_bases(n, seed=2024)
 sc = vkzg.random_scalars(curve, n, np.random.default_rng(1234))
 d = torch.from_numpy(sc.view(np.int64).copy()).cuda()
