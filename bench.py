@@ -226,7 +226,8 @@ def kzg_line(a, rank, world, local, dev, stream):
             dt = float(tt.item())
         keng.enable_timing(False)
         qk = {}
-        for k in ("kzg_den", "binv_prep", "binv_finish", "kzg_q_in", "kzg_q_out", "kzg_bary", "powers", "to_mont"):
+        for k in ("kzg_den", "binv_prep", "binv_finish", "kzg_q_in", "kzg_q_out", "kzg_bary", "kzg_fold",
+                  "kzg_inv_shift", "powers", "to_mont"):
             ms, cnt = keng.kernel_time(k)
             if cnt:
                 qk[k] = round(ms / cnt, 4)

@@ -219,6 +219,7 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         ctx->pin_io.release();
         ctx->pin_small.release();
         ctx->pin_norm.release();
+        ctx->pin_y.release();
         for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
         ctx->pool_free.clear();
         for (auto& p : ctx->pending) {

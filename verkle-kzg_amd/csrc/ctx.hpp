@@ -176,6 +176,7 @@ struct vc_ctx {
     vk::PinBuf pin_io;              // host <-> device staging of the scheme paths (commit_batch)
     vk::PinBuf pin_small;           // block partials of the small-batch commit path
     vk::PinBuf pin_norm;            // block products / inverses of the split normalisation
+    vk::PinBuf pin_y;               // the KZG opening's y, copied back asynchronously
     // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
     // (or are synchronised), so a block freed by one call is safely reused by the next in
     // stream order; vc_ctx_set_stream drains the old stream first

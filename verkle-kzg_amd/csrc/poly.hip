@@ -138,22 +138,14 @@ __global__ void __launch_bounds__(256) k_bary_partial(const fe<F>* __restrict__ 
     if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
 }
 
-// q_i = (f_i - y) * inv_i   (outside domain)
-template <class F>
-__global__ void k_q_out(const fe<F>* __restrict__ f, size_t max, const fe<F>* __restrict__ inv, size_t n, fe<F> y,
-                        fe<F>* __restrict__ q) {
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fe<F> fi = i < max ? f[i] : fe_zero<F>();
-    q[i] = fe_mul<F>(fe_sub<F>(fi, y), inv[i]);
-}
-
 // in domain at m: q_i = (f_i - f_m) * inv_i (i != m); partial sums of q_i * w^i for q_m
+// (f_m read here: the host needs no round trip before the launch)
 template <class F>
 __global__ void __launch_bounds__(256) k_q_in(const fe<F>* __restrict__ f, size_t max, const fe<F>* __restrict__ inv,
-                                             const fe<F>* __restrict__ pw, size_t n, size_t m, fe<F> fm,
+                                             const fe<F>* __restrict__ pw, size_t n, size_t m,
                                              fe<F>* __restrict__ q, fe<F>* __restrict__ partial) {
     __shared__ fe<F> sh[256];
+    const fe<F> fm = m < max ? f[m] : fe_zero<F>();
     size_t i0 = (size_t)blockIdx.x * 256 * 8 + threadIdx.x;
     fe<F> acc = fe_zero<F>();
     for (int k = 0; k < 8; k++) {
@@ -180,6 +172,35 @@ __global__ void __launch_bounds__(256) k_q_in(const fe<F>* __restrict__ f, size_
 template <class F>
 __global__ void k_set(fe<F>* __restrict__ a, size_t i, fe<F> v) {
     if (blockIdx.x == 0 && threadIdx.x == 0) a[i] = v;
+}
+
+// one block: s = sum of the nb block partials; in domain a[m] = k s (q_m = -w^-m sum q_i w^i),
+// outside *y = k s (y = -t sum f_i w^i inv_i) -- on the device, so the open has no host round
+// trip between the quotient and the MSM
+template <class F>
+__global__ void __launch_bounds__(256) k_fold_partials(const fe<F>* __restrict__ partial, size_t nb, fe<F> k,
+                                                      fe<F>* __restrict__ dst) {
+    __shared__ fe<F> sh[256];
+    fe<F> acc = fe_zero<F>();
+    for (size_t b = threadIdx.x; b < nb; b += 256) acc = fe_add<F>(acc, partial[b]);
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) sh[threadIdx.x] = fe_add<F>(sh[threadIdx.x], sh[threadIdx.x + h]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *dst = fe_mul<F>(k, sh[0]);
+}
+
+// q_i = (f_i - y) * inv_i (outside domain), y on the device
+template <class F>
+__global__ void k_q_out(const fe<F>* __restrict__ f, size_t max, const fe<F>* __restrict__ inv, size_t n,
+                          const fe<F>* __restrict__ yp, fe<F>* __restrict__ q) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const fe<F> y = *yp;
+    fe<F> fi = i < max ? f[i] : fe_zero<F>();
+    q[i] = fe_mul<F>(fe_sub<F>(fi, y), inv[i]);
 }
 
 // ---------------------------------------------------------------- Lagrange SRS (A.7)
@@ -224,10 +245,13 @@ __global__ void k_fixed_mul_gen(const fe<Fr>* __restrict__ sc_mont, size_t n, ty
 
 // ---------------------------------------------------------------- host drivers
 template <class F>
-static fe<F> host_sum(const std::vector<fe<F>>& v) {
-    fe<F> a = fe_zero<F>();
-    for (auto& x : v) a = fe_add<F>(a, x);
-    return a;
+static fe<F> host_pow(fe<F> a, uint64_t e) {
+    fe<F> r = fe_one<F>();
+    for (; e; e >>= 1) {
+        if (e & 1) r = fe_mul<F>(r, a);
+        a = fe_sqr<F>(a);
+    }
+    return r;
 }
 
 template <class F>
@@ -338,7 +362,10 @@ int domain_tables(vc_ctx* ctx, const fe<F>& w, size_t n, const fe<F>** pw, const
     return VC_OK;
 }
 
-// q and y for KZG prove_point (device, Montgomery). point given in Montgomery form.
+// q and y for KZG prove_point (device, Montgomery). point given in Montgomery form. The stream is
+// not synchronised in the domain and once (the batch inversion's host step) outside it: y (a
+// device value) is copied into *y_out (page-locked host memory) asynchronously, so the caller
+// reads *y_out only after synchronising ctx->stream (its MSM does).
 template <class F>
 int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
                      fe<F>* d_q, fe<F>* y_out, DevBuf& pw, DevBuf& tmp, DevBuf& part) {
@@ -347,11 +374,11 @@ int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const 
     VK_TRY(tmp.ensure(n * sizeof(fe<F>)));
     fe<F>* den = d_q;  // denominators staged in the output buffer, inverses in tmp
     size_t nblk = (n + 2047) / 2048;
-    VK_TRY(part.ensure(nblk * sizeof(fe<F>)));
+    VK_TRY(part.ensure((nblk + 1) * sizeof(fe<F>)));
+    fe<F>* d_y = part.as<fe<F>>() + nblk;  // the device y, after the block partials
     fe<F>* pwp = nullptr;
     VK_TRY(cached_powers<F>(ctx, omega, n, &pwp));
     fe<F>* inv = tmp.as<fe<F>>();
-    std::vector<fe<F>> hp(nblk);
     // prove_point: `point <= size` -> in-domain branch with index to_usize(point)
     fe<F> pc = fe_from_mont<F>(point);
     bool small = true;
@@ -360,45 +387,33 @@ int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const 
     if (small && pv <= n) {
         if (pv == n) return VC_E_DOMAIN;  // reference: vanishing_at(size) out of bounds
         size_t m = (size_t)pv;
-        // y = evaluate(point): stored value, or 0 inside [max, size]
-        fe<F> fm = fe_zero<F>();
-        if (m < max) VK_CHECK_HIP(hipMemcpyAsync(&fm, d_f + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
-        fe<F> wm, wminv;
-        VK_CHECK_HIP(hipMemcpyAsync(&wm, pwp + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
-        VK_CHECK_HIP(hipMemcpyAsync(&wminv, pwp + ((n - m) & (n - 1)), sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        // w^-m = w^(n - m) on the host (the powers table holds the same values)
+        const fe<F> wminv = host_pow<F>(omega, (n - m) & (n - 1));
         fe<F>* inv1 = nullptr;
         VK_TRY(cached_inv1<F>(ctx, pwp, n, &inv1));
-        VK_CHECK_HIP(hipStreamSynchronize(st));
         VK_LAUNCH(ctx, "kzg_inv_shift", (k_inv_shift<F>), (n + 255) / 256, 256, 0, inv1, n, m, wminv, inv);
-        VK_LAUNCH(ctx, "kzg_q_in", (k_q_in<F>), nblk, 256, 0, d_f, max, inv, pwp, n, m, fm, d_q,
-                  part.as<fe<F>>());
-        VK_CHECK_HIP(hipMemcpyAsync(hp.data(), part.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, st));
-        VK_CHECK_HIP(hipStreamSynchronize(st));
+        VK_LAUNCH(ctx, "kzg_q_in", (k_q_in<F>), nblk, 256, 0, d_f, max, inv, pwp, n, m, d_q, part.as<fe<F>>());
         // q_m = -w^-m * sum_{i != m} q_i w^i
-        fe<F> s = host_sum<F>(hp);
-        fe<F> qm = fe_neg<F>(fe_mul<F>(s, fe_inv_bin<F>(wm)));
-        VK_LAUNCH(ctx, "kzg_set", (k_set<F>), 1, 64, 0, d_q, m, qm);
-        *y_out = fm;
+        VK_LAUNCH(ctx, "kzg_fold", (k_fold_partials<F>), 1, 256, 0, part.as<fe<F>>(), nblk, fe_neg<F>(wminv), d_q + m);
+        // y = evaluate(point): the stored value, or 0 inside [max, size]
+        if (m < max) {
+            VK_CHECK_HIP(hipMemcpyAsync(y_out, d_f + m, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+        } else {
+            *y_out = fe_zero<F>();
+        }
         return VC_OK;
     }
     // outside: inv_i = 1/(w^i - z); y = -t * sum f_i w^i inv_i, t = (z^n - 1)/n
     VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (n + 255) / 256, 256, 0, pwp, n, point, (long long)-1, den);
     VK_TRY(batch_inverse<F>(ctx, den, inv, n));
-    VK_LAUNCH(ctx, "kzg_bary", (k_bary_partial<F>), nblk, 256, 0, d_f, max, pwp, inv, n, part.as<fe<F>>());
-    VK_CHECK_HIP(hipMemcpyAsync(hp.data(), part.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipStreamSynchronize(st));
-    fe<F> zn = fe_one<F>(), b = point;
-    for (uint64_t e = n; e; e >>= 1) {
-        if (e & 1) zn = fe_mul<F>(zn, b);
-        b = fe_sqr<F>(b);
-    }
     fe<F> nn = fe_zero<F>();
     nn.v[0] = (uint32_t)n;
     nn.v[1] = (uint32_t)((uint64_t)n >> 32);
-    fe<F> t = fe_mul<F>(fe_sub<F>(zn, fe_one<F>()), fe_inv_bin<F>(fe_to_mont<F>(nn)));
-    fe<F> y = fe_neg<F>(fe_mul<F>(t, host_sum<F>(hp)));
-    VK_LAUNCH(ctx, "kzg_q_out", (k_q_out<F>), (n + 255) / 256, 256, 0, d_f, max, inv, n, y, d_q);
-    *y_out = y;
+    const fe<F> t = fe_mul<F>(fe_sub<F>(host_pow<F>(point, n), fe_one<F>()), fe_inv_bin<F>(fe_to_mont<F>(nn)));
+    VK_LAUNCH(ctx, "kzg_bary", (k_bary_partial<F>), nblk, 256, 0, d_f, max, pwp, inv, n, part.as<fe<F>>());
+    VK_LAUNCH(ctx, "kzg_fold", (k_fold_partials<F>), 1, 256, 0, part.as<fe<F>>(), nblk, fe_neg<F>(t), d_y);
+    VK_LAUNCH(ctx, "kzg_q_out", (k_q_out<F>), (n + 255) / 256, 256, 0, d_f, max, inv, n, d_y, d_q);
+    VK_CHECK_HIP(hipMemcpyAsync(y_out, d_y, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
     return VC_OK;
 }
 

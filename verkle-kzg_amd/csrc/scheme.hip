@@ -419,10 +419,19 @@ static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals
     VK_TRY(canon_to_mont_dev<Fr_>(ctx, ev_dev, size, max, d_f.as<fe<Fr_>>()));
     fe<Fr_> pm = canon_to_mont<Fr_>(point);
     fe<Fr_> omega = group_gen_t<Fr_>(size, fr_generator<Fr_>());
-    fe<Fr_> y;
-    VK_TRY(kzg_quotient_dev<Fr_>(ctx, size, d_f.as<fe<Fr_>>(), max, pm, omega, d_q.as<fe<Fr_>>(), &y, pw, tmp,
+    // y arrives in page-locked memory once the stream has passed the quotient (read after a sync)
+    VK_TRY(ctx->pin_y.ensure(sizeof(fe<Fr_>)));
+    fe<Fr_>* yp = ctx->pin_y.as<fe<Fr_>>();
+    VK_TRY(kzg_quotient_dev<Fr_>(ctx, size, d_f.as<fe<Fr_>>(), max, pm, omega, d_q.as<fe<Fr_>>(), yp, pw, tmp,
                                  part_buf));
-    mont_to_canon<Fr_>(y, y_out);
+    struct YOut {  // every return path below has synchronised the stream (or fails)
+        vc_ctx* c;
+        const fe<Fr_>* yp;
+        uint64_t* out;
+        ~YOut() {
+            if (hipStreamSynchronize(c->stream) == hipSuccess) mont_to_canon<Fr_>(*yp, out);
+        }
+    } y_fin{ctx, yp, y_out};
     if (q_out) {
         VK_TRY(mont_to_canon_dev<Fr_>(ctx, d_q.as<fe<Fr_>>(), size, tmp.p));
         VK_CHECK_HIP(hipMemcpyAsync(q_out, tmp.p, size * 32, hipMemcpyDeviceToHost, ctx->stream));
