@@ -266,10 +266,23 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
     __syncthreads();
     if (cnt_lane) h[t] = excl;  // cursors
     __syncthreads();
-    for (uint32_t p = start + t; p < end; p += blockDim.x) {
-        const T e = tmp[p];
-        uint32_t pos = start + atomicAdd(&h[sort_fine_of<T>(e, FB)], 1u);
-        sorted[pos] = sort_entry_of<T>(e, FB);
+    // the scatter RS entries at a time (loads, then LDS cursor atomics, then stores: RS atomics in
+    // flight per thread)
+    constexpr uint32_t RS = 4;
+    for (uint32_t p0 = start + t; p0 < end; p0 += RS * blockDim.x) {
+        T e[RS];
+        uint32_t pos[RS];
+#pragma unroll
+        for (uint32_t k = 0; k < RS; k++) {
+            const uint32_t p = p0 + k * blockDim.x;
+            e[k] = p < end ? tmp[p] : T(0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < RS; k++)
+            if (p0 + k * blockDim.x < end) pos[k] = start + atomicAdd(&h[sort_fine_of<T>(e[k], FB)], 1u);
+#pragma unroll
+        for (uint32_t k = 0; k < RS; k++)
+            if (p0 + k * blockDim.x < end) sorted[pos[k]] = sort_entry_of<T>(e[k], FB);
     }
 }
 
