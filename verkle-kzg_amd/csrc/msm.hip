@@ -232,15 +232,83 @@ __global__ void __launch_bounds__(1024) k_sort_coarse(Src src, uint32_t n, int c
     }
 }
 
+// Staged coarse scatter over precomputed radix digits (RadixDigits, narrow entries): the block's
+// entries are counting-sorted by coarse bin in LDS (local offsets from its own per-bin counts,
+// written by k_sort_hist), then every bin's run is written in one burst by one wave. The direct
+// scatter wrote each run one 4-B entry at a time over the block's whole life; with 1280 bins x 32
+// blocks per XCD of open runs the partly written lines left L2 repeatedly (PMC WRITE_SIZE ~6x
+// the entries). LDS: 2 bins + 1 + chunk * we words (<= 160 KB: chunk 4096 at 7 windows).
+__global__ void __launch_bounds__(1024) k_sort_coarse_st(const int32_t* __restrict__ dig, uint32_t n, int we,
+                                                        uint32_t FB, uint32_t NBC, uint32_t nblk, uint32_t stride,
+                                                        uint32_t wps, uint32_t chunk,
+                                                        const uint32_t* __restrict__ counts,
+                                                        const uint32_t* __restrict__ base,
+                                                        uint32_t* __restrict__ tmp) {
+    extern __shared__ uint32_t sm[];
+    __shared__ uint32_t part[1024];
+    const uint32_t bins = ((uint32_t)we + wps - 1) / wps * NBC;
+    uint32_t* loff = sm;             // bins + 1 local run starts
+    uint32_t* lcur = sm + bins + 1;  // bins cursors
+    uint32_t* stage = lcur + bins;   // the block's entries, bin-major
+    const uint32_t t = threadIdx.x, slot = sort_slot(blockIdx.x, nblk);
+    // local exclusive scan of the block's per-bin counts: ceil(bins / 1024) bins per thread
+    const uint32_t per = (bins + blockDim.x - 1) / blockDim.x, b0 = t * per;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per; k++)
+        if (b0 + k < bins) s += counts[(size_t)(b0 + k) * nblk + slot];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
+        const uint32_t a = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += a;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;  // exclusive prefix of this thread's first bin
+    for (uint32_t k = 0; k < per; k++)
+        if (b0 + k < bins) {
+            loff[b0 + k] = run;
+            lcur[b0 + k] = run;
+            run += counts[(size_t)(b0 + k) * nblk + slot];
+        }
+    if (t == blockDim.x - 1) loff[bins] = part[t];
+    __syncthreads();
+    const uint32_t fmask = (1u << FB) - 1;
+    const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, n);
+    for (uint32_t i = lo + t; i < hi; i += blockDim.x) {
+        for (int w = 0; w < we; w++) {
+            const int32_t d = dig[(size_t)w * n + i];
+            if (d != 0) {
+                const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+                const uint32_t p = atomicAdd(&lcur[(uint32_t)w / wps * NBC + (b >> FB)], 1u);
+                stage[p] = sort_pack<uint32_t>(b & fmask, i + ((uint32_t)w % wps) * stride, d < 0, FB);
+            }
+        }
+    }
+    __syncthreads();
+    // every bin's run in one burst: a wave per bin, lanes over the run
+    const uint32_t wave = t >> 6, lane = t & 63, nw = blockDim.x >> 6;
+    for (uint32_t g = wave; g < bins; g += nw) {
+        const uint32_t l0 = loff[g], len = loff[g + 1] - l0;
+        const uint32_t gb = base[(size_t)g * nblk + slot];
+        for (uint32_t j = lane; j < len; j += 64) tmp[gb + j] = stage[l0 + j];
+    }
+}
+
 // one block per coarse bin; offsets[g * 2^FB + f] = start of fine bucket f of bin g. Block 0
 // also clears the accumulate's chain_max word (no separate memset in the pipeline). Blocks of
 // 256 or 1024 threads (large bins): the 256 fine counters are scanned by the first 256.
+// cap > 0: a bin of at most cap entries is scattered into LDS (dynamic, cap words) and written
+// out in one coalesced pass -- the direct scatter wrote each bucket's 4-B entries one at a time
+// over the block's life, and the partly written lines left L2 several times (PMC WRITE_SIZE
+// ~4x the entries); larger bins scatter directly.
 template <class T>
 __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, const uint32_t* __restrict__ base,
                                                    uint32_t nblk, uint32_t bins, uint32_t FB,
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
-                                                   uint32_t* __restrict__ zero_word) {
+                                                   uint32_t* __restrict__ zero_word, uint32_t cap) {
     __shared__ uint32_t h[256], x[256];
+    extern __shared__ uint32_t stage[];
     const uint32_t g = blockIdx.x, F = 1u << FB, t = threadIdx.x;
     const bool cnt_lane = t < 256;
     if (zero_word != nullptr && g == 0 && t == 0) *zero_word = 0;
@@ -269,6 +337,26 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
     // the scatter RS entries at a time (loads, then LDS cursor atomics, then stores: RS atomics in
     // flight per thread)
     constexpr uint32_t RS = 4;
+    if (end - start <= cap) {  // uniform over the block
+        for (uint32_t p0 = start + t; p0 < end; p0 += RS * blockDim.x) {
+            T e[RS];
+            uint32_t pos[RS];
+#pragma unroll
+            for (uint32_t k = 0; k < RS; k++) {
+                const uint32_t p = p0 + k * blockDim.x;
+                e[k] = p < end ? tmp[p] : T(0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < RS; k++)
+                if (p0 + k * blockDim.x < end) pos[k] = atomicAdd(&h[sort_fine_of<T>(e[k], FB)], 1u);
+#pragma unroll
+            for (uint32_t k = 0; k < RS; k++)
+                if (p0 + k * blockDim.x < end) stage[pos[k]] = sort_entry_of<T>(e[k], FB);
+        }
+        __syncthreads();
+        for (uint32_t p = t; p < end - start; p += blockDim.x) sorted[start + p] = stage[p];
+        return;
+    }
     for (uint32_t p0 = start + t; p0 < end; p0 += RS * blockDim.x) {
         T e[RS];
         uint32_t pos[RS];
@@ -815,7 +903,7 @@ template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
                         uint32_t NBC, uint32_t nblk, uint32_t chunk, uint32_t stride, uint32_t wps, size_t ncnt,
                         uint32_t* counts, uint32_t* base, void* tmp, uint32_t* offsets, uint32_t* sorted,
-                        uint32_t* zero_word) {
+                        uint32_t* zero_word, bool coarse_stage = false) {
     hipStream_t st = L.st;
     if (stride && wps == 0) return VC_E_INVALID;
     const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
@@ -843,17 +931,43 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     // fine-pass block: 1024 threads once bins average >= 2^15 entries (one block per bin)
     static const int fine_env = getenv("VKZG_SORT_FINE_BLOCK") ? atoi(getenv("VKZG_SORT_FINE_BLOCK")) : 0;  // probe
     const uint64_t total = stride ? (uint64_t)(we - wb) * stride : (uint64_t)nv * (uint32_t)(we - wb);
-    const int fblk = fine_env == 256 || fine_env == 1024 ? fine_env : (total / bins >= (1u << 15) ? 1024 : 256);
-    if (narrow) {
+    int fblk = fine_env == 256 || fine_env == 1024 ? fine_env : (total / bins >= (1u << 15) ? 1024 : 256);
+    // LDS staging of the fine scatter (16K entries, 64 KB: two blocks per CU, 1024 threads) when the
+    // mean bin leaves it ~40 % headroom (radix 2^20: 11.5K); a bin beyond it scatters directly
+    static const int stage_env = getenv("VKZG_SORT_STAGE") ? atoi(getenv("VKZG_SORT_STAGE")) : 1;  // A/B probe
+    uint32_t cap = 0;
+    if (stage_env && total / bins <= 12000) {
+        cap = 16384;
+        if (fine_env == 0) fblk = 1024;
+    }
+    // staged coarse scatter (k_sort_coarse_st): radix digits, narrow entries, the block's entries in LDS
+    const size_t st_lds = ((size_t)2 * bins + 1 + (size_t)chunk * (uint32_t)(we - wb)) * 4;
+    bool staged = false;
+    if constexpr (std::is_same<Src, RadixDigits>::value)
+        staged = coarse_stage && narrow && stride != 0 && wb == 0 && st_lds <= 152 * 1024;
+    if (staged) {
+        if constexpr (std::is_same<Src, RadixDigits>::value) {
+            static bool attr = false;
+            if (!attr) {
+                VK_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_coarse_st),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+                attr = true;
+            }
+            VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", k_sort_coarse_st, nblk, 1024, st_lds, src.dig, nv, we, FB, NBC,
+                         nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp));
+        }
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, cap * 4,
+                     static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
+    } else if (narrow) {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, sblk, lds, src, nv, c, wb, we,
                      FB, NBC, nblk, stride, wps, chunk, base, static_cast<uint32_t*>(tmp));
-        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, 0, static_cast<const uint32_t*>(tmp),
-                     base, nblk, bins, FB, offsets, sorted, zero_word);
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, cap * 4,
+                     static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
     } else {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, sblk, lds, src, nv, c, wb, we,
                      FB, NBC, nblk, stride, wps, chunk, base, static_cast<uint64_t*>(tmp));
-        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, fblk, 0, static_cast<const uint64_t*>(tmp),
-                     base, nblk, bins, FB, offsets, sorted, zero_word);
+        VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, fblk, cap * 4,
+                     static_cast<const uint64_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
     }
     return VC_OK;
 }
@@ -977,6 +1091,21 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     }
     static const int chunk_env = getenv("VKZG_SORT_CHUNK") ? atoi(getenv("VKZG_SORT_CHUNK")) : 0;  // tuning probe
     static const int fb_env = getenv("VKZG_SORT_FB") ? atoi(getenv("VKZG_SORT_FB")) : 0;           // tuning probe
+    // radix buckets: the staged coarse scatter (k_sort_coarse_st) holds a block's chunk x W entries in
+    // LDS, so the chunk is the largest power of two that fits 152 KB beside the 2 x bins counters
+    static const int cstage_env = getenv("VKZG_SORT_CSTAGE") ? atoi(getenv("VKZG_SORT_CSTAGE")) : 1;  // A/B probe
+    bool cstage = false;
+    // (one bucket set: with the two sets of the one-call KZG, 2048-scalar blocks measured slower)
+    if (sl.m > 1 && sl.shared && Wr == 1 && cstage_env) {
+        const uint64_t bins_all = (uint64_t)Wr * (NB >> FB);
+        const uint64_t room = (152u * 1024 / 4 > 2 * bins_all + 1) ? 152u * 1024 / 4 - 2 * bins_all - 1 : 0;
+        uint32_t ch = 1u << 12;
+        while (ch > 256 && (uint64_t)ch * (uint32_t)W > room) ch >>= 1;
+        if ((uint64_t)ch * (uint32_t)W <= room) {
+            chunk = ch;
+            cstage = true;
+        }
+    }
     if (chunk_env >= 256) chunk = (uint32_t)chunk_env;
     // shared windows: ~64K entries per coarse bin (one 1024-thread k_sort_fine block each) but at
     // least 256 bins (a fine block per CU). Measured at 2^21 x 8 entries (hist + coarse + fine):
@@ -1034,7 +1163,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
                         sl.wps, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
-                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max));
+                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max, cstage));
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W;
     // chain_max was cleared by k_sort_fine
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
