@@ -96,9 +96,10 @@ def kernel_table(eng):
     return out
 
 
-def cpu_baseline(curve, n_full, sample):
+def cpu_baseline(curve, n_full, sample, reps=3):
     """Reference algorithm (naive per-term double-and-add + sequential sum, utils.rs:16-19)
-    restated in C (oracle/), 1 thread, on `sample` terms; extrapolated linearly to n_full."""
+    restated in C (oracle/), 1 thread: `reps` disjoint slices of `sample` terms, each timed, the
+    median per-term time extrapolated linearly to n_full (median of the runs)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import cref  # CPU baseline leg only (checker/baseline, never the measured path)
     if not os.path.exists(cref.LIB_PATH):
@@ -110,29 +111,39 @@ def cpu_baseline(curve, n_full, sample):
     xy, inf = e.download_bases(tid)
     e.close()
     sc = vkzg.random_scalars(curve, sample, rng)
-    t0 = time.perf_counter()
-    cref.msm_arrays(curve, xy, inf, sc, 1)
-    dt = time.perf_counter() - t0
-    per_msm_s = dt * n_full / sample
+    part = sample // reps
+    ts = []
+    for k in range(reps):
+        lo = k * part
+        t0 = time.perf_counter()
+        cref.msm_arrays(curve, xy[lo:lo + part], inf[lo:lo + part], sc[lo:lo + part], 1)
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
+    per_msm_s = dt * n_full / part
     return {"value": 1.0 / per_msm_s, "unit": "MSM/s", "cores": 1, "kind": "port",
-            "sample": f"{sample} of {n_full} terms of the naive {curve} MSM (reference utils.rs:16-19 "
-                      f"restated in C, oracle/c/ref_curve.c), 1 thread, {dt:.2f} s, extrapolated linearly",
+            "sample": f"{reps} slices of {part} of {n_full} terms of the naive {curve} MSM (reference utils.rs:16-19 "
+                      f"restated in C, oracle/c/ref_curve.c), 1 thread, {[round(t, 2) for t in ts]} s, the median "
+                      f"extrapolated linearly",
             "ms_per_msm": per_msm_s * 1e3, "host_cpus": os.cpu_count()}
 
 
-def cpu_pippenger(curve, xy, inf, scalars, want, threads):
+def cpu_pippenger(curve, xy, inf, scalars, want, threads, reps=3):
     """The fair all-core CPU bound: the same 2^20 MSM by the bucket method in C
     (oracle/c/ref_curve.c pip_msm: per-thread point chunks, signed windows, mixed bucket adds),
-    on `threads` host threads, the whole workload once (no extrapolation); its result is
-    checked against the GPU's."""
+    on `threads` host threads, the whole workload `reps` times (no extrapolation), the median;
+    its result is checked against the GPU's."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import cref  # CPU baseline leg only
-    t0 = time.perf_counter()
-    got = cref.pip_msm_arrays(curve, xy, inf, scalars, threads)
-    dt = time.perf_counter() - t0
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        got = cref.pip_msm_arrays(curve, xy, inf, scalars, threads)
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
     return {"value": 1.0 / dt, "unit": "MSM/s", "cores": threads, "kind": "pippenger",
             "sample": f"the full {scalars.shape[0]}-term {curve} MSM of the bench (bases and scalars of the timed "
-                      f"step), Pippenger in C on {threads} threads (oracle/c/ref_curve.c pip_msm), {dt:.2f} s",
+                      f"step), Pippenger in C on {threads} threads (oracle/c/ref_curve.c pip_msm), "
+                      f"{[round(t, 2) for t in ts]} s, the median",
             "ms_per_msm": dt * 1e3, "same_result_as_gpu": bool(got[1] == int(want[1]) and np.array_equal(got[0], np.asarray(want[0])))}
 
 
