@@ -7,6 +7,7 @@
 #include <condition_variable>
 #include <exception>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <utility>
@@ -87,6 +88,25 @@ inline HostPool& host_pool() {
     static HostPool* p = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
     return *p;
 }
+
+// std::vector whose resize leaves new elements uninitialised (value-init only when asked): the
+// host staging of big batched calls (verkle rows, outputs) is written in full right after, and
+// zero-filling 8-16 MB per level on one thread cost ~1 ms per level
+template <class T>
+struct default_init_alloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = default_init_alloc<U>;
+    };
+    using std::allocator<T>::allocator;
+    template <class U, class... Args>
+    void construct(U* p, Args&&... args) {
+        if constexpr (sizeof...(Args) == 0) ::new (static_cast<void*>(p)) U;
+        else ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+    }
+};
+template <class T>
+using uvec = std::vector<T, default_init_alloc<T>>;
 
 // fn(i) for i in [lo, hi) on the pool in contiguous ranges, or serially below `min_par` items
 template <class Fn>

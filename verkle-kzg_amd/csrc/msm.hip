@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "host/pool.hpp"
 #include "ec.hpp"
 #include "msm_tail.hpp"
 #include "ec29.hpp"
@@ -1631,10 +1632,19 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     using Acc = typename C::Acc;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
-    for (size_t g = 0; g < batch; g++)
-        if (row_ptr[g + 1] < row_ptr[g]) return VC_E_INVALID;
-    for (size_t j = 0; j < nnz; j++)
-        if (cols[j] >= t->n) return VC_E_RANGE;
+    // argument checks and the chunk lists on the host pool (verkle levels: 10^5 rows / non-zeros)
+    std::vector<uint8_t> bad_part(host_pool().size(), 0);
+    host_pool().run([&](unsigned k) {
+        const unsigned T = host_pool().size();
+        uint8_t b = 0;
+        for (size_t g = batch * k / T; g < batch * (k + 1) / T; g++) b |= row_ptr[g + 1] < row_ptr[g] ? 1 : 0;
+        for (size_t j = nnz * k / T; j < nnz * (k + 1) / T; j++) b |= cols[j] >= t->n ? 2 : 0;
+        bad_part[k] = b;
+    });
+    uint8_t bad = 0;
+    for (uint8_t b : bad_part) bad |= b;
+    if (bad & 1) return VC_E_INVALID;
+    if (bad & 2) return VC_E_RANGE;
     if (t->fb_c == 0) VK_TRY(fixed_base_precompute(ctx, t, 8));
     const FbGeom fg = t->fb_geom();
     const int W = fg.W;
@@ -1643,15 +1653,29 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     // hundreds of threads -- whose pieces the fix-up would add serially; chunk sums are folded
     // per row by k_sparse_combine
     const size_t CHNZ = 4;
-    std::vector<uint64_t> cptr{0};
-    std::vector<uint32_t> rc(batch + 1);
-    for (size_t g = 0; g < batch; g++) {
-        rc[g] = (uint32_t)(cptr.size() - 1);
-        if (row_ptr[g + 1] == row_ptr[g]) cptr.push_back(row_ptr[g]);  // empty row -> one empty chunk
-        for (uint64_t j = row_ptr[g]; j < row_ptr[g + 1]; j += CHNZ) cptr.push_back(std::min<uint64_t>(j + CHNZ, row_ptr[g + 1]));
+    // rc[g] = first chunk of row g (an empty row gets one empty chunk); cptr = chunk ends
+    uvec<uint32_t> rc(batch + 1);
+    pool_for(0, batch, 4096, [&](size_t g) {
+        const uint64_t len = row_ptr[g + 1] - row_ptr[g];
+        rc[g] = (uint32_t)(len == 0 ? 1 : (len + CHNZ - 1) / CHNZ);
+    });
+    uint32_t run = 0;
+    for (size_t g = 0; g <= batch; g++) {
+        const uint32_t c = g < batch ? rc[g] : 0u;
+        rc[g] = run;
+        run += c;
     }
-    rc[batch] = (uint32_t)(cptr.size() - 1);
-    const size_t nch = cptr.size() - 1;
+    const size_t nch = run;
+    uvec<uint64_t> cptr(nch + 1);
+    cptr[0] = 0;
+    pool_for(0, batch, 4096, [&](size_t g) {
+        uint64_t* out = &cptr[rc[g] + 1];
+        if (row_ptr[g + 1] == row_ptr[g]) {
+            out[0] = row_ptr[g];
+            return;
+        }
+        for (uint64_t j = row_ptr[g]; j < row_ptr[g + 1]; j += CHNZ) *out++ = std::min<uint64_t>(j + CHNZ, row_ptr[g + 1]);
+    });
     if ((uint64_t)t->n * fg.stride() >= (1ull << 31)) return VC_E_RANGE;  // entry index + sign bit
     const size_t maxL = nnz * (size_t)W;
     if (maxL >= 0xffffffffull) return VC_E_RANGE;

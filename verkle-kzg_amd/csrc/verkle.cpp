@@ -337,9 +337,9 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     }
     // batched sparse commits (vc_msm_batch_sparse): rows of (column, value) non-zeros
     struct Rows {
-        std::vector<uint64_t> ptr{0};
-        std::vector<uint32_t> cols;
-        std::vector<uint64_t> vals;
+        uvec<uint64_t> ptr{0};
+        uvec<uint32_t> cols;
+        uvec<uint64_t> vals;
         void reserve(size_t rows, size_t nnz) {
             ptr.reserve(rows + 1);
             cols.reserve(nnz);
@@ -377,7 +377,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             roff[k + 1] = roff[k] + part[k].n();
             noff[k + 1] = noff[k] + part[k].cols.size();
         }
-        out.ptr.assign(roff[T] + 1, 0);
+        out.ptr.resize(roff[T] + 1);
+        out.ptr[0] = 0;
         out.cols.resize(noff[T]);
         out.vals.resize(4 * noff[T]);
         pool.run([&](unsigned k) {
@@ -402,12 +403,12 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         });
     };
     lap("collect dirty");
-    auto commit_rows = [&](const Rows& r, std::vector<uint64_t>& xy, std::vector<uint8_t>& inf,
-                           std::vector<uint64_t>& items) -> int {
+    // outputs are written in full by the two calls (uninitialised staging, host/pool.hpp uvec)
+    auto commit_rows = [&](const Rows& r, uvec<uint64_t>& xy, uvec<uint8_t>& inf, uvec<uint64_t>& items) -> int {
         const size_t B = r.n();
-        xy.assign(B * 8, 0);
-        inf.assign(B, 0);
-        items.assign(B * 4, 0);
+        xy.resize(B * 8);
+        inf.resize(B);
+        items.resize(B * 4);
         if (B == 0) return VC_OK;
         lap("build rows");
         VK_TRY(vc_msm_batch_sparse(ctx, table, B, r.ptr.data(), r.cols.data(), r.vals.data(), 0, xy.data(), inf.data()));
@@ -421,8 +422,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     // rank stores the whole level
     // st: this rank's status for the level -- a failed share still enters the exchange with it
     // (include/vc_comm.h), so every rank stops at the same level with an error
-    auto store_level = [&](const std::vector<int>& ids, size_t lo, size_t hi, const std::vector<uint64_t>& xy,
-                           const std::vector<uint8_t>& inf, const std::vector<uint64_t>& items, int st) -> int {
+    auto store_level = [&](const std::vector<int>& ids, size_t lo, size_t hi, const uvec<uint64_t>& xy,
+                           const uvec<uint8_t>& inf, const uvec<uint64_t>& items, int st) -> int {
         auto put = [&](size_t i, const uint64_t* rxy, uint8_t rinf, const uint64_t* ritem) {
             VNode& n = t->nodes[ids[i]];
             memcpy(n.cxy, rxy, 64);
@@ -462,8 +463,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         *lo = sh ? B * sh->rank / sh->world : 0;
         *hi = sh ? B * (sh->rank + 1) / sh->world : B;
     };
-    std::vector<uint64_t> xy, items, xy2, items2;
-    std::vector<uint8_t> inf, inf2;
+    uvec<uint64_t> xy, items, xy2, items2;
+    uvec<uint8_t> inf, inf2;
     // extension nodes: c1, c2 (width N), then [1, stem, c1, c2] (width 4) -- both steps only need
     // the node's own values, so a rank runs both on its slice and exchanges once
     if (!exts.empty()) {
