@@ -948,12 +948,10 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
         staged = coarse_stage && narrow && stride != 0 && wb == 0 && st_lds <= 152 * 1024;
     if (staged) {
         if constexpr (std::is_same<Src, RadixDigits>::value) {
-            static bool attr = false;
-            if (!attr) {
-                VK_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_coarse_st),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
-                attr = true;
-            }
+            // once per process (thread-safe static initialisation)
+            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_coarse_st),
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+            VK_CHECK_HIP(attr);
             VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", k_sort_coarse_st, nblk, 1024, st_lds, src.dig, nv, we, FB, NBC,
                          nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp));
         }
