@@ -287,12 +287,13 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(const int32_t* __restri
         }
     }
     __syncthreads();
-    // every bin's run in one burst: a wave per bin, lanes over the run
-    const uint32_t wave = t >> 6, lane = t & 63, nw = blockDim.x >> 6;
-    for (uint32_t g = wave; g < bins; g += nw) {
+    // every bin's run in one burst: 16 lanes per bin (runs are ~10-25 entries: a whole wave per bin
+    // left most lanes idle), 4 bins per wave at a time
+    const uint32_t grp = t >> 4, sub = t & 15, ngrp = blockDim.x >> 4;
+    for (uint32_t g = grp; g < bins; g += ngrp) {
         const uint32_t l0 = loff[g], len = loff[g + 1] - l0;
         const uint32_t gb = base[(size_t)g * nblk + slot];
-        for (uint32_t j = lane; j < len; j += 64) tmp[gb + j] = stage[l0 + j];
+        for (uint32_t j = sub; j < len; j += 16) tmp[gb + j] = stage[l0 + j];
     }
 }
 
@@ -1094,13 +1095,12 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     // LDS, so the chunk is the largest power of two that fits 152 KB beside the 2 x bins counters
     static const int cstage_env = getenv("VKZG_SORT_CSTAGE") ? atoi(getenv("VKZG_SORT_CSTAGE")) : 1;  // A/B probe
     bool cstage = false;
-    // (one bucket set: with the two sets of the one-call KZG, 2048-scalar blocks measured slower)
-    if (sl.m > 1 && sl.shared && Wr == 1 && cstage_env) {
+    if (sl.m > 1 && sl.shared && cstage_env) {
         const uint64_t bins_all = (uint64_t)Wr * (NB >> FB);
         const uint64_t room = (152u * 1024 / 4 > 2 * bins_all + 1) ? 152u * 1024 / 4 - 2 * bins_all - 1 : 0;
         uint32_t ch = 1u << 12;
-        while (ch > 256 && (uint64_t)ch * (uint32_t)W > room) ch >>= 1;
-        if ((uint64_t)ch * (uint32_t)W <= room) {
+        while (ch > 1024 && (uint64_t)ch * (uint32_t)W > room) ch >>= 1;
+        if ((uint64_t)ch * (uint32_t)W <= room) {  // one set: 4096 scalars; the KZG's two sets: 2048
             chunk = ch;
             cstage = true;
         }
