@@ -239,15 +239,15 @@ __global__ void __launch_bounds__(1024) k_sort_coarse(Src src, uint32_t n, int c
 // scatter wrote each run one 4-B entry at a time over the block's whole life; with 1280 bins x 32
 // blocks per XCD of open runs the partly written lines left L2 repeatedly (PMC WRITE_SIZE ~6x
 // the entries). LDS: 2 bins + 1 + chunk * we words (<= 160 KB: chunk 4096 at 7 windows).
-__global__ void __launch_bounds__(1024) k_sort_coarse_st(const int32_t* __restrict__ dig, uint32_t n, int we,
-                                                        uint32_t FB, uint32_t NBC, uint32_t nblk, uint32_t stride,
-                                                        uint32_t wps, uint32_t chunk,
-                                                        const uint32_t* __restrict__ counts,
+template <class Src>
+__global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, int c, int wb, int we, uint32_t FB,
+                                                        uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t wps,
+                                                        uint32_t chunk, const uint32_t* __restrict__ counts,
                                                         const uint32_t* __restrict__ base,
                                                         uint32_t* __restrict__ tmp) {
     extern __shared__ uint32_t sm[];
     __shared__ uint32_t part[1024];
-    const uint32_t bins = ((uint32_t)we + wps - 1) / wps * NBC;
+    const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
     uint32_t* loff = sm;             // bins + 1 local run starts
     uint32_t* lcur = sm + bins + 1;  // bins cursors
     uint32_t* stage = lcur + bins;   // the block's entries, bin-major
@@ -277,14 +277,14 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(const int32_t* __restri
     const uint32_t fmask = (1u << FB) - 1;
     const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, n);
     for (uint32_t i = lo + t; i < hi; i += blockDim.x) {
-        for (int w = 0; w < we; w++) {
-            const int32_t d = dig[(size_t)w * n + i];
-            if (d != 0) {
+        src(i, c, we, [&](int w, int32_t d) {
+            if (d != 0 && w >= wb) {
                 const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-                const uint32_t p = atomicAdd(&lcur[(uint32_t)w / wps * NBC + (b >> FB)], 1u);
-                stage[p] = sort_pack<uint32_t>(b & fmask, i + ((uint32_t)w % wps) * stride, d < 0, FB);
+                const uint32_t p = atomicAdd(
+                    &lcur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
+                stage[p] = sort_pack<uint32_t>(b & fmask, stride ? i + ((uint32_t)w % wps) * stride : i, d < 0, FB);
             }
-        }
+        });
     }
     __syncthreads();
     // every bin's run in one burst: 16 lanes per bin (runs are ~10-25 entries: a whole wave per bin
@@ -942,20 +942,16 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
         cap = 16384;
         if (fine_env == 0) fblk = 1024;
     }
-    // staged coarse scatter (k_sort_coarse_st): radix digits, narrow entries, the block's entries in LDS
+    // staged coarse scatter (k_sort_coarse_st): narrow entries, the block's entries in LDS
     const size_t st_lds = ((size_t)2 * bins + 1 + (size_t)chunk * (uint32_t)(we - wb)) * 4;
-    bool staged = false;
-    if constexpr (std::is_same<Src, RadixDigits>::value)
-        staged = coarse_stage && narrow && stride != 0 && wb == 0 && st_lds <= 152 * 1024;
+    const bool staged = coarse_stage && narrow && st_lds <= 152 * 1024;
     if (staged) {
-        if constexpr (std::is_same<Src, RadixDigits>::value) {
-            // once per process (thread-safe static initialisation)
-            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_coarse_st),
-                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
-            VK_CHECK_HIP(attr);
-            VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", k_sort_coarse_st, nblk, 1024, st_lds, src.dig, nv, we, FB, NBC,
-                         nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp));
-        }
+        // once per process and instantiation (thread-safe static initialisation)
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_coarse_st<Src>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+        VK_CHECK_HIP(attr);
+        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", k_sort_coarse_st<Src>, nblk, 1024, st_lds, src, nv, c, wb, we, FB,
+                     NBC, nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, cap * 4,
                      static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
     } else if (narrow) {
@@ -1105,6 +1101,9 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
             cstage = true;
         }
     }
+    // per-window buckets: one more coarse bit when the fine bins would be too big to stage in LDS
+    // (GLV variable-base 2^21 x 8: 16K -> 8K entries; fine pass 0.118 -> 0.041 ms)
+    if (sl.m == 1 && !sl.shared && cstage_env && FB > 1 && load / (NB >> FB) > 12000) FB--;
     if (chunk_env >= 256) chunk = (uint32_t)chunk_env;
     // shared windows: ~64K entries per coarse bin (one 1024-thread k_sort_fine block each) but at
     // least 256 bins (a fine block per CU). Measured at 2^21 x 8 entries (hist + coarse + fine):
@@ -1116,6 +1115,16 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     if (fb_env >= 1 && fb_env <= (int)std::min<uint32_t>(lgNB, 8)) FB = (uint32_t)fb_env;
     const uint32_t NBC = NB >> FB;
     const uint32_t nblk = (uint32_t)((nv + chunk - 1) / chunk);
+    // the staged coarse pass pays for its LDS sort and write-out with >= 4096 entries per block and
+    // either runs of >= 10 entries per bin (radix: 22, or 11 with two sets) or LDS <= 64 KB (two or
+    // more blocks per CU: GLV variable-base 2^21 x 8, 4-entry runs, 0.129 -> 0.106 ms). Measured
+    // slower: BN254 2^20 (16 windows, 98 KB, 0.119 -> 0.169 ms) and the 8-way window slice (1024
+    // entries per block, 0.016 -> 0.029 ms)
+    if (sl.m == 1 && cstage_env) {
+        const uint64_t per_blk = (uint64_t)chunk * (uint32_t)(sl.we - sl.wb), bins_all = (uint64_t)Wr * NBC;
+        const uint64_t lds_b = (2 * bins_all + 1 + per_blk) * 4;
+        cstage = per_blk >= 4096 && (per_blk >= 10 * bins_all || lds_b <= 64 * 1024);
+    }
     const size_t ncnt = (size_t)Wr * NBC * nblk + 1;
 
     DevBuf* ws = L.ws;
