@@ -59,8 +59,11 @@ def parse():
     ap.add_argument("--curve", default="bls12_381")
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--commit-batch", type=int, default=10000)
-    ap.add_argument("--commit-window", type=int, default=20,
-                    help="fixed-base window bits of the config-3 table (20: 13 windows, 167 GB; falls back to 16)")
+    ap.add_argument("--commit-window", type=int, default=19,
+                    help="fixed-base window bits of the config-3 table (19 with --commit-windows 13: 13 windows of "
+                         "19 / 20 bits, 145 GB, the speed of the 188 GB c = 20 table; falls back to 16)")
+    ap.add_argument("--commit-windows", type=int, default=13,
+                    help="windows of the config-3 table (0: uniform c-bit windows)")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kzg", action="store_true", help="skip the KZG commit+open line (configs[3])")
@@ -904,7 +907,7 @@ def main():
     progress("variable-base / host-scalar lines done")
     if not a.no_secondary:
         # config 3: batched width-256 commits (fixed-base tables), batch split across ranks; timed
-        # on the c = commit_window table (167 GB at c = 20) and on the deployable c = 16 one (12.9 GB)
+        # on the commit_window / commit_windows table (145 GB at 19 / 13) and on the deployable c = 16 one (14.5 GB)
         cstate = {}
 
         def cengine():  # (re)create: closing the engine frees a table a peer rank could not fit
@@ -972,7 +975,7 @@ def main():
                     "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
                     "table_bytes": 256 * (gw + gbig) * (1 << (gc - 1)) * 108}  # FbE: 3 x 9 limbs
 
-        big = ctime(a.commit_window)
+        big = ctime(a.commit_window, a.commit_windows if a.commit_window != 16 else 0)
         small = ctime(16) if a.commit_window != 16 else big
         # the <= 60 GB table: 14 windows (12 of 18 bits, 2 of 19), 58 GB
         mixed = ctime(18, 14)
@@ -983,7 +986,8 @@ def main():
         else:
             out["secondary"] = {
                 "workload": f"{B} batched width-256 Bandersnatch commits (configs[2]), fixed-base "
-                            f"c={head['window_bits']}, batch split over {world} rank(s)",
+                            f"c={head['window_bits']} ({head['windows']} windows, {head['wide_windows']} of them "
+                            f"{head['window_bits'] + 1} bits), batch split over {world} rank(s)",
                 **head,
                 "c16": small,
                 "mixed_c18_w14": mixed,
