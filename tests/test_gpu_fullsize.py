@@ -215,17 +215,19 @@ def test_commit_10k_width256_c20(oracle_c):
         e.close()
 
 
-def test_commit_10k_width256_mixed_c18_w14(oracle_c):
-    """configs[2] on the deployable mixed table: 14 windows (12 of 18 bits, 2 of 19), 58 GB for
-    256 Bandersnatch bases; 8 sampled commits against the oracle."""
+@pytest.mark.parametrize("c,windows,wide", [(18, 14, 2), (19, 13, 7)])
+def test_commit_10k_width256_mixed(oracle_c, c, windows, wide):
+    """configs[2] on the mixed tables: 14 windows (12 of 18 bits, 2 of 19), 58 GB, and the bench's
+    13 windows (6 of 19 bits, 7 of 20), 145 GB, for 256 Bandersnatch bases; 8 sampled commits
+    against the oracle."""
     import torch
     import vkzg
     e = vkzg.Engine("bandersnatch")
     try:
         tab = e.random_bases(256, seed=3)
         xy, inf = e.download_bases(tab)
-        e.fixed_base_precompute(tab, 18, 14)
-        assert e.fixed_base_geometry(tab) == (18, 14, 2)
+        e.fixed_base_precompute(tab, c, windows)
+        assert e.fixed_base_geometry(tab) == (c, windows, wide)
         B = 10_000
         sc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(15))
         d_sc = torch.from_numpy(sc.view(np.int64).copy()).cuda()
