@@ -337,8 +337,93 @@ VK_HD bool fe_is_one_raw(const fe<F>& a) {
     for (int i = 1; i < F::N; i++) o |= a.v[i];
     return o == 0;
 }
+#ifndef __HIP_DEVICE_COMPILE__
+// Host inverse: the binary extended Euclid below on 64-bit limbs (half the limb steps of the
+// 32-bit version). On the GPU box's host, BLS12-381 Fq: 7.4 us against 13.2 us (32-bit limbs) and
+// 15 us for Fermat with a 5-bit window (tools/hostinv.cpp). It is the last serial step of every
+// MSM call (acc_to_affine) and of every IPA round's normalisation.
+template <class F>
+inline fe<F> fe_inv_host(const fe<F>& a_mont) {
+    constexpr int M = F::N / 2;
+    typedef unsigned __int128 u128;
+    uint64_t p[M], u[M], v[M], x1[M] = {1}, x2[M] = {0};
+    for (int i = 0; i < M; i++) p[i] = (uint64_t)F::p(2 * i) | ((uint64_t)F::p(2 * i + 1) << 32);
+    memcpy(u, a_mont.v, sizeof u);
+    memcpy(v, p, sizeof v);
+    auto one = [](const uint64_t* a) {
+        if (a[0] != 1) return false;
+        for (int i = 1; i < M; i++)
+            if (a[i]) return false;
+        return true;
+    };
+    auto shr1 = [](uint64_t* a, uint64_t top) {
+        for (int i = 0; i < M - 1; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 63);
+        a[M - 1] = (a[M - 1] >> 1) | (top << 63);
+    };
+    auto addp = [&](uint64_t* a) {
+        u128 c = 0;
+        for (int i = 0; i < M; i++) {
+            c += (u128)a[i] + p[i];
+            a[i] = (uint64_t)c;
+            c >>= 64;
+        }
+        return (uint64_t)c;
+    };
+    auto geq = [](const uint64_t* a, const uint64_t* b) {
+        for (int i = M - 1; i >= 0; i--)
+            if (a[i] != b[i]) return a[i] > b[i];
+        return true;
+    };
+    auto sub = [](uint64_t* a, const uint64_t* b) {
+        uint64_t br = 0;
+        for (int i = 0; i < M; i++) {
+            const u128 d = (u128)a[i] - b[i] - br;
+            a[i] = (uint64_t)d;
+            br = (uint64_t)(d >> 64) & 1;
+        }
+    };
+    auto subm = [&](uint64_t* a, const uint64_t* b) {  // a - b mod p, both in [0, p)
+        if (geq(a, b)) {
+            sub(a, b);
+        } else {
+            uint64_t t[M];
+            memcpy(t, b, sizeof t);
+            sub(t, a);
+            memcpy(a, p, sizeof t);
+            sub(a, t);
+        }
+    };
+    while (!one(u) && !one(v)) {
+        while ((u[0] & 1) == 0) {
+            shr1(u, 0);
+            const uint64_t c = (x1[0] & 1) ? addp(x1) : 0;
+            shr1(x1, c);
+        }
+        while ((v[0] & 1) == 0) {
+            shr1(v, 0);
+            const uint64_t c = (x2[0] & 1) ? addp(x2) : 0;
+            shr1(x2, c);
+        }
+        if (geq(u, v)) {
+            sub(u, v);
+            subm(x1, x2);
+        } else {
+            sub(v, u);
+            subm(x2, x1);
+        }
+    }
+    fe<F> r, r2;
+    memcpy(r.v, one(u) ? x1 : x2, sizeof u);  // (aR)^-1
+    for (int i = 0; i < F::N; i++) r2.v[i] = F::r2(i);
+    return fe_mul<F>(fe_mul<F>(r, r2), r2);  // (aR)^-1 R^2 = a^-1 R
+}
+#endif
+
 template <class F>
 VK_HD fe<F> fe_inv_bin(const fe<F>& a_mont) {
+#ifndef __HIP_DEVICE_COMPILE__
+    if constexpr (F::N % 2 == 0) return fe_is_zero<F>(a_mont) ? fe_zero<F>() : fe_inv_host<F>(a_mont);
+#endif
     fe<F> u = a_mont, v, x1 = fe_zero<F>(), x2 = fe_zero<F>();
 #pragma unroll
     for (int i = 0; i < F::N; i++) v.v[i] = F::p(i);
