@@ -682,8 +682,8 @@ __device__ __forceinline__ uint32_t div_step(uint32_t x, uint32_t& rem) {
     return q;
 }
 
-template <uint32_t MUL, int C0>
-__device__ __forceinline__ void radix_digits(u128 k, bool neg, int W, int32_t* __restrict__ out, size_t stride) {
+template <uint32_t MUL, int C0, class Fn>
+__device__ __forceinline__ void radix_digits(u128 k, bool neg, int W, Fn&& f) {
     constexpr uint32_t B = MUL << C0, H = B / 2, LO = (1u << C0) - 1;
     uint32_t x0 = (uint32_t)k, x1 = (uint32_t)(k >> 32), x2 = (uint32_t)(k >> 64), x3 = (uint32_t)(k >> 96);
     uint32_t carry = 0;
@@ -707,7 +707,7 @@ __device__ __forceinline__ void radix_digits(u128 k, bool neg, int W, int32_t* _
             d = (int32_t)raw;
             carry = 0;
         }
-        out[(size_t)w * stride] = neg ? -d : d;
+        f(w, neg ? -d : d);
     }
 }
 
@@ -728,8 +728,52 @@ __global__ void __launch_bounds__(256) k_glv_radix(const uint32_t* __restrict__ 
     u128 rem, q;
     bool nr, nq;
     glv_decompose(s, K, rem, nr, q, nq);
-    radix_digits<MUL, C0>(rem, nr, W, dig + i, nv);
-    radix_digits<MUL, C0>(q, nq, W, dig + n + i, nv);
+    radix_digits<MUL, C0>(rem, nr, W, [&](int w, int32_t d) { dig[(size_t)w * nv + i] = d; });
+    radix_digits<MUL, C0>(q, nq, W, [&](int w, int32_t d) { dig[(size_t)w * nv + n + i] = d; });
+}
+
+// k_glv_radix fused with k_sort_hist for one shared bucket set (windows [0, W) into one set of
+// m 2^(c-1) buckets): a block takes `chunk` scalars, i.e. the entries of sort blocks blockIdx.x
+// (k1 terms, entries i) and n / chunk + blockIdx.x (k2 terms, entries n + i), and writes both
+// blocks' coarse-bin counts where k_sort_hist would (n % chunk == 0). Saves the hist pass's
+// re-read of the W x 2n digits and one launch.
+template <class Fr, uint32_t MUL, int C0>
+__global__ void __launch_bounds__(1024) k_glv_radix_hist(const uint32_t* __restrict__ sc,
+                                                        const uint8_t* __restrict__ inf, uint32_t n, int mont,
+                                                        GlvK K, int W, int32_t* __restrict__ dig, uint32_t FB,
+                                                        uint32_t NBC, uint32_t nblk, uint32_t chunk,
+                                                        uint32_t* __restrict__ counts) {
+    extern __shared__ uint32_t hist[];  // [2][NBC]: k1 block, k2 block
+    for (uint32_t k = threadIdx.x; k < 2 * NBC; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    const size_t nv = 2 * (size_t)n;
+    const uint32_t lo = blockIdx.x * chunk, hi = lo + chunk;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        if (inf != nullptr && inf[i]) {
+            for (int w = 0; w < W; w++) dig[(size_t)w * nv + i] = dig[(size_t)w * nv + n + i] = 0;
+            continue;
+        }
+        uint64_t s[4];
+        glv_load<Fr>(sc, i, mont, s);
+        u128 rem, q;
+        bool nr, nq;
+        glv_decompose(s, K, rem, nr, q, nq);
+        radix_digits<MUL, C0>(rem, nr, W, [&](int w, int32_t d) {
+            dig[(size_t)w * nv + i] = d;
+            if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1) >> FB], 1u);
+        });
+        radix_digits<MUL, C0>(q, nq, W, [&](int w, int32_t d) {
+            dig[(size_t)w * nv + n + i] = d;
+            if (d != 0) atomicAdd(&hist[NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
+        });
+    }
+    __syncthreads();
+    const uint32_t s1 = sort_slot(blockIdx.x, nblk), s2 = sort_slot(blockIdx.x + n / chunk, nblk);
+    for (uint32_t k = threadIdx.x; k < NBC; k += blockDim.x) {
+        counts[(size_t)k * nblk + s1] = hist[k];
+        counts[(size_t)k * nblk + s2] = hist[NBC + k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(size_t)NBC * nblk] = 0;  // the scan's terminal slot
 }
 
 template <class C>
@@ -905,7 +949,7 @@ template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
                         uint32_t NBC, uint32_t nblk, uint32_t chunk, uint32_t stride, uint32_t wps, size_t ncnt,
                         uint32_t* counts, uint32_t* base, void* tmp, uint32_t* offsets, uint32_t* sorted,
-                        uint32_t* zero_word, bool coarse_stage = false) {
+                        uint32_t* zero_word, bool coarse_stage = false, bool counts_ready = false) {
     hipStream_t st = L.st;
     if (stride && wps == 0) return VC_E_INVALID;
     const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
@@ -919,8 +963,9 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     // entries long, so a big bucket set (many coarse bins) takes bigger blocks to keep the
     // scatter's runs near a cache line
     const uint32_t sblk = chunk >= 4096 ? 1024 : 256;
-    VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, sblk, lds, src, nv, c, wb, we, FB, NBC, nblk,
-                 stride, wps, chunk, counts);
+    if (!counts_ready)  // else written by k_glv_radix_hist
+        VK_LAUNCH_ON(ctx, st, "msm_sort_hist", (k_sort_hist<Src>), nblk, sblk, lds, src, nv, c, wb, we, FB, NBC,
+                     nblk, stride, wps, chunk, counts);
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, base, ncnt, st));
     VK_TRY(L.ws[WS_SCAN_TMP].ensure(tmp_bytes));
@@ -1028,6 +1073,15 @@ struct MsmSlice {
     Acc* tail = nullptr;
     std::vector<Acc> ht;
     uint32_t Lmax = 0;
+    // BLS12-381 radix digits still to be made (msm_run_t leaves the GLV split to slice_enqueue,
+    // which fuses the sort histogram into it when the geometry allows): sc == nullptr otherwise
+    struct {
+        const uint32_t* sc = nullptr;
+        const uint8_t* inf = nullptr;
+        uint32_t n = 0;
+        int mont = 0;
+        int32_t* dig = nullptr;
+    } radix;
 };
 
 template <class C, class BT, class Src>
@@ -1167,11 +1221,28 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.bsum_part = ws[WS_WIN].as<RAcc>();
     sl.tail = ws[WS_TAIL].as<Acc>();
 
+    bool counts_ready = false;
+    if constexpr (std::is_same<C, BLS381G1>::value) {
+        if (sl.radix.sc != nullptr) {
+            // one set over all windows, whole sort blocks of scalars: GLV split + sort histogram
+            static const int fuse_env = getenv("VKZG_RADIX_HIST") ? atoi(getenv("VKZG_RADIX_HIST")) : 1;  // A/B
+            const uint32_t rn = sl.radix.n;
+            counts_ready = fuse_env && sl.shared && Wr == 1 && sl.wb == 0 && (uint32_t)sl.we == sl.wps &&
+                           nv == 2 * (size_t)rn && rn % chunk == 0 && (size_t)2 * NBC * 4 <= 64 * 1024;
+            if (counts_ready)
+                VK_LAUNCH_ON(ctx, st, "glv_split", (k_glv_radix_hist<BLS381Fr, 5, 16>), rn / chunk, 1024,
+                             (size_t)2 * NBC * 4, sl.radix.sc, sl.radix.inf, rn, sl.radix.mont, glv_consts(),
+                             (int)sl.wps, sl.radix.dig, FB, NBC, nblk, chunk, ws[WS_COUNTS].as<uint32_t>());
+            else
+                VK_LAUNCH_ON(ctx, st, "glv_split", (k_glv_radix<BLS381Fr, 5, 16>), (rn + 255) / 256, 256, 0,
+                             sl.radix.sc, sl.radix.inf, rn, sl.radix.mont, glv_consts(), (int)sl.wps, sl.radix.dig);
+        }
+    }
     VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (uint32_t)nv : 0u,
                         sl.wps, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
-                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max, cstage));
+                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max, cstage, counts_ready));
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W;
     // chain_max was cleared by k_sort_fine
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
@@ -1398,7 +1469,9 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
             VK_TRY(ctx->ws[WS_GLV_SC].ensure(radix_m > 1 ? nv * 4 * (size_t)Wfull : nv * 16));
             uint4* halves = ctx->ws[WS_GLV_SC].as<uint4>();
             const Aff* dphi = t->fast.as<Aff>() + t->n + offset;
-            if (radix_m > 1)
+            if (radix_m > 1 && nsl == 1)  // the split runs in slice_enqueue (sort histogram fused)
+                sl[0].radix = {d_sc, inf, (uint32_t)n, mont, ctx->ws[WS_GLV_SC].as<int32_t>()};
+            else if (radix_m > 1)
                 VK_LAUNCH(ctx, "glv_split", (k_glv_radix<Fr, 5, 16>), (n + 255) / 256, 256, 0, d_sc, inf, (uint32_t)n,
                           mont, glv_consts(), Wfull, ctx->ws[WS_GLV_SC].as<int32_t>());
             else
