@@ -144,3 +144,19 @@ def radix_bucket_sum_residue(buckets, lseg):
         suf += U[r]
         v += suf
     return v
+
+
+def bit_sums_marginal(R, h):
+    """T_j = sum_{s: bit j of s} R_s by the marginal form of msm_tail.hip k_msm_bitsum /
+    PartLoc (msm_tail.hpp msm_tail_plan): with s = G hi + lo (G = 2^h), the column sums
+    L_lo = sum_hi R_{G hi + lo} and row sums H_hi = sum_lo R_{G hi + lo}; T_j is the sum of the
+    L_lo with bit j of lo (j < h) or of the H_hi with bit j - h of hi (j >= h)."""
+    S = len(R)
+    J = max(1, (S - 1).bit_length())
+    assert S == 1 << J and 0 < h < J
+    G, Hn = 1 << h, 1 << (J - h)
+    Lc = [sum(R[hi * G + lo] for hi in range(Hn)) for lo in range(G)]
+    Hr = [sum(R[hi * G + lo] for lo in range(G)) for hi in range(Hn)]
+    return [sum(Lc[lo] for lo in range(G) if (lo >> j) & 1) if j < h else
+            sum(Hr[hi] for hi in range(Hn) if (hi >> (j - h)) & 1) for j in range(J)]
+

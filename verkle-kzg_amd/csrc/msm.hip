@@ -1194,8 +1194,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     VK_TRY(ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(ws[WS_SEG].ensure((size_t)S * Wr * sizeof(RAcc)));
     VK_TRY(ws[WS_TREE].ensure((size_t)S * Wr * sizeof(RAcc)));
-    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * (J + nU) * msm_bitsum_pw(S, msm_bitsum_k(S, (uint32_t)Wr, J, 64, nU)) *
-                             sizeof(RAcc)));
+    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * msm_tail_plan(S, (uint32_t)Wr, J, nU, Fast29<C>::type::quad).per_w * sizeof(RAcc)));
     // tail points, then the chain_max word: one read-back
     const size_t tail_bytes = ((size_t)Wr * (J + nU) * sizeof(Acc) + 15) & ~(size_t)15;
     VK_TRY(ws[WS_TAIL].ensure(tail_bytes + 16));

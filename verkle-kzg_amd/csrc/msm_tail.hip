@@ -301,38 +301,49 @@ __device__ __forceinline__ typename A::Acc shfl_acc(const typename A::Acc& v, ui
 // Waves are laid out compactly (window by window: J x nb1 bit-sum waves, then nb2), so the grid
 // holds only busy waves and every CU gets at most one block (a grid with idle waves let the
 // dispatcher stack two busy blocks on some CUs: their SIMDs ran two waves, twice as long).
+// Marginal form (h > 0, msm_tail_plan): per set, waves [0, G) make the column sums L_lo (Hn items
+// lo + G m), waves [G, G + Hn) the row sums H_hi (G items G hi + m) -- one wave and one partial
+// slot each, Hn / 64 or G / 64 items per lane -- and the rest the U partials as in the bit form.
 template <class A>
 __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __restrict__ usrc,
                                                    const typename A::Acc* __restrict__ tsrc, uint32_t S, uint32_t J,
-                                                   uint32_t nU, uint32_t K, uint32_t nb1, uint32_t nb2,
+                                                   uint32_t h, uint32_t nU, uint32_t K, uint32_t nb1, uint32_t nb2,
                                                    uint32_t n_waves, const uint32_t* __restrict__ toff,
                                                    const uint32_t* __restrict__ uoff,
                                                    typename A::Acc* __restrict__ partial) {
     using Acc = typename A::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
-    const uint32_t per_w = J * nb1 + nU * nb2;
+    const uint32_t G = h ? 1u << h : 0u, Hn = h ? 1u << (J - h) : 0u;
+    const uint32_t nT = h ? G + Hn : J * nb1;  // waves of the T side per set
+    const uint32_t per_w = nT + nU * nb2;
     const uint32_t w = gw / per_w, r = gw % per_w;
-    const uint32_t q = r < J * nb1 ? r / nb1 : J + (r - J * nb1) / nb2;
-    const uint32_t wv = r < J * nb1 ? r % nb1 : (r - J * nb1) % nb2;
-    const uint32_t n_items = q < J ? S / 2 : S;
-    const uint32_t base = wv * 64 * K;
-    const uint32_t u = q - J;  // q >= J: the column of the U sum
-    const size_t set0 = q < J ? (size_t)w * S : (size_t)w * S * nU;
-    const Acc* src = (q < J ? tsrc : usrc) + set0;
-    const uint32_t* off = (q < J ? toff : uoff);
+    // kind: 0 = T_q (bit form), 1 = L_lo, 2 = H_hi, 3 = U_u; sel = q, lo, hi or u
+    const uint32_t kind = r >= nT ? 3u : h == 0 ? 0u : r < G ? 1u : 2u;
+    const uint32_t sel = kind == 0 ? r / nb1 : kind == 1 ? r : kind == 2 ? r - G : (r - nT) / nb2;
+    const uint32_t wv = kind == 0 ? r % nb1 : kind == 3 ? (r - nT) % nb2 : 0u;
+    const uint32_t n_items = kind == 0 ? S / 2 : kind == 1 ? Hn : kind == 2 ? G : S;
+    const uint32_t Kw = kind == 1 ? Hn / 64 : kind == 2 ? G / 64 : K;
+    const uint32_t base = wv * 64 * Kw;
+    const size_t set0 = kind < 3 ? (size_t)w * S : (size_t)w * S * nU;
+    const Acc* src = (kind < 3 ? tsrc : usrc) + set0;
+    const uint32_t* off = (kind < 3 ? toff : uoff);
     if (off) off += set0;
-    // item m of this sum -> its index in src (T_q: the m-th s with bit q set; U_u: nU m + u)
+    // item m of this sum -> its index in src (T_q: the m-th s with bit q set; L_lo: G m + lo;
+    // H_hi: G hi + m; U_u: nU m + u)
     auto item = [&](uint32_t m) -> uint32_t {
-        return q < J ? (((m >> q) << (q + 1)) | (1u << q) | (m & ((1u << q) - 1))) : m * nU + u;
+        return kind == 0   ? (((m >> sel) << (sel + 1)) | (1u << sel) | (m & ((1u << sel) - 1)))
+               : kind == 1 ? m * G + sel
+               : kind == 2 ? sel * G + m
+                           : m * nU + sel;
     };
     Acc v = A::zero();
     if constexpr (A::quad) {
-        // K serial full adds per lane (every SIMD busy: issue-bound), then the wave's 64 lane sums
+        // Kw serial full adds per lane (every SIMD busy: issue-bound), then the wave's 64 lane sums
         // on 4-lane cooperative adds: each quad first folds its own 4 lanes (3 rounds), then the
         // 16 quads by xor (4) -- 7 adds of ~14.6k cycles instead of the 6-level butterfly of full
         // adds (~30k cycles each)
-        for (uint32_t it = 0; it < K; it++) {
+        for (uint32_t it = 0; it < Kw; it++) {
             const uint32_t m = base + it * 64 + lane;
             const uint32_t idx = item(m);
             const bool live = m < n_items && (!off || off[idx + 1] > off[idx]);
@@ -348,32 +359,66 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
         if (lane == 0) partial[gw] = s;
         return;
     }
-    for (uint32_t it = 0; it < K + 6; it++) {
+    for (uint32_t it = 0; it < Kw + 6; it++) {
         Acc o;
-        if (it < K) {
+        if (it < Kw) {
             const uint32_t m = base + it * 64 + lane;  // lane-interleaved rows
             const uint32_t idx = item(m);
             const bool live = m < n_items && (!off || off[idx + 1] > off[idx]);
             o = live ? src[idx] : A::zero();
         } else {
-            o = shfl_acc<A>(v, 1u << (it - K));
+            o = shfl_acc<A>(v, 1u << (it - Kw));
         }
         v = A::add(v, o);
     }
     if (lane == 0) partial[gw] = v;
 }
 
+// where sum `sum` (= w (J + nU) + q) of the final stage finds its items in `partial`: cnt items,
+// the k-th at index pos(k). Bit form: the sum's own nb1 / nb2 wave partials. Marginal form:
+// T_q (q < h) = the G / 2 column sums L_lo with bit q of lo set, T_q (q >= h) = the Hn / 2 row
+// sums H_hi with bit q - h of hi set, U_u = its nb2 partials.
+struct PartLoc {
+    size_t start;
+    uint32_t cnt, bit;  // bit < 32: the items are the slots with this bit set, from start
+    __device__ PartLoc(uint32_t sum, uint32_t J, uint32_t h, uint32_t nU, uint32_t nb1, uint32_t nb2) {
+        const uint32_t w = sum / (J + nU), q = sum % (J + nU);
+        const uint32_t G = h ? 1u << h : 0u, Hn = h ? 1u << (J - h) : 0u;
+        const uint32_t nT = h ? G + Hn : J * nb1;
+        const size_t set0 = (size_t)w * (nT + nU * nb2);
+        bit = 32;
+        if (q >= J) {
+            start = set0 + nT + (size_t)(q - J) * nb2;
+            cnt = nb2;
+        } else if (h == 0) {
+            start = set0 + (size_t)q * nb1;
+            cnt = nb1;
+        } else if (q < h) {
+            start = set0;
+            cnt = G / 2;
+            bit = q;
+        } else {
+            start = set0 + G;
+            cnt = Hn / 2;
+            bit = q - h;
+        }
+    }
+    __device__ size_t pos(uint32_t k) const {
+        if (bit >= 32) return start + k;
+        return start + (((k >> bit) << (bit + 1)) | (1u << bit) | (k & ((1u << bit) - 1)));
+    }
+};
+
 // stage 2: one wave per (w, q) sum folds its partials (nb1 or nb2: ceil(n/64) per lane, then
 // the butterfly)
 template <class C, class A>
 __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __restrict__ partial, uint32_t J,
-                                                   uint32_t nU, uint32_t nb1, uint32_t nb2,
+                                                   uint32_t h, uint32_t nU, uint32_t nb1, uint32_t nb2,
                                                    typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
-    const uint32_t w = sum / (J + nU), q = sum % (J + nU);
-    const uint32_t cnt = q < J ? nb1 : nb2;
-    const size_t start = (size_t)w * (J * nb1 + nU * nb2) + (q < J ? q * nb1 : J * nb1 + (q - J) * nb2);
+    const PartLoc loc(sum, J, h, nU, nb1, nb2);
+    const uint32_t cnt = loc.cnt;
     uint32_t span = 1, lg = 0;
     while (span < cnt && span < 64) {
         span <<= 1;
@@ -385,7 +430,7 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
         Acc o;
         if (it < nk) {
             const uint32_t k = lane + it * 64;
-            o = k < cnt ? partial[start + k] : A::zero();
+            o = k < cnt ? partial[loc.pos(k)] : A::zero();
         } else {
             o = shfl_acc<A>(v, 1u << (it - nk));
         }
@@ -403,23 +448,23 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
 constexpr uint32_t SUMPART_WAVES = 4;
 template <class C, class A>
 __global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial,
-                                                                     uint32_t J, uint32_t nU, uint32_t nb1,
-                                                                     uint32_t nb2, typename C::Acc* __restrict__ out) {
+                                                                     uint32_t J, uint32_t h, uint32_t nU,
+                                                                     uint32_t nb1, uint32_t nb2,
+                                                                     typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
     constexpr uint32_t QPB = 16 * SUMPART_WAVES, LGW = SUMPART_WAVES == 4 ? 2 : SUMPART_WAVES == 2 ? 1 : 0;
     static_assert((1u << LGW) == SUMPART_WAVES, "SUMPART_WAVES: 1, 2 or 4");
     __shared__ Acc wave_sum[SUMPART_WAVES];
     const uint32_t sum = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, role = lane & 3;
-    const uint32_t w = sum / (J + nU), q = sum % (J + nU);
-    const uint32_t cnt = q < J ? nb1 : nb2;
-    const size_t start = (size_t)w * (J * nb1 + nU * nb2) + (q < J ? q * nb1 : J * nb1 + (q - J) * nb2);
+    const PartLoc loc(sum, J, h, nU, nb1, nb2);
+    const uint32_t cnt = loc.cnt;
     const uint32_t nk = (cnt + QPB - 1) / QPB;
     Acc v = A::zero();
     for (uint32_t it = 0; it < nk + 4 + LGW; it++) {  // one add call site
         Acc o;
         if (it < nk) {
             const uint32_t k = (tid >> 2) + it * QPB;  // quad index within the block
-            o = k < cnt ? partial[start + k] : A::zero();
+            o = k < cnt ? partial[loc.pos(k)] : A::zero();
         } else if (it < nk + 4) {
             o = shfl_acc<A>(v, 4u << (it - nk));  // quad to quad inside the wave: xor of a multiple of 4
         } else {
@@ -577,16 +622,16 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
                          offsets, NB, W, Lseg, S, accs, Rs);
     }
     const uint32_t sums = (uint32_t)W * (J + nU);
-    const uint32_t K = msm_bitsum_k(S, (uint32_t)W, J, 64, nU);
-    const uint32_t nb1 = msm_bitsum_pw(S / 2, K), nb2 = msm_bitsum_pw(S, K);
-    const uint32_t n_waves = (uint32_t)W * (J * nb1 + nU * nb2);
-    VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, usrc, Rs, S, J, nU, K,
-                 nb1, nb2, n_waves, toff, uoff, partial);
+    const TailPlan tp = msm_tail_plan(S, (uint32_t)W, J, nU, A::quad);
+    const uint32_t n_waves = (uint32_t)W * tp.per_w;
+    VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, usrc, Rs, S, J, tp.h,
+                 nU, tp.K, tp.nb1, tp.nb2, n_waves, toff, uoff, partial);
     if constexpr (A::quad)
-        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, nU,
-                     nb1, nb2, out);
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, tp.h,
+                     nU, tp.nb1, tp.nb2, out);
     else
-        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, nU, nb1, nb2, out);
+        VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, tp.h, nU, tp.nb1,
+                     tp.nb2, out);
     return VC_OK;
 }
 

@@ -1,5 +1,9 @@
 // Launchers of the latency-bound Pippenger tail kernels (msm_tail.hip).
 #pragma once
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "ctx.hpp"
 #include "ec.hpp"
 #include "ec29.hpp"
@@ -23,6 +27,50 @@ inline uint32_t msm_bitsum_k(uint32_t S, uint32_t W, uint32_t J, uint32_t lanes 
 // waves (= partial slots) of one bit-stage sum over `items` items (K per logical lane)
 inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K, uint32_t lanes = 64) {
     return (items + lanes * K - 1) / (lanes * K);
+}
+// Geometry of the bit stage. Bit form (h = 0): J sums T_j over S/2 items each (nb1 waves per
+// sum) + nU sums U over S items (nb2 waves). Marginal form (h > 0, J >= 12): with s = G hi + lo
+// (G = 2^h, Hn = 2^(J-h) high values) the stage instead makes the G column sums L_lo = sum_hi
+// R_(G hi + lo) (Hn items) and the Hn row sums H_hi = sum_lo R_(G hi + lo) (G items), each by one
+// wave, plus the U sums as before; the final stage then reads T_j = sum over lo with bit j of L_lo
+// (j < h) or over hi with bit j - h of H_hi (j >= h) -- the same T_j from 2 S + ~S adds instead of
+// J S / 2. per_w = partial slots per set (the WS_WIN layout).
+struct TailPlan {
+    uint32_t h = 0, K = 0, nb1 = 0, nb2 = 0, per_w = 0;
+};
+// Chosen by a cost model in full-add times: a wave costs its K serial adds plus the in-wave
+// butterfly (7 quad adds ~ 3.5 full adds; 6 full adds without quads), and a stage whose waves fit
+// one round (<= 1024, a wave per SIMD) takes its longest wave. The marginal form is taken only
+// within one round and when shorter: measured on one MI355X, the 2^20 radix MSM's one set 10.5 ->
+// 7.5 units, 0.165 -> 0.118 ms; the 8-way window slice 8.5 -> 7.5, 0.121 -> 0.107 ms. Stacked
+// rounds do not follow the model (8 and 16 windows of 2^13 segments, 1744+ waves of 1-5 items
+// per lane: 0.170 -> 0.198 and 0.139 -> 0.179 ms), so several sets keep the bit form.
+inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, bool quad = true) {
+    static const int marg_env = getenv("VKZG_TAIL_MARGINAL") ? atoi(getenv("VKZG_TAIL_MARGINAL")) : 1;  // A/B probe
+    const double bf = quad ? 3.5 : 6.0;
+    TailPlan p;
+    p.K = msm_bitsum_k(S, W, J, 64, nU);
+    p.nb1 = msm_bitsum_pw(S / 2, p.K);
+    p.nb2 = msm_bitsum_pw(S, p.K);
+    p.per_w = J * p.nb1 + nU * p.nb2;
+    if (!(marg_env && J >= 12 && S == (1u << J))) return p;
+    if ((uint64_t)W * p.per_w > 1024) return p;
+    const uint32_t h = J / 2, G = 1u << h, Hn = 1u << (J - h), kl = Hn / 64;  // Hn >= G >= 64
+    double best = p.K + bf;
+    for (uint32_t k = kl; k <= 32; k++) {  // U sums: no fewer items per lane than the L waves
+        const uint32_t nb = msm_bitsum_pw(S, k);
+        if ((uint64_t)W * (G + Hn + nU * nb) > 1024) continue;
+        const double t = k + bf;  // one round: the longest wave (k >= kl >= G / 64)
+        if (t < best - 1e-9) {
+            best = t;
+            p.h = h;
+            p.K = k;
+            p.nb1 = 0;
+            p.nb2 = nb;
+            p.per_w = G + Hn + nU * nb;
+        }
+    }
+    return p;
 }
 // guarded = 0: read the longest chain back (host sync) and run exactly the rounds it needs;
 // guarded = r > 0: r device-guarded rounds, no sync (chains up to 2^r threads; longer ones are
