@@ -12,7 +12,7 @@ import torch  # noqa: E402
 import vkzg  # noqa: E402
 
 NAMES = ("glv_split", "glv_phi", "msm_sort_hist", "msm_scan", "msm_sort_coarse", "msm_sort_fine", "msm_accumulate",
-         "msm_fixup_init", "msm_fixup_jump", "msm_fixup", "msm_segsum", "msm_bitsum", "msm_sumpart")
+         "msm_fixup_init", "msm_fixup_jump", "msm_fixup", "msm_fixup_long", "msm_segsum", "msm_bitsum", "msm_sumpart")
 
 curve = sys.argv[1] if len(sys.argv) > 1 else "bls12_381"
 n = 1 << (int(sys.argv[2]) if len(sys.argv) > 2 else 20)
