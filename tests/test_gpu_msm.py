@@ -26,8 +26,10 @@ def _oracle(cref, curve, xy, inf, sc, threads=16):
 
 
 @pytest.mark.parametrize("curve", CURVES)
-@pytest.mark.parametrize("n", [1, 2, 7, 64, 255, 1000, 4099])
+@pytest.mark.parametrize("n", [1, 2, 7, 64, 255, 1000, 4099, 20000])
 def test_msm_random(engines, oracle_c, curve, n):
+    """bit-exact against the C oracle; n = 20000 (GLV: 40000 terms, shared windows of c = 13, one
+    set of 2^12 buckets) runs the tail's bit stage in its marginal form (msm_tail_plan, J = 12)"""
     import vkzg
     e = engines[curve]
     rng = np.random.default_rng(1000 + n)
