@@ -130,6 +130,24 @@ def cpu_baseline(curve, n_full, sample, reps=3):
             "ms_per_msm": per_msm_s * 1e3, "host_cpus": os.cpu_count()}
 
 
+def host_cpu_share():
+    """What the process may actually run on: the CPUs it reports, its affinity mask and the cgroup
+    v2 CPU quota (cpu.max "quota period"; None when unlimited or unreadable). On the GPU boxes the
+    OS reports 256 CPUs while the quota is one GPU's share, so a 256-thread run time-slices."""
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"reported": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_pippenger(curve, xy, inf, scalars, want, threads, reps=3):
     """The fair all-core CPU bound: the same 2^20 MSM by the bucket method in C
     (oracle/c/ref_curve.c pip_msm: per-thread point chunks, signed windows, mixed bucket adds),
@@ -1020,7 +1038,14 @@ def main():
         bxy, binf = eng.download_bases(table)
         out["cpu_baseline_pippenger"] = cpu_pippenger(curve, bxy, binf, scalars, res, thr)
         # and on every host core the box reports ("Pippenger on all host cores")
-        out["cpu_baseline_pippenger_allcores"] = cpu_pippenger(curve, bxy, binf, scalars, res, os.cpu_count() or 1)
+        allc = cpu_pippenger(curve, bxy, binf, scalars, res, os.cpu_count() or 1)
+        share = host_cpu_share()
+        allc["host_cpu_share"] = share
+        if share["cgroup_quota_cpus"] is not None and share["cgroup_quota_cpus"] < allc["cores"]:
+            allc["note"] = (f"{allc['cores']} threads time-slice a cgroup quota of {share['cgroup_quota_cpus']} CPUs: "
+                            f"slower than the {thr}-thread line; the true all-core figure of a whole host is not "
+                            f"measurable from this box")
+        out["cpu_baseline_pippenger_allcores"] = allc
         del bxy, binf
         out["cpu_baselines_other"]["C3_width256_commits_pippenger"] = cpu_pippenger_commits(a.commit_batch, thr)
         if "kzg" in out:  # configs[3] on the CPU: its two 2^20 MSMs alone (quotient not counted)

@@ -16,7 +16,8 @@ e.set_stream(torch.cuda.current_stream().cuda_stream)
 tid = e.random_bases(n, seed=2024)
 sc = vkzg.random_scalars("bls12_381", n, np.random.default_rng(1234))
 d = torch.from_numpy(sc.view(np.int64).copy()).cuda()
-for G in (1, 2, 4, 8):
+GS = [int(g) for g in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 2, 4, 8]
+for G in GS:
     for k in sorted({0, G - 1}):
         for _ in range(2):
             e.msm_device_window_part(tid, d.data_ptr(), n, k, G)
