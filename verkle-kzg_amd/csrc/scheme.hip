@@ -12,6 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -309,11 +312,20 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
 }
 
 // ---------------------------------------------------------------- IPA verify (a10)
+// VKZG_HOST_TIMING=1: the verifier's host / GPU phases on stderr (probe)
+static double verify_clock_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool verify_timing() {
+    static const bool on = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+    return on;
+}
 int ipa_verify_impl(vc_ctx* ctx, Table* t, size_t N, const Acc& com, const Fr& point, const vc_ipa_proof* pr,
                     vc_transcript* tr_in, int* result) {
     if (!is_pow2(N) || t->n < N + 1) return VC_E_INVALID;
     size_t K = pr->rounds;
     if ((1ull << K) != N) return VC_E_INVALID;  // gens = g[0..2^rounds], zip with points_coeffs
+    const double t0 = verify_timing() ? verify_clock_us() : 0.0;
     Fr omega = bn254_group_gen(N);
     if (barycentric_panics(N, point)) return VC_E_DOMAIN;
     std::vector<Fr> b = barycentric(N, point, omega);
@@ -353,7 +365,9 @@ int ipa_verify_impl(vc_ctx* ctx, Table* t, size_t N, const Acc& com, const Fr& p
     fs[N] = fe_sub<F>(fe_mul<F>(fe_mul<F>(prodx, w), y), fe_mul<F>(fe_mul<F>(w, tip), cb));
     uint64_t axy[8];
     uint8_t ainf;
+    const double t1 = verify_timing() ? verify_clock_us() : 0.0;
     VK_TRY(commit_batch(ctx, t, N + 1, fs.data(), 1, axy, &ainf));
+    const double t2 = verify_timing() ? verify_clock_us() : 0.0;
     // variable part: prodx*C + sum_k P_k L_k + P_k x_k^2 R_k,  P_k = prod_{j>k} x_j
     std::vector<uint64_t> vxy(8 * (1 + 2 * K));
     std::vector<uint8_t> vinf(1 + 2 * K);
@@ -373,6 +387,9 @@ int ipa_verify_impl(vc_ctx* ctx, Table* t, size_t N, const Acc& com, const Fr& p
     }
     Acc vb;
     VK_TRY(msm_points(ctx, vxy.data(), vinf.data(), vs, &vb));
+    if (verify_timing())
+        fprintf(stderr, "ipa_verify host_prep_us=%.1f commit_us=%.1f straus_us=%.1f\n", t1 - t0, t2 - t1,
+                verify_clock_us() - t2);
     Acc tot = C::add(acc_of(axy, ainf), vb);
     *result = C::is_zero(tot) ? 1 : 0;
     return VC_OK;
