@@ -160,3 +160,23 @@ def bit_sums_marginal(R, h):
     return [sum(Lc[lo] for lo in range(G) if (lo >> j) & 1) if j < h else
             sum(Hr[hi] for hi in range(Hn) if (hi >> (j - h)) & 1) for j in range(J)]
 
+
+def bit_sums_marginal_urow(R, h, pL):
+    """The row-derived total of the marginal form (msm_tail.hpp TailPlan::urow, msm_tail.hip
+    PartLoc, msm.hip slice_finish), for Lseg = 1 where the total U = sum_s R_s is wanted beside the
+    T_j: every column sum L_lo is made as pL partials (pL waves over Hn / pL rows each); T_j (j < h)
+    sums the partials of the columns with bit j of lo, T_j (j >= h) the row sums H_hi with bit j - h
+    of hi; the final stage's U slot holds X = the row sums of even hi, and the host adds T_h.
+    Returns (T, U)."""
+    S = len(R)
+    J = max(1, (S - 1).bit_length())
+    G, Hn = 1 << h, 1 << (J - h)
+    assert S == 1 << J and 0 < h < J and pL >= 1 and Hn % pL == 0
+    part = [[sum(R[hi * G + lo] for hi in range(p * Hn // pL, (p + 1) * Hn // pL)) for p in range(pL)]
+            for lo in range(G)]
+    Hr = [sum(R[hi * G + lo] for lo in range(G)) for hi in range(Hn)]
+    T = [sum(x for lo in range(G) if (lo >> j) & 1 for x in part[lo]) if j < h else
+         sum(Hr[hi] for hi in range(Hn) if (hi >> (j - h)) & 1) for j in range(J)]
+    X = sum(Hr[hi] for hi in range(0, Hn, 2))
+    return T, X + T[h]
+

@@ -131,3 +131,20 @@ def test_bit_sums_marginal_form():
         for h in range(1, J):
             assert pippenger.bit_sums_marginal(R, h) == want
 
+
+
+def test_bit_sums_marginal_row_total():
+    """the row-derived total of the marginal form (TailPlan::urow, Lseg = 1): column sums split
+    into pL partial waves give the same T_j, and X (even-hi row sums) + T_h is the total U --
+    checked over integers for every split h of J = 2..8 and pL = 1, 2, 4 (where pL divides Hn)."""
+    from pyoracle import pippenger
+    rng = random.Random(13)
+    for J in range(2, 9):
+        R = [rng.randrange(1 << 64) for _ in range(1 << J)]
+        want = [sum(R[s] for s in range(1 << J) if (s >> j) & 1) for j in range(J)]
+        for h in range(1, J):
+            for pL in (1, 2, 4):
+                if (1 << (J - h)) % pL:
+                    continue
+                T, U = pippenger.bit_sums_marginal_urow(R, h, pL)
+                assert T == want and U == sum(R)

@@ -1194,7 +1194,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     VK_TRY(ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(ws[WS_SEG].ensure((size_t)S * Wr * sizeof(RAcc)));
     VK_TRY(ws[WS_TREE].ensure((size_t)S * Wr * sizeof(RAcc)));
-    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * msm_tail_plan(S, (uint32_t)Wr, J, nU, Fast29<C>::type::quad).per_w * sizeof(RAcc)));
+    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * msm_tail_plan(S, (uint32_t)Wr, J, nU, Fast29<C>::type::quad, Lseg == 1).per_w *
+                             sizeof(RAcc)));
     // tail points, then the chain_max word: one read-back
     const size_t tail_bytes = ((size_t)Wr * (J + nU) * sizeof(Acc) + 15) & ~(size_t)15;
     VK_TRY(ws[WS_TAIL].ensure(tail_bytes + 16));
@@ -1319,6 +1320,14 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
                                     sl.L.st));
         VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
     }
+    // row-derived totals (TailPlan::urow): the final stage left X = sum of the even-hi row sums in
+    // each set's U slot; U = X + T_h (the odd-hi rows)
+    const TailPlan tp = msm_tail_plan(sl.S, (uint32_t)sl.Wr, sl.J, sl.nU, Fast29<C>::type::quad, sl.Lseg == 1);
+    if (tp.urow)
+        for (int w = 0; w < sl.Wr; w++) {
+            Acc* u = &sl.ht[(size_t)w * (sl.J + sl.nU) + sl.J];
+            *u = C::add(*u, sl.ht[(size_t)w * (sl.J + sl.nU) + tp.h]);
+        }
     // slice = sum_w 2^(c w) (A_w + Lseg sum_j 2^j T_wj): Horner over bit positions (host); with
     // shared windows the one bucket set already holds the 2^(c w) factors: A + Lseg sum_j 2^j T_j
     const uint32_t J = sl.J;

@@ -308,22 +308,22 @@ template <class A>
 __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __restrict__ usrc,
                                                    const typename A::Acc* __restrict__ tsrc, uint32_t S, uint32_t J,
                                                    uint32_t h, uint32_t nU, uint32_t K, uint32_t nb1, uint32_t nb2,
-                                                   uint32_t n_waves, const uint32_t* __restrict__ toff,
+                                                   uint32_t pL, uint32_t n_waves, const uint32_t* __restrict__ toff,
                                                    const uint32_t* __restrict__ uoff,
                                                    typename A::Acc* __restrict__ partial) {
     using Acc = typename A::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
     const uint32_t G = h ? 1u << h : 0u, Hn = h ? 1u << (J - h) : 0u;
-    const uint32_t nT = h ? G + Hn : J * nb1;  // waves of the T side per set
-    const uint32_t per_w = nT + nU * nb2;
+    const uint32_t nT = h ? G * pL + Hn : J * nb1;  // waves of the T side per set (pL per column sum)
+    const uint32_t per_w = nT + nU * nb2;             // urow: nb2 = 0, no U waves
     const uint32_t w = gw / per_w, r = gw % per_w;
     // kind: 0 = T_q (bit form), 1 = L_lo, 2 = H_hi, 3 = U_u; sel = q, lo, hi or u
-    const uint32_t kind = r >= nT ? 3u : h == 0 ? 0u : r < G ? 1u : 2u;
-    const uint32_t sel = kind == 0 ? r / nb1 : kind == 1 ? r : kind == 2 ? r - G : (r - nT) / nb2;
-    const uint32_t wv = kind == 0 ? r % nb1 : kind == 3 ? (r - nT) % nb2 : 0u;
+    const uint32_t kind = r >= nT ? 3u : h == 0 ? 0u : r < G * pL ? 1u : 2u;
+    const uint32_t sel = kind == 0 ? r / nb1 : kind == 1 ? r / pL : kind == 2 ? r - G * pL : (r - nT) / nb2;
+    const uint32_t wv = kind == 0 ? r % nb1 : kind == 1 ? r % pL : kind == 3 ? (r - nT) % nb2 : 0u;
     const uint32_t n_items = kind == 0 ? S / 2 : kind == 1 ? Hn : kind == 2 ? G : S;
-    const uint32_t Kw = kind == 1 ? Hn / 64 : kind == 2 ? G / 64 : K;
+    const uint32_t Kw = kind == 1 ? Hn / (64 * pL) : kind == 2 ? G / 64 : K;
     const uint32_t base = wv * 64 * Kw;
     const size_t set0 = kind < 3 ? (size_t)w * S : (size_t)w * S * nU;
     const Acc* src = (kind < 3 ? tsrc : usrc) + set0;
@@ -380,14 +380,22 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
 // sums H_hi with bit q - h of hi set, U_u = its nb2 partials.
 struct PartLoc {
     size_t start;
-    uint32_t cnt, bit;  // bit < 32: the items are the slots with this bit set, from start
-    __device__ PartLoc(uint32_t sum, uint32_t J, uint32_t h, uint32_t nU, uint32_t nb1, uint32_t nb2) {
+    uint32_t cnt, bit;  // bit < 32: the items are the slots with this bit set (clear: unset), from start
+    uint32_t lgp = 0;   // column sums: 2^lgp partial slots each (pL), all taken
+    bool clear = false;
+    __device__ PartLoc(uint32_t sum, uint32_t J, uint32_t h, uint32_t nU, uint32_t nb1, uint32_t nb2, uint32_t pL,
+                       bool urow) {
         const uint32_t w = sum / (J + nU), q = sum % (J + nU);
         const uint32_t G = h ? 1u << h : 0u, Hn = h ? 1u << (J - h) : 0u;
-        const uint32_t nT = h ? G + Hn : J * nb1;
+        const uint32_t nT = h ? G * pL + Hn : J * nb1;
         const size_t set0 = (size_t)w * (nT + nU * nb2);
         bit = 32;
-        if (q >= J) {
+        if (q >= J && urow) {  // X = the row sums of even hi (the host adds T_h: U = T_h + X)
+            start = set0 + (size_t)G * pL;
+            cnt = Hn / 2;
+            bit = 0;
+            clear = true;
+        } else if (q >= J) {
             start = set0 + nT + (size_t)(q - J) * nb2;
             cnt = nb2;
         } else if (h == 0) {
@@ -395,17 +403,20 @@ struct PartLoc {
             cnt = nb1;
         } else if (q < h) {
             start = set0;
-            cnt = G / 2;
+            cnt = G / 2 * pL;
             bit = q;
+            while ((1u << lgp) < pL) lgp++;
         } else {
-            start = set0 + G;
+            start = set0 + (size_t)G * pL;
             cnt = Hn / 2;
             bit = q - h;
         }
     }
     __device__ size_t pos(uint32_t k) const {
         if (bit >= 32) return start + k;
-        return start + (((k >> bit) << (bit + 1)) | (1u << bit) | (k & ((1u << bit) - 1)));
+        const uint32_t i = k >> lgp, sub = k & ((1u << lgp) - 1);
+        const uint32_t e = ((i >> bit) << (bit + 1)) | (clear ? 0u : 1u << bit) | (i & ((1u << bit) - 1));
+        return start + ((size_t)e << lgp) + sub;
     }
 };
 
@@ -414,10 +425,10 @@ struct PartLoc {
 template <class C, class A>
 __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __restrict__ partial, uint32_t J,
                                                    uint32_t h, uint32_t nU, uint32_t nb1, uint32_t nb2,
-                                                   typename C::Acc* __restrict__ out) {
+                                                   uint32_t pL, uint32_t urow, typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
-    const PartLoc loc(sum, J, h, nU, nb1, nb2);
+    const PartLoc loc(sum, J, h, nU, nb1, nb2, pL, urow != 0);
     const uint32_t cnt = loc.cnt;
     uint32_t span = 1, lg = 0;
     while (span < cnt && span < 64) {
@@ -449,14 +460,14 @@ constexpr uint32_t SUMPART_WAVES = 4;
 template <class C, class A>
 __global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial,
                                                                      uint32_t J, uint32_t h, uint32_t nU,
-                                                                     uint32_t nb1, uint32_t nb2,
-                                                                     typename C::Acc* __restrict__ out) {
+                                                                     uint32_t nb1, uint32_t nb2, uint32_t pL,
+                                                                     uint32_t urow, typename C::Acc* __restrict__ out) {
     using Acc = typename A::Acc;
     constexpr uint32_t QPB = 16 * SUMPART_WAVES, LGW = SUMPART_WAVES == 4 ? 2 : SUMPART_WAVES == 2 ? 1 : 0;
     static_assert((1u << LGW) == SUMPART_WAVES, "SUMPART_WAVES: 1, 2 or 4");
     __shared__ Acc wave_sum[SUMPART_WAVES];
     const uint32_t sum = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, role = lane & 3;
-    const PartLoc loc(sum, J, h, nU, nb1, nb2);
+    const PartLoc loc(sum, J, h, nU, nb1, nb2, pL, urow != 0);
     const uint32_t cnt = loc.cnt;
     const uint32_t nk = (cnt + QPB - 1) / QPB;
     Acc v = A::zero();
@@ -622,16 +633,18 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
                          offsets, NB, W, Lseg, S, accs, Rs);
     }
     const uint32_t sums = (uint32_t)W * (J + nU);
-    const TailPlan tp = msm_tail_plan(S, (uint32_t)W, J, nU, A::quad);
+    // Lseg = 1: the U items are the R_s themselves, so U can come from the row sums (TailPlan::urow;
+    // the caller's fold then adds T_h to it, msm_tail_fix_urow)
+    const TailPlan tp = msm_tail_plan(S, (uint32_t)W, J, nU, A::quad, Lseg == 1);
     const uint32_t n_waves = (uint32_t)W * tp.per_w;
     VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, usrc, Rs, S, J, tp.h,
-                 nU, tp.K, tp.nb1, tp.nb2, n_waves, toff, uoff, partial);
+                 nU, tp.K, tp.nb1, tp.nb2, tp.pL, n_waves, toff, uoff, partial);
     if constexpr (A::quad)
         VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, tp.h,
-                     nU, tp.nb1, tp.nb2, out);
+                     nU, tp.nb1, tp.nb2, tp.pL, tp.urow ? 1u : 0u, out);
     else
         VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, tp.h, nU, tp.nb1,
-                     tp.nb2, out);
+                     tp.nb2, tp.pL, tp.urow ? 1u : 0u, out);
     return VC_OK;
 }
 

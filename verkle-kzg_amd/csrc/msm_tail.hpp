@@ -35,8 +35,13 @@ inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K, uint32_t lanes = 64) {
 // wave, plus the U sums as before; the final stage then reads T_j = sum over lo with bit j of L_lo
 // (j < h) or over hi with bit j - h of H_hi (j >= h) -- the same T_j from 2 S + ~S adds instead of
 // J S / 2. per_w = partial slots per set (the WS_WIN layout).
+// Row-derived total (urow, marginal form with nU = 1 and Lseg = 1, where U = sum_s R_s is the
+// total of the row sums): no U waves; the final stage sums X = the H_hi of even hi (Hn / 2 items, as
+// every T_j >= h) and the host adds T_h (the odd hi) to it. The column sums may then take pL waves
+// each (Hn / pL items per wave, pL <= Hn / G, so the T_j < h sums still read <= Hn / 2 partials).
 struct TailPlan {
-    uint32_t h = 0, K = 0, nb1 = 0, nb2 = 0, per_w = 0;
+    uint32_t h = 0, K = 0, nb1 = 0, nb2 = 0, per_w = 0, pL = 1;
+    bool urow = false;
 };
 // Chosen by a cost model in full-add times: a wave costs its K serial adds plus the in-wave
 // butterfly (7 quad adds ~ 3.5 full adds; 6 full adds without quads), and a stage whose waves fit
@@ -45,8 +50,10 @@ struct TailPlan {
 // 7.5 units, 0.165 -> 0.118 ms; the 8-way window slice 8.5 -> 7.5, 0.121 -> 0.107 ms. Stacked
 // rounds do not follow the model (8 and 16 windows of 2^13 segments, 1744+ waves of 1-5 items
 // per lane: 0.170 -> 0.198 and 0.139 -> 0.179 ms), so several sets keep the bit form.
-inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, bool quad = true) {
+inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, bool quad = true,
+                              bool u_total = false) {
     static const int marg_env = getenv("VKZG_TAIL_MARGINAL") ? atoi(getenv("VKZG_TAIL_MARGINAL")) : 1;  // A/B probe
+    static const int urow_env = getenv("VKZG_TAIL_UROW") ? atoi(getenv("VKZG_TAIL_UROW")) : 1;          // A/B probe
     const double bf = quad ? 3.5 : 6.0;
     TailPlan p;
     p.K = msm_bitsum_k(S, W, J, 64, nU);
@@ -68,6 +75,23 @@ inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, b
             p.nb1 = 0;
             p.nb2 = nb;
             p.per_w = G + Hn + nU * nb;
+        }
+    }
+    if (urow_env && u_total && nU == 1) {  // U from the row sums (u_total: the U items are the R_s)
+        for (uint32_t pl = 1; pl <= Hn / G; pl *= 2) {
+            if ((uint64_t)W * (G * pl + Hn) > 1024) break;
+            const uint32_t k = std::max(Hn / (64 * pl), G / 64);
+            const double t = k + bf;
+            if (t < best + 1e-9) {  // ties too: no U waves, and X reads half the U sum's partials
+                best = t;
+                p.h = h;
+                p.K = k;
+                p.nb1 = 0;
+                p.nb2 = 0;
+                p.pL = pl;
+                p.urow = true;
+                p.per_w = G * pl + Hn;
+            }
         }
     }
     return p;
