@@ -1124,7 +1124,12 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     while ((1u << J) < S) J++;
     // shared windows with segments: the residue form of the reduction (msm_tail.hip k_msm_segr)
     static const int resid_env = getenv("VKZG_TAIL_RESIDUE") ? atoi(getenv("VKZG_TAIL_RESIDUE")) : 1;  // A/B probe
-    const uint32_t nU = (sl.shared && Lseg > 1 && resid_env) ? Lseg : 1;
+    // per-window bucket sets too, up to 8 of them (VKZG_TAIL_RESIDUE=2: shared windows only -- A/B
+    // probe): the segment stage's 2 Lseg dependent adds become Lseg - 1 for Lseg more U sums in the bit
+    // stage. Measured (`profiles/r03/probes/residue_perwin/`): the GLV variable-base 2^20 MSM (8 sets)
+    // tail 0.436 -> 0.38 ms; 16-20 sets (BN254, Bandersnatch) 0.05-0.16 ms slower, so they keep acc_s
+    const bool resid_sets = sl.shared || Wr <= 8;
+    const uint32_t nU = (Lseg > 1 && resid_sets && (resid_env == 1 || (resid_env == 2 && sl.shared))) ? Lseg : 1;
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     hipStream_t st = L.st;
 
@@ -1343,15 +1348,23 @@ static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     while ((1u << lg_seg) < sl.Lseg) lg_seg++;
     const int maxpos = (sl.shared ? 0 : sl.c * (sl.we - 1)) + lg_seg + (int)J;
     std::vector<std::vector<int>> at(maxpos + 1);
+    const int st = (int)(J + sl.nU);  // reduced points per window: T_0 .. T_{J-1}, then the U sums
+    std::vector<Acc> aw(sl.Wr);       // A_w = sum_r (r + 1) U_r by suffix sums (nU = 1: the sum A)
     for (int w = 0; w < sl.Wr; w++) {
         const int p0 = sl.shared ? 0 : sl.c * (sl.wb + w);  // absolute bit position of window wb + w
-        at[p0].push_back(w * (int)(J + 1) + (int)J);
-        for (uint32_t j = 0; j < J; j++) at[p0 + lg_seg + (int)j].push_back(w * (int)(J + 1) + (int)j);
+        Acc a = C::zero(), suf = C::zero();
+        for (int k = (int)sl.nU - 1; k >= 0; k--) {
+            suf = C::add(suf, sl.ht[(size_t)w * st + J + k]);
+            a = C::add(a, suf);
+        }
+        aw[w] = a;
+        at[p0].push_back(-1 - w);  // < 0: A_w
+        for (uint32_t j = 0; j < J; j++) at[p0 + lg_seg + (int)j].push_back(w * st + (int)j);
     }
     Acc r = C::zero();
     for (int pos = maxpos; pos >= 0; pos--) {
         if (!C::is_zero(r)) r = C::dbl(r);
-        for (int idx : at[pos]) r = C::add(r, sl.ht[idx]);
+        for (int idx : at[pos]) r = C::add(r, idx < 0 ? aw[-1 - idx] : sl.ht[idx]);
     }
     *res = r;
     return VC_OK;
