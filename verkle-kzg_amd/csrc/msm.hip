@@ -1852,8 +1852,13 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C, FA>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
                   d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
                   d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max);
-        VK_TRY(msm_tail_fixup<C>(ctx, ctx->lane(0), Tmax, d_off.as<uint32_t>() + nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
-                                 d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max));
+        // straddling chunks merged by the serial walk of their owners, no chain limit: a chunk holds at
+        // most CHNZ x W entries, so it spans at most CHNZ W / M + 2 threads. (The pointer-jumping rounds
+        // used before read the longest chain back first -- a host sync per level -- and ran ~3 guarded
+        // launches: 0.6 ms of the 65,536-key full commitment's kernels.)
+        VK_TRY(msm_tail_fixup_walk<C>(ctx, ctx->lane(0), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(),
+                                      d_carry.as<RAcc>(), d_own.as<RAcc>(), 0xffffffffu, d_ownb.as<uint32_t>(),
+                                      d_thr.as<uint8_t>(), Tmax));
         VK_LAUNCH(ctx, "sparse_store", (k_fast_store<C>), (nch + 255) / 256, 256, 0, d_raw.as<RAcc>(), (uint32_t)nch,
                   d_off.as<uint32_t>(), d_chunks.as<Acc>());
     }
