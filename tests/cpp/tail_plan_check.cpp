@@ -6,8 +6,9 @@ using namespace vk;
 
 static void show(const char* name, uint32_t S, uint32_t W, uint32_t J, uint32_t nU, bool u_total) {
     const TailPlan p = msm_tail_plan(S, W, J, nU, true, u_total);
-    printf("{\"name\": \"%s\", \"h\": %u, \"K\": %u, \"nb1\": %u, \"nb2\": %u, \"per_w\": %u, \"pL\": %u, \"urow\": %d}\n",
-           name, p.h, p.K, p.nb1, p.nb2, p.per_w, p.pL, p.urow ? 1 : 0);
+    printf("{\"name\": \"%s\", \"h\": %u, \"K\": %u, \"nb1\": %u, \"nb2\": %u, \"per_w\": %u, \"pL\": %u, "
+           "\"gL\": %u, \"gH\": %u, \"slots\": %u, \"urow\": %d}\n",
+           name, p.h, p.K, p.nb1, p.nb2, p.per_w, p.pL, p.gL, p.gH, p.slots, p.urow ? 1 : 0);
 }
 
 int main() {
@@ -15,6 +16,7 @@ int main() {
     show("radix1", 1u << 15, 1, 15, 5, false);     // one-GPU radix MSM: 2^15 segments of 5 buckets
     show("shared12", 1u << 12, 1, 12, 1, true);    // a 20000-point shared-window MSM: 2^12 buckets
     show("kzg2", 1u << 15, 2, 15, 5, false);       // the one-call KZG: two radix sets
-    show("perwin8", 1u << 13, 8, 13, 1, false);    // variable base: 8 windows, segments of 4
+    show("perwin8", 1u << 13, 8, 13, 4, false);    // variable base: 8 windows, segments of 4, residue U sums
+    show("perwin16", 1u << 13, 16, 13, 1, false);  // BN254 / Bandersnatch 2^20: 16 windows, acc_s
     return 0;
 }

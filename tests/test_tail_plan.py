@@ -26,11 +26,21 @@ def test_tail_plan_geometries(tmp_path):
     # a 2^12-bucket shared set: urow on the tie (no U waves), one wave per column
     t = p["shared12"]
     assert (t["urow"], t["h"], t["pL"], t["nb2"]) == (1, 6, 1, 0) and t["per_w"] == 64 + 64
-    # two radix sets: 2 x per_w waves must fit one round
+    # two radix sets (the one-call KZG): packed marginal waves, 2 column / 4 row sums per wave, 8 items
+    # per lane everywhere, one round; one partial slot per sum
     k = p["kzg2"]
-    assert k["urow"] == 0 and 2 * k["per_w"] <= 1024 or k["h"] == 0
-    # several per-window sets keep the bit form
+    assert (k["urow"], k["h"], k["K"], k["gL"], k["gH"]) == (0, 7, 8, 2, 4)
+    assert k["per_w"] == 128 // 2 + 256 // 4 + 5 * k["nb2"] and 2 * k["per_w"] <= 1024
+    assert k["slots"] == 128 + 256 + 5 * k["nb2"]
+    # eight per-window sets (GLV variable base): packed marginal waves within one round
     v = p["perwin8"]
-    assert v["h"] == 0 and v["urow"] == 0 and v["per_w"] == 13 * v["nb1"] + v["nb2"]
+    assert v["h"] == 6 and v["urow"] == 0 and v["gL"] * v["gH"] > 1 and 8 * v["per_w"] <= 1024
+    assert v["slots"] == 64 + 128 + 4 * v["nb2"]
+    # sixteen sets (BN254 2^20): packed too (4 column / 8 row sums per wave), still one round
+    b = p["perwin16"]
+    assert b["h"] == 6 and (b["gL"], b["gH"]) == (4, 8) and 16 * b["per_w"] <= 1024
+    assert b["slots"] == 64 + 128 + b["nb2"]
     for d in p.values():
         assert d["pL"] >= 1 and d["K"] >= 1
+        if d["gL"] == 1 and d["gH"] == 1:
+            assert d["slots"] == d["per_w"]

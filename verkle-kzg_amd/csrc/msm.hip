@@ -1199,7 +1199,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     VK_TRY(ws[WS_OWNER_B].ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(ws[WS_SEG].ensure((size_t)S * Wr * sizeof(RAcc)));
     VK_TRY(ws[WS_TREE].ensure((size_t)S * Wr * sizeof(RAcc)));
-    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * msm_tail_plan(S, (uint32_t)Wr, J, nU, Fast29<C>::type::quad, Lseg == 1).per_w *
+    VK_TRY(ws[WS_WIN].ensure((size_t)Wr * msm_tail_plan(S, (uint32_t)Wr, J, nU, Fast29<C>::type::quad, Lseg == 1).slots *
                              sizeof(RAcc)));
     // tail points, then the chain_max word: one read-back
     const size_t tail_bytes = ((size_t)Wr * (J + nU) * sizeof(Acc) + 15) & ~(size_t)15;

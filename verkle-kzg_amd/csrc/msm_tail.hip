@@ -308,23 +308,32 @@ template <class A>
 __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __restrict__ usrc,
                                                    const typename A::Acc* __restrict__ tsrc, uint32_t S, uint32_t J,
                                                    uint32_t h, uint32_t nU, uint32_t K, uint32_t nb1, uint32_t nb2,
-                                                   uint32_t pL, uint32_t n_waves, const uint32_t* __restrict__ toff,
+                                                   uint32_t pL, uint32_t gL, uint32_t gH, uint32_t n_waves,
+                                                   const uint32_t* __restrict__ toff,
                                                    const uint32_t* __restrict__ uoff,
                                                    typename A::Acc* __restrict__ partial) {
     using Acc = typename A::Acc;
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
     const uint32_t G = h ? 1u << h : 0u, Hn = h ? 1u << (J - h) : 0u;
-    const uint32_t nT = h ? G * pL + Hn : J * nb1;  // waves of the T side per set (pL per column sum)
-    const uint32_t per_w = nT + nU * nb2;             // urow: nb2 = 0, no U waves
+    // waves of the T side per set: a column sum takes pL waves, or a wave makes gL column sums (gH row
+    // sums) on 64 / g lanes each; partial slots stay one per sum (pL per column sum)
+    const uint32_t nLw = h ? G * pL / gL : 0u, nT = h ? nLw + Hn / gH : J * nb1;
+    const uint32_t nTs = h ? G * pL + Hn : J * nb1;  // partial slots of the T side per set
+    const uint32_t per_w = nT + nU * nb2;            // urow: nb2 = 0, no U waves
     const uint32_t w = gw / per_w, r = gw % per_w;
     // kind: 0 = T_q (bit form), 1 = L_lo, 2 = H_hi, 3 = U_u; sel = q, lo, hi or u
-    const uint32_t kind = r >= nT ? 3u : h == 0 ? 0u : r < G * pL ? 1u : 2u;
-    const uint32_t sel = kind == 0 ? r / nb1 : kind == 1 ? r / pL : kind == 2 ? r - G * pL : (r - nT) / nb2;
-    const uint32_t wv = kind == 0 ? r % nb1 : kind == 1 ? r % pL : kind == 3 ? (r - nT) % nb2 : 0u;
+    const uint32_t kind = r >= nT ? 3u : h == 0 ? 0u : r < nLw ? 1u : 2u;
+    const uint32_t g = kind == 1 ? gL : kind == 2 ? gH : 1u;  // sums per wave
+    const uint32_t lanes = 64 / g, gi = lane / lanes, li = lane % lanes;
+    const uint32_t sel = kind == 0 ? r / nb1 : kind == 1 ? (gL > 1 ? r * gL + gi : r / pL)
+                         : kind == 2 ? (r - nLw) * gH + gi : (r - nT) / nb2;
+    const uint32_t wv = kind == 0 ? r % nb1 : kind == 1 ? (gL > 1 ? 0u : r % pL) : kind == 3 ? (r - nT) % nb2 : 0u;
     const uint32_t n_items = kind == 0 ? S / 2 : kind == 1 ? Hn : kind == 2 ? G : S;
-    const uint32_t Kw = kind == 1 ? Hn / (64 * pL) : kind == 2 ? G / 64 : K;
-    const uint32_t base = wv * 64 * Kw;
+    const uint32_t Kw = kind == 1 ? Hn / (lanes * pL) : kind == 2 ? G / lanes : K;
+    const uint32_t base = wv * lanes * Kw;
+    const uint32_t slot = kind == 0 ? sel * nb1 + wv : kind == 1 ? sel * pL + wv : kind == 2 ? G * pL + sel
+                                                                                 : nTs + sel * nb2 + wv;
     const size_t set0 = kind < 3 ? (size_t)w * S : (size_t)w * S * nU;
     const Acc* src = (kind < 3 ? tsrc : usrc) + set0;
     const uint32_t* off = (kind < 3 ? toff : uoff);
@@ -337,6 +346,9 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
                : kind == 2 ? sel * G + m
                            : m * nU + sel;
     };
+    uint32_t lg_lanes = 0;  // xor levels of the fold inside a sum's lane group
+    while ((1u << lg_lanes) < lanes) lg_lanes++;
+    const size_t out = (size_t)w * (nTs + nU * nb2) + slot;
     Acc v = A::zero();
     if constexpr (A::quad) {
         // Kw serial full adds per lane (every SIMD busy: issue-bound), then the wave's 64 lane sums
@@ -344,7 +356,7 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
         // 16 quads by xor (4) -- 7 adds of ~14.6k cycles instead of the 6-level butterfly of full
         // adds (~30k cycles each)
         for (uint32_t it = 0; it < Kw; it++) {
-            const uint32_t m = base + it * 64 + lane;
+            const uint32_t m = base + it * lanes + li;
             const uint32_t idx = item(m);
             const bool live = m < n_items && (!off || off[idx + 1] > off[idx]);
             const Acc o = live ? src[idx] : A::zero();
@@ -352,17 +364,17 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
         }
         const uint32_t role = lane & 3, q0 = lane & ~3u;
         Acc s = shfl_idx_pod(v, q0);
-        for (uint32_t it = 0; it < 7; it++) {
+        for (uint32_t it = 0; it < 3 + (lg_lanes - 2); it++) {  // xor levels stay inside the group
             const Acc o = it < 3 ? shfl_idx_pod(v, q0 + it + 1) : shfl_acc<A>(s, 4u << (it - 3));
             s = A::add_quad(s, o, role);
         }
-        if (lane == 0) partial[gw] = s;
+        if (li == 0) partial[out] = s;
         return;
     }
-    for (uint32_t it = 0; it < Kw + 6; it++) {
+    for (uint32_t it = 0; it < Kw + lg_lanes; it++) {
         Acc o;
         if (it < Kw) {
-            const uint32_t m = base + it * 64 + lane;  // lane-interleaved rows
+            const uint32_t m = base + it * lanes + li;  // lane-interleaved rows
             const uint32_t idx = item(m);
             const bool live = m < n_items && (!off || off[idx + 1] > off[idx]);
             o = live ? src[idx] : A::zero();
@@ -371,7 +383,7 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
         }
         v = A::add(v, o);
     }
-    if (lane == 0) partial[gw] = v;
+    if (li == 0) partial[out] = v;
 }
 
 // where sum `sum` (= w (J + nU) + q) of the final stage finds its items in `partial`: cnt items,
@@ -638,7 +650,7 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
     const TailPlan tp = msm_tail_plan(S, (uint32_t)W, J, nU, A::quad, Lseg == 1);
     const uint32_t n_waves = (uint32_t)W * tp.per_w;
     VK_LAUNCH_ON(ctx, L.st, "msm_bitsum", (k_msm_bitsum<A>), (n_waves * 64 + 255) / 256, 256, 0, usrc, Rs, S, J, tp.h,
-                 nU, tp.K, tp.nb1, tp.nb2, tp.pL, n_waves, toff, uoff, partial);
+                 nU, tp.K, tp.nb1, tp.nb2, tp.pL, tp.gL, tp.gH, n_waves, toff, uoff, partial);
     if constexpr (A::quad)
         VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, tp.h,
                      nU, tp.nb1, tp.nb2, tp.pL, tp.urow ? 1u : 0u, out);

@@ -39,8 +39,13 @@ inline uint32_t msm_bitsum_pw(uint32_t items, uint32_t K, uint32_t lanes = 64) {
 // total of the row sums): no U waves; the final stage sums X = the H_hi of even hi (Hn / 2 items, as
 // every T_j >= h) and the host adds T_h (the odd hi) to it. The column sums may then take pL waves
 // each (Hn / pL items per wave, pL <= Hn / G, so the T_j < h sums still read <= Hn / 2 partials).
+// Packed marginal waves (gL, gH > 1, several sets on quads): a wave makes gL column sums (or gH row
+// sums) on 64 / g lanes each, so the column / row waves carry as many items per lane as the U waves
+// and leave room for them in one round (the one-call KZG's two radix sets: 2 x (64 + 64 + 5 x 64)
+// waves of 8 items instead of the bit form's 13). Partial slots stay one per sum (`slots` per set;
+// per_w counts waves).
 struct TailPlan {
-    uint32_t h = 0, K = 0, nb1 = 0, nb2 = 0, per_w = 0, pL = 1;
+    uint32_t h = 0, K = 0, nb1 = 0, nb2 = 0, per_w = 0, pL = 1, gL = 1, gH = 1, slots = 0;
     bool urow = false;
 };
 // Chosen by a cost model in full-add times: a wave costs its K serial adds plus the in-wave
@@ -60,6 +65,7 @@ inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, b
     p.nb1 = msm_bitsum_pw(S / 2, p.K);
     p.nb2 = msm_bitsum_pw(S, p.K);
     p.per_w = J * p.nb1 + nU * p.nb2;
+    p.slots = p.per_w;
     if (!(marg_env && J >= 12 && S == (1u << J))) return p;
     if ((uint64_t)W * p.per_w > 1024) return p;
     const uint32_t h = J / 2, G = 1u << h, Hn = 1u << (J - h), kl = Hn / 64;  // Hn >= G >= 64
@@ -75,6 +81,31 @@ inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, b
             p.nb1 = 0;
             p.nb2 = nb;
             p.per_w = G + Hn + nU * nb;
+            p.slots = p.per_w;
+        }
+    }
+    static const int pack_env = getenv("VKZG_TAIL_PACK") ? atoi(getenv("VKZG_TAIL_PACK")) : 1;  // A/B probe
+    if (pack_env && quad && W > 1) {  // several sets: pack 2-4 column / row sums per wave
+        for (uint32_t k = kl; k <= 32; k++) {
+            uint32_t gL = 1, gH = 1;
+            while (gL < 16 && Hn * (gL * 2) / 64 <= k) gL *= 2;  // items per lane of a column wave <= k
+            while (gH < 16 && G * (gH * 2) / 64 <= k) gH *= 2;
+            if (gL == 1 && gH == 1) continue;  // the plain marginal form above
+            const uint32_t nb = msm_bitsum_pw(S, k);
+            const uint32_t waves = G / gL + Hn / gH + nU * nb;
+            if ((uint64_t)W * waves > 1024) continue;
+            const double t = k + bf;
+            if (t < best - 1e-9) {
+                best = t;
+                p.h = h;
+                p.K = k;
+                p.nb1 = 0;
+                p.nb2 = nb;
+                p.gL = gL;
+                p.gH = gH;
+                p.per_w = waves;
+                p.slots = G + Hn + nU * nb;
+            }
         }
     }
     if (urow_env && u_total && nU == 1) {  // U from the row sums (u_total: the U items are the R_s)
@@ -89,8 +120,10 @@ inline TailPlan msm_tail_plan(uint32_t S, uint32_t W, uint32_t J, uint32_t nU, b
                 p.nb1 = 0;
                 p.nb2 = 0;
                 p.pL = pl;
+                p.gL = p.gH = 1;
                 p.urow = true;
                 p.per_w = G * pl + Hn;
+                p.slots = p.per_w;
             }
         }
     }
