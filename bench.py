@@ -378,7 +378,8 @@ def mp_line(a, rank, world, local, dev, stream, comm=None):
                            f"({t_begin * 1e3:.2f} ms) and the finish on every rank: at most ~1.15x on 8 GPUs "
                            "(DESIGN.md 6); proof_parallel scales with the ranks")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_multiproof(N, data, z, cxy, crs, a.cpu_threads or min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_multiproof(N, data, z, cxy, cinf, crs, a.cpu_threads or min(16, os.cpu_count() or 1),
+                                             mp["d"])
     return out
 
 
@@ -510,41 +511,73 @@ def mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, want, P=6):
             "note": "phase 1 (host transcript) of proof k+1 overlapped with proof k's GPU phases and IPA rounds"}
 
 
-def cpu_multiproof(N, data, z, cxy, crs, threads):
-    """configs[4] on the CPU, the reference's prove_multiproof (multiproof.rs:99-176) restated:
-    transcript bytes (Q x (C, z, y) records) hashed with SHA-256 (hashlib), the field phases in C
-    with the reference's thread structure (oracle/c/ref_multiproof.c: scaling par_iter over
-    queries, grouped quotients par_bridge over points, g and h serial) on `threads` threads, the
-    D and E commits by the naive inner_product in C (utils.rs:16-19, what IPA::commit runs), and
-    the inner IPA proof as its 8 rounds of L / R commits and generator folds (naive per-term
-    scalar multiplications of the same sizes). Challenges r, t are random field elements (their
-    values do not change the work)."""
-    import hashlib
+BN254_P = 21888242871839275222246405745257275088696311157297823662689037894645226208583  # base field
+
+
+def _mp_records(cxy, cinf, z, y):
+    """The multiproof transcript's per-query bytes (multiproof.rs:109-113, transcript.rs:28-49):
+    "C" ++ compressed(C_i) ++ "z" ++ le64(z_i) ++ "y" ++ le(y_i), 75 B each, with the compressed
+    point's flags (x LE, 0x80 in the last byte when y is the larger root, 0x40 for the identity:
+    SURVEY Appendix A.3) -- vectorised, so the baseline pays SHA-256 and not Python."""
+    Q = z.shape[0]
+    half = (BN254_P - 1) // 2
+    hl = [(half >> (64 * k)) & ((1 << 64) - 1) for k in range(4)]
+    yl = cxy[:, 4:8]
+    gt = np.zeros(Q, dtype=bool)
+    eq = np.ones(Q, dtype=bool)
+    for k in (3, 2, 1, 0):
+        gt |= eq & (yl[:, k] > np.uint64(hl[k]))
+        eq &= yl[:, k] == np.uint64(hl[k])
+    rec = np.zeros((Q, 75), dtype=np.uint8)
+    rec[:, 0], rec[:, 33], rec[:, 42] = ord("C"), ord("z"), ord("y")
+    rec[:, 1:33] = np.ascontiguousarray(cxy[:, :4]).view(np.uint8).reshape(Q, 32)
+    rec[gt, 32] |= 0x80
+    inf = cinf.astype(bool)
+    rec[inf, 1:33] = 0
+    rec[inf, 32] = 0x40
+    rec[:, 34:42] = np.ascontiguousarray(z).view(np.uint8).reshape(Q, 8)
+    rec[:, 43:75] = np.ascontiguousarray(y).view(np.uint8).reshape(Q, 32)
+    return rec
+
+
+def cpu_multiproof(N, data, z, cxy, cinf, crs, threads, gpu_d=None):
+    """configs[4] on the CPU, the reference's prove_multiproof (multiproof.rs:99-176) restated with
+    its real challenges: the transcript over the Q (C, z, y) records and hash_to_field -> r
+    (oracle/pyoracle/arkser.py, transcript.rs:28-62), the field phases in C with the reference's
+    thread structure (oracle/c/ref_multiproof.c: scaling par_iter over queries, grouped quotients
+    par_bridge over points, g and h serial) on `threads` threads, D = commit(g) by the naive
+    inner_product in C (utils.rs:16-19, what IPA::commit runs), t from the transcript, h, E =
+    commit(h), and the inner IPA proof as its 8 rounds of L / R commits and generator folds (naive
+    per-term scalar multiplications of the same sizes; work-equivalent). D is compared with the
+    GPU's D of the same inputs (`same_d_as_gpu`)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from pyoracle import cref  # CPU baseline leg only
+    from pyoracle import arkser, cref  # CPU baseline leg only
     from pyoracle import protocol
     Q = z.shape[0]
     r_mod = vkzg.SCALAR_R["bn254"]
-    rng = np.random.default_rng(5)
-    r, t = (int.from_bytes(rng.bytes(32), "little") % r_mod for _ in range(2))
     crs_xy, crs_inf = cref.points_to_array("bn254", crs)
     omega = protocol.group_gen(N)
+    y = data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)]
     t0 = time.perf_counter()
-    rec = np.zeros((Q, 75), dtype=np.uint8)           # "C" x[32] "z" z[8] "y" y[32]
-    rec[:, 0], rec[:, 33], rec[:, 42] = ord("C"), ord("z"), ord("y")
-    rec[:, 1:33] = np.ascontiguousarray(cxy[:, :4]).view(np.uint8).reshape(Q, 32)
-    rec[:, 34:42] = np.ascontiguousarray(z).view(np.uint8).reshape(Q, 8)
-    rec[:, 43:75] = np.ascontiguousarray(data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)]).view(
-        np.uint8).reshape(Q, 32)
-    hashlib.sha256(rec.tobytes()).digest()
+    state = _mp_records(cxy, cinf, z, y).tobytes() + b"r"
+    r = arkser.hash_to_field(state, b"multiproof", r_mod)
     t_tr = time.perf_counter() - t0
     t0 = time.perf_counter()
-    g, h = cref.mp_field_phases(N, data, z, r, t, omega, threads)
+    st, g = cref.mp_g(N, data, z, r, omega, threads)
     t_field = time.perf_counter() - t0
     t0 = time.perf_counter()
-    cref.msm_arrays("bn254", crs_xy[:N], crs_inf[:N], g, 1)
-    cref.msm_arrays("bn254", crs_xy[:N], crs_inf[:N], h, 1)
+    dxy, dinf = cref.msm_arrays("bn254", crs_xy[:N], crs_inf[:N], g, 1)
     t_commit = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    d = cref.array_to_point("bn254", dxy, dinf)
+    t = arkser.hash_to_field(arkser.ser_fr(r) + b"r" + b"D" + arkser.ser_point_compressed(d) + b"t",
+                             b"multiproof", r_mod)
+    h = cref.mp_h(st, N, t)
+    cref.mp_free(st)
+    t_field += time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cref.msm_arrays("bn254", crs_xy[:N], crs_inf[:N], h, 1)
+    t_commit += time.perf_counter() - t0
     t0 = time.perf_counter()
     m = N
     sc = np.asarray(g, dtype=np.uint64)
@@ -555,11 +588,13 @@ def cpu_multiproof(N, data, z, cxy, crs, threads):
     t_ipa = time.perf_counter() - t0
     total = t_tr + t_field + t_commit + t_ipa
     return {"value": 1.0 / total, "unit": "multiproofs/s", "ms_per_multiproof": total * 1e3, "cores": threads,
-            "kind": "port", "parts_ms": {"transcript_sha256": t_tr * 1e3, "field_phases": t_field * 1e3,
+            "kind": "port", "parts_ms": {"transcript_hash_to_field": t_tr * 1e3, "field_phases": t_field * 1e3,
                                          "d_e_commits_naive": t_commit * 1e3, "inner_ipa_naive": t_ipa * 1e3},
-            "sample": f"the full Q = {Q} x N = {N} workload once: field phases in C on {threads} threads with the "
-                      "reference's rayon structure (oracle/c/ref_multiproof.c), naive commits / IPA rounds in C "
-                      "(1 thread, as the reference's serial IPA), SHA-256 transcript via hashlib"}
+            "same_d_as_gpu": (d == gpu_d) if gpu_d is not None else None,
+            "sample": f"the full Q = {Q} x N = {N} workload once with the transcript's own r and t: field phases "
+                      f"in C on {threads} threads with the reference's rayon structure (oracle/c/ref_multiproof.c), "
+                      "naive D / E commits and IPA rounds in C (1 thread, as the reference's serial IPA; the "
+                      "rounds are work-equivalent), SHA-256 transcript and hash_to_field"}
 
 
 def ipa_line(local, stream, batch=256):

@@ -98,7 +98,10 @@ int vc_multiproof_prove_many_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int
                                      vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y);
 /* Its exchange alone: this rank holds proofs shard_range(P, k, G) (at their global positions in
  * the outputs) and its share's status; afterwards every rank holds all P, or every rank returns
- * an error (its own status, or VC_E_PEER). ctx may be NULL over a host-callback comm. */
+ * an error (its own status, or VC_E_PEER). A rank whose output buffers are unusable for the P
+ * proofs (NULL arrays, an IPA proof with fewer than log2 N rounds) fails like a failed share:
+ * it still enters the exchange and no rank writes its outputs. scheme and N size the records and
+ * must be the same on every rank. ctx may be NULL over a host-callback comm. */
 int vc_multiproof_gather(vc_comm* comm, vc_ctx* ctx, int status, int scheme, size_t N, size_t P, uint64_t* d_xy,
                          uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf,
                          uint64_t* kzg_y);

@@ -12,7 +12,7 @@
  *   inv = invert_domain_at(t, N)                      (utils.rs:57-62, batch inversion)
  *   h = sum_z sum_i scaled_i * inv[z]                 (:160-165, serial)
  * r and t (transcript challenges), the commitments D / E and the inner proof are the caller's
- * (bench.py times the transcript hash and the two commits beside it).
+ * (oracle/pyoracle/mpcheck.py assembles the whole proof; bench.py times the parts).
  * Inversions use the binary extended Euclid algorithm on Montgomery residues (what arkworks'
  * Fp::inverse runs), not Fermat. Pinned by tests/test_oracle.py against the Python restatement
  * (oracle/pyoracle/protocol.py).
@@ -187,18 +187,28 @@ static void run_threads(void* (*fn)(void*), mp_job* base, size_t count, int T) {
     free(th);
 }
 
-/* N = domain size (power of two, every query's data has N values), z[i] < N; r, t, omega canonical.
- * g_out, h_out: N x 4 canonical. Returns 0, or -1 on a bad argument. */
-int bn254fr_mp_field_phases(size_t N, size_t Q, const u64* data, const u64* z, const u64* r_c, const u64* t_c,
-                            const u64* omega_c, int nthreads, u64* g_out, u64* h_out) {
+/* Two-phase form (prove_multiproof needs g before the transcript yields t, and h after it):
+ * bn254fr_mp_g runs :117-150 (scaling, grouped quotients, g) and keeps the scaled data and the
+ * grouping; bn254fr_mp_h runs :155-165 (invert_domain_at(t), h) on them; bn254fr_mp_free releases.
+ * N = domain size (power of two, every query's data has N values), z[i] < N; r, omega canonical.
+ * g_out: N x 4 canonical. Returns the state, or NULL on a bad argument. */
+typedef struct {
+    size_t N, Q, npts;
+    u64* pts;
+    size_t* qstart;
+    size_t* qidx;
+    fe* scaled;
+} mp_state;
+
+void* bn254fr_mp_g(size_t N, size_t Q, const u64* data, const u64* z, const u64* r_c, const u64* omega_c,
+                   int nthreads, u64* g_out) {
     init();
-    if (N == 0 || (N & (N - 1)) || Q == 0) return -1;
+    if (N == 0 || (N & (N - 1)) || Q == 0) return NULL;
     for (size_t i = 0; i < Q; i++)
-        if (z[i] >= N) return -1;
+        if (z[i] >= N) return NULL;
     const int T = nthreads < 1 ? 1 : nthreads;
-    fe r, t, omega;
+    fe r, omega;
     to_mont(&r, r_c);
-    to_mont(&t, t_c);
     to_mont(&omega, omega_c);
     /* precompute.rs:47-58: van[i] = N / w^i, van_inv = 1 / van */
     fe* van = (fe*)malloc(sizeof(fe) * N);
@@ -260,14 +270,40 @@ int bn254fr_mp_field_phases(size_t N, size_t Q, const u64* data, const u64* z, c
     fe* g = (fe*)calloc(N, sizeof(fe));
     for (size_t p = 0; p < npts; p++)
         for (size_t k = 0; k < N; k++) fadd(&g[k], &g[k], &quot[p * N + k]);
+    for (size_t k = 0; k < N; k++) from_mont(g_out + 4 * k, &g[k]);
+    free(g), free(quot), free(slot), free(pos), free(cnt), free(rp), free(van_inv), free(van);
+    mp_state* st = (mp_state*)calloc(1, sizeof(mp_state));
+    st->N = N;
+    st->Q = Q;
+    st->npts = npts;
+    st->pts = pts;
+    st->qstart = qstart;
+    st->qidx = qidx;
+    st->scaled = scaled;
+    return st;
+}
+
+/* t canonical; h_out: N x 4 canonical. Returns 0, or -1 when t - i = 0 for some i < N. */
+int bn254fr_mp_h(void* state, const u64* t_c, u64* h_out) {
+    mp_state* st = (mp_state*)state;
+    const size_t N = st->N;
+    if (N == 0) return -1;
+    fe t;
+    to_mont(&t, t_c);
     /* invert_domain_at(t, N): 1 / (t - i), batch inversion (one inversion + 3 (N - 1) products) */
     fe* inv = (fe*)malloc(sizeof(fe) * N);
     fe* pre = (fe*)malloc(sizeof(fe) * N);
+    int bad = 0;
     for (size_t i = 0; i < N; i++) {
         u64 ii[NL] = {i, 0, 0, 0};
         fe fi;
         to_mont(&fi, ii);
         fsub(&inv[i], &t, &fi);
+        if (fiszero(&inv[i])) bad = 1;
+    }
+    if (bad) {
+        free(inv), free(pre);
+        return -1;
     }
     pre[0] = inv[0];
     for (size_t i = 1; i < N; i++) fmul(&pre[i], &pre[i - 1], &inv[i]);
@@ -280,20 +316,33 @@ int bn254fr_mp_field_phases(size_t N, size_t Q, const u64* data, const u64* z, c
     }
     inv[0] = run;
     fe* h = (fe*)calloc(N, sizeof(fe));
-    for (size_t p = 0; p < npts; p++)
-        for (size_t s = qstart[p]; s < qstart[p + 1]; s++) {
-            const fe* src = scaled + qidx[s] * N;
+    for (size_t p = 0; p < st->npts; p++)
+        for (size_t s = st->qstart[p]; s < st->qstart[p + 1]; s++) {
+            const fe* src = st->scaled + st->qidx[s] * N;
             for (size_t k = 0; k < N; k++) {
                 fe m;
-                fmul(&m, &src[k], &inv[pts[p]]);
+                fmul(&m, &src[k], &inv[st->pts[p]]);
                 fadd(&h[k], &h[k], &m);
             }
         }
-    for (size_t k = 0; k < N; k++) {
-        from_mont(g_out + 4 * k, &g[k]);
-        from_mont(h_out + 4 * k, &h[k]);
-    }
-    free(h), free(pre), free(inv), free(g), free(quot), free(qidx), free(slot), free(pos), free(qstart);
-    free(pts), free(cnt), free(scaled), free(rp), free(van_inv), free(van);
+    for (size_t k = 0; k < N; k++) from_mont(h_out + 4 * k, &h[k]);
+    free(h), free(pre), free(inv);
     return 0;
+}
+
+void bn254fr_mp_free(void* state) {
+    mp_state* st = (mp_state*)state;
+    if (!st) return;
+    free(st->pts), free(st->qstart), free(st->qidx), free(st->scaled);
+    free(st);
+}
+
+/* One-call form: g and h for given r and t. Returns 0, or -1 on a bad argument. */
+int bn254fr_mp_field_phases(size_t N, size_t Q, const u64* data, const u64* z, const u64* r_c, const u64* t_c,
+                            const u64* omega_c, int nthreads, u64* g_out, u64* h_out) {
+    void* st = bn254fr_mp_g(N, Q, data, z, r_c, omega_c, nthreads, g_out);
+    if (!st) return -1;
+    int rc = bn254fr_mp_h(st, t_c, h_out);
+    bn254fr_mp_free(st);
+    return rc;
 }

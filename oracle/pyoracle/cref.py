@@ -149,3 +149,35 @@ def mp_field_phases(N, data, z, r, t, omega, nthreads=1):
     if st != 0:
         raise ValueError("bn254fr_mp_field_phases: bad argument")
     return g, h
+
+
+def mp_g(N, data, z, r, omega, nthreads=1):
+    """prove_multiproof's first field phase (multiproof.rs:117-150: scaling, grouped quotients,
+    g) in C. Returns (state, g (N, 4) uint64 canonical); pass the state to mp_h, then mp_free."""
+    data = np.ascontiguousarray(data, dtype=np.uint64)
+    z = np.ascontiguousarray(z, dtype=np.uint64)
+    limbs = [ints_to_limbs([int(v)], 4)[0] for v in (r, omega)]
+    g = np.zeros((N, 4), dtype=np.uint64)
+    fn = lib().bn254fr_mp_g
+    fn.restype = ctypes.c_void_p
+    st = fn(ctypes.c_size_t(N), ctypes.c_size_t(z.shape[0]), data.ctypes.data_as(ctypes.c_void_p),
+            z.ctypes.data_as(ctypes.c_void_p), limbs[0].ctypes.data_as(ctypes.c_void_p),
+            limbs[1].ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nthreads), g.ctypes.data_as(ctypes.c_void_p))
+    if not st:
+        raise ValueError("bn254fr_mp_g: bad argument")
+    return ctypes.c_void_p(st), g
+
+
+def mp_h(state, N, t):
+    """The second field phase (multiproof.rs:155-165: invert_domain_at(t), h) on mp_g's state."""
+    tl = ints_to_limbs([int(t)], 4)[0]
+    h = np.zeros((N, 4), dtype=np.uint64)
+    fn = lib().bn254fr_mp_h
+    fn.restype = ctypes.c_int
+    if fn(state, tl.ctypes.data_as(ctypes.c_void_p), h.ctypes.data_as(ctypes.c_void_p)) != 0:
+        raise ValueError("bn254fr_mp_h: t - i = 0")
+    return h
+
+
+def mp_free(state):
+    lib().bn254fr_mp_free(state)

@@ -9,6 +9,7 @@ reference's round-trip/tamper tests restated in tests/test_oracle.py); byte conv
 (transcript, CRS hashing, compressed flags) are "parity unpinned vs arkworks".
 
     python tests/golden/make_golden.py        # rewrites tests/golden/*.json (deterministic)
+    python tests/golden/make_golden.py multiproof_256   # only multiproof_256.json
 """
 import json
 import os
@@ -140,8 +141,44 @@ def main():
             ent["proof"] = {"proof": pt(proof["proof"]["proof"]), "y": hexs(proof["proof"]["y"])}
         mp[name] = ent
     dump("multiproof_32.json", mp)
+    multiproof_256(crs)
     print("golden fixtures written to", HERE)
 
 
+def multiproof_256(crs=None):
+    """multiproof at the reference's width N = 256 (benches/ipa.rs:18, data r_j + i as :38-49),
+    Q = 64 queries: 20 on z = 5 and 20 on z = 200 (more than one 16-query chunk of the engine's
+    per-point sums on a row), the rest random; IPA and KZG (multiproof.rs:99-176). Data are stored
+    as r_j (f_j[i] = r_j + i). Query commitments by msm_fast (the same group elements as the naive
+    commit, which prove_multiproof itself runs for D and E)."""
+    if crs is None:
+        crs = protocol.ipa_gen_points(257, max_=512)
+    N, Q = 256, 64
+    rng = random.Random(61)
+    zs = [5] * 20 + [200] * 20 + [rng.randrange(N) for _ in range(Q - 40)]
+    rng.shuffle(zs)
+    r0s = [rng.randrange(BN254.r) for _ in range(Q)]
+    out = {"N": N, "Q": Q, "data_rule": "f_j[i] = r0_j + i mod r", "r0": [hexs(x) for x in r0s], "z": zs}
+    for name, vc in (("ipa", protocol.IPA(N, points=crs)), ("kzg", protocol.KZG(N))):
+        bases = vc.g if name == "ipa" else vc.lagrange
+        qs = []
+        for r0, z in zip(r0s, zs):
+            d = protocol.LagrangeBasis.from_vec([(r0 + i) % BN254.r for i in range(N)])
+            qs.append((d, BN254.msm_fast(bases, d.evals), z, d[z]))
+        proof = protocol.prove_multiproof(vc, qs)
+        ent = {"commits": [pt(q[1]) for q in qs], "d": pt(proof["d"])}
+        if name == "ipa":
+            p = proof["proof"]
+            ent["proof"] = {"l": [pt(x) for x in p["l"]], "r": [pt(x) for x in p["r"]], "tip": hexs(p["tip"]),
+                            "y": hexs(p["y"])}
+        else:
+            ent["proof"] = {"proof": pt(proof["proof"]["proof"]), "y": hexs(proof["proof"]["y"])}
+        out[name] = ent
+    dump("multiproof_256.json", out)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["multiproof_256"]:
+        multiproof_256()
+    else:
+        main()

@@ -277,6 +277,25 @@ def _mp_gather_worker(rank, world, port, q):
             ok = False
         except vkzg.VCError as ex:
             ok = ok and ex.status == (-3 if rank == 1 else -10)
+        # rank 1's output buffers are unusable (an IPA proof with too few rounds, a NULL KZG y):
+        # it fails with VC_E_INVALID inside the exchange, its peer gets VC_E_PEER, and neither
+        # rank's outputs are written (no partial copy-out before the group agrees)
+        bad = scheme.MultiproofSet(sid, N, P)
+        for p in range(lo, hi):
+            fill(bad, p, np.random.default_rng(100 * sid + p))
+        before = [snapshot(bad, p) for p in range(P)]
+        args = list(bad.args())
+        if rank == 1:
+            if sid == 0:
+                bad.bufs[P - 1].rounds = 1
+            else:
+                args[5] = None
+        from vkzg._lib import lib
+        st = lib().vc_multiproof_gather(c.h, None, 0, sid, N, P, *args)
+        ok = ok and st == (-1 if rank == 1 else -10)
+        if sid == 0 and rank == 1:
+            bad.bufs[P - 1].rounds = 3
+        ok = ok and [snapshot(bad, p) for p in range(P)] == before
     c.close()
     q.put((rank, ok))
     dist.destroy_process_group()

@@ -1,0 +1,208 @@
+"""GPU: one process, several members (include/vc_group.h). Members may repeat a device, so these
+run G = 2 and 3 members on the one card of the test box: every group call == the one-context
+call and the oracle / golden fixtures (utils.rs:16-19, ipa/mod.rs:130-135, kzg/mod.rs:136-154,
+multiproof.rs:99-176, verkle-tree node.rs:205-277)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load(name):
+    with open(os.path.join(HERE, "golden", name)) as f:
+        return json.load(f)
+
+
+def P(h):
+    return None if h is None else (int(h[0], 16), int(h[1], 16))
+
+
+def _group(curve, G):
+    from vkzg.group import Group
+    return Group(curve, [0] * G)
+
+
+@pytest.mark.parametrize("curve,n", [("bls12_381", 20000), ("bn254", 4099), ("bandersnatch", 3001)])
+@pytest.mark.parametrize("G", [2, 3])
+def test_group_msm_both_splits(oracle_c, curve, n, G):
+    """vc_group_msm (host scalars) with the point split and the window split == the oracle's
+    naive MSM; a sub-range (offset) too."""
+    import vkzg
+    from vkzg import group as vgroup
+    g = _group(curve, G)
+    try:
+        tid = g.random_bases(n, seed=71)
+        e = vkzg.Engine(curve)
+        try:
+            xy, inf = e.download_bases(e.random_bases(n, seed=71))
+        finally:
+            e.close()
+        sc = vkzg.random_scalars(curve, n, np.random.default_rng(72))
+        sc[5] = 0
+        want = oracle_c.msm_arrays(curve, xy, inf, sc, 8)
+        want_off = oracle_c.msm_arrays(curve, xy[100:], inf[100:], sc[:n - 100], 8)
+        for split in (vgroup.SPLIT_POINTS, vgroup.SPLIT_WINDOWS, vgroup.SPLIT_AUTO):
+            g.set_msm_split(split)
+            got = g.msm(tid, sc)
+            assert got[1] == want[1] and np.array_equal(got[0], want[0]), split
+            got = g.msm(tid, sc[:n - 100], offset=100)
+            assert got[1] == want_off[1] and np.array_equal(got[0], want_off[0]), split
+        tiny = g.msm(tid, sc[:1])                      # fewer points than members
+        w1 = oracle_c.msm_arrays(curve, xy[:1], inf[:1], sc[:1], 1)
+        assert tiny[1] == w1[1] and np.array_equal(tiny[0], w1[0])
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_group_msm_batch(oracle_c, G):
+    """vc_group_msm_batch: contiguous batch slices per member == one context == the oracle."""
+    import vkzg
+    g = _group("bandersnatch", G)
+    e = vkzg.Engine("bandersnatch")
+    try:
+        tid = g.random_bases(256, seed=9)
+        etid = e.random_bases(256, seed=9)
+        xy, inf = e.download_bases(etid)
+        sc = vkzg.random_scalars("bandersnatch", 256 * 37, np.random.default_rng(3))
+        gxy, ginf = g.msm_batch(tid, sc, 256)
+        exy, einf = e.msm_batch(etid, sc, 256)
+        assert np.array_equal(gxy, exy) and np.array_equal(ginf, einf)
+        for j in (0, 17, 36):
+            w = oracle_c.msm_arrays("bandersnatch", xy, inf, sc[j * 256:(j + 1) * 256], 4)
+            assert np.array_equal(gxy[j], w[0])
+    finally:
+        e.close()
+        g.close()
+
+
+def test_group_kzg_prove_golden():
+    """vc_group_kzg_prove (window-split proof MSM over 2 members) == the golden KZG d = 256 openings."""
+    import vkzg
+    from vkzg import scheme
+    gd = load("kzg_256.json")
+    g = _group("bn254", 2)
+    try:
+        tid, size = g.kzg_setup(256)
+        ev = vkzg.ints_to_limbs([int(x, 16) for x in gd["evals"]])
+        for op in gd["openings"]:
+            if "error" in op:
+                with pytest.raises(vkzg.VCError):
+                    g.kzg_prove(tid, size, ev, op["point"])
+                continue
+            xy, inf, y = g.kzg_prove(tid, size, ev, op["point"])
+            assert scheme._pt(xy, inf) == P(op["proof"]) and hex(y) == op["y"]
+    finally:
+        g.close()
+
+
+def _golden_mp(name):
+    from vkzg import scheme
+    gd = load("multiproof_256.json")
+    N, Q = 256, gd["Q"]
+    data = scheme.ints_to_limbs([(int(r0, 16) + i) % scheme.R_BN254 for r0 in gd["r0"] for i in range(N)])
+    cxy, cinf = scheme._pt_arrays([P(c) for c in gd[name]["commits"]])
+    z = np.array(gd["z"], dtype=np.uint64)
+    y = np.ascontiguousarray(data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)])
+    return gd[name], data, cxy, cinf, z, y
+
+
+def _check_mp(name, mp, want):
+    assert mp["d"] == P(want["d"])
+    if name == "ipa":
+        pr = mp["proof"]
+        assert pr.l == [P(x) for x in want["proof"]["l"]] and pr.r == [P(x) for x in want["proof"]["r"]]
+        assert pr.tip == int(want["proof"]["tip"], 16) and pr.y == int(want["proof"]["y"], 16)
+    else:
+        assert mp["proof"]["proof"] == P(want["proof"]["proof"]) and mp["proof"]["y"] == int(want["proof"]["y"], 16)
+
+
+@pytest.mark.parametrize("name", ["ipa", "kzg"])
+@pytest.mark.parametrize("G", [2, 3])
+def test_group_multiproof_golden(name, G):
+    """vc_group_multiproof_prove (transcript once, per-point sums of query slices on the members,
+    finish on member 0) and vc_group_multiproof_prove_many (P = 4 proofs over the members) ==
+    multiproof_256.json (N = 256)."""
+    g = _group("bn254", G)
+    try:
+        if name == "ipa":
+            tid = g.upload_points([P(h) for h in load("ipa_crs_bn254.json")["points"]])
+        else:
+            tid, _ = g.kzg_setup(256)
+        want, data, cxy, cinf, z, y = _golden_mp(name)
+        sid = 0 if name == "ipa" else 1
+        _check_mp(name, g.multiproof_prove(sid, tid, 256, data, cxy, cinf, z, y), want)
+        Pn = 4
+        tile = lambda a: np.ascontiguousarray(np.broadcast_to(a, (Pn,) + a.shape))  # noqa: E731
+        many = g.multiproof_prove_many(sid, tid, 256, tile(data), tile(cxy), tile(cinf), tile(z), tile(y))
+        assert len(many) == Pn
+        for mp in many:
+            _check_mp(name, mp, want)
+    finally:
+        g.close()
+
+
+def test_group_verkle_commitment():
+    """vc_group_verkle_commitment (one tree, each level's commits in member slices) == the
+    one-context commitment, fresh and after an incremental update."""
+    import vkzg
+    from vkzg import scheme
+    from vkzg.verkle import VerkleTree
+    rng = random.Random(17)
+    N = 4
+    keys1 = [tuple(rng.randrange(12) for _ in range(N)) for _ in range(600)]
+    keys2 = [tuple(rng.randrange(12) for _ in range(N)) for _ in range(80)]
+    vals = {k: bytes(rng.randrange(256) for _ in range(32)) for k in keys1 + keys2}
+
+    def build(keys, t):
+        for k in keys:
+            try:
+                t.insert_single(k, vals[k])
+            except Exception:
+                pass
+
+    def commitments(commit):
+        t = VerkleTree(N)
+        build(keys1, t)
+        a = commit(t)
+        build(keys2, t)
+        b = commit(t)
+        assert t.stats()["dirty"] == 0
+        return a, b
+
+    e = vkzg.Engine("bn254")
+    try:
+        kz = scheme.KZG(e, 256)
+        want = commitments(lambda t: t.commitment(e, kz.table))
+    finally:
+        e.close()
+    for G in (2, 3):
+        g = _group("bn254", G)
+        try:
+            tid, _ = g.kzg_setup(256)
+            assert commitments(lambda t: g.verkle_commitment(t, tid)) == want
+        finally:
+            g.close()
+
+
+def test_group_errors():
+    """unknown table -> VC_E_TABLE; a bad argument -> VC_E_INVALID; the group stays usable."""
+    import vkzg
+    g = _group("bn254", 2)
+    try:
+        with pytest.raises(vkzg.VCError) as ex:
+            g.msm(7, np.zeros((4, 4), dtype=np.uint64))
+        assert ex.value.status == -4
+        tid = g.random_bases(64, seed=1)
+        with pytest.raises(vkzg.VCError) as ex:
+            g.msm(tid, np.zeros((65, 4), dtype=np.uint64))
+        assert ex.value.status == -5
+        xy, inf = g.msm(tid, np.zeros((64, 4), dtype=np.uint64))
+        assert inf == 1
+    finally:
+        g.close()

@@ -164,6 +164,64 @@ def test_golden_multiproof_verifies_and_tamper():
         assert not protocol.verify_multiproof(vc, vq2, mp)
 
 
+def _mp_golden_arrays(oracle_c, ent, queries_data, N):
+    import numpy as np
+    coms = [P(c) for c in ent]
+    cxy, cinf = oracle_c.points_to_array("bn254", coms)
+    data = oracle_c.ints_to_limbs([v for d in queries_data for v in d], 4)
+    return data, cxy, cinf
+
+
+@pytest.mark.parametrize("name", ["ipa", "kzg"])
+def test_mpcheck_matches_python_multiproof_goldens(oracle_c, name):
+    """oracle/pyoracle/mpcheck.py (the N = 256 / Q = 2^16 checker of the GPU multiproof: field
+    phases and commits in C, transcript and inner proof in Python) == the pure-Python
+    protocol.prove_multiproof fixtures: multiproof_32.json (N = 32) and multiproof_256.json (the
+    reference's width, 20 queries on one z) -- D, the inner proof, and y of every query."""
+    import numpy as np
+    from pyoracle import mpcheck, protocol
+    from pyoracle.curves import BN254
+    crs = [P(h) for h in load("ipa_crs_bn254.json")["points"]]
+    g32 = load("multiproof_32.json")[name]
+    g256 = load("multiproof_256.json")
+    cases = [(32, [[int(x, 16) for x in q["data"]] for q in g32["queries"]], [q["commit"] for q in g32["queries"]],
+              [q["z"] for q in g32["queries"]], g32),
+             (256, [[(int(r0, 16) + i) % BN254.r for i in range(256)] for r0 in g256["r0"]], g256[name]["commits"],
+              g256["z"], g256[name])]
+    for N, datas, commits, z, ent in cases:
+        vc = protocol.IPA(N, points=crs[:N + 1]) if name == "ipa" else protocol.KZG(N)
+        data, cxy, cinf = _mp_golden_arrays(oracle_c, commits, datas, N)
+        got = mpcheck.multiproof(vc, N, data, cxy, cinf, np.array(z, dtype=np.uint64), nthreads=2)
+        assert got["d"] == P(ent["d"])
+        if name == "ipa":
+            pr = got["proof"]
+            assert pr["l"] == [P(x) for x in ent["proof"]["l"]] and pr["r"] == [P(x) for x in ent["proof"]["r"]]
+            assert pr["tip"] == int(ent["proof"]["tip"], 16) and pr["y"] == int(ent["proof"]["y"], 16)
+        else:
+            assert got["proof"]["proof"] == P(ent["proof"]["proof"]) and got["proof"]["y"] == int(ent["proof"]["y"], 16)
+
+
+def test_multiproof_256_golden_verifies():
+    """multiproof_256.json verifies through the oracle verifier (multiproof.rs:178-215) and a
+    tampered y is rejected; its z rows hold 20 queries on z = 5 and on z = 200."""
+    from pyoracle import protocol
+    from pyoracle.curves import BN254
+    crs = [P(h) for h in load("ipa_crs_bn254.json")["points"]]
+    g = load("multiproof_256.json")
+    assert g["z"].count(5) >= 20 and g["z"].count(200) >= 20
+    ys = [(int(r0, 16) + z) % BN254.r for r0, z in zip(g["r0"], g["z"])]
+    ent = g["ipa"]
+    vq = [(P(c), z, y) for c, z, y in zip(ent["commits"], g["z"], ys)]
+    pr = ent["proof"]
+    proof = {"l": [P(x) for x in pr["l"]], "r": [P(x) for x in pr["r"]], "tip": int(pr["tip"], 16),
+             "y": int(pr["y"], 16)}
+    vc = protocol.IPA(256, points=crs)
+    mp = {"proof": proof, "d": P(ent["d"])}
+    assert protocol.verify_multiproof(vc, vq, mp)
+    vq[7] = (vq[7][0], vq[7][1], (vq[7][2] + 1) % BN254.r)
+    assert not protocol.verify_multiproof(vc, vq, mp)
+
+
 @pytest.mark.parametrize("curve", ["bn254", "bls12_381", "bandersnatch"])
 def test_pippenger_baseline_matches_naive(oracle_c, curve):
     """the all-core CPU Pippenger baseline (bench cpu_baseline leg) == the naive restatement of

@@ -360,19 +360,30 @@ int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int tabl
 int vc_multiproof_gather(vc_comm* comm, vc_ctx* ctx, int status, int scheme, size_t N, size_t P, uint64_t* d_xy,
                          uint8_t* d_inf, vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf,
                          uint64_t* kzg_y) {
+    // a rank that cannot enter the exchange at all, or group-wide parameters that size the records
+    // (every rank of an SPMD call passes the same scheme and N, so all of them return here alike)
     if (!comm || (comm->nccl && !valid(comm, ctx)) || (scheme != 0 && scheme != 1) || N == 0 || (N & (N - 1)))
-        return VC_E_INVALID;
-    if (P && (!d_xy || !d_inf || (scheme == 0 && !ipa_proofs) || (scheme == 1 && (!kzg_xy || !kzg_inf || !kzg_y))))
         return VC_E_INVALID;
     size_t K = 0;
     while ((size_t(1) << K) < N) K++;
+    // this rank's output buffers, for all P proofs (it receives every rank's): a bad buffer is this
+    // rank's failure, carried in its record like a failed share, so the peers return VC_E_PEER and
+    // no rank writes any output before the group has agreed
+    int st = status;
+    if (st == VC_OK && P && (!d_xy || !d_inf || (scheme == 0 && !ipa_proofs) || (scheme == 1 && (!kzg_xy || !kzg_inf || !kzg_y))))
+        st = VC_E_INVALID;
+    for (size_t p = 0; st == VC_OK && scheme == 0 && p < P; p++) {
+        const vc_ipa_proof& pr = ipa_proofs[p];
+        if (pr.rounds < K || (K && (!pr.l_xy || !pr.r_xy || !pr.l_inf || !pr.r_inf)))
+            st = VC_E_INVALID;
+    }
     const size_t rec = scheme == 0 ? 9 + 18 * K + 8 : 9 + 13;  // u64 words per proof
     size_t lo, hi;
     vk::shard_range(P, comm->rank, comm->world, &lo, &hi);
     const size_t bmax = (P + comm->world - 1) / comm->world, slot = 1 + bmax * rec;
     std::vector<uint64_t> send(slot, 0), recv(slot * comm->world);
-    send[0] = (uint64_t)(uint32_t)status;
-    for (size_t p = lo; status == VC_OK && p < hi; p++) {
+    send[0] = (uint64_t)(uint32_t)st;
+    for (size_t p = lo; st == VC_OK && p < hi; p++) {
         uint64_t* r = &send[1 + (p - lo) * rec];
         memcpy(r, d_xy + p * 8, 64);
         r[8] = d_inf[p];
@@ -393,7 +404,7 @@ int vc_multiproof_gather(vc_comm* comm, vc_ctx* ctx, int status, int scheme, siz
         }
     }
     VK_TRY(comm_allgather_host(comm, ctx, send.data(), send.size() * 8, recv.data()));
-    VK_TRY(agree_in(comm, status, reinterpret_cast<const uint8_t*>(recv.data()), slot * 8));
+    VK_TRY(agree_in(comm, st, reinterpret_cast<const uint8_t*>(recv.data()), slot * 8));
     for (int k = 0; k < comm->world; k++) {
         size_t a, e;
         vk::shard_range(P, k, comm->world, &a, &e);
@@ -403,7 +414,6 @@ int vc_multiproof_gather(vc_comm* comm, vc_ctx* ctx, int status, int scheme, siz
             d_inf[p] = (uint8_t)r[8];
             if (scheme == 0) {
                 vc_ipa_proof& pr = ipa_proofs[p];
-                if (pr.rounds < K || !pr.l_xy || !pr.r_xy || !pr.l_inf || !pr.r_inf) return VC_E_INVALID;
                 pr.rounds = K;
                 for (size_t j = 0; j < K; j++) {
                     memcpy(pr.l_xy + 8 * j, r + 9 + 18 * j, 64);

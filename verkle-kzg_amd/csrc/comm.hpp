@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <functional>
+#include <vector>
 
 #include "../../include/vc_verkle.h"
 
@@ -22,7 +23,18 @@ inline void shard_range(size_t n, int rank, int world, size_t* lo, size_t* hi) {
     *hi = n * (size_t)(rank + 1) / (size_t)world;
 }
 
-// Node::gen_commitment level by level (verkle.cpp); sh = nullptr: the whole tree on this ctx
-int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh);
+// in-process members of a vc_group (group.cpp): their contexts and member-local table ids, and
+// run(f) = f(k) for every member concurrently, returning when all have finished
+struct Multi {
+    std::vector<vc_ctx*> ctx;
+    std::vector<int> table;
+    std::function<void(const std::function<void(int)>&)> run;
+};
+
+// Node::gen_commitment level by level (verkle.cpp); sh = nullptr: the whole tree on this ctx, or
+// with mu every level's commits cut into member slices committed concurrently (no exchange: the
+// members write into the one tree's level records directly)
+int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh,
+                      const Multi* mu = nullptr);
 
 }  // namespace vk

@@ -1,0 +1,402 @@
+// One process, several GPUs (include/vc_group.h): one vc_ctx and one host worker per member; every
+// call runs the members' shares concurrently and combines them in host memory. The reference's
+// callers are single-process (vector-commit/src/lib.rs:70-174, multiproof.rs:119-144 with rayon),
+// so this is the shape a stateless `impl VectorCommitment` needs to use a whole node without
+// becoming SPMD itself (the vc_comm.h entry points remain for one-process-per-GPU deployments).
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/vc_group.h"
+#include "comm.hpp"
+#include "ctx.hpp"
+
+namespace {
+
+// G workers; run(f) calls f(k) for every member k concurrently (k = 0 on the caller's thread) and
+// returns when all have finished. Threads live as long as the group.
+class Team {
+public:
+    explicit Team(int n) : n_(n) {
+        for (int k = 1; k < n; k++) th_.emplace_back([this, k] { loop(k); });
+    }
+    ~Team() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(const std::function<void(int)>& f) {
+        if (n_ == 1) {
+            f(0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            pending_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(int k) {
+        unsigned seen = 0;
+        for (;;) {
+            const std::function<void(int)>* f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (quit_) return;
+                f = job_;
+            }
+            (*f)(k);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int pending_ = 0;
+    unsigned gen_ = 0;
+    bool quit_ = false;
+};
+
+// grow-only device buffer on one device (the member's input staging)
+struct MemBuf {
+    int dev = 0;
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return VC_OK;
+        VK_CHECK_HIP(hipSetDevice(dev));
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        VK_CHECK_HIP(hipMalloc(&p, bytes ? bytes : 16));
+        cap = bytes ? bytes : 16;
+        return VC_OK;
+    }
+    ~MemBuf() {
+        if (p) {
+            (void)hipSetDevice(dev);
+            (void)hipFree(p);
+        }
+    }
+};
+
+// the first failing member's status
+int first_error(const std::vector<int>& st) {
+    for (int s : st)
+        if (s != VC_OK) return s;
+    return VC_OK;
+}
+
+}  // namespace
+
+struct vc_group {
+    int curve = 0;
+    std::vector<vc_ctx*> ctx;
+    std::vector<std::vector<int>> tables;  // [group table id][member] -> member table id
+    std::vector<MemBuf> data, sums;        // per member: input staging, multiproof sums
+    int split = VC_GROUP_SPLIT_AUTO;
+    std::mutex mu;  // one group call at a time
+    Team* team = nullptr;
+    int size() const { return (int)ctx.size(); }
+    bool table_ok(int id) const { return id >= 0 && id < (int)tables.size(); }
+};
+
+extern "C" {
+
+int vc_group_create(int curve, int ndev, const int* devices, vc_group** out) {
+    if (!out || ndev < 1 || ndev > 64) return VC_E_INVALID;
+    *out = nullptr;
+    vc_group* g = new vc_group();
+    g->curve = curve;
+    for (int k = 0; k < ndev; k++) {
+        vc_ctx* c = nullptr;
+        const int st = vc_ctx_create(curve, devices ? devices[k] : k, &c);
+        if (st != VC_OK) {
+            for (auto* x : g->ctx) vc_ctx_destroy(x);
+            delete g;
+            return st;
+        }
+        g->ctx.push_back(c);
+    }
+    g->data.resize(ndev);
+    g->sums.resize(ndev);
+    for (int k = 0; k < ndev; k++) g->data[k].dev = g->sums[k].dev = g->ctx[k]->device;
+    g->team = new Team(ndev);
+    *out = g;
+    return VC_OK;
+}
+
+void vc_group_destroy(vc_group* g) {
+    if (!g) return;
+    delete g->team;
+    g->data.clear();
+    g->sums.clear();
+    for (auto* c : g->ctx) vc_ctx_destroy(c);
+    delete g;
+}
+
+int vc_group_size(const vc_group* g) { return g ? g->size() : VC_E_INVALID; }
+
+vc_ctx* vc_group_member(vc_group* g, int k) { return (g && k >= 0 && k < g->size()) ? g->ctx[k] : nullptr; }
+
+int vc_group_member_table(const vc_group* g, int id, int member, int* member_table) {
+    if (!g || !member_table || member < 0 || member >= g->size()) return VC_E_INVALID;
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    *member_table = g->tables[id][member];
+    return VC_OK;
+}
+
+int vc_group_set_msm_split(vc_group* g, int split) {
+    if (!g || split < VC_GROUP_SPLIT_AUTO || split > VC_GROUP_SPLIT_POINTS) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->split = split;
+    return VC_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// a new group table from per-member creators
+int new_table(vc_group* g, const std::function<int(int k, int* id)>& make, int* table_id) {
+    const int G = g->size();
+    std::vector<int> ids(G, -1), st(G, VC_OK);
+    g->team->run([&](int k) { st[k] = make(k, &ids[k]); });
+    VK_TRY(first_error(st));
+    g->tables.push_back(ids);
+    *table_id = (int)g->tables.size() - 1;
+    return VC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vc_group_bases_upload(vc_group* g, const uint64_t* xy, const uint8_t* inf, size_t n, int* table_id) {
+    if (!g || !table_id || (n && !xy)) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return new_table(g, [&](int k, int* id) { return vc_bases_upload(g->ctx[k], xy, inf, n, id); }, table_id);
+}
+
+int vc_group_bases_random(vc_group* g, uint64_t seed, size_t n, int* table_id) {
+    if (!g || !table_id) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return new_table(g, [&](int k, int* id) { return vc_bases_random(g->ctx[k], seed, n, id); }, table_id);
+}
+
+int vc_group_kzg_setup(vc_group* g, size_t max_items, const uint64_t* secret_fr, int* table_id, size_t* size) {
+    if (!g || !table_id || !size || !secret_fr) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    std::vector<size_t> sz(g->size(), 0);
+    VK_TRY(new_table(g, [&](int k, int* id) { return vc_kzg_setup(g->ctx[k], max_items, secret_fr, id, &sz[k]); },
+                     table_id));
+    *size = sz[0];
+    return VC_OK;
+}
+
+int vc_group_fixed_base_precompute(vc_group* g, int id, int window_bits, int windows) {
+    if (!g) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    std::vector<int> st(g->size(), VC_OK);
+    g->team->run([&](int k) {
+        st[k] = vc_fixed_base_precompute_windows(g->ctx[k], g->tables[id][k], window_bits, windows);
+    });
+    return first_error(st);
+}
+
+int vc_group_msm(vc_group* g, int id, size_t offset, const uint64_t* scalars, size_t n, int mont, uint64_t* out_xy,
+                 uint8_t* out_inf) {
+    if (!g || !out_xy || !out_inf || (n && !scalars)) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    const int G = g->size();
+    if (G == 1) return vc_msm(g->ctx[0], g->tables[id][0], offset, scalars, n, mont, out_xy, out_inf);
+    const bool windows = g->split == VC_GROUP_SPLIT_WINDOWS;
+    if (n < (size_t)G) return vc_msm(g->ctx[0], g->tables[id][0], offset, scalars, n, mont, out_xy, out_inf);
+    const int words = vc_point_words(g->curve);
+    std::vector<uint32_t> accs((size_t)words * G, 0);
+    std::vector<int> st(G, VC_OK);
+    g->team->run([&](int k) {
+        auto share = [&]() -> int {
+            size_t lo = 0, hi = n;
+            if (!windows) vk::shard_range(n, k, G, &lo, &hi);  // n >= G: no empty share
+            VK_TRY(g->data[k].ensure((hi - lo) * 32));
+            VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+            VK_CHECK_HIP(hipMemcpy(g->data[k].p, scalars + lo * 4, (hi - lo) * 32, hipMemcpyHostToDevice));
+            uint32_t* acc = accs.data() + (size_t)k * words;
+            if (windows)
+                return vc_msm_device_window_part(g->ctx[k], g->tables[id][k], offset, g->data[k].p, n, mont, k, G, acc);
+            return vc_msm_device_partial(g->ctx[k], g->tables[id][k], offset + lo, g->data[k].p, hi - lo, mont, acc);
+        };
+        st[k] = share();
+    });
+    VK_TRY(first_error(st));
+    return vc_partials_sum(g->curve, accs.data(), G, out_xy, out_inf);
+}
+
+int vc_group_msm_batch(vc_group* g, int id, size_t width, const uint64_t* scalars, size_t batch, int mont,
+                       uint64_t* out_xy, uint8_t* out_inf) {
+    if (!g || width == 0 || (batch && (!scalars || !out_xy || !out_inf))) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    const int G = g->size();
+    const size_t W2 = 2 * (size_t)vk::aff_limbs64(g->curve);
+    std::vector<int> st(G, VC_OK);
+    g->team->run([&](int k) {
+        size_t lo, hi;
+        vk::shard_range(batch, k, G, &lo, &hi);
+        if (hi > lo)
+            st[k] = vc_msm_batch(g->ctx[k], g->tables[id][k], width, scalars + lo * width * 4, hi - lo, mont,
+                                 out_xy + lo * W2, out_inf + lo);
+    });
+    return first_error(st);
+}
+
+int vc_group_kzg_prove(vc_group* g, int id, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                       uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y) {
+    if (!g || !point || !proof_xy || !proof_inf || !y || (max && !evals) || max > size) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    const int G = g->size();
+    if (G == 1) return vc_kzg_prove(g->ctx[0], g->tables[id][0], size, evals, max, point, proof_xy, proof_inf, y);
+    const int words = vc_point_words(g->curve);
+    std::vector<uint32_t> accs((size_t)words * G, 0);
+    std::vector<uint64_t> ys((size_t)4 * G, 0);
+    std::vector<int> st(G, VC_OK);
+    g->team->run([&](int k) {
+        auto share = [&]() -> int {
+            VK_TRY(g->data[k].ensure(max * 32));
+            VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+            if (max) VK_CHECK_HIP(hipMemcpy(g->data[k].p, evals, max * 32, hipMemcpyHostToDevice));
+            return vc_kzg_prove_device_part(g->ctx[k], g->tables[id][k], size, g->data[k].p, max, point, k, G,
+                                            accs.data() + (size_t)k * words, &ys[(size_t)4 * k]);
+        };
+        st[k] = share();
+    });
+    VK_TRY(first_error(st));
+    memcpy(y, ys.data(), 32);
+    return vc_partials_sum(g->curve, accs.data(), G, proof_xy, proof_inf);
+}
+
+int vc_group_multiproof_prove(vc_group* g, int scheme, int id, size_t N, size_t Q, const uint64_t* data,
+                              const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                              uint64_t* d_xy, uint8_t* d_inf, vc_ipa_proof* ipa_proof, uint64_t* kzg_proof_xy,
+                              uint8_t* kzg_proof_inf, uint64_t* kzg_y) {
+    if (!g || !data || !com_xy || !com_inf || !z || !y || !d_xy || !d_inf || Q == 0) return VC_E_INVALID;
+    if (scheme != 0 && scheme != 1) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    const int G = g->size();
+    if (G == 1)
+        return vc_multiproof_prove(g->ctx[0], scheme, g->tables[id][0], N, Q, data, com_xy, com_inf, z, y, d_xy, d_inf,
+                                   ipa_proof, kzg_proof_xy, kzg_proof_inf, kzg_y);
+    // phase 1 once (the serial transcript over all queries, multiproof.rs:106-115)
+    vc_transcript* tr = nullptr;
+    uint64_t r[4];
+    size_t rows = 0;
+    VK_TRY(vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows));
+    const size_t sbytes = rows * N * 32;
+    // member 0 holds every member's sums contiguously (vc_multiproof_finish adds G parts)
+    int st0 = g->sums[0].ensure(sbytes * G);
+    std::vector<int> st(G, st0);
+    if (st0 == VC_OK)
+        g->team->run([&](int k) {
+            auto share = [&]() -> int {
+                size_t lo, hi;
+                vk::shard_range(Q, k, G, &lo, &hi);
+                uint8_t* dst0 = static_cast<uint8_t*>(g->sums[0].p) + (size_t)k * sbytes;
+                VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+                if (hi == lo) {  // an empty slice contributes zero sums
+                    VK_CHECK_HIP(hipSetDevice(g->ctx[0]->device));
+                    VK_CHECK_HIP(hipMemset(dst0, 0, sbytes));
+                    return VC_OK;
+                }
+                VK_TRY(g->data[k].ensure((hi - lo) * N * 32));
+                VK_CHECK_HIP(hipMemcpy(g->data[k].p, data + lo * N * 4, (hi - lo) * N * 32, hipMemcpyHostToDevice));
+                void* dS = dst0;
+                if (k != 0) {
+                    VK_TRY(g->sums[k].ensure(sbytes));
+                    dS = g->sums[k].p;
+                }
+                VK_TRY(vc_multiproof_accumulate(g->ctx[k], N, Q, z, lo, hi - lo, g->data[k].p, r, dS));
+                if (k != 0)
+                    VK_CHECK_HIP(hipMemcpyPeer(dst0, g->ctx[0]->device, dS, g->ctx[k]->device, sbytes));
+                return VC_OK;
+            };
+            st[k] = share();
+        });
+    int s = first_error(st);
+    if (s == VC_OK)
+        s = vc_multiproof_finish(g->ctx[0], scheme, g->tables[id][0], N, Q, z, g->sums[0].p, G, tr, d_xy, d_inf,
+                                 ipa_proof, kzg_proof_xy, kzg_proof_inf, kzg_y);
+    vc_transcript_free(tr);
+    return s;
+}
+
+int vc_group_multiproof_prove_many(vc_group* g, int scheme, int id, size_t N, size_t Q, size_t P,
+                                   const uint64_t* data, const uint64_t* com_xy, const uint8_t* com_inf,
+                                   const uint64_t* z, const uint64_t* y, uint64_t* d_xy, uint8_t* d_inf,
+                                   vc_ipa_proof* ipa_proofs, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
+    if (!g || (P && (!data || !com_xy || !com_inf || !z || !y || !d_xy || !d_inf))) return VC_E_INVALID;
+    if ((scheme != 0 && scheme != 1) || (P && scheme == 0 && !ipa_proofs) ||
+        (P && scheme == 1 && (!kzg_xy || !kzg_inf || !kzg_y)))
+        return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    const int G = g->size();
+    std::vector<int> st(G, VC_OK);
+    g->team->run([&](int k) {
+        auto share = [&]() -> int {
+            size_t lo, hi;
+            vk::shard_range(P, k, G, &lo, &hi);
+            if (hi == lo) return VC_OK;
+            const size_t bytes = (hi - lo) * Q * N * 32;
+            VK_TRY(g->data[k].ensure(bytes));
+            VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+            VK_CHECK_HIP(hipMemcpy(g->data[k].p, data + lo * Q * N * 4, bytes, hipMemcpyHostToDevice));
+            return vc_multiproof_prove_many(g->ctx[k], scheme, g->tables[id][k], N, Q, hi - lo, g->data[k].p,
+                                            com_xy + lo * Q * 8, com_inf + lo * Q, z + lo * Q, y + lo * Q * 4,
+                                            d_xy + lo * 8, d_inf + lo, scheme == 0 ? ipa_proofs + lo : nullptr,
+                                            scheme == 1 ? kzg_xy + lo * 8 : nullptr,
+                                            scheme == 1 ? kzg_inf + lo : nullptr, scheme == 1 ? kzg_y + lo * 4 : nullptr);
+        };
+        st[k] = share();
+    });
+    return first_error(st);
+}
+
+int vc_group_verkle_commitment(vc_group* g, int id, vc_verkle* tree, uint64_t* out_xy, uint8_t* out_inf) {
+    if (!g || !tree || !out_xy || !out_inf) return VC_E_INVALID;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->table_ok(id)) return VC_E_TABLE;
+    vk::Multi mu;
+    mu.ctx = g->ctx;
+    mu.table = g->tables[id];
+    mu.run = [&](const std::function<void(int)>& f) { g->team->run(f); };
+    return vk::verkle_commitment(g->ctx[0], g->tables[id][0], tree, out_xy, out_inf, nullptr, &mu);
+}
+
+}  // extern "C"

@@ -272,8 +272,9 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
 
 namespace vk {
 
-int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh) {
-    if (!ctx || !t || !out_xy || !out_inf) return VC_E_INVALID;
+int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh,
+                      const Multi* mu) {
+    if (!ctx || !t || !out_xy || !out_inf || (sh && mu)) return VC_E_INVALID;
     const int N = t->N;
     static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
     auto tic = std::chrono::steady_clock::now();
@@ -411,6 +412,28 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         items.resize(B * 4);
         if (B == 0) return VC_OK;
         lap("build rows");
+        if (mu) {  // member k commits rows [B k / G, B (k + 1) / G) of the level on its own device
+            const int G = (int)mu->ctx.size();
+            std::vector<int> st(G, VC_OK);
+            mu->run([&](int k) {
+                size_t a, e;
+                shard_range(B, k, G, &a, &e);
+                if (a == e) return;
+                std::vector<uint64_t> rp(e - a + 1);
+                const uint64_t base = r.ptr[a];
+                for (size_t i = 0; i <= e - a; i++) rp[i] = r.ptr[a + i] - base;
+                const uint32_t* cols = r.cols.size() ? r.cols.data() + base : nullptr;
+                const uint64_t* vals = r.vals.size() ? r.vals.data() + 4 * base : nullptr;
+                st[k] = vc_msm_batch_sparse(mu->ctx[k], mu->table[k], e - a, rp.data(), cols, vals, 0, xy.data() + 8 * a,
+                                            inf.data() + a);
+                if (st[k] == VC_OK)
+                    st[k] = vc_to_data_item_batch(mu->ctx[k], xy.data() + 8 * a, inf.data() + a, e - a, items.data() + 4 * a);
+            });
+            for (int s : st)
+                if (s != VC_OK) return s;
+            lap("sparse commit + to_data_item (members)");
+            return VC_OK;
+        }
         VK_TRY(vc_msm_batch_sparse(ctx, table, B, r.ptr.data(), r.cols.data(), r.vals.data(), 0, xy.data(), inf.data()));
         lap("sparse commit");
         int st = vc_to_data_item_batch(ctx, xy.data(), inf.data(), B, items.data());

@@ -11,7 +11,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)
 LIB_PATH = os.environ.get("VKZG_LIB") or os.path.join(ROOT, "lib", "libvkzg.so")
 HEADERS = [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("vc_msm.h", "vc_scheme.h", "vc_verkle.h",
-                                                                     "vc_comm.h")]
+                                                                     "vc_comm.h", "vc_group.h")]
 
 c_void_p, c_int, c_size_t, c_uint64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
 c_double, c_long, c_char_p = ctypes.c_double, ctypes.c_long, ctypes.c_char_p
@@ -114,6 +114,25 @@ SIGNATURES = {
     "vc_multiproof_prove_many_sharded": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, c_size_t,
                                                  c_void_p, P, P, P, P, P, P, P, P, P, P]),
     "vc_multiproof_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P]),
+    # vc_group.h
+    "vc_group_create": (c_int, [c_int, c_int, P, ctypes.POINTER(c_void_p)]),
+    "vc_group_destroy": (None, [c_void_p]),
+    "vc_group_size": (c_int, [c_void_p]),
+    "vc_group_member": (c_void_p, [c_void_p, c_int]),
+    "vc_group_bases_upload": (c_int, [c_void_p, P, P, c_size_t, ctypes.POINTER(c_int)]),
+    "vc_group_bases_random": (c_int, [c_void_p, c_uint64, c_size_t, ctypes.POINTER(c_int)]),
+    "vc_group_kzg_setup": (c_int, [c_void_p, c_size_t, P, ctypes.POINTER(c_int), ctypes.POINTER(c_size_t)]),
+    "vc_group_fixed_base_precompute": (c_int, [c_void_p, c_int, c_int, c_int]),
+    "vc_group_member_table": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_int)]),
+    "vc_group_set_msm_split": (c_int, [c_void_p, c_int]),
+    "vc_group_msm": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_group_msm_batch": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
+    "vc_group_kzg_prove": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, P, P, P, P]),
+    "vc_group_multiproof_prove": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P, P, P, P, P,
+                                          P]),
+    "vc_group_multiproof_prove_many": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, c_size_t, P, P, P, P, P,
+                                               P, P, P, P, P, P]),
+    "vc_group_verkle_commitment": (c_int, [c_void_p, c_int, c_void_p, P, P]),
 }
 
 _lib = None
