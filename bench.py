@@ -362,7 +362,9 @@ def mp_line(a, rank, world, local, dev, stream, comm=None):
     pipe = mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, mp) if world == 1 else None
     par = mp_proof_parallel(ipa, N, cxy, cinf, z, y, d_all, dev, rank, world, comm, mp) \
         if (world == 1 or comm is not None) else {"skipped": "no vc_comm for the proof exchange"}
-    ref_shapes = mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev) if rank == 0 else None
+    cpu = ({"data": data, "crs": crs, "threads": a.cpu_threads or min(16, os.cpu_count() or 1)}
+           if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None)
+    ref_shapes = mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, cpu=cpu) if rank == 0 else None
     meng.close()
     alg = Q * N * 32 + Q * 64 + Q * 40
     out = {"workload": f"IPA multiproof, Q = 2^{a.mp_log_q} width-256 queries, BN254 (configs[4]), query set "
@@ -383,7 +385,7 @@ def mp_line(a, rank, world, local, dev, stream, comm=None):
     return out
 
 
-def mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, reps=5):
+def mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, reps=5, cpu=None):
     """The reference's multiproof benches (vector-commit/benches/ipa.rs:111-159): prove_multiproof
     and verify_multiproof at Q = MAX_MULTIPROOF/8 x {1, 4, 8} = 4096, 16384, 32768 width-256 queries
     (the first Q of this line's query set; evaluations device-resident). Prove = the three phases
@@ -428,6 +430,15 @@ def mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, reps=5):
         out[str(q)] = {"prove_ms_median": float(np.median(tp)), "verify_ms_median": float(np.median(tv)),
                        "prove_ms": [round(x, 3) for x in tp], "verify_ms": [round(x, 3) for x in tv],
                        "verified": ok}
+        if cpu is not None:  # the CPU restatement of the same prove and verify, real challenges
+            data_q = cpu["data"][:q * N]
+            pr = cpu_multiproof(N, data_q, zq, cq, ciq, cpu["crs"], cpu["threads"], mp["d"])
+            vf = cpu_multiproof_verify(N, cq, ciq, zq, yq, cpu["crs"][:N])
+            out[str(q)]["cpu_baseline"] = {"prove_ms": pr["ms_per_multiproof"], "prove_cores": pr["cores"],
+                                           "prove_same_d_as_gpu": pr["same_d_as_gpu"],
+                                           "prove_parts_ms": pr["parts_ms"], "verify_ms": vf["ms"],
+                                           "verify_cores": vf["cores"], "verify_parts_ms": vf["parts_ms"],
+                                           "kind": "port", "sample": pr["sample"] + "; verify: " + vf["sample"]}
     return out
 
 
@@ -597,7 +608,148 @@ def cpu_multiproof(N, data, z, cxy, cinf, crs, threads, gpu_d=None):
                       "rounds are work-equivalent), SHA-256 transcript and hash_to_field"}
 
 
-def ipa_line(local, stream, batch=256):
+def _naive_ms(cref, xy, inf, sc):
+    """one naive MSM (utils.rs:16-19 restated in C, 1 thread): wall ms"""
+    t0 = time.perf_counter()
+    cref.msm_arrays("bn254", xy, inf, sc, 1)
+    return (time.perf_counter() - t0) * 1e3
+
+
+def cpu_multiproof_verify(N, cxy, cinf, z, y, crs, sample=512):
+    """verify_multiproof (multiproof.rs:178-215) on the CPU, restated: the transcript over the Q
+    (C, z, y) records + hash_to_field (r), t, the e-coefficient MSM over the Q commitments as the
+    naive inner_product (utils.rs:16-19; timed on `sample` terms and extrapolated linearly to Q),
+    and the inner IPA verification (low_level_verify_ipa, ipa/mod.rs:321-360: 2 scalar
+    multiplications per round and the 256-point naive MSM <g, s>)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import arkser, cref  # CPU baseline leg only
+    Q = z.shape[0]
+    r_mod = vkzg.SCALAR_R["bn254"]
+    t0 = time.perf_counter()
+    arkser.hash_to_field(_mp_records(cxy, cinf, z, y).tobytes() + b"r", b"multiproof", r_mod)
+    t_tr = (time.perf_counter() - t0) * 1e3
+    m = min(sample, Q)
+    sc = vkzg.random_scalars("bn254", m, np.random.default_rng(6))
+    t_e = _naive_ms(cref, cxy[:m], cinf[:m], sc) * Q / m
+    crs_xy, crs_inf = cref.points_to_array("bn254", crs)
+    K = N.bit_length() - 1
+    s2 = vkzg.random_scalars("bn254", max(N, 2), np.random.default_rng(8))
+    t_ipa = sum(_naive_ms(cref, crs_xy[:2], crs_inf[:2], s2[:2]) for _ in range(K))
+    t_ipa += _naive_ms(cref, crs_xy[:N], crs_inf[:N], s2[:N])
+    total = t_tr + t_e + t_ipa
+    return {"ms": total, "cores": 1, "kind": "port",
+            "parts_ms": {"transcript_hash_to_field": t_tr, "e_msm_naive": t_e, "inner_ipa_verify_naive": t_ipa},
+            "sample": f"transcript over all {Q} queries; the e-coefficient naive MSM timed on {m} of the {Q} "
+                      "commitments and extrapolated linearly; the inner IPA verification's scalar multiplications "
+                      "and 256-point MSM in C, 1 thread"}
+
+
+def cpu_ipa_single(crs, N=256):
+    """benches/ipa.rs:85-109 on the CPU (1 thread, the reference's serial prover/verifier), work-
+    equivalent in C: prove = low_level_ipa's log2 N rounds, each two half-size naive MSMs (L, R), a
+    generator fold of m/2 scalar multiplications (vec_add_and_distribute on points) and two
+    multiplications by q' (ipa/mod.rs:268-319); verify = 2 scalar multiplications per round and the
+    N-point naive MSM <g, s> (:321-360). Median of 3."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import cref  # CPU baseline leg only
+    xy, inf = cref.points_to_array("bn254", crs)
+    sc = vkzg.random_scalars("bn254", N, np.random.default_rng(10))
+
+    def prove():
+        t, m = 0.0, N
+        while m > 1:
+            h = m // 2
+            t += 3 * _naive_ms(cref, xy[:h], inf[:h], sc[:h]) + _naive_ms(cref, xy[:2], inf[:2], sc[:2])
+            m = h
+        return t
+
+    def verify():
+        K = N.bit_length() - 1
+        return sum(_naive_ms(cref, xy[:2], inf[:2], sc[:2]) for _ in range(K)) + _naive_ms(cref, xy[:N], inf[:N], sc)
+
+    p = float(np.median([prove() for _ in range(3)]))
+    v = float(np.median([verify() for _ in range(3)]))
+    return {"prove_ms": p, "verify_ms": v, "cores": 1, "kind": "port",
+            "sample": f"N = {N}: the rounds' naive MSMs and scalar multiplications in C (oracle/c/ref_curve.c), "
+                      "1 thread, median of 3 (work-equivalent: the same MSM sizes and scalar multiplications)"}
+
+
+def kzg_reference_shapes(local, stream, cpu=True):
+    """The reference's KZG benches (vector-commit/benches/kzg.rs:45-75) on BN254: KZG::setup at
+    32 / 2048 / 4096 / 16384 (vc_kzg_setup: the Lagrange SRS on the GPU), commit of 20 values over a
+    32-point CRS, and a single proof at an in-range index; GPU medians, and beside them the CPU port:
+    setup = max_items scalar multiplications (s^i G, kzg_point_generator.rs:32-43) + the G1 iFFT's
+    n/2 log2 n twiddle multiplications (kzg/mod.rs:119-121), timed on a sample and extrapolated;
+    commit = the 20-term naive MSM; proof = divide_by_vanishing in C (lagrange_basis.rs:91-119) +
+    the 32-term naive MSM."""
+    import ctypes
+    from vkzg import scheme
+    from vkzg._lib import check, lib
+    e = vkzg.Engine("bn254", local)
+    e.set_stream(stream.cuda_stream)
+    out = {"workload": "KZG on BN254, benches/kzg.rs shapes (DATA_SIZE 20, MAX_CRS 32; setup 32..16384)"}
+    secret = vkzg.ints_to_limbs([100])[0].copy()
+
+    def med(f, reps=7):
+        f()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            f()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return float(np.median(ts))
+
+    def setup_once(size):
+        tid, sz = ctypes.c_int(), ctypes.c_size_t()
+        check(lib().vc_kzg_setup(e.h, size, ctypes.c_void_p(secret.ctypes.data), ctypes.byref(tid), ctypes.byref(sz)),
+              "vc_kzg_setup")
+
+    out["setup_ms"] = {str(sz): med(lambda: setup_once(sz), reps=3) for sz in (32, 2048, 4096, 16384)}
+    kz = scheme.KZG(e, 32)
+    rng = np.random.default_rng(12)
+    data = scheme.LagrangeBasis([int(v) for v in rng.integers(0, 1 << 62, size=20)], 32)
+    com = kz.commit(data)
+    out["commit_ms"] = med(lambda: kz.commit(data))
+    out["single_proof_ms"] = med(lambda: kz.prove(com, 7, data))
+    e.close()
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from pyoracle import cref, protocol  # CPU baseline leg only
+        ceng = vkzg.Engine("bn254", local)
+        try:
+            tid = ceng.random_bases(512, seed=21)
+            xy, inf = ceng.download_bases(tid)
+        finally:
+            ceng.close()
+        sc = vkzg.random_scalars("bn254", 512, np.random.default_rng(13))
+        per_mul = _naive_ms(cref, xy, inf, sc) / 512          # one naive scalar multiplication (+ add)
+        setup = {}
+        for sz in (32, 2048, 4096, 16384):
+            setup[str(sz)] = per_mul * (sz + sz // 2 * (sz.bit_length() - 1))
+        dl = vkzg.ints_to_limbs([int(v) for v in data.evals] + [0] * 12)
+        omega = protocol.group_gen(32)
+
+        def proof():
+            st, _g = cref.mp_g(32, dl, np.array([7], dtype=np.uint64), 1, omega, 1)
+            cref.mp_free(st)
+            cref.msm_arrays("bn254", xy[:32], inf[:32], sc[:32], 1)
+
+        t_c = float(np.median([_naive_ms(cref, xy[:20], inf[:20], sc[:20]) for _ in range(5)]))
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            proof()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        out["cpu_baseline"] = {"setup_ms": setup, "commit_ms": t_c, "single_proof_ms": float(np.median(ts)),
+                               "cores": 1, "kind": "port",
+                               "sample": f"setup: {per_mul * 1e3:.1f} us per naive scalar multiplication (a 512-term "
+                                         "naive MSM in C) x (max_items + n/2 log2 n iFFT twiddles), extrapolated; "
+                                         "commit: the 20-term naive MSM; proof: divide_by_vanishing in C "
+                                         "(oracle/c/ref_multiproof.c) + the 32-term naive MSM; 1 thread, medians"}
+    return out
+
+
+def ipa_line(local, stream, batch=256, cpu=False):
     """The reference's IPA bench shapes (vector-commit/benches/ipa.rs:79-109, N = 256, BN254,
     data r + i): single commit, prove in / out of domain, verify in domain -- latency of one
     call each -- and a batch of independent proofs in one vc_ipa_prove call (proofs/s)."""
@@ -630,6 +782,8 @@ def ipa_line(local, stream, batch=256):
     out["batch_prove"] = {"proofs": batch, "ms": ms, "proofs_per_s": batch / ms * 1e3}
     out["concurrent_contexts"] = ipa_concurrent(N, datas, coms)
     ieng.close()
+    if cpu:
+        out["cpu_baseline"] = cpu_ipa_single(scheme.ipa_crs(N + 1, max_=512)[:N])
     return out
 
 
@@ -1059,8 +1213,10 @@ def main():
         progress("multiproof line done")
 
     if rank == 0 and not a.no_ipa:
-        out["ipa"] = ipa_line(local, stream)
+        out["ipa"] = ipa_line(local, stream, cpu=(world == 1 and not a.no_cpu_baseline))
         progress("ipa line done")
+        out["kzg_reference_shapes"] = kzg_reference_shapes(local, stream, cpu=(world == 1 and not a.no_cpu_baseline))
+        progress("kzg reference shapes done")
 
     if rank == 0 and not a.no_verkle:
         out["verkle"] = verkle_line(a, local, stream)

@@ -329,6 +329,26 @@ def test_msm_device_many(curve, n):
         e.close()
 
 
+def test_msm_device_many_more_sets_than_one_pipeline():
+    """K = 10 scalar sets over a 2^18 BLS12-381 table: pipelines of at most 8 bucket sets (the
+    sort's LDS histogram), then the rest (2 sets) -- every result == its single vc_msm_device."""
+    import torch
+    import vkzg
+    n, K = 1 << 18, 10
+    e = vkzg.Engine("bls12_381")
+    try:
+        tid = e.random_bases(n, seed=41)
+        rng = np.random.default_rng(42)
+        d = [torch.from_numpy(vkzg.random_scalars("bls12_381", n, rng).view(np.int64).copy()).cuda() for _ in range(K)]
+        torch.cuda.synchronize()
+        got = e.msm_device_many(tid, [x.data_ptr() for x in d], n)
+        for k in range(K):
+            want = e.msm_device(tid, d[k].data_ptr(), n)
+            assert got[k][1] == want[1] and np.array_equal(got[k][0], want[0]), k
+    finally:
+        e.close()
+
+
 def _mp_inputs(eng, ipa, Q, N=256, seed=77):
     """The bench's multiproof inputs: data < 2^252, commitments (batched commits), z, y = f(z)."""
     import torch

@@ -23,6 +23,9 @@
 #include <type_traits>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
+#include <utility>
 #include <vector>
 
 #include "ctx.hpp"
@@ -134,9 +137,10 @@ struct GlvDigits {
 struct RadixDigits {
     const int32_t* dig;
     uint32_t nv;
+    int w0 = 0;  // first window read (a per-set coarse pass of several bucket sets starts at its set)
     template <class Fn>
     __device__ __forceinline__ void operator()(uint32_t i, int, int W, Fn&& f) const {
-        for (int w = 0; w < W; w++) f(w, dig[(size_t)w * nv + i]);
+        for (int w = w0; w < W; w++) f(w, dig[(size_t)w * nv + i]);
     }
 };
 
@@ -244,10 +248,11 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
                                                         uint32_t NBC, uint32_t nblk, uint32_t stride, uint32_t wps,
                                                         uint32_t chunk, const uint32_t* __restrict__ counts,
                                                         const uint32_t* __restrict__ base,
-                                                        uint32_t* __restrict__ tmp) {
+                                                        uint32_t* __restrict__ tmp, uint32_t bin0, uint32_t bins) {
     extern __shared__ uint32_t sm[];
     __shared__ uint32_t part[1024];
-    const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
+    // this launch's coarse bins [bin0, bin0 + bins): all of them, or one bucket set's (windows
+    // [wb, we) of a several-set sort, one launch per set so a block's entries fit LDS)
     uint32_t* loff = sm;             // bins + 1 local run starts
     uint32_t* lcur = sm + bins + 1;  // bins cursors
     uint32_t* stage = lcur + bins;   // the block's entries, bin-major
@@ -256,7 +261,7 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
     const uint32_t per = (bins + blockDim.x - 1) / blockDim.x, b0 = t * per;
     uint32_t s = 0;
     for (uint32_t k = 0; k < per; k++)
-        if (b0 + k < bins) s += counts[(size_t)(b0 + k) * nblk + slot];
+        if (b0 + k < bins) s += counts[(size_t)(bin0 + b0 + k) * nblk + slot];
     part[t] = s;
     __syncthreads();
     for (uint32_t o = 1; o < blockDim.x; o <<= 1) {
@@ -270,7 +275,7 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
         if (b0 + k < bins) {
             loff[b0 + k] = run;
             lcur[b0 + k] = run;
-            run += counts[(size_t)(b0 + k) * nblk + slot];
+            run += counts[(size_t)(bin0 + b0 + k) * nblk + slot];
         }
     if (t == blockDim.x - 1) loff[bins] = part[t];
     __syncthreads();
@@ -281,7 +286,7 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
             if (d != 0 && w >= wb) {
                 const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
                 const uint32_t p = atomicAdd(
-                    &lcur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
+                    &lcur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB) - bin0], 1u);
                 stage[p] = sort_pack<uint32_t>(b & fmask, stride ? i + ((uint32_t)w % wps) * stride : i, d < 0, FB);
             }
         });
@@ -292,7 +297,7 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
     const uint32_t grp = t >> 4, sub = t & 15, ngrp = blockDim.x >> 4;
     for (uint32_t g = grp; g < bins; g += ngrp) {
         const uint32_t l0 = loff[g], len = loff[g + 1] - l0;
-        const uint32_t gb = base[(size_t)g * nblk + slot];
+        const uint32_t gb = base[(size_t)(bin0 + g) * nblk + slot];
         for (uint32_t j = sub; j < len; j += 16) tmp[gb + j] = stage[l0 + j];
     }
 }
@@ -736,13 +741,15 @@ __global__ void __launch_bounds__(256) k_glv_radix(const uint32_t* __restrict__ 
 // m 2^(c-1) buckets): a block takes `chunk` scalars, i.e. the entries of sort blocks blockIdx.x
 // (k1 terms, entries i) and n / chunk + blockIdx.x (k2 terms, entries n + i), and writes both
 // blocks' coarse-bin counts where k_sort_hist would (n % chunk == 0). Saves the hist pass's
-// re-read of the W x 2n digits and one launch.
+// re-read of the W x 2n digits and one launch. Several sets (several MSMs over one table): one
+// launch per set, its coarse bins at [bin0, bin0 + NBC) of bins_total.
 template <class Fr, uint32_t MUL, int C0>
 __global__ void __launch_bounds__(1024) k_glv_radix_hist(const uint32_t* __restrict__ sc,
                                                         const uint8_t* __restrict__ inf, uint32_t n, int mont,
                                                         GlvK K, int W, int32_t* __restrict__ dig, uint32_t FB,
                                                         uint32_t NBC, uint32_t nblk, uint32_t chunk,
-                                                        uint32_t* __restrict__ counts) {
+                                                        uint32_t* __restrict__ counts, uint32_t bin0,
+                                                        uint32_t bins_total) {
     extern __shared__ uint32_t hist[];  // [2][NBC]: k1 block, k2 block
     for (uint32_t k = threadIdx.x; k < 2 * NBC; k += blockDim.x) hist[k] = 0;
     __syncthreads();
@@ -770,10 +777,10 @@ __global__ void __launch_bounds__(1024) k_glv_radix_hist(const uint32_t* __restr
     __syncthreads();
     const uint32_t s1 = sort_slot(blockIdx.x, nblk), s2 = sort_slot(blockIdx.x + n / chunk, nblk);
     for (uint32_t k = threadIdx.x; k < NBC; k += blockDim.x) {
-        counts[(size_t)k * nblk + s1] = hist[k];
-        counts[(size_t)k * nblk + s2] = hist[NBC + k];
+        counts[(size_t)(bin0 + k) * nblk + s1] = hist[k];
+        counts[(size_t)(bin0 + k) * nblk + s2] = hist[NBC + k];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(size_t)NBC * nblk] = 0;  // the scan's terminal slot
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(size_t)bins_total * nblk] = 0;  // the scan's terminal slot
 }
 
 template <class C>
@@ -945,11 +952,24 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul 
     return VC_OK;
 }
 
+// hipFuncAttributeMaxDynamicSharedMemorySize is per device: set it once per (kernel, device), so
+// a process driving several GPUs (one vc_ctx each, or a vc_group) has it on every device it launches on
+static int coarse_st_lds_attr(const void* fn, int device) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({fn, device})) return VC_OK;
+    VK_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024));
+    done.insert({fn, device});
+    return VC_OK;
+}
+
 template <class Src>
 static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb, int we, uint32_t FB,
                         uint32_t NBC, uint32_t nblk, uint32_t chunk, uint32_t stride, uint32_t wps, size_t ncnt,
                         uint32_t* counts, uint32_t* base, void* tmp, uint32_t* offsets, uint32_t* sorted,
-                        uint32_t* zero_word, bool coarse_stage = false, bool counts_ready = false) {
+                        uint32_t* zero_word, bool coarse_stage = false, bool counts_ready = false,
+                        uint32_t sets_split = 1) {
     hipStream_t st = L.st;
     if (stride && wps == 0) return VC_E_INVALID;
     const uint32_t bins = (stride ? ((uint32_t)we + wps - 1) / wps : (uint32_t)(we - wb)) * NBC;
@@ -987,16 +1007,24 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
         cap = 16384;
         if (fine_env == 0) fblk = 1024;
     }
-    // staged coarse scatter (k_sort_coarse_st): narrow entries, the block's entries in LDS
-    const size_t st_lds = ((size_t)2 * bins + 1 + (size_t)chunk * (uint32_t)(we - wb)) * 4;
+    // staged coarse scatter (k_sort_coarse_st): narrow entries, the block's entries in LDS; with
+    // several shared bucket sets (windows [s wps, (s + 1) wps) -> set s) one launch per set, so a
+    // block holds one set's chunk x wps entries (the KZG commit + open's two sets keep 4096-scalar
+    // blocks, as one set does)
+    const uint32_t nsplit = (stride && sets_split > 1 && wb == 0 && (uint32_t)we == sets_split * wps) ? sets_split : 1;
+    const uint32_t bins_l = bins / nsplit;
+    const uint32_t wl = (uint32_t)(we - wb) / nsplit;
+    const size_t st_lds = ((size_t)2 * bins_l + 1 + (size_t)chunk * wl) * 4;
     const bool staged = coarse_stage && narrow && st_lds <= 152 * 1024;
     if (staged) {
-        // once per process and instantiation (thread-safe static initialisation)
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_coarse_st<Src>),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
-        VK_CHECK_HIP(attr);
-        VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", k_sort_coarse_st<Src>, nblk, 1024, st_lds, src, nv, c, wb, we, FB,
-                     NBC, nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp));
+        VK_TRY(coarse_st_lds_attr(reinterpret_cast<const void*>(&k_sort_coarse_st<Src>), ctx->device));
+        for (uint32_t s = 0; s < nsplit; s++) {
+            Src ss = src;
+            const int wbs = nsplit > 1 ? (int)(s * wps) : wb, wes = nsplit > 1 ? (int)((s + 1) * wps) : we;
+            if constexpr (std::is_same<Src, RadixDigits>::value) ss.w0 = wbs;
+            VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", k_sort_coarse_st<Src>, nblk, 1024, st_lds, ss, nv, c, wbs, wes, FB,
+                         NBC, nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp), s * bins_l, bins_l);
+        }
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, cap * 4,
                      static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
     } else if (narrow) {
@@ -1076,11 +1104,11 @@ struct MsmSlice {
     // BLS12-381 radix digits still to be made (msm_run_t leaves the GLV split to slice_enqueue,
     // which fuses the sort histogram into it when the geometry allows): sc == nullptr otherwise
     struct {
-        const uint32_t* sc = nullptr;
+        std::vector<const uint32_t*> sc;  // one scalar set per bucket set (empty: digits made already)
+        std::vector<int> mont;
         const uint8_t* inf = nullptr;
         uint32_t n = 0;
-        int mont = 0;
-        int32_t* dig = nullptr;
+        int32_t* dig = nullptr;  // set s at dig + s W 2n
     } radix;
 };
 
@@ -1151,11 +1179,13 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     static const int cstage_env = getenv("VKZG_SORT_CSTAGE") ? atoi(getenv("VKZG_SORT_CSTAGE")) : 1;  // A/B probe
     bool cstage = false;
     if (sl.m > 1 && sl.shared && cstage_env) {
-        const uint64_t bins_all = (uint64_t)Wr * (NB >> FB);
-        const uint64_t room = (152u * 1024 / 4 > 2 * bins_all + 1) ? 152u * 1024 / 4 - 2 * bins_all - 1 : 0;
+        // one coarse launch per bucket set (sort_entries): a block stages one set's windows
+        const uint64_t bins_l = (uint64_t)(NB >> FB);
+        const uint32_t Wl = (uint32_t)W / (uint32_t)Wr;
+        const uint64_t room = (152u * 1024 / 4 > 2 * bins_l + 1) ? 152u * 1024 / 4 - 2 * bins_l - 1 : 0;
         uint32_t ch = 1u << 12;
-        while (ch > 1024 && (uint64_t)ch * (uint32_t)W > room) ch >>= 1;
-        if ((uint64_t)ch * (uint32_t)W <= room) {  // one set: 4096 scalars; the KZG's two sets: 2048
+        while (ch > 1024 && (uint64_t)ch * Wl > room) ch >>= 1;
+        if ((uint64_t)ch * Wl <= room) {  // 4096 scalars for one set and for each of several
             chunk = ch;
             cstage = true;
         }
@@ -1228,26 +1258,33 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
 
     bool counts_ready = false;
     if constexpr (std::is_same<C, BLS381G1>::value) {
-        if (sl.radix.sc != nullptr) {
-            // one set over all windows, whole sort blocks of scalars: GLV split + sort histogram
+        if (!sl.radix.sc.empty()) {
+            // whole bucket sets over all their windows, whole sort blocks of scalars: the GLV split
+            // of set s writes the sort histogram of its bins [s NBC, (s + 1) NBC) itself
             static const int fuse_env = getenv("VKZG_RADIX_HIST") ? atoi(getenv("VKZG_RADIX_HIST")) : 1;  // A/B
             const uint32_t rn = sl.radix.n;
-            counts_ready = fuse_env && sl.shared && Wr == 1 && sl.wb == 0 && (uint32_t)sl.we == sl.wps &&
+            const int ns = (int)sl.radix.sc.size();
+            counts_ready = fuse_env && sl.shared && Wr == ns && sl.wb == 0 && (uint32_t)sl.we == sl.wps * (uint32_t)ns &&
                            nv == 2 * (size_t)rn && rn % chunk == 0 && (size_t)2 * NBC * 4 <= 64 * 1024;
-            if (counts_ready)
-                VK_LAUNCH_ON(ctx, st, "glv_split", (k_glv_radix_hist<BLS381Fr, 5, 16>), rn / chunk, 1024,
-                             (size_t)2 * NBC * 4, sl.radix.sc, sl.radix.inf, rn, sl.radix.mont, glv_consts(),
-                             (int)sl.wps, sl.radix.dig, FB, NBC, nblk, chunk, ws[WS_COUNTS].as<uint32_t>());
-            else
-                VK_LAUNCH_ON(ctx, st, "glv_split", (k_glv_radix<BLS381Fr, 5, 16>), (rn + 255) / 256, 256, 0,
-                             sl.radix.sc, sl.radix.inf, rn, sl.radix.mont, glv_consts(), (int)sl.wps, sl.radix.dig);
+            for (int s2 = 0; s2 < ns; s2++) {
+                int32_t* dig = sl.radix.dig + (size_t)s2 * sl.wps * nv;
+                if (counts_ready)
+                    VK_LAUNCH_ON(ctx, st, "glv_split", (k_glv_radix_hist<BLS381Fr, 5, 16>), rn / chunk, 1024,
+                                 (size_t)2 * NBC * 4, sl.radix.sc[s2], sl.radix.inf, rn, sl.radix.mont[s2], glv_consts(),
+                                 (int)sl.wps, dig, FB, NBC, nblk, chunk, ws[WS_COUNTS].as<uint32_t>(),
+                                 (uint32_t)s2 * NBC, (uint32_t)Wr * NBC);
+                else
+                    VK_LAUNCH_ON(ctx, st, "glv_split", (k_glv_radix<BLS381Fr, 5, 16>), (rn + 255) / 256, 256, 0,
+                                 sl.radix.sc[s2], sl.radix.inf, rn, sl.radix.mont[s2], glv_consts(), (int)sl.wps, dig);
+            }
         }
     }
     VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (uint32_t)nv : 0u,
                         sl.wps, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
-                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max, cstage, counts_ready));
+                        ws[WS_SORTED].as<uint32_t>(), sl.chain_max, cstage, counts_ready,
+                        sl.shared ? (uint32_t)Wr : 1u));
     // entry count L = offsets[NBtot] stays on the device; grids are sized for L <= nv*W;
     // chain_max was cleared by k_sort_fine
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
@@ -1490,8 +1527,13 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
             VK_TRY(ctx->ws[WS_GLV_SC].ensure(radix_m > 1 ? nv * 4 * (size_t)Wfull : nv * 16));
             uint4* halves = ctx->ws[WS_GLV_SC].as<uint4>();
             const Aff* dphi = t->fast.as<Aff>() + t->n + offset;
-            if (radix_m > 1 && nsl == 1)  // the split runs in slice_enqueue (sort histogram fused)
-                sl[0].radix = {d_sc, inf, (uint32_t)n, mont, ctx->ws[WS_GLV_SC].as<int32_t>()};
+            if (radix_m > 1 && nsl == 1) {  // the split runs in slice_enqueue (sort histogram fused)
+                sl[0].radix.sc = {d_sc};
+                sl[0].radix.mont = {mont};
+                sl[0].radix.inf = inf;
+                sl[0].radix.n = (uint32_t)n;
+                sl[0].radix.dig = ctx->ws[WS_GLV_SC].as<int32_t>();
+            }
             else if (radix_m > 1)
                 VK_LAUNCH(ctx, "glv_split", (k_glv_radix<Fr, 5, 16>), (n + 255) / 256, 256, 0, d_sc, inf, (uint32_t)n,
                           mont, glv_consts(), Wfull, ctx->ws[WS_GLV_SC].as<int32_t>());
@@ -1575,7 +1617,7 @@ static int msm_run_many_t(vc_ctx* ctx, Table* t, const void* const* d_sc, const 
         bool glv = false;
         if (K > 1 && n == t->n && n >= (1u << 18) && n < (1u << 30) && ctx->opt_shared_windows != 0 &&
             !getenv("VKZG_MSM_RADIX") && !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED") &&
-            (uint64_t)2 * n * 7 * K < 0xffffffffull)
+            (uint64_t)2 * n * 7 * std::min<size_t>(K, 8) < 0xffffffffull)
             VK_TRY(glv_table_ok(ctx, t, &glv));
         if (glv) {
             VK_TRY(fast_tables<C>(ctx, t, true));
@@ -1587,28 +1629,39 @@ static int msm_run_many_t(vc_ctx* ctx, Table* t, const void* const* d_sc, const 
         if (batched) {
             const size_t nv = 2 * n;
             const int Ws = 7;
-            VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 4 * (size_t)Ws * K));
-            int32_t* dig = ctx->ws[WS_GLV_SC].as<int32_t>();
-            for (size_t k = 0; k < K; k++)
-                VK_LAUNCH(ctx, "glv_split", (k_glv_radix<Fr, 5, 16>), (n + 255) / 256, 256, 0,
-                          static_cast<const uint32_t*>(d_sc[k]), t->inf.as<uint8_t>(), (uint32_t)n, mont[k], glv_consts(),
-                          Ws, dig + k * (size_t)Ws * nv);
-            MsmSlice<C> sl;
-            sl.L = ctx->lane(0);
-            sl.c = 16;
-            sl.m = 5;
-            sl.shared = true;
-            sl.sets = (int)K;
-            sl.wps = (uint32_t)Ws;
-            sl.wb = 0;
-            sl.we = Ws * (int)K;
-            sl.W = sl.we;
-            const auto* win = t->win.as<typename Fast29<C>::type::AffN>();
-            VK_TRY(slice_enqueue<C>(ctx, sl, RadixDigits{dig, (uint32_t)nv}, nv, win, win, 0xffffffffu, nullptr, nullptr));
-            VK_TRY(slice_fetch<C>(sl));
-            std::vector<Acc> res(K);
-            VK_TRY(slice_finish<C>(ctx, sl, res.data()));
-            memcpy(out_accs, res.data(), K * sizeof(Acc));
+            // up to 8 bucket sets per pipeline (the sort's LDS histogram holds 8 x 1280 coarse bins)
+            for (size_t k0 = 0; k0 < K; k0 += 8) {
+                const size_t Kb = std::min<size_t>(8, K - k0);
+                if (Kb == 1) {
+                    VK_TRY(msm_run(ctx, t, 0, d_sc[k0], n, mont[k0], out_accs + k0 * (sizeof(Acc) / 4)));
+                    continue;
+                }
+                VK_TRY(ctx->ws[WS_GLV_SC].ensure(nv * 4 * (size_t)Ws * Kb));
+                MsmSlice<C> sl;
+                sl.L = ctx->lane(0);
+                sl.c = 16;
+                sl.m = 5;
+                sl.shared = true;
+                sl.sets = (int)Kb;
+                sl.wps = (uint32_t)Ws;
+                sl.wb = 0;
+                sl.we = Ws * (int)Kb;
+                sl.W = sl.we;
+                sl.radix.inf = t->inf.as<uint8_t>();
+                sl.radix.n = (uint32_t)n;
+                sl.radix.dig = ctx->ws[WS_GLV_SC].as<int32_t>();
+                for (size_t k = k0; k < k0 + Kb; k++) {  // the GLV split of every set runs in slice_enqueue
+                    sl.radix.sc.push_back(static_cast<const uint32_t*>(d_sc[k]));
+                    sl.radix.mont.push_back(mont[k]);
+                }
+                const auto* win = t->win.as<typename Fast29<C>::type::AffN>();
+                VK_TRY(slice_enqueue<C>(ctx, sl, RadixDigits{sl.radix.dig, (uint32_t)nv}, nv, win, win, 0xffffffffu,
+                                        nullptr, nullptr));
+                VK_TRY(slice_fetch<C>(sl));
+                std::vector<Acc> res(Kb);
+                VK_TRY(slice_finish<C>(ctx, sl, res.data()));
+                memcpy(out_accs + k0 * (sizeof(Acc) / 4), res.data(), Kb * sizeof(Acc));
+            }
             ctx->plan = {16, Ws, 2, 5, 1};
             return VC_OK;
         }

@@ -1224,10 +1224,25 @@ __global__ void __launch_bounds__(256) k_mp_chunk(const Fr* __restrict__ f, cons
     const uint32_t c = blockIdx.x / kblk;  // 1-D grid: chunks can outnumber gridDim.y's 65535
     const size_t k = (size_t)(blockIdx.x % kblk) * blockDim.x + threadIdx.x;
     if (k >= N) return;
+    // the chunk's query indices first (uniform over the block), then every query's evaluation
+    // load issued before the first multiply: up to MP_CHUNK / 2 independent 32-B loads in flight
+    // per lane instead of one load -> multiply chain per query
+    const uint32_t u0 = be[2 * c], cnt = be[2 * c + 1] - u0;
+    uint32_t idx[MP_CHUNK];
+#pragma unroll
+    for (uint32_t j = 0; j < MP_CHUNK; j++) idx[j] = j < cnt ? order[u0 + j] : 0u;
     Fr acc = fe_zero<F>();
-    for (uint32_t u = be[2 * c]; u < be[2 * c + 1]; u++) {
-        const uint32_t i = order[u];
-        acc = fe_add<F>(acc, fe_mul<F>(rp[i], f[(size_t)i * N + k]));
+    constexpr uint32_t B = MP_CHUNK / 2;
+#pragma unroll
+    for (uint32_t h = 0; h < MP_CHUNK; h += B) {
+        if (h >= cnt) break;
+        Fr v[B];
+#pragma unroll
+        for (uint32_t j = 0; j < B; j++)
+            if (h + j < cnt) v[j] = f[(size_t)idx[h + j] * N + k];
+#pragma unroll
+        for (uint32_t j = 0; j < B; j++)
+            if (h + j < cnt) acc = fe_add<F>(acc, fe_mul<F>(rp[idx[h + j]], v[j]));
     }
     partial[(size_t)c * N + k] = acc;
 }
