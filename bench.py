@@ -280,14 +280,22 @@ def kzg_line(a, rank, world, local, dev, stream):
                 fused()
                 ts.append((time.perf_counter() - t0) * 1e3)
             com_s, prf_s = step(point)
-            same = (vkzg.arrays_to_points("bls12_381", bufs[0][None, :], bufs[1])[0] ==
-                    vkzg.arrays_to_points("bls12_381", np.asarray(com_s[0])[None, :], np.array([com_s[1]], np.uint8))[0])
-            # the C4 number on one GPU is the one-call commit + open (vc_kzg_commit_prove_device);
-            # the two separate calls (commit MSM, then open) stay beside it
+            pts = lambda xy, inf: vkzg.arrays_to_points("bls12_381", np.asarray(xy)[None, :],  # noqa: E731
+                                                        np.array([inf], np.uint8))[0]
+            same_c = pts(bufs[0], bufs[1][0]) == pts(com_s[0], com_s[1])
+            same_p = pts(bufs[2], bufs[3][0]) == pts(prf_s[0], prf_s[1])
+            same_y = bool(np.array_equal(bufs[4], np.asarray(prf_s[2], dtype=np.uint64)))
             res[name]["separate_calls_ms"] = res[name]["ms_per_commit_open"]
-            res[name]["ms_per_commit_open"] = float(np.median(ts))
             res[name]["fused_ms_all"] = [round(t, 3) for t in ts]
-            res[name]["fused_same_commitment"] = bool(same)
+            res[name]["fused_same_commitment"] = bool(same_c)
+            res[name]["fused_same_proof_and_y"] = bool(same_p and same_y)
+            # the C4 number on one GPU is the one-call commit + open (vc_kzg_commit_prove_device)
+            # when its commitment, proof and y all equal the two separate calls' (commit MSM, then
+            # open); otherwise the separate-call number stays and the mismatch is flagged
+            if same_c and same_p and same_y:
+                res[name]["ms_per_commit_open"] = float(np.median(ts))
+            else:
+                res[name]["fused_mismatch"] = True
     keng.close()
     fused_bytes = d * (96 + 32) + 2 * 96  # SURVEY 8(d) C4 fused minimum
     return {"workload": f"KZG commit + open, d = 2^{a.kzg_log_d}, BLS12-381 (configs[3]), MSMs window-split "

@@ -64,9 +64,14 @@ int vc_ctx_curve(const vc_ctx* ctx);
 int vc_ctx_set_stream(vc_ctx* ctx, void* hip_stream);
 /* Engine knobs (per context; defaults in brackets). None changes a result, only the path:
  *   VC_OPT_MSM_SHARED_WINDOWS [1]: a GLV MSM (BLS12-381, n >= 4096) over a WHOLE table sends all
- *     windows to one bucket set through per-table shifted copies 2^(c w) P_i, 2^(c w) phi(P_i)
- *     (W x 2n points, 1.6 GB at n = 2^20, built once per table on first use and kept -- a
- *     fixed-base precomputation over the CRS). 0: plain variable-base Pippenger, no copies.
+ *     windows to one bucket set through per-table window copies B^w P_i, B^w phi(P_i), each as
+ *     x, y and -y in radix-2^29 limbs (168 B): one GPU, n >= 2^18: mixed radix B = 5 x 2^16, 7
+ *     windows, 7 x 2n copies = 2.47 GB at n = 2^20; window slices of a multi-GPU MSM
+ *     (vc_msm_device_window_part) use B = 2^16, 8 windows (2.82 GB). Built once per table on
+ *     first use and kept (a fixed-base precomputation over the CRS). A table holds ONE copy
+ *     layout: alternating whole-table MSMs and window-part MSMs on the same table rebuilds the
+ *     copies (~0.1 s at 2^20) on every switch, so keep one table on one path.
+ *     0: plain variable-base Pippenger, no copies.
  *   VC_OPT_MSM_CHUNK_POINTS [2^27]: MSMs of more points run as summed chunks of this many
  *     (keeps the u32 entry space of the bucket sort from wrapping). */
 #define VC_OPT_MSM_SHARED_WINDOWS 1

@@ -1130,8 +1130,10 @@ struct MpPrep {
 // multiproof.rs:106-112: per query "C" || compress(C) || "z" || z (u64 LE) || "y" || y -- 75
 // bytes at offset 75 i, so the records are written straight into the transcript on up to 16
 // host threads (the point compression is the costly part); the SHA-256 over them stays serial.
+// pool_ok = false: fill serially on the calling thread (mp_prove_many's transcript workers already
+// run one proof each; nesting the shared host pool there serialised them on its one-loop lock)
 static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
-                                    const uint64_t* y) {
+                                    const uint64_t* y, bool pool_ok = true) {
     constexpr size_t REC = 75;
     vc_transcript* tr = vc_transcript_new("multiproof");
     vc_transcript_reserve(tr, Q * REC + 64);
@@ -1148,7 +1150,7 @@ static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint
             memcpy(o + 43, y + 4 * i, 32);
         }
     };
-    if (Q < 8192 || host_pool().size() == 1) {
+    if (!pool_ok || Q < 8192 || host_pool().size() == 1) {
         fill(0, Q);
     } else {
         const unsigned T = host_pool().size();
@@ -1173,11 +1175,11 @@ static std::vector<Fr> invert_domain_at(const Fr& t, size_t N) {  // utils.rs:57
 // Grouping queries by z and summing per group first is the same field arithmetic as the
 // reference's per-group LagrangeBasis sums; rows of z with no query are zero and add nothing.
 static int mp_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
-                    const uint64_t* y, vc_transcript** tr_out, Fr* r_out) {
+                    const uint64_t* y, vc_transcript** tr_out, Fr* r_out, bool pool_ok = true) {
     if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
-    vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y);
+    vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y, pool_ok);
     *r_out = transcript_digest(tr, "r");
     *tr_out = tr;
     return VC_OK;
@@ -1433,13 +1435,17 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<size_t> next{0};
+    std::atomic<bool> cancel{false};  // set once phase 2 fails: the workers start no further transcript
+    // one proof per worker at a time, each filled serially (no nested host pool): T workers share
+    // the host's CPUs instead of queueing on the pool's one-loop lock
     const unsigned T = (unsigned)std::min<size_t>(P, std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)));
     std::vector<std::thread> workers;
     for (unsigned k = 0; k < T; k++)
         workers.emplace_back([&] {
-            for (size_t p; (p = next.fetch_add(1)) < P;) {
+            for (size_t p; !cancel.load(std::memory_order_relaxed) && (p = next.fetch_add(1)) < P;) {
                 Begun b;
-                b.st = mp_begin(N, Q, com_xy + p * Q * 8, com_inf + p * Q, z + p * Q, y + p * Q * 4, &b.tr, &b.r);
+                b.st = mp_begin(N, Q, com_xy + p * Q * 8, com_inf + p * Q, z + p * Q, y + p * Q * 4, &b.tr, &b.r,
+                                false);
                 if (b.st == VC_OK) b.st = mp_points(N, Q, z + p * Q, &b.zval);
                 std::lock_guard<std::mutex> lk(mu);
                 B[p] = std::move(b);
@@ -1467,6 +1473,7 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
         if (st == VC_OK)
             st = mp_accumulate(ctx, N, Q, d_data + p * Q * N * 32, z + p * Q, B[p].r, 0, B[p].zval, S[p]->p);
     }
+    if (st != VC_OK) cancel.store(true);
     for (auto& w : workers) w.join();
     workers.clear();
     if (st != VC_OK) {
