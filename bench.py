@@ -40,7 +40,7 @@ OUT_BYTES = {"bls12_381": 96, "bn254": 64, "bandersnatch": 64}
 CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD"}  # kernel-name match
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
-# (tools_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
+# (scripts/bench_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
 PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r03", "r02", "r01"))
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_summary.json"))
 

@@ -59,10 +59,16 @@ int vc_comm_is_rccl(const vc_comm* comm);
 int vc_comm_allgather(vc_comm* comm, vc_ctx* ctx, const void* send, size_t bytes, void* recv);
 
 /* ------------------------------------------------------------------ sharded workloads
- * One MSM (utils::inner_product, utils.rs:16-19) over all ranks: rank k computes Pippenger
- * windows [kW/G, (k+1)W/G) of all n terms (vc_msm_device_window_part); one all-gather of the
- * <= 192-byte projective partials; every rank adds them. d_scalars: all n scalars on this
- * rank's device. */
+ * One MSM (utils::inner_product, utils.rs:16-19) over all ranks: by default rank k computes
+ * Pippenger windows [kW/G, (k+1)W/G) of all n terms (vc_msm_device_window_part); with
+ * vc_comm_set_msm_split(comm, VC_COMM_SPLIT_POINTS) rank k computes the MSM of its point range
+ * shard_range(n, k, G) (vc_msm_device_partial, on the table's radix window copies). One
+ * all-gather of the <= 192-byte projective partials; every rank adds them. d_scalars: all n
+ * scalars on this rank's device (the point split reads only its range). The split must be the
+ * same on every rank. */
+#define VC_COMM_SPLIT_WINDOWS 1
+#define VC_COMM_SPLIT_POINTS 2
+int vc_comm_set_msm_split(vc_comm* comm, int split);
 int vc_msm_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t offset, const void* d_scalars, size_t n,
                    int mont, uint64_t* out_xy, uint8_t* out_inf);
 /* Batched width-w commits (IPA::commit ipa/mod.rs:130-135, node.rs:243-271) over all ranks:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 recipe used for profiles/ (kernel trace + stats, then HBM PMC passes, then summary).
-# usage: bash tools_profile.sh <tag> [bench args...]
+# usage: bash scripts/bench_profile.sh <tag> [bench args...]
 set -e
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-end rehearsal on one MI355X: every -m gpu test, smoke(), the default bench line (with the
-# CPU baselines), then the rocprofv3 kernel-trace + PMC passes of tools_profile.sh.
+# CPU baselines), then the rocprofv3 kernel-trace + PMC passes of scripts/bench_profile.sh.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-final}
@@ -13,4 +13,4 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 echo smoke-done
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
 echo bench-done
-[ "${2:-}" = "noprof" ] || bash $R/tools_profile.sh $TAG
+[ "${2:-}" = "noprof" ] || bash $R/scripts/bench_profile.sh $TAG

@@ -68,15 +68,18 @@ def test_msm_sharded(curve, n):
     finally:
         eng.close()
 
-    def body(k, comm, e):
+    def body(k, comm, e, split):
         tab = e.random_bases(n, seed=21)
         d = torch.from_numpy(sc.view(np.int64).copy()).cuda()
         torch.cuda.synchronize()
+        comm.set_msm_split(split)
         return comm.msm(e, tab, d.data_ptr(), n)
 
-    for G in (2, 3):
-        for xy, inf in run_ranks(G, curve, body):
-            assert inf == want[1] and np.array_equal(xy, want[0])
+    from vkzg.comm import Comm
+    for split in (Comm.SPLIT_WINDOWS, Comm.SPLIT_POINTS):
+        for G in (2, 3):
+            for xy, inf in run_ranks(G, curve, lambda k, c, e: body(k, c, e, split)):
+                assert inf == want[1] and np.array_equal(xy, want[0]), (split, G)
 
 
 def test_msm_batch_sharded():

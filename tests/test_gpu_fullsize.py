@@ -51,8 +51,9 @@ def _check_synthetic_bases(e, curve, tid, seed, n, samples=64):
 
 @pytest.mark.parametrize("path", ["shared_windows", "variable_base", "chunked"])
 def test_msm_2e20_bls12_381(bls, path):
-    """configs[1] at full size: the bench's inputs (seeds 2024 / 1234) and geometry (GLV, c = 16,
-    8 windows; shared windows = one 2^15-bucket set, narrow sort entries, 1024-thread fine sort)."""
+    """configs[1] at full size: the bench's inputs (seeds 2024 / 1234) and geometry (GLV; shared
+    windows = mixed radix B = 5 x 2^16, 7 windows into one set of 5 x 2^15 buckets, narrow sort
+    entries, staged coarse / fine sort; variable base = 8 per-window sets of 2^15 buckets)."""
     import torch
     import vkzg
     from pyoracle.curves import BLS12_381 as C
@@ -188,8 +189,9 @@ def test_msm_chunk_option_small(oracle_c):
 
 
 def test_commit_10k_width256_c20(oracle_c):
-    """configs[2]: 10,000 width-256 Bandersnatch commits on the bench's c = 20 table (167 GB;
-    c = 16 if it does not fit next to the rest), 16 sampled commits against the oracle."""
+    """configs[2]: 10,000 width-256 Bandersnatch commits on the c = 20 table (13 windows, 188.4 GB:
+    256 x 13 x 2^19 x 108 B; c = 16 if it does not fit next to the rest), 16 sampled commits
+    against the oracle."""
     import torch
     import vkzg
     e = vkzg.Engine("bandersnatch")
@@ -327,6 +329,29 @@ def test_msm_device_many(curve, n):
             assert _pt(curve, *got[0]) == C.mul(C.g, vkzg.dot_mod(sets[0], s, C.r))
     finally:
         e.close()
+
+
+def test_msm_point_ranges_on_shared_windows(bls):
+    """point ranges [offset, offset + n) of the 2^20 table (one GPU's share of a point-split MSM)
+    on the radix shared-window copies of the whole table (entries at their table positions):
+    == (sum k_i s_{offset+i}) G by linearity; the plan reports the radix geometry; a whole-table
+    MSM between them reuses the same copies; identity-free ranges at odd offsets and lengths."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    n = 1 << 20
+    e = bls
+    tid = e.random_bases(n, seed=2024)
+    s = vkzg.random_base_scalars("bls12_381", 2024, n)
+    k = vkzg.random_scalars("bls12_381", n, np.random.default_rng(77))
+    d_k = torch.from_numpy(k.view(np.int64).copy()).cuda()
+    for off, m in ((0, 1 << 19), ((1 << 19) + 3, (1 << 18) + 5), (12345, n - 12345), (1 << 19, 1 << 19)):
+        got = e.msm_device(tid, d_k.data_ptr(), m, offset=off)
+        want = C.mul(C.g, vkzg.dot_mod(k[:m], s[off:off + m], C.r))
+        assert _pt("bls12_381", *got) == want, (off, m)
+        assert e.msm_last_plan()["radix_mul"] == 5, (off, m)
+        whole = e.msm_device(tid, d_k.data_ptr(), n)
+        assert _pt("bls12_381", *whole) == C.mul(C.g, vkzg.dot_mod(k, s, C.r))
 
 
 def test_msm_device_many_more_sets_than_one_pipeline():

@@ -74,6 +74,7 @@ struct Stage {
 
 struct vc_comm {
     int rank = 0, world = 1, device = -1;
+    int msm_split = VC_COMM_SPLIT_WINDOWS;  // vc_comm_set_msm_split
     ncclComm_t nccl = nullptr;
     vc_allgather_fn fn = nullptr;
     void* user = nullptr;
@@ -253,9 +254,22 @@ int vc_comm_allgather(vc_comm* c, vc_ctx* ctx, const void* send, size_t bytes, v
 
 
 
+int vc_comm_set_msm_split(vc_comm* c, int split) {
+    if (!c || (split != VC_COMM_SPLIT_WINDOWS && split != VC_COMM_SPLIT_POINTS)) return VC_E_INVALID;
+    c->msm_split = split;
+    return VC_OK;
+}
+
 int vc_msm_sharded(vc_ctx* ctx, vc_comm* comm, int table_id, size_t offset, const void* d_scalars, size_t n, int mont,
                    uint64_t* out_xy, uint8_t* out_inf) {
     if (!valid(comm, ctx) || !out_xy || !out_inf) return VC_E_INVALID;
+    if (comm->msm_split == VC_COMM_SPLIT_POINTS)
+        return partial_step(ctx, comm, [&](uint32_t* part) {
+            size_t lo, hi;
+            vk::shard_range(n, comm->rank, comm->world, &lo, &hi);
+            const uint8_t* sc = static_cast<const uint8_t*>(d_scalars);
+            return vc_msm_device_partial(ctx, table_id, offset + lo, sc ? sc + lo * 32 : nullptr, hi - lo, mont, part);
+        }, out_xy, out_inf);
     return partial_step(ctx, comm, [&](uint32_t* part) {
         return vc_msm_device_window_part(ctx, table_id, offset, d_scalars, n, mont, comm->rank, comm->world, part);
     }, out_xy, out_inf);

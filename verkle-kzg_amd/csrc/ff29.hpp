@@ -349,5 +349,9 @@ template <>
 struct F29Of<BLS381Fr> {
     using type = F29BLS381Fr;
 };
+template <>
+struct F29Of<BN254Fr> {
+    using type = F29BN254Fr;
+};
 
 }  // namespace vk

@@ -97,11 +97,16 @@ __device__ __forceinline__ void for_each_digit4(uint32_t s0, uint32_t s1, uint32
 }
 
 // Digit sources of the sort: entry i of the MSM -> its signed digits (nothing for an identity base).
+// Every digit source maps its term i to the point index of the shared-window copies (Table::win,
+// [w][2N] for a table of N points): the identity for a whole-table MSM; a point range [off, off + n)
+// of the table (RadixDigits with half = n, gap = N - n) puts k1 term i < n at off + i and k2 term
+// n + j at N + off + j.
 template <class Fr>
 struct ScalarDigits {  // plain scalars, canonical or Montgomery
     const uint32_t* sc;
     const uint8_t* inf;
     int mont;
+    __device__ __forceinline__ uint32_t pt(uint32_t i) const { return i; }
     template <class Fn>
     __device__ __forceinline__ void operator()(uint32_t i, int c, int W, Fn&& f) const {
         if (inf != nullptr && inf[i]) return;
@@ -120,6 +125,7 @@ struct GlvDigits {
     const uint8_t* inf;
     uint32_t n;
     int tw = -1, ts = 0;
+    __device__ __forceinline__ uint32_t pt(uint32_t i) const { return i; }
     template <class Fn>
     __device__ __forceinline__ void operator()(uint32_t i, int c, int W, Fn&& f) const {
         if (inf != nullptr && inf[i < n ? i : i - n]) return;
@@ -138,6 +144,8 @@ struct RadixDigits {
     const int32_t* dig;
     uint32_t nv;
     int w0 = 0;  // first window read (a per-set coarse pass of several bucket sets starts at its set)
+    uint32_t off = 0, half = 0xffffffffu, gap = 0;  // point range of the table (see above)
+    __device__ __forceinline__ uint32_t pt(uint32_t i) const { return i + off + (i >= half ? gap : 0u); }
     template <class Fn>
     __device__ __forceinline__ void operator()(uint32_t i, int, int W, Fn&& f) const {
         for (int w = w0; w < W; w++) f(w, dig[(size_t)w * nv + i]);
@@ -230,7 +238,7 @@ __global__ void __launch_bounds__(1024) k_sort_coarse(Src src, uint32_t n, int c
             if (d != 0 && w >= wb) {
                 uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
                 uint32_t pos = atomicAdd(&cur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB)], 1u);
-                const uint32_t e = stride ? i + ((uint32_t)w % wps) * stride : i;
+                const uint32_t e = stride ? src.pt(i) + ((uint32_t)w % wps) * stride : i;
                 tmp[pos] = sort_pack<T>(b & fmask, e, d < 0, FB);
             }
         });
@@ -287,7 +295,8 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
                 const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
                 const uint32_t p = atomicAdd(
                     &lcur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB) - bin0], 1u);
-                stage[p] = sort_pack<uint32_t>(b & fmask, stride ? i + ((uint32_t)w % wps) * stride : i, d < 0, FB);
+                stage[p] = sort_pack<uint32_t>(b & fmask, stride ? src.pt(i) + ((uint32_t)w % wps) * stride : i, d < 0,
+                                               FB);
             }
         });
     }
@@ -997,7 +1006,7 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     }
     // fine-pass block: 1024 threads once bins average >= 2^15 entries (one block per bin)
     static const int fine_env = getenv("VKZG_SORT_FINE_BLOCK") ? atoi(getenv("VKZG_SORT_FINE_BLOCK")) : 0;  // probe
-    const uint64_t total = stride ? (uint64_t)(we - wb) * stride : (uint64_t)nv * (uint32_t)(we - wb);
+    const uint64_t total = (uint64_t)nv * (uint32_t)(we - wb);
     int fblk = fine_env == 256 || fine_env == 1024 ? fine_env : (total / bins >= (1u << 15) ? 1024 : 256);
     // LDS staging of the fine scatter (16K entries, 64 KB: two blocks per CU, 1024 threads) when the
     // mean bin leaves it ~40 % headroom (radix 2^20: 11.5K); a bin beyond it scatters directly
@@ -1084,6 +1093,7 @@ struct MsmSlice {
     uint32_t m = 1;       // > 1: radix m 2^c digits (RadixDigits), m 2^(c-1) buckets
     int sets = 1;         // shared windows: bucket sets = MSMs over the table in this slice
     uint32_t wps = 0;     // shared windows: windows per set (the window copies' count)
+    uint32_t stride = 0;  // shared windows: points per window copy (2N for a table of N); 0 = the terms
     int Wr = 0;           // bucket sets reduced: `sets` shared, W otherwise
     uint32_t NB = 0, NBtot = 0, Tmax = 0, M = 0, Lseg = 0, S = 0, J = 0, guard = 0;
     uint32_t nU = 1;  // sums per set after the J bit sums: A (1), or the Lseg residue sums U_r
@@ -1279,7 +1289,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
             }
         }
     }
-    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (uint32_t)nv : 0u,
+    VK_TRY(sort_entries(ctx, L, src, (uint32_t)nv, c, sl.wb, sl.we, FB, NBC, nblk, chunk, sl.shared ? (sl.stride ? sl.stride : (uint32_t)nv) : 0u,
                         sl.wps, ncnt,
                         ws[WS_COUNTS].as<uint32_t>(),
                         ws[WS_CURSOR].as<uint32_t>(), ws[WS_DIGITS].p, sl.offsets,
@@ -1453,7 +1463,12 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         // reduce. Window-sliced (multi-GPU) parts keep c = 16: a one-window slice would reduce
         // the whole bucket set for 1/7 of the adds. VKZG_MSM_RADIX=1: power-of-two windows (probe).
         static const int radix_env = getenv("VKZG_MSM_RADIX") ? atoi(getenv("VKZG_MSM_RADIX")) : 5;
-        if (glv && shared_env && offset == 0 && n == t->n && parts == 1 && nv >= (1u << 19) && radix_env == 5 &&
+        // a point range [offset, offset + n) of >= 2^18 points (one GPU's share of a point-split
+        // MSM, vc_msm_device_partial) reads the same whole-table copies, its entries at their table
+        // positions (RadixDigits::pt): one copy layout serves whole-table and point-range MSMs
+        static const int range_env = getenv("VKZG_MSM_RANGE") ? atoi(getenv("VKZG_MSM_RANGE")) : 1;  // A/B
+        const bool whole = offset == 0 && n == t->n;
+        if (glv && shared_env && (whole || range_env) && parts == 1 && nv >= (1u << 19) && radix_env == 5 &&
             !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED")) {
             const size_t win_bytes = (size_t)7 * 2 * t->n * sizeof(typename Fast29<C>::type::AffN);
             if (win_bytes <= (8ull << 30)) {
@@ -1553,10 +1568,16 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                 src.ts = top_shift;
             }
             for (int k = 0; k < nsl; k++) {
-                if (radix_m > 1)
-                    VK_TRY(slice_enqueue<C>(ctx, sl[k], RadixDigits{ctx->ws[WS_GLV_SC].as<int32_t>(), (uint32_t)nv}, nv,
-                                            win, win, 0xffffffffu, k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
-                else if (shared && !t->win_limbs)
+                if (radix_m > 1) {
+                    RadixDigits rd{ctx->ws[WS_GLV_SC].as<int32_t>(), (uint32_t)nv};
+                    rd.off = (uint32_t)offset;  // the point range inside the table's copies
+                    rd.half = (uint32_t)n;
+                    rd.gap = (uint32_t)(t->n - n);
+                    sl[k].stride = (uint32_t)(2 * t->n);
+                    VK_TRY(slice_enqueue<C>(ctx, sl[k], rd, nv, win, win, 0xffffffffu, k == 1 ? acc0 : nullptr,
+                                            k == 0 ? acc0 : nullptr));
+                }
+                else if (shared && !t->win_limbs)  // (power-of-two shared windows: whole tables only)
                     VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, t->win.as<Aff>(), t->win.as<Aff>(), 0xffffffffu,
                                             k == 1 ? acc0 : nullptr, k == 0 ? acc0 : nullptr));
                 else if (shared)

@@ -25,6 +25,7 @@
 
 #include "ctx.hpp"
 #include "ec.hpp"
+#include "ff29.hpp"
 #include "poly.hpp"
 #include "scheme_internal.hpp"
 #include "host/pool.hpp"
@@ -1202,8 +1203,11 @@ static int mp_points(size_t N, size_t Q, const uint64_t* z, std::vector<uint32_t
     return VC_OK;
 }
 
-// rp[i] = r^(first + i) (Montgomery)
-__global__ void k_mp_rpow(Fr r, size_t first, size_t n, Fr* __restrict__ rp) {
+// rp[i] = r^(first + i) as radix-2^29 Montgomery limbs (x R', R' = 2^261, ff29.hpp), canonical, at
+// a stride of MP_RP_WORDS words (the chunk kernel reads them as uniform scalar loads)
+using P29 = F29BN254Fr;
+constexpr uint32_t MP_RP_WORDS = 16;
+__global__ void k_mp_rpow(Fr r, size_t first, size_t n, uint32_t* __restrict__ rp) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Fr acc = fe_one<F>(), b = r;
@@ -1213,40 +1217,79 @@ __global__ void k_mp_rpow(Fr r, size_t first, size_t n, Fr* __restrict__ rp) {
         e >>= 1;
         if (e) b = fe_sqr<F>(b);
     }
-    rp[i] = acc;
+    const f29<P29> v = canon29<P29>(from_mont32<P29, F>(acc));
+#pragma unroll
+    for (int j = 0; j < P29::L; j++) rp[i * MP_RP_WORDS + j] = v.v[j];
 }
 
 // one block per (k block, chunk c of <= MP_CHUNK queries of one z): partial[c][k] =
-// sum over sorted positions [be[2c], be[2c+1]) of r^i f_i[k] (f canonical, r^i Montgomery ->
-// canonical products)
+// sum over sorted positions [be[2c], be[2c+1]) of r^i f_i[k] (f canonical; partial canonical).
+// HBM-bound stream of the Q x N evaluations (the r^i are uniform over a block). Radix-2^29 with
+// lazy reduction: the products f_i[k] (r^i R') of MP_LAZY queries add into 17 64-bit columns (9 x
+// 9 products of < 2^58 per query: 27 x 2^58 < 2^62.8) and ONE Montgomery reduction (9 rows)
+// serves them -- ~120 instructions per element instead of a full 32-bit-limb multiply (~270)
+// and an add; the block results (< 1.03 p each) are added with one conditional subtraction.
 constexpr uint32_t MP_CHUNK = 16;
-__global__ void __launch_bounds__(256) k_mp_chunk(const Fr* __restrict__ f, const Fr* __restrict__ rp,
+constexpr uint32_t MP_LAZY = 3;
+__global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f, const uint32_t* __restrict__ rp,
                                                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ be,
                                                  size_t N, uint32_t kblk, Fr* __restrict__ partial) {
+    constexpr int L = P29::L;
     const uint32_t c = blockIdx.x / kblk;  // 1-D grid: chunks can outnumber gridDim.y's 65535
     const size_t k = (size_t)(blockIdx.x % kblk) * blockDim.x + threadIdx.x;
     if (k >= N) return;
-    // the chunk's query indices first (uniform over the block), then every query's evaluation
-    // load issued before the first multiply: up to MP_CHUNK / 2 independent 32-B loads in flight
-    // per lane instead of one load -> multiply chain per query
     const uint32_t u0 = be[2 * c], cnt = be[2 * c + 1] - u0;
-    uint32_t idx[MP_CHUNK];
+    f29<P29> total = zero29<P29>();
 #pragma unroll
-    for (uint32_t j = 0; j < MP_CHUNK; j++) idx[j] = j < cnt ? order[u0 + j] : 0u;
-    Fr acc = fe_zero<F>();
-    constexpr uint32_t B = MP_CHUNK / 2;
-#pragma unroll
-    for (uint32_t h = 0; h < MP_CHUNK; h += B) {
+    for (uint32_t h = 0; h < MP_CHUNK; h += MP_LAZY) {
         if (h >= cnt) break;
-        Fr v[B];
+        // the block's evaluations first: MP_LAZY independent 32-B loads in flight per lane
+        uint4 v[MP_LAZY][2];
+        uint32_t qi[MP_LAZY];
 #pragma unroll
-        for (uint32_t j = 0; j < B; j++)
-            if (h + j < cnt) v[j] = f[(size_t)idx[h + j] * N + k];
+        for (uint32_t j = 0; j < MP_LAZY; j++) {
+            qi[j] = h + j < cnt ? order[u0 + h + j] : 0u;
+            if (h + j < cnt) {
+                const uint4* src = reinterpret_cast<const uint4*>(f + ((size_t)qi[j] * N + k) * 8);
+                v[j][0] = src[0];
+                v[j][1] = src[1];
+            }
+        }
+        uint64_t t[2 * L];  // 2L - 1 product columns and the reduction's top carry
 #pragma unroll
-        for (uint32_t j = 0; j < B; j++)
-            if (h + j < cnt) acc = fe_add<F>(acc, fe_mul<F>(rp[idx[h + j]], v[j]));
+        for (int x = 0; x < 2 * L; x++) t[x] = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < MP_LAZY; j++) {
+            if (h + j >= cnt) break;
+            const uint32_t w[8] = {v[j][0].x, v[j][0].y, v[j][0].z, v[j][0].w, v[j][1].x, v[j][1].y, v[j][1].z, v[j][1].w};
+            const f29<P29> a = unpack29<P29>(w);
+            const uint32_t* b = rp + (size_t)qi[j] * MP_RP_WORDS;
+#pragma unroll
+            for (int y = 0; y < L; y++) {
+                const uint32_t by = b[y];
+#pragma unroll
+                for (int x = 0; x < L; x++) t[x + y] += (uint64_t)a.v[x] * by;
+            }
+        }
+        // Montgomery reduction of the columns (separated operand scanning): t / R' mod p
+#pragma unroll
+        for (int i = 0; i < L; i++) {
+            const uint32_t m = ((uint32_t)t[i] * P29::inv) & M29;
+#pragma unroll
+            for (int j = 0; j < L; j++) t[i + j] += (uint64_t)m * P29::p(j);
+            t[i + 1] += t[i] >> 29;
+        }
+        f29<P29> r;  // columns L .. 2L - 1 are the reduced value (as sqr29)
+#pragma unroll
+        for (int j = L; j < 2 * L - 1; j++) {
+            t[j + 1] += t[j] >> 29;
+            r.v[j - L] = (uint32_t)t[j] & M29;
+        }
+        r.v[L - 1] = (uint32_t)t[2 * L - 1];
+        total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
     }
-    partial[(size_t)c * N + k] = acc;
+    total = csub29<P29>(carry29<P29>(total));
+    pack29<P29>(total, partial[(size_t)c * N + k].v);
 }
 
 // S[row][k] = sum of the partials of the row's chunks [zc[row], zc[row+1])
@@ -1298,18 +1341,18 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     const uint32_t nch = (uint32_t)(be.size() / 2);
     zc[Z] = nch;
     DevBuf d_rp(ctx), d_order(ctx), d_be(ctx), d_zc(ctx), d_part(ctx);
-    VK_TRY(d_rp.ensure(Qs * 32));
+    VK_TRY(d_rp.ensure(Qs * MP_RP_WORDS * 4));
     VK_TRY(d_order.ensure(Qs * 4));
     VK_TRY(d_be.ensure(be.size() * 4));
     VK_TRY(d_zc.ensure((Z + 1) * 4));
     VK_TRY(d_part.ensure(std::max<size_t>(nch, 1) * N * 32));
-    VK_LAUNCH(ctx, "mp_rpow", k_mp_rpow, (Qs + 255) / 256, 256, 0, r, first, Qs, d_rp.as<Fr>());
+    VK_LAUNCH(ctx, "mp_rpow", k_mp_rpow, (Qs + 255) / 256, 256, 0, r, first, Qs, d_rp.as<uint32_t>());
     VK_CHECK_HIP(hipMemcpyAsync(d_order.p, order.data(), Qs * 4, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_be.p, be.data(), be.size() * 4, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
     const uint32_t kblk = (uint32_t)((N + 255) / 256);
-    VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk, (size_t)nch * kblk, 256, 0, reinterpret_cast<const Fr*>(d_data),
-              d_rp.as<Fr>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
+    VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
+              d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
     VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,
               kblk, reinterpret_cast<Fr*>(d_S));
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host vectors above die on return

@@ -1,4 +1,4 @@
-"""Summarise a tools_profile.sh run: kernel durations (trace pass) + HBM bytes per launch
+"""Summarise a scripts/bench_profile.sh run: kernel durations (trace pass) + HBM bytes per launch
 from the FETCH_SIZE / WRITE_SIZE PMC passes (+ SQ_INSTS_VALU, wave-level VALU instructions), with the gfx950 correction of
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts 64 B per 128-B read request, so it is
 doubled; WRITE_SIZE is taken as is.  usage: prof_summary.py <prof dir> <out json>"""

@@ -114,6 +114,7 @@ SIGNATURES = {
     "vc_multiproof_prove_many_sharded": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, c_size_t,
                                                  c_void_p, P, P, P, P, P, P, P, P, P, P]),
     "vc_multiproof_gather": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, P, P, P, P]),
+    "vc_comm_set_msm_split": (c_int, [c_void_p, c_int]),
     # vc_group.h
     "vc_group_create": (c_int, [c_int, c_int, P, ctypes.POINTER(c_void_p)]),
     "vc_group_destroy": (None, [c_void_p]),

@@ -105,8 +105,15 @@ class Comm:
         return out[:len(send) * self.world].tobytes()
 
     # ---------------------------------------------------------------- sharded workloads
+    SPLIT_WINDOWS, SPLIT_POINTS = 1, 2
+
+    def set_msm_split(self, split):
+        """how vc_msm_sharded splits one MSM: SPLIT_WINDOWS (default) or SPLIT_POINTS (same on every rank)"""
+        check(lib().vc_comm_set_msm_split(self.h, split), "vc_comm_set_msm_split")
+
     def msm(self, engine, table, d_scalars_ptr, n, offset=0, mont=False):
-        """whole MSM of n device-resident scalars; rank k computes its window slice."""
+        """whole MSM of n device-resident scalars; rank k computes its window slice (or, after
+        set_msm_split(SPLIT_POINTS), the MSM of its point range)."""
         from .engine import NL
         xy = np.zeros(2 * NL[engine.curve], dtype=np.uint64)
         inf = np.zeros(1, dtype=np.uint8)
