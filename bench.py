@@ -85,7 +85,21 @@ def parse():
                          "not scaling numbers")
     ap.add_argument("--comm", choices=["capi", "torch"], default="capi",
                     help="N > 1 exchange: vc_comm (C ABI, RCCL) or torch.distributed all-gather")
+    ap.add_argument("--msm-split", choices=["auto", "windows", "points"], default="auto",
+                    help="N > 1: how one MSM splits over the ranks (auto: by N, from the one-card split probe)")
     return ap.parse_args()
+
+
+# N > 1 split of the headline MSM, chosen per N from the one-card per-rank probe
+# (verkle-kzg_amd/tools/split_probe.py: the slowest rank's share of a 2^20 MSM, point range vs
+# window part; profiles/r04/split_probe.txt)
+AUTO_SPLIT = {2: "points", 3: "points", 4: "points"}
+
+
+def msm_split(a, world):
+    if a.msm_split != "auto":
+        return a.msm_split
+    return AUTO_SPLIT.get(world, "windows")
 
 
 def kernel_table(eng):
@@ -933,15 +947,19 @@ def main():
         if int(ok.item()) == 0 and comm is not None:  # every rank must take the same path
             comm.close()
             comm, comm_kind = None, "torch (vc_comm init failed on a peer)"
+    split = msm_split(a, world)
+    if comm is not None:
+        comm.set_msm_split(comm.SPLIT_POINTS if split == "points" else comm.SPLIT_WINDOWS)
+    plo, _phi = vdist.shard_range(n, rank, world)
 
     def step():
         if world == 1:  # one call: vc_msm_device (sort .. reduction, host fold, affine result)
             return eng.msm_device(table, d_sc.data_ptr(), n)
-        if comm is not None:  # window slice (HIP) -> vc_comm RCCL all-gather -> host sum, all in C
+        if comm is not None:  # window slice or point range (HIP) -> vc_comm RCCL all-gather -> host sum, all in C
             return comm.msm(eng, table, d_sc.data_ptr(), n)
-        # window-slice partial (HIP) -> torch RCCL all-gather of projective partials -> host sum
-        return vdist.msm_sharded(eng, table, d_sc.data_ptr(), n, rank, world, dev if world > 1 else None,
-                                 split="windows")
+        # partial (HIP) -> torch RCCL all-gather of projective partials -> host sum
+        return vdist.msm_sharded(eng, table, d_sc.data_ptr() + (plo * 32 if split == "points" else 0), n, rank, world,
+                                 dev if world > 1 else None, split=split)
 
     for _ in range(a.warmup):
         res = step()
@@ -1050,7 +1068,7 @@ def main():
     # plain 32-bit adds in half: tools/issueprobe.hip), i.e. lanes x SIMDs x clock / 4
     c_bits, w_total, terms = plan["window_bits"], plan["windows"], plan["terms_per_point"]
     w_rank = (rank + 1) * w_total // world - rank * w_total // world
-    madds = terms * n * w_rank
+    madds = terms * n * w_rank if (world == 1 or split == "windows") else terms * (_phi - plo) * w_total
     mad_peak = eng.device_mad_rate()
     pmc = json.load(open(PMC_SUMMARY)) if os.path.exists(PMC_SUMMARY) else None
     # the committed counters count only if they were taken on this geometry (same n, windows, radix)
@@ -1095,7 +1113,10 @@ def main():
         "dtype": "u32",
         "data": "synthetic (random subgroup bases s_i*G generated on device, uniform scalars < r)",
         "config": {"workload": f"single 2^{a.log_n}-point {curve} G1 Pippenger MSM (configs[1])",
-                   "n_points": n, "curve": curve, "parallelism": f"Pippenger-window slices x{world}",
+                   "n_points": n, "curve": curve,
+                   "parallelism": (f"Pippenger-window slices x{world}" if split == "windows" else
+                                   f"point ranges x{world}") if world > 1 else "one GPU",
+                   "msm_split": split if world > 1 else None,
                    "exchange": comm_kind,
                    "window_bits": c_bits, "windows": w_total, "radix": plan["radix_mul"] << c_bits,
                    "radix_form": f"{plan['radix_mul']} * 2^{c_bits}", "terms_per_point": terms,

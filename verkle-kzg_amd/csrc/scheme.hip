@@ -1231,62 +1231,91 @@ __global__ void k_mp_rpow(Fr r, size_t first, size_t n, uint32_t* __restrict__ r
 // and an add; the block results (< 1.03 p each) are added with one conditional subtraction.
 constexpr uint32_t MP_CHUNK = 16;
 constexpr uint32_t MP_LAZY = 3;
+// one block of <= MP_LAZY queries: products into the columns, one Montgomery reduction -> r < 1.03 p
+__device__ __forceinline__ f29<P29> mp_block(const uint4 (&v)[MP_LAZY][2], const uint32_t (&qi)[MP_LAZY], uint32_t nq,
+                                             const uint32_t* __restrict__ rp) {
+    constexpr int L = P29::L;
+    uint64_t t[2 * L];  // 2L - 1 product columns and the reduction's top carry
+#pragma unroll
+    for (int x = 0; x < 2 * L; x++) t[x] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < MP_LAZY; j++) {
+        if (j >= nq) break;
+        const uint32_t w[8] = {v[j][0].x, v[j][0].y, v[j][0].z, v[j][0].w, v[j][1].x, v[j][1].y, v[j][1].z, v[j][1].w};
+        const f29<P29> a = unpack29<P29>(w);
+        const uint32_t* b = rp + (size_t)qi[j] * MP_RP_WORDS;
+#pragma unroll
+        for (int y = 0; y < L; y++) {
+            const uint32_t by = b[y];
+#pragma unroll
+            for (int x = 0; x < L; x++) t[x + y] += (uint64_t)a.v[x] * by;
+        }
+    }
+    // Montgomery reduction of the columns (separated operand scanning): t / R' mod p
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+        const uint32_t m = ((uint32_t)t[i] * P29::inv) & M29;
+#pragma unroll
+        for (int j = 0; j < L; j++) t[i + j] += (uint64_t)m * P29::p(j);
+        t[i + 1] += t[i] >> 29;
+    }
+    f29<P29> r;  // columns L .. 2L - 1 are the reduced value (as sqr29)
+#pragma unroll
+    for (int j = L; j < 2 * L - 1; j++) {
+        t[j + 1] += t[j] >> 29;
+        r.v[j - L] = (uint32_t)t[j] & M29;
+    }
+    r.v[L - 1] = (uint32_t)t[2 * L - 1];
+    return r;
+}
+
+__device__ __forceinline__ void mp_load(const uint32_t* __restrict__ f, const uint32_t* __restrict__ order, uint32_t u,
+                                        uint32_t nq, size_t N, size_t k, uint4 (&v)[MP_LAZY][2],
+                                        uint32_t (&qi)[MP_LAZY]) {
+#pragma unroll
+    for (uint32_t j = 0; j < MP_LAZY; j++) {
+        qi[j] = j < nq ? order[u + j] : 0u;
+        if (j < nq) {
+            const uint4* src = reinterpret_cast<const uint4*>(f + ((size_t)qi[j] * N + k) * 8);
+            v[j][0] = src[0];
+            v[j][1] = src[1];
+        }
+    }
+}
+
+// PF = 1: the next block's loads are issued before the current block's arithmetic (two blocks of
+// loads in flight per lane)
+template <int PF>
 __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f, const uint32_t* __restrict__ rp,
                                                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ be,
                                                  size_t N, uint32_t kblk, Fr* __restrict__ partial) {
-    constexpr int L = P29::L;
     const uint32_t c = blockIdx.x / kblk;  // 1-D grid: chunks can outnumber gridDim.y's 65535
     const size_t k = (size_t)(blockIdx.x % kblk) * blockDim.x + threadIdx.x;
     if (k >= N) return;
     const uint32_t u0 = be[2 * c], cnt = be[2 * c + 1] - u0;
     f29<P29> total = zero29<P29>();
+    uint4 v[MP_LAZY][2], w[MP_LAZY][2];
+    uint32_t qi[MP_LAZY], qw[MP_LAZY];
+    if (PF) mp_load(f, order, u0, min(cnt, MP_LAZY), N, k, v, qi);
 #pragma unroll
     for (uint32_t h = 0; h < MP_CHUNK; h += MP_LAZY) {
         if (h >= cnt) break;
-        // the block's evaluations first: MP_LAZY independent 32-B loads in flight per lane
-        uint4 v[MP_LAZY][2];
-        uint32_t qi[MP_LAZY];
-#pragma unroll
-        for (uint32_t j = 0; j < MP_LAZY; j++) {
-            qi[j] = h + j < cnt ? order[u0 + h + j] : 0u;
-            if (h + j < cnt) {
-                const uint4* src = reinterpret_cast<const uint4*>(f + ((size_t)qi[j] * N + k) * 8);
-                v[j][0] = src[0];
-                v[j][1] = src[1];
-            }
+        const uint32_t nq = min(cnt - h, MP_LAZY);
+        if (PF) {
+            if (h + MP_LAZY < cnt) mp_load(f, order, u0 + h + MP_LAZY, min(cnt - h - MP_LAZY, MP_LAZY), N, k, w, qw);
+        } else {
+            mp_load(f, order, u0 + h, nq, N, k, v, qi);
         }
-        uint64_t t[2 * L];  // 2L - 1 product columns and the reduction's top carry
-#pragma unroll
-        for (int x = 0; x < 2 * L; x++) t[x] = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < MP_LAZY; j++) {
-            if (h + j >= cnt) break;
-            const uint32_t w[8] = {v[j][0].x, v[j][0].y, v[j][0].z, v[j][0].w, v[j][1].x, v[j][1].y, v[j][1].z, v[j][1].w};
-            const f29<P29> a = unpack29<P29>(w);
-            const uint32_t* b = rp + (size_t)qi[j] * MP_RP_WORDS;
-#pragma unroll
-            for (int y = 0; y < L; y++) {
-                const uint32_t by = b[y];
-#pragma unroll
-                for (int x = 0; x < L; x++) t[x + y] += (uint64_t)a.v[x] * by;
-            }
-        }
-        // Montgomery reduction of the columns (separated operand scanning): t / R' mod p
-#pragma unroll
-        for (int i = 0; i < L; i++) {
-            const uint32_t m = ((uint32_t)t[i] * P29::inv) & M29;
-#pragma unroll
-            for (int j = 0; j < L; j++) t[i + j] += (uint64_t)m * P29::p(j);
-            t[i + 1] += t[i] >> 29;
-        }
-        f29<P29> r;  // columns L .. 2L - 1 are the reduced value (as sqr29)
-#pragma unroll
-        for (int j = L; j < 2 * L - 1; j++) {
-            t[j + 1] += t[j] >> 29;
-            r.v[j - L] = (uint32_t)t[j] & M29;
-        }
-        r.v[L - 1] = (uint32_t)t[2 * L - 1];
+        const f29<P29> r = mp_block(v, qi, nq, rp);
         total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
+        if (PF) {
+#pragma unroll
+            for (uint32_t j = 0; j < MP_LAZY; j++) {
+                v[j][0] = w[j][0];
+                v[j][1] = w[j][1];
+                qi[j] = qw[j];
+            }
+        }
     }
     total = csub29<P29>(carry29<P29>(total));
     pack29<P29>(total, partial[(size_t)c * N + k].v);
@@ -1351,8 +1380,13 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     VK_CHECK_HIP(hipMemcpyAsync(d_be.p, be.data(), be.size() * 4, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
     const uint32_t kblk = (uint32_t)((N + 255) / 256);
-    VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
-              d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
+    static const int pf_env = getenv("VKZG_MP_PREFETCH") ? atoi(getenv("VKZG_MP_PREFETCH")) : 0;  // A/B probe
+    if (pf_env)
+        VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk<1>, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
+                  d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
+    else
+        VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk<0>, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
+                  d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
     VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,
               kblk, reinterpret_cast<Fr*>(d_S));
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host vectors above die on return

@@ -28,7 +28,9 @@ e.msm_batch_device(ipa.table, N, d_all.data_ptr(), Q, cxy_d.data_ptr(), cinf_d.d
 torch.cuda.synchronize()
 cxy = cxy_d.cpu().numpy().view(np.uint64).copy()
 cinf = cinf_d.cpu().numpy().copy()
-for it in range(3):
+e.enable_timing(True)
+for it in range(5):
+    e.reset_timing()
     t0 = time.perf_counter()
     tr, r, rows = scheme.multiproof_begin(N, cxy, cinf, z, y)
     t1 = time.perf_counter()
@@ -38,8 +40,10 @@ for it in range(3):
     t2 = time.perf_counter()
     mp = scheme.multiproof_finish_ipa(ipa, z, S.data_ptr(), 1, tr)
     t3 = time.perf_counter()
-    print(f"begin {1e3 * (t1 - t0):.2f} ms  accumulate {1e3 * (t2 - t1):.2f} ms  finish {1e3 * (t3 - t2):.2f} ms",
-          flush=True)
+    ms, cnt = e.kernel_time("mp_chunk")
+    print(f"begin {1e3 * (t1 - t0):.2f} ms  accumulate {1e3 * (t2 - t1):.2f} ms  finish {1e3 * (t3 - t2):.2f} ms  "
+          f"mp_chunk {ms / max(cnt, 1):.4f} ms ({Q * N * 32 / (ms / max(cnt, 1) * 1e-3) / 1e12:.2f} TB/s)", flush=True)
+e.enable_timing(False)
 # IPA prove alone (single proof)
 d = scheme.LagrangeBasis([int(v) for v in range(N)])
 c = ipa.commit(d)
