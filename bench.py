@@ -92,8 +92,10 @@ def parse():
 
 # N > 1 split of the headline MSM, chosen per N from the one-card per-rank probe
 # (verkle-kzg_amd/tools/split_probe.py: the slowest rank's share of a 2^20 MSM, point range vs
-# window part; profiles/r04/split_probe.txt)
-AUTO_SPLIT = {2: "points", 3: "points", 4: "points"}
+# window part; profiles/r04/split_probe.txt: G = 2 points 1.70 ms against windows 1.80, G = 4 a tie
+# at 1.09 / 1.08, G = 8 windows 0.75 against points 1.81 -- an eighth of the points is too few for
+# the radix copies' 163,840-bucket tail)
+AUTO_SPLIT = {2: "points", 3: "points"}
 
 
 def msm_split(a, world):

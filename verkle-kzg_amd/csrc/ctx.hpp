@@ -103,6 +103,7 @@ struct Table {
     // windows"); built on first use for the window size c in win_c
     int win_ok = 0, win_c = 0, win_W = 0, win_ts = 0, win_m = 1;  // win_m > 1: radix win_m 2^win_c
     int win_limbs = 1;  // copies in radix-2^29 limbs (1) or packed-29 (0, VKZG_WIN_PACKED probe)
+    int win_pair = 0;   // radix copies in the pair layout (SW29::AffP, one 128-B record per signed copy)
     DevBuf win;
 };
 

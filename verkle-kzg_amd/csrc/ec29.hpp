@@ -30,6 +30,15 @@ struct SW29 {
     struct AffN {
         f29<P> x, y, ny;
     };
+    // pair layout of the same copies: one signed copy of a base per 128-B record -- record 2 i
+    // holds (x, y), 2 i + 1 (x, -y) -- so the accumulate's gather is ONE aligned line (the x, y,
+    // -y record straddles two or three); 256 B per base instead of 168
+    static constexpr int PADW = ((2 * P::L * 4 + 127) / 128 * 128 - 2 * P::L * 4) / 4;
+    static_assert(PADW > 0, "pair record padding");
+    struct AffP {
+        f29<P> x, y;
+        uint32_t pad[PADW];
+    };
     struct Acc {
         f29<P> x, y, zz, zzz;
         bool inf;

@@ -403,6 +403,10 @@ template <class FC, class BT, class = void>
 struct is_affn : std::false_type {};
 template <class FC, class BT>
 struct is_affn<FC, BT, std::void_t<typename FC::AffN>> : std::is_same<BT, typename FC::AffN> {};
+template <class FC, class BT, class = void>
+struct is_affp : std::false_type {};
+template <class FC, class BT>
+struct is_affp<FC, BT, std::void_t<typename FC::AffP>> : std::is_same<BT, typename FC::AffP> {};
 
 template <class C, class BT = typename C::Aff>
 __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
@@ -434,18 +438,27 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     // entry j < nphi: bases[j]; j >= nphi: phi[j - nphi] (the GLV endomorphism images)
     auto base_of = [&](uint32_t j) -> const Aff* { return j < nphi ? bases + j : phi + (j - nphi); };
     constexpr bool SN = is_affn<FC, BT>::value;
-    using Pre = std::conditional_t<SN, typename FC::Aff, Aff>;  // the prefetched entry
+    constexpr bool SP = is_affp<FC, BT>::value;  // pair layout: the sign picks the record
+    using Pre = std::conditional_t<SN || SP, typename FC::Aff, Aff>;  // the prefetched entry
     auto fetch = [&](uint32_t id) -> Pre {
-        const Aff* b = base_of(id & 0x7fffffffu);
-        if constexpr (SN) {
+        if constexpr (SP) {
+            const Aff* r = bases + 2 * (size_t)(id & 0x7fffffffu) + (id >> 31);
             typename FC::Aff a;
-            a.x = b->x;
-            // y or -y through the address (a select of values would load both)
-            a.y = *reinterpret_cast<const decltype(a.y)*>(reinterpret_cast<const char*>(&b->y) +
-                                                          ((id >> 31) ? sizeof(a.y) : 0u));
+            a.x = r->x;
+            a.y = r->y;
             return a;
         } else {
-            return *b;
+            const Aff* b = base_of(id & 0x7fffffffu);
+            if constexpr (SN) {
+                typename FC::Aff a;
+                a.x = b->x;
+                // y or -y through the address (a select of values would load both)
+                a.y = *reinterpret_cast<const decltype(a.y)*>(reinterpret_cast<const char*>(&b->y) +
+                                                              ((id >> 31) ? sizeof(a.y) : 0u));
+                return a;
+            } else {
+                return *b;
+            }
         }
     };
     uint32_t idx = sorted[k];
@@ -453,13 +466,13 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     while (true) {
         uint32_t cur = idx;
         typename FC::Aff Q;
-        if constexpr (SN) Q = P;
+        if constexpr (SN || SP) Q = P;
         else Q = FC::load(&P);
         if (k + 1 < e) {  // prefetch next base
             idx = sorted[k + 1];
             P = fetch(idx);
         }
-        acc = FC::madd(acc, Q, !SN && (cur >> 31) != 0);
+        acc = FC::madd(acc, Q, !SN && !SP && (cur >> 31) != 0);
         k++;
         if (k == bend || k == e) {
             bool right_open = (k == e) && (bend > e);
@@ -534,6 +547,28 @@ __global__ void __launch_bounds__(256) k_to_limbs_n(const typename C::Aff* __res
     o.y = l.y;
     o.ny = FC::load(&packed).y;
     out[i] = o;
+}
+
+// ... and to the pair layout (x, y) | (x, -y), one 128-B record each
+template <class C>
+__global__ void __launch_bounds__(256) k_to_limbs_p(const typename C::Aff* __restrict__ in, size_t n,
+                                                   typename Fast29<C>::type::AffP* __restrict__ out) {
+    using FC = typename Fast29<C>::type;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    typename C::Aff a = in[i], packed;
+    FC::pack_aff(a, &packed);
+    const typename FC::Aff l = FC::load(&packed);
+    a.y = fe_neg<typename C::F>(a.y);
+    FC::pack_aff(a, &packed);
+    typename FC::AffP o;
+#pragma unroll
+    for (int k = 0; k < FC::PADW; k++) o.pad[k] = 0;
+    o.x = l.x;
+    o.y = l.y;
+    out[2 * i] = o;
+    o.y = FC::load(&packed).y;
+    out[2 * i + 1] = o;
 }
 
 // ------------------------------------------------------------------ GLV endomorphism (BLS12-381 G1)
@@ -914,19 +949,23 @@ __global__ void __launch_bounds__(256) k_win_next(const typename C::Aff* __restr
 // built once per table and window size: W - 1 steps of c doublings + a batch normalisation.
 // mul > 1: radix B = mul 2^c (the radix-B shared windows): the copy of window w holds B^w P.
 template <class C>
-static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul = 1) {
+static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul = 1, bool pair = false) {
     using Aff = typename C::Aff;
     using Acc = typename C::Acc;
-    if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts && t->win_m == (int)mul) return VC_OK;
+    if (t->win_ok && t->win_c == c && t->win_W == W && t->win_ts == ts && t->win_m == (int)mul &&
+        t->win_pair == (pair ? 1 : 0))
+        return VC_OK;
     const size_t n = t->n;
     t->win_ok = 0;
     using FA = typename Fast29<C>::type::AffN;  // signed limb form (k_to_limbs_n)
+    using FP = typename Fast29<C>::type::AffP;  // pair layout (k_to_limbs_p)
     // VKZG_WIN_PACKED=1 keeps the packed-29 form (A/B probe: unpacking costs the accumulate ~84 of
     // 5,044 instructions per add, the limb form 16 B more per gather); the limb form holds
     // x, y and -y (168 B) so the accumulate never negates
     static const bool packed = getenv("VKZG_WIN_PACKED") != nullptr;
     t->win_limbs = packed ? 0 : 1;
-    VK_TRY(t->win.ensure((size_t)W * 2 * n * (packed ? sizeof(Aff) : sizeof(FA))));
+    t->win_pair = (pair && !packed) ? 1 : 0;
+    VK_TRY(t->win.ensure((size_t)W * 2 * n * (packed ? sizeof(Aff) : t->win_pair ? 2 * sizeof(FP) : sizeof(FA))));
     Table cur;  // 2^(c w) P (affine, Montgomery): normalised by table_from_acc (commit.hip)
     DevBuf nxt, acc;
     VK_TRY(nxt.ensure(n * sizeof(Aff)));
@@ -947,6 +986,10 @@ static int win_tables(vc_ctx* ctx, Table* t, int c, int W, int ts, uint32_t mul 
             Aff* wp = t->win.as<Aff>();
             VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, src, n, wp + (size_t)w * 2 * n);
             VK_LAUNCH(ctx, "to_fast", (k_to_fast<C>), g, 256, 0, nxt.as<Aff>(), n, wp + (size_t)w * 2 * n + n);
+        } else if (t->win_pair) {
+            FP* wp = t->win.as<FP>();
+            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs_p<C>), g, 256, 0, src, n, wp + 2 * ((size_t)w * 2 * n));
+            VK_LAUNCH(ctx, "to_limbs", (k_to_limbs_p<C>), g, 256, 0, nxt.as<Aff>(), n, wp + 2 * ((size_t)w * 2 * n + n));
         } else {
             VK_LAUNCH(ctx, "to_limbs", (k_to_limbs_n<C>), g, 256, 0, src, n, win + (size_t)w * 2 * n);
             VK_LAUNCH(ctx, "to_limbs", (k_to_limbs_n<C>), g, 256, 0, nxt.as<Aff>(), n, win + (size_t)w * 2 * n + n);
@@ -1055,6 +1098,14 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
 // (16 -> 8 windows, top 15 of 16 bits; 13 -> 10, top 10; 10 -> 13, top 7). A nearly empty
 // top window (c = 15 leaves 7 bits, c = 14 one) piles all its entries into a few buckets:
 // one fine-sort block and long fix-up chains (measured 0.25 + 0.23 ms at 2^16 with c = 15).
+// the radix shared-window copies in the pair layout (SW29::AffP: one aligned 128-B record per
+// signed copy, 3.76 GB at 2^20 instead of 2.47). Default on: the 2^20 accumulate 2.15 ms against
+// 2.17-2.38 with the (x, y, -y) records (profiles/r04/pair_ab.txt); VKZG_WIN_PAIR=0 for the A/B
+static bool win_pair_on() {
+    static const int env = getenv("VKZG_WIN_PAIR") ? atoi(getenv("VKZG_WIN_PAIR")) : 1;
+    return env != 0;
+}
+
 static int glv_window(size_t nv) {
     if (nv >= (1u << 19)) return 16;
     if (nv >= (1u << 15)) return 13;
@@ -1470,9 +1521,11 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         const bool whole = offset == 0 && n == t->n;
         if (glv && shared_env && (whole || range_env) && parts == 1 && nv >= (1u << 19) && radix_env == 5 &&
             !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED")) {
-            const size_t win_bytes = (size_t)7 * 2 * t->n * sizeof(typename Fast29<C>::type::AffN);
+            const size_t win_bytes = (size_t)7 * 2 * t->n *
+                                     (win_pair_on() ? 2 * sizeof(typename Fast29<C>::type::AffP)
+                                                    : sizeof(typename Fast29<C>::type::AffN));
             if (win_bytes <= (8ull << 30)) {
-                const int st = win_tables<C>(ctx, t, 16, 7, 0, 5);
+                const int st = win_tables<C>(ctx, t, 16, 7, 0, 5, win_pair_on());
                 if (st == VC_OK) {
                     shared = true;
                     c = 16;
@@ -1574,8 +1627,14 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
                     rd.half = (uint32_t)n;
                     rd.gap = (uint32_t)(t->n - n);
                     sl[k].stride = (uint32_t)(2 * t->n);
-                    VK_TRY(slice_enqueue<C>(ctx, sl[k], rd, nv, win, win, 0xffffffffu, k == 1 ? acc0 : nullptr,
-                                            k == 0 ? acc0 : nullptr));
+                    if (t->win_pair) {
+                        const auto* wp = t->win.as<typename Fast29<C>::type::AffP>();
+                        VK_TRY(slice_enqueue<C>(ctx, sl[k], rd, nv, wp, wp, 0xffffffffu, k == 1 ? acc0 : nullptr,
+                                                k == 0 ? acc0 : nullptr));
+                    } else {
+                        VK_TRY(slice_enqueue<C>(ctx, sl[k], rd, nv, win, win, 0xffffffffu, k == 1 ? acc0 : nullptr,
+                                                k == 0 ? acc0 : nullptr));
+                    }
                 }
                 else if (shared && !t->win_limbs)  // (power-of-two shared windows: whole tables only)
                     VK_TRY(slice_enqueue<C>(ctx, sl[k], src, nv, t->win.as<Aff>(), t->win.as<Aff>(), 0xffffffffu,
@@ -1642,7 +1701,7 @@ static int msm_run_many_t(vc_ctx* ctx, Table* t, const void* const* d_sc, const 
             VK_TRY(glv_table_ok(ctx, t, &glv));
         if (glv) {
             VK_TRY(fast_tables<C>(ctx, t, true));
-            const int st = win_tables<C>(ctx, t, 16, 7, 0, 5);
+            const int st = win_tables<C>(ctx, t, 16, 7, 0, 5, win_pair_on());
             if (st == VC_E_OOM) t->win.release();
             else if (st != VC_OK) return st;
             batched = st == VC_OK;
@@ -1675,9 +1734,15 @@ static int msm_run_many_t(vc_ctx* ctx, Table* t, const void* const* d_sc, const 
                     sl.radix.sc.push_back(static_cast<const uint32_t*>(d_sc[k]));
                     sl.radix.mont.push_back(mont[k]);
                 }
-                const auto* win = t->win.as<typename Fast29<C>::type::AffN>();
-                VK_TRY(slice_enqueue<C>(ctx, sl, RadixDigits{sl.radix.dig, (uint32_t)nv}, nv, win, win, 0xffffffffu,
-                                        nullptr, nullptr));
+                if (t->win_pair) {
+                    const auto* wp = t->win.as<typename Fast29<C>::type::AffP>();
+                    VK_TRY(slice_enqueue<C>(ctx, sl, RadixDigits{sl.radix.dig, (uint32_t)nv}, nv, wp, wp, 0xffffffffu,
+                                            nullptr, nullptr));
+                } else {
+                    const auto* win = t->win.as<typename Fast29<C>::type::AffN>();
+                    VK_TRY(slice_enqueue<C>(ctx, sl, RadixDigits{sl.radix.dig, (uint32_t)nv}, nv, win, win,
+                                            0xffffffffu, nullptr, nullptr));
+                }
                 VK_TRY(slice_fetch<C>(sl));
                 std::vector<Acc> res(Kb);
                 VK_TRY(slice_finish<C>(ctx, sl, res.data()));
