@@ -13,6 +13,7 @@
 //    a product output < 1.9p (fixed point of the bounds with inputs < 2p).
 #pragma once
 #include "ec.hpp"
+#include "ec30.hpp"
 #include "ff29.hpp"
 
 namespace vk {
@@ -348,12 +349,18 @@ __device__ __forceinline__ T shfl_idx_pod(const T& v, uint32_t src_lane) {
 }
 #endif
 
-// curve of ec.hpp -> its radix-2^29 mixed-add engine
+// curve of ec.hpp -> its mixed-add engine: radix 2^29, except BLS12-381 G1 on the signed
+// radix-2^30 engine of ec30.hpp (13 limbs instead of 14: -14 % of the multiply's products;
+// -DVKZG_BLS_R29 builds the radix-2^29 one for A/B runs)
 template <class C>
 struct Fast29;
 template <>
 struct Fast29<BLS381G1> {
+#ifdef VKZG_BLS_R29
     using type = SW29<BLS381G1, F29BLS381Fq>;
+#else
+    using type = SW30<BLS381G1, F30BLS381Fq>;
+#endif
 };
 template <>
 struct Fast29<BN254G1> {

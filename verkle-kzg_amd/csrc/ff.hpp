@@ -13,7 +13,15 @@
 #include <string.h>
 
 #define VK_HD __host__ __device__ __forceinline__
-// occupancy targets for the two VALU-heavy kernels (waves per SIMD; 0 = compiler's choice)
+// occupancy targets for the two VALU-heavy kernels (waves per SIMD; 0 = compiler's choice).
+// Default 2 (<= 256 VGPRs + AGPRs): the 13-limb BLS12-381 commit loop otherwise takes 264 and
+// runs one wave per SIMD
+#ifndef VK_COMMIT_WPE
+#define VK_COMMIT_WPE 2
+#endif
+#ifndef VK_ACC_WPE
+#define VK_ACC_WPE 2
+#endif
 #if defined(VK_COMMIT_WPE) && VK_COMMIT_WPE > 0
 #define VK_COMMIT_OCC __attribute__((amdgpu_waves_per_eu(VK_COMMIT_WPE)))
 #else

@@ -1872,6 +1872,17 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     using Acc = typename C::Acc;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
+    // VKZG_VERBOSE: per-phase wall times (with a stream sync at each lap: diagnostics only)
+    static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
+    auto tic = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!verbose) return;
+        (void)hipStreamSynchronize(ctx->stream);
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[sparse %zu rows %zu nnz] %s %.3f ms\n", batch, nnz, what,
+                std::chrono::duration<double, std::milli>(now - tic).count());
+        tic = now;
+    };
     // argument checks and the chunk lists on the host pool (verkle levels: 10^5 rows / non-zeros)
     std::vector<uint8_t> bad_part(host_pool().size(), 0);
     host_pool().run([&](unsigned k) {
@@ -1957,12 +1968,14 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_TRY(d_ownb.ensure((size_t)(Tmax + 8) * 4));
     VK_TRY(d_xy.ensure(batch * 2 * C::F::N * 4));
     VK_TRY(d_inf.ensure(batch));
+    lap("host chunk lists");
     VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, cptr.data(), (nch + 1) * 8, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, rc.data(), (batch + 1) * 4, hipMemcpyHostToDevice, st));
     if (nnz) {
         VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, cols, nnz * 4, hipMemcpyHostToDevice, st));
         VK_CHECK_HIP(hipMemcpyAsync(d_sc.p, scalars, nnz * 32, hipMemcpyHostToDevice, st));
     }
+    lap("H2D");
     VK_CHECK_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + nnz, 0, 4, st));
     if (nnz)
         VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(), nnz, mont,
@@ -2003,10 +2016,13 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     }
     VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
               d_rc.as<uint32_t>(), d_rows.as<Acc>());
+    lap("kernels");
     VK_TRY(normalize_to_canon(ctx, ctx->curve, d_rows.p, batch, d_xy.p, d_inf.as<uint8_t>()));
+    lap("normalise");
     VK_CHECK_HIP(hipMemcpyAsync(out_xy, d_xy.p, batch * 2 * C::F::N * 4, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipMemcpyAsync(out_inf, d_inf.p, batch, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host staging vectors die on return
+    lap("D2H");
     return VC_OK;
 }
 

@@ -1269,6 +1269,8 @@ __device__ __forceinline__ f29<P29> mp_block(const uint4 (&v)[MP_LAZY][2], const
     return r;
 }
 
+// NT = 1: non-temporal loads (the evaluations are read once per proof; A/B knob VKZG_MP_NT)
+template <int NT>
 __device__ __forceinline__ void mp_load(const uint32_t* __restrict__ f, const uint32_t* __restrict__ order, uint32_t u,
                                         uint32_t nq, size_t N, size_t k, uint4 (&v)[MP_LAZY][2],
                                         uint32_t (&qi)[MP_LAZY]) {
@@ -1277,15 +1279,23 @@ __device__ __forceinline__ void mp_load(const uint32_t* __restrict__ f, const ui
         qi[j] = j < nq ? order[u + j] : 0u;
         if (j < nq) {
             const uint4* src = reinterpret_cast<const uint4*>(f + ((size_t)qi[j] * N + k) * 8);
-            v[j][0] = src[0];
-            v[j][1] = src[1];
+            if constexpr (NT) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+                const u32x4 a = __builtin_nontemporal_load(s4), b = __builtin_nontemporal_load(s4 + 1);
+                v[j][0] = make_uint4(a.x, a.y, a.z, a.w);
+                v[j][1] = make_uint4(b.x, b.y, b.z, b.w);
+            } else {
+                v[j][0] = src[0];
+                v[j][1] = src[1];
+            }
         }
     }
 }
 
 // PF = 1: the next block's loads are issued before the current block's arithmetic (two blocks of
 // loads in flight per lane)
-template <int PF>
+template <int PF, int NT>
 __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f, const uint32_t* __restrict__ rp,
                                                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ be,
                                                  size_t N, uint32_t kblk, Fr* __restrict__ partial) {
@@ -1296,15 +1306,15 @@ __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f
     f29<P29> total = zero29<P29>();
     uint4 v[MP_LAZY][2], w[MP_LAZY][2];
     uint32_t qi[MP_LAZY], qw[MP_LAZY];
-    if (PF) mp_load(f, order, u0, min(cnt, MP_LAZY), N, k, v, qi);
+    if (PF) mp_load<NT>(f, order, u0, min(cnt, MP_LAZY), N, k, v, qi);
 #pragma unroll
     for (uint32_t h = 0; h < MP_CHUNK; h += MP_LAZY) {
         if (h >= cnt) break;
         const uint32_t nq = min(cnt - h, MP_LAZY);
         if (PF) {
-            if (h + MP_LAZY < cnt) mp_load(f, order, u0 + h + MP_LAZY, min(cnt - h - MP_LAZY, MP_LAZY), N, k, w, qw);
+            if (h + MP_LAZY < cnt) mp_load<NT>(f, order, u0 + h + MP_LAZY, min(cnt - h - MP_LAZY, MP_LAZY), N, k, w, qw);
         } else {
-            mp_load(f, order, u0 + h, nq, N, k, v, qi);
+            mp_load<NT>(f, order, u0 + h, nq, N, k, v, qi);
         }
         const f29<P29> r = mp_block(v, qi, nq, rp);
         total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
@@ -1380,13 +1390,11 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     VK_CHECK_HIP(hipMemcpyAsync(d_be.p, be.data(), be.size() * 4, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
     const uint32_t kblk = (uint32_t)((N + 255) / 256);
-    static const int pf_env = getenv("VKZG_MP_PREFETCH") ? atoi(getenv("VKZG_MP_PREFETCH")) : 0;  // A/B probe
-    if (pf_env)
-        VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk<1>, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
-                  d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
-    else
-        VK_LAUNCH(ctx, "mp_chunk", k_mp_chunk<0>, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
-                  d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
+    static const int pf_env = getenv("VKZG_MP_PREFETCH") ? atoi(getenv("VKZG_MP_PREFETCH")) : 0;  // A/B probes
+    static const int nt_env = getenv("VKZG_MP_NT") ? atoi(getenv("VKZG_MP_NT")) : 0;
+    auto kern = pf_env ? (nt_env ? k_mp_chunk<1, 1> : k_mp_chunk<1, 0>) : (nt_env ? k_mp_chunk<0, 1> : k_mp_chunk<0, 0>);
+    VK_LAUNCH(ctx, "mp_chunk", kern, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
+              d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
     VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,
               kblk, reinterpret_cast<Fr*>(d_S));
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host vectors above die on return
