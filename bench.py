@@ -2,10 +2,11 @@
 """Benchmark: single 2^20-point BLS12-381 G1 MSM (BASELINE.json configs[1]) on N MI355X.
 
 A step = one 2^20-point MSM over synthetic inputs already resident in HBM (bases uploaded
-once, scalars on the device). With N ranks the MSM is split by Pippenger windows (rank k
-computes windows [kW/N, (k+1)W/N) of all n terms; vkzg.dist), the per-rank projective
-partial sums are all-gathered over RCCL and added on the host: one exchange step
-(SURVEY.md 8(e)), so scaling is "strong" (total work fixed).
+once, scalars on the device). With N ranks the MSM is split (AUTO_SPLIT below, from the
+one-card split probe): into point ranges on the shared radix copies for 2-3 ranks, into
+Pippenger window parts from 4 (rank k computes windows [kW/N, (k+1)W/N) of all n terms);
+the per-rank projective partial sums are all-gathered over RCCL and added on the host: one
+exchange step, so scaling is "strong" (total work fixed).
 
 Secondary line items (same JSON object): 10k batched width-256 Bandersnatch commits/s
 (config 3; the batch split across the N ranks, results all-gathered), and the CPU baseline:
@@ -41,8 +42,14 @@ CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
 # (scripts/bench_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
-PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r03", "r02", "r01"))
-                    if os.path.exists(p)), os.path.join(ROOT, "profiles", "r03", "pmc_summary.json"))
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r04", "r03", "r02", "r01"))
+                    if os.path.exists(p)), os.path.join(ROOT, "profiles", "r04", "pmc_summary.json"))
+# the headline's accumulate instantiation in the PMC summary: the shared-window copies in the pair
+# layout (AffP, the default), else the (x, y, -y) records (AffN), else the packed tables
+
+
+def _acc_key_rank(k):
+    return 0 if "::AffP" in k else 1 if "::AffN" in k else 2
 
 
 def progress(msg):
@@ -1078,23 +1085,24 @@ def main():
                                   (("log_n", a.log_n), ("windows", w_total), ("radix", plan["radix_mul"] << c_bits)))
     insts = None
     if pmc_match and world == 1:
-        # the headline's instantiation: limb-form shared-window copies (BT = SW29<..>::Aff)
+        # the headline's instantiation (the radix copies' limb records)
         key = [k for k in pmc["kernels"] if k.startswith("vk::k_msm_accumulate") and CURVE_TAG[curve] in k]
-        key = sorted(key, key=lambda k: "SW29" not in k)
+        key = sorted(key, key=_acc_key_rank)
         if key:
             insts = pmc["kernels"][key[0]].get("SQ_INSTS_VALU_per_launch")
     ach = insts * 64 / acc_s / 1e12 if (insts and acc_s) else None
     valu = {"achieved": ach, "peak": mad_peak, "unit": "T VALU lane-instructions/s",
             "frac": (ach / mad_peak) if ach else None,
-            "work": f"{madds} mixed adds (radix-2^29 XYZZ: 8 products + 2 squares, 9 Montgomery reductions -- Y3 is one lazy sum of two products); "
+            "work": f"{madds} mixed adds ({'signed radix-2^30, 13 limbs' if curve == 'bls12_381' else 'radix-2^29'} XYZZ: "
+                    f"8 products + 2 squares, 9 Montgomery reductions -- Y3 is one lazy sum of two products); "
                     f"{insts / madds * 64 if insts else float('nan'):.0f} VALU lane-instructions per mixed add (PMC)",
             "madds_per_s": madds / acc_s if acc_s else None,
-            "peak_source": "vc_device_mad_rate: v_mad_u64_u32 issue rate measured live on this GPU",
+            "peak_source": "vc_device_mad_rate: v_mad_u64_u32 issue rate measured live on this GPU (v_mad_i64_i32 issues the same)",
             "insts_source": os.path.relpath(PMC_SUMMARY, ROOT) if insts else None}
     traffic, traffic_src = None, None
     if world == 1 and pmc_match:
         key = sorted([k for k in pmc.get("kernels", {}) if "k_msm_accumulate<vk::SWCurve<vk::BLS381Fq" in k],
-                     key=lambda k: "SW29" not in k)
+                     key=_acc_key_rank)
         if key and curve == "bls12_381":
             traffic = pmc["kernels"][key[0]].get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)

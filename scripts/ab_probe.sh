@@ -14,7 +14,7 @@ OUT=$1; VAR=$2; VALUES=$3; ROUNDS=$4; SECS=$5; shift 5
 mkdir -p "$OUT"
 for r in $(seq 1 "$ROUNDS"); do
     for v in $VALUES; do
-        f="$OUT/${VAR}_${v}_r$r.txt"
+        f="$OUT/${VAR}_$(basename "$v")_r$r.txt"  # a path value (VKZG_LIB=...) by its file name
         env "$VAR=$v" timeout -k 10 "$SECS" "$@" > "$f" 2>&1
         rc=$?
         echo "$VAR=$v round $r rc=$rc -> $f"

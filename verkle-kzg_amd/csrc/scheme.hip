@@ -1391,7 +1391,9 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
     const uint32_t kblk = (uint32_t)((N + 255) / 256);
     static const int pf_env = getenv("VKZG_MP_PREFETCH") ? atoi(getenv("VKZG_MP_PREFETCH")) : 0;  // A/B probes
-    static const int nt_env = getenv("VKZG_MP_NT") ? atoi(getenv("VKZG_MP_NT")) : 0;
+    // non-temporal loads by default: 0.119-0.121 ms (4.43-4.51 TB/s) against 0.125-0.127 at 2^16 x 256
+    // (profiles/r04/mp_nt_ab.txt)
+    static const int nt_env = getenv("VKZG_MP_NT") ? atoi(getenv("VKZG_MP_NT")) : 1;
     auto kern = pf_env ? (nt_env ? k_mp_chunk<1, 1> : k_mp_chunk<1, 0>) : (nt_env ? k_mp_chunk<0, 1> : k_mp_chunk<0, 0>);
     VK_LAUNCH(ctx, "mp_chunk", kern, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
               d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
