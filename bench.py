@@ -1089,7 +1089,10 @@ def main():
         key = [k for k in pmc["kernels"] if k.startswith("vk::k_msm_accumulate") and CURVE_TAG[curve] in k]
         key = sorted(key, key=_acc_key_rank)
         if key:
-            insts = pmc["kernels"][key[0]].get("SQ_INSTS_VALU_per_launch")
+            ke = pmc["kernels"][key[0]]
+            # the headline's launch class (one bucket set; the KZG line's two-set launches share
+            # the kernel instance: prof_summary.py by_class)
+            insts = ke.get("by_class", {}).get("1", ke).get("SQ_INSTS_VALU_per_launch")
     ach = insts * 64 / acc_s / 1e12 if (insts and acc_s) else None
     valu = {"achieved": ach, "peak": mad_peak, "unit": "T VALU lane-instructions/s",
             "frac": (ach / mad_peak) if ach else None,
@@ -1104,7 +1107,8 @@ def main():
         key = sorted([k for k in pmc.get("kernels", {}) if "k_msm_accumulate<vk::SWCurve<vk::BLS381Fq" in k],
                      key=_acc_key_rank)
         if key and curve == "bls12_381":
-            traffic = pmc["kernels"][key[0]].get("hbm_bytes_per_launch")
+            ke = pmc["kernels"][key[0]]
+            traffic = ke.get("by_class", {}).get("1", ke).get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
 
     out = {

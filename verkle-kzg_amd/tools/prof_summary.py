@@ -21,6 +21,17 @@ def main(d, out):
         for r in csv.DictReader(f):
             stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                       "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+    # per launch class: one kernel instance serves several workloads (the headline MSM and the KZG
+    # commit + open's K-set pipelines share the accumulate, at the same grid), so launches are also
+    # grouped by their work in units of the smallest launch -- class round(x / min) of the duration
+    # (trace pass) or of SQ_INSTS_VALU (PMC pass): class 1 = one MSM's bucket set, 2 = two, ...
+    per_launch = defaultdict(lambda: defaultdict(list))
+    try:
+        with open(f"{d}/trace/run_kernel_trace.csv") as f:
+            for r in csv.DictReader(f):
+                per_launch[short(r["Kernel_Name"])]["ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    except (FileNotFoundError, KeyError):
+        pass
     pmc = defaultdict(lambda: defaultdict(list))
     for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"), ("valu", "SQ_INSTS_VALU")):
         try:
@@ -43,6 +54,29 @@ def main(d, out):
         if "FETCH_SIZE_KB_per_launch_raw" in e and "WRITE_SIZE_KB_per_launch" in e:
             e["hbm_bytes_per_launch"] = 1024.0 * (2.0 * e["FETCH_SIZE_KB_per_launch_raw"]
                                                   + e["WRITE_SIZE_KB_per_launch"])
+        ns = per_launch.get(k, {}).get("ns", [])
+        def classes(xs):
+            lo = min(xs)
+            out = defaultdict(list)
+            for x in xs:
+                out[str(max(1, round(x / lo)))].append(x)
+            return out
+        if ("k_msm_accumulate" in k and len(ns) > 1 and min(ns) > 0 and max(ns) / min(ns) >= 1.6
+                and len(classes(ns)) <= 3):  # a few clean classes (K = 1, 2 bucket sets), not a size sweep
+            cls = {}
+            for c, xs in classes(ns).items():
+                cls[c] = {"calls": len(xs), "avg_ns": sum(xs) / len(xs)}
+            for ctr, name in (("SQ_INSTS_VALU", "SQ_INSTS_VALU_per_launch"), ("FETCH_SIZE", "FETCH_SIZE_KB_per_launch_raw"),
+                              ("WRITE_SIZE", "WRITE_SIZE_KB_per_launch")):
+                xs_all = p.get(ctr, [])
+                if xs_all and min(xs_all) > 0 and len(classes(xs_all)) <= 3:
+                    for c, xs in classes(xs_all).items():
+                        cls.setdefault(c, {})[name] = sum(xs) / len(xs)
+            for c, ce in cls.items():
+                if "FETCH_SIZE_KB_per_launch_raw" in ce and "WRITE_SIZE_KB_per_launch" in ce:
+                    ce["hbm_bytes_per_launch"] = 1024.0 * (2.0 * ce["FETCH_SIZE_KB_per_launch_raw"]
+                                                           + ce["WRITE_SIZE_KB_per_launch"])
+            e["by_class"] = dict(sorted(cls.items()))
         res[k] = e
     res = dict(sorted(res.items(), key=lambda kv: -kv[1]["total_ns"]))
     bench, config = None, {}
@@ -58,7 +92,9 @@ def main(d, out):
     with open(out, "w") as f:
         json.dump({"config": config, "bench_under_rocprof": bench, "note": "avg_ns from the kernel-trace pass; FETCH/WRITE from separate --pmc passes of the "
                            "same command; hbm_bytes_per_launch = 1024*(2*FETCH_KB + WRITE_KB) (gfx950 FETCH "
-                           "correction, MI355X_MICROARCH.md HBM section)", "kernels": res}, f, indent=1)
+                           "correction, MI355X_MICROARCH.md HBM section); by_class (accumulate): launches grouped by "
+                           "work in units of the smallest (1 = one MSM's bucket set: the headline; 2 = the KZG "
+                           "commit + open's two sets)", "kernels": res}, f, indent=1)
 
 
 if __name__ == "__main__":
