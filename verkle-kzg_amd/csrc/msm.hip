@@ -1519,7 +1519,11 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         // positions (RadixDigits::pt): one copy layout serves whole-table and point-range MSMs
         static const int range_env = getenv("VKZG_MSM_RANGE") ? atoi(getenv("VKZG_MSM_RANGE")) : 1;  // A/B
         const bool whole = offset == 0 && n == t->n;
-        if (glv && shared_env && (whole || range_env) && parts == 1 && nv >= (1u << 19) && radix_env == 5 &&
+        // ranges down to 2^16 points of a >= 2^18-point table: an eighth of 2^20 on the copies (the
+        // 163,840-bucket tail is a fixed cost, but a standalone 2^17-term plan took 1.8 ms against
+        // ~0.6: profiles/r04/split_probe*.txt)
+        const bool big = whole ? nv >= (1u << 19) : (2 * (size_t)t->n >= (1u << 19) && nv >= (1u << 17));
+        if (glv && shared_env && (whole || range_env) && parts == 1 && big && radix_env == 5 &&
             !getenv("VKZG_MSM_C") && !getenv("VKZG_WIN_PACKED")) {
             const size_t win_bytes = (size_t)7 * 2 * t->n *
                                      (win_pair_on() ? 2 * sizeof(typename Fast29<C>::type::AffP)
