@@ -79,12 +79,14 @@ def test_ff29_zero_test(lines):
             assert d["zero_mo"] == (1 if val(d["a"]) % p == 0 else 0)
 
 
-def test_mp_chunk_lazy_reduction_bn254_fr():
-    """k_mp_chunk's arithmetic (csrc/scheme.hip) restated with Python integers: evaluations f
-    (canonical) times r^i R' (radix-2^29 Montgomery, R' = 2^261) added into 17 64-bit columns for up
-    to 3 queries, one Montgomery reduction per 3, the block results added with one conditional
-    subtraction each -- == sum f_i r^i mod r for chunks of 1..16 queries, near-r inputs included;
-    every column stays below 2^64."""
+@pytest.mark.parametrize("lz,ch", [(3, 16), (4, 16), (4, 32), (6, 24)])
+def test_mp_chunk_lazy_reduction_bn254_fr(lz, ch):
+    """k_mp_chunk's arithmetic (csrc/scheme.hip, shapes LZ x CH of VKZG_MP_SHAPE) restated with
+    Python integers: evaluations f (canonical) times r^i R' (radix-2^29 Montgomery, R' = 2^261)
+    added into 17 64-bit columns for up to LZ queries, one Montgomery reduction per LZ, the block
+    results added with one conditional subtraction each -- == sum f_i r^i mod r for chunks of
+    1..CH queries, near-r inputs and all-max-limb canonical inputs included; every column stays
+    below 2^64 at every step."""
     import random
     p = 21888242871839275222246405745257275088548364400416034343698204186575808495617
     L, M = 9, (1 << 29) - 1
@@ -93,30 +95,37 @@ def test_mp_chunk_lazy_reduction_bn254_fr():
     limbs = lambda x: [(x >> (29 * j)) & M for j in range(L - 1)] + [x >> (29 * (L - 1))]  # noqa: E731
     val = lambda v: sum(a << (29 * j) for j, a in enumerate(v))  # noqa: E731
     pl = limbs(p)
+    # the largest limbs a canonical value can have: 8 limbs of 2^29 - 1 under p's top limb - 1
+    vmax = val([M] * (L - 1) + [pl[-1] - 1])
+    assert vmax < p
 
     def carry_csub(x):
         v = val(x)
+        assert v < 2 * p
         return limbs(v - p if v >= p else v)
 
-    rng = random.Random(3)
-    for trial in range(400):
-        cnt = rng.randint(1, 16)
-        fs = [rng.randrange(p) if trial % 3 else p - 1 - rng.randrange(5) for _ in range(cnt)]
+    rng = random.Random(3 + lz)
+    for trial in range(300):
+        cnt = rng.randint(1, ch)
+        stress = trial % 4 == 0
+        fs = [vmax if stress else rng.randrange(p) if trial % 3 else p - 1 - rng.randrange(5) for _ in range(cnt)]
         rs = [rng.randrange(p) for _ in range(cnt)]
+        rm = [vmax if stress else r * Rp % p for r in rs]  # the radix-29 words the kernel reads
         total = [0] * L
-        for h in range(0, cnt, 3):
+        for h in range(0, cnt, lz):
             t = [0] * (2 * L)
-            for j in range(h, min(h + 3, cnt)):
-                a, b = limbs(fs[j]), limbs(rs[j] * Rp % p)
+            for j in range(h, min(h + lz, cnt)):
+                a, b = limbs(fs[j]), limbs(rm[j])
                 for y in range(L):
                     for x in range(L):
                         t[x + y] += a[x] * b[y]
+            assert max(t) < 1 << 64
             for i in range(L):
                 m = ((t[i] & 0xFFFFFFFF) * inv) & M
                 for j in range(L):
                     t[i + j] += m * pl[j]
+                assert max(t) < 1 << 64
                 t[i + 1] += t[i] >> 29
-            assert max(t) < 1 << 64
             r = [0] * L
             for j in range(L, 2 * L - 1):
                 t[j + 1] += t[j] >> 29
@@ -124,4 +133,5 @@ def test_mp_chunk_lazy_reduction_bn254_fr():
             r[L - 1] = t[2 * L - 1]
             total = carry_csub([u + w for u, w in zip(total, r)])
         total = carry_csub(total)
-        assert val(total) == sum(f * r for f, r in zip(fs, rs)) % p
+        want = sum(f * (r if not stress else vmax * pow(Rp, -1, p)) for f, r in zip(fs, rs)) % p
+        assert val(total) == want

@@ -335,7 +335,8 @@ def test_msm_point_ranges_on_shared_windows(bls):
     """point ranges [offset, offset + n) of the 2^20 table (one GPU's share of a point-split MSM)
     on the radix shared-window copies of the whole table (entries at their table positions):
     == (sum k_i s_{offset+i}) G by linearity; the plan reports the radix geometry; a whole-table
-    MSM between them reuses the same copies; identity-free ranges at odd offsets and lengths."""
+    MSM between them reuses the same copies; identity-free ranges at odd offsets and lengths,
+    down to 2^16 + 7 points."""
     import torch
     import vkzg
     from pyoracle.curves import BLS12_381 as C
@@ -345,7 +346,9 @@ def test_msm_point_ranges_on_shared_windows(bls):
     s = vkzg.random_base_scalars("bls12_381", 2024, n)
     k = vkzg.random_scalars("bls12_381", n, np.random.default_rng(77))
     d_k = torch.from_numpy(k.view(np.int64).copy()).cuda()
-    for off, m in ((0, 1 << 19), ((1 << 19) + 3, (1 << 18) + 5), (12345, n - 12345), (1 << 19, 1 << 19)):
+    # ... down to an eighth of the table (the 8-rank point split) and just above 2^16 points
+    for off, m in ((0, 1 << 19), ((1 << 19) + 3, (1 << 18) + 5), (12345, n - 12345), (1 << 19, 1 << 19),
+                   (7 << 17, 1 << 17), ((1 << 18) + 11, (1 << 16) + 7)):
         got = e.msm_device(tid, d_k.data_ptr(), m, offset=off)
         want = C.mul(C.g, vkzg.dot_mod(k[:m], s[off:off + m], C.r))
         assert _pt("bls12_381", *got) == want, (off, m)

@@ -1222,24 +1222,32 @@ __global__ void k_mp_rpow(Fr r, size_t first, size_t n, uint32_t* __restrict__ r
     for (int j = 0; j < P29::L; j++) rp[i * MP_RP_WORDS + j] = v.v[j];
 }
 
-// one block per (k block, chunk c of <= MP_CHUNK queries of one z): partial[c][k] =
+// one block per (k block, chunk c of <= CH queries of one z): partial[c][k] =
 // sum over sorted positions [be[2c], be[2c+1]) of r^i f_i[k] (f canonical; partial canonical).
 // HBM-bound stream of the Q x N evaluations (the r^i are uniform over a block). Radix-2^29 with
-// lazy reduction: the products f_i[k] (r^i R') of MP_LAZY queries add into 17 64-bit columns (9 x
-// 9 products of < 2^58 per query: 27 x 2^58 < 2^62.8) and ONE Montgomery reduction (9 rows)
-// serves them -- ~120 instructions per element instead of a full 32-bit-limb multiply (~270)
-// and an add; the block results (< 1.03 p each) are added with one conditional subtraction.
-constexpr uint32_t MP_CHUNK = 16;
-constexpr uint32_t MP_LAZY = 3;
-// one block of <= MP_LAZY queries: products into the columns, one Montgomery reduction -> r < 1.03 p
-__device__ __forceinline__ f29<P29> mp_block(const uint4 (&v)[MP_LAZY][2], const uint32_t (&qi)[MP_LAZY], uint32_t nq,
+// lazy reduction: the products f_i[k] (r^i R') of LZ queries add into 17 unsigned 64-bit columns
+// (<= 9 products of < 2^58 per query and column) and ONE Montgomery reduction (9 rows, <= 9 more
+// products per column) serves them: (9 LZ + 9) 2^58 + 2^35 < 2^64 for LZ <= 6 -- ~100-120
+// instructions per element instead of a full 32-bit-limb multiply (~270) and an add. A block
+// result is below (LZ p^2 / R' + p) = (1 + LZ 2^-7) p; the block results are added with one
+// conditional subtraction each, so the running total stays below 2 p over a chunk of CH / LZ
+// blocks, and a last one makes it canonical.
+// Shapes (LZ x CH, A/B knob VKZG_MP_SHAPE): 3 x 16 (round 4's first), 4 x 16, 4 x 32, 6 x 24.
+constexpr uint32_t MP_LZ_MAX = 6;
+struct MpShape {
+    uint32_t lz, ch;
+};
+// one block of <= LZ queries: products into the columns, one Montgomery reduction
+template <uint32_t LZ>
+__device__ __forceinline__ f29<P29> mp_block(const uint4 (&v)[LZ][2], const uint32_t (&qi)[LZ], uint32_t nq,
                                              const uint32_t* __restrict__ rp) {
+    static_assert(LZ <= MP_LZ_MAX, "column bound");
     constexpr int L = P29::L;
     uint64_t t[2 * L];  // 2L - 1 product columns and the reduction's top carry
 #pragma unroll
     for (int x = 0; x < 2 * L; x++) t[x] = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < MP_LAZY; j++) {
+    for (uint32_t j = 0; j < LZ; j++) {
         if (j >= nq) break;
         const uint32_t w[8] = {v[j][0].x, v[j][0].y, v[j][0].z, v[j][0].w, v[j][1].x, v[j][1].y, v[j][1].z, v[j][1].w};
         const f29<P29> a = unpack29<P29>(w);
@@ -1270,12 +1278,11 @@ __device__ __forceinline__ f29<P29> mp_block(const uint4 (&v)[MP_LAZY][2], const
 }
 
 // NT = 1: non-temporal loads (the evaluations are read once per proof; A/B knob VKZG_MP_NT)
-template <int NT>
+template <int NT, uint32_t LZ>
 __device__ __forceinline__ void mp_load(const uint32_t* __restrict__ f, const uint32_t* __restrict__ order, uint32_t u,
-                                        uint32_t nq, size_t N, size_t k, uint4 (&v)[MP_LAZY][2],
-                                        uint32_t (&qi)[MP_LAZY]) {
+                                        uint32_t nq, size_t N, size_t k, uint4 (&v)[LZ][2], uint32_t (&qi)[LZ]) {
 #pragma unroll
-    for (uint32_t j = 0; j < MP_LAZY; j++) {
+    for (uint32_t j = 0; j < LZ; j++) {
         qi[j] = j < nq ? order[u + j] : 0u;
         if (j < nq) {
             const uint4* src = reinterpret_cast<const uint4*>(f + ((size_t)qi[j] * N + k) * 8);
@@ -1293,9 +1300,7 @@ __device__ __forceinline__ void mp_load(const uint32_t* __restrict__ f, const ui
     }
 }
 
-// PF = 1: the next block's loads are issued before the current block's arithmetic (two blocks of
-// loads in flight per lane)
-template <int PF, int NT>
+template <int NT, uint32_t LZ, uint32_t CH>
 __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f, const uint32_t* __restrict__ rp,
                                                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ be,
                                                  size_t N, uint32_t kblk, Fr* __restrict__ partial) {
@@ -1304,28 +1309,15 @@ __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f
     if (k >= N) return;
     const uint32_t u0 = be[2 * c], cnt = be[2 * c + 1] - u0;
     f29<P29> total = zero29<P29>();
-    uint4 v[MP_LAZY][2], w[MP_LAZY][2];
-    uint32_t qi[MP_LAZY], qw[MP_LAZY];
-    if (PF) mp_load<NT>(f, order, u0, min(cnt, MP_LAZY), N, k, v, qi);
+    uint4 v[LZ][2];
+    uint32_t qi[LZ];
 #pragma unroll
-    for (uint32_t h = 0; h < MP_CHUNK; h += MP_LAZY) {
+    for (uint32_t h = 0; h < CH; h += LZ) {
         if (h >= cnt) break;
-        const uint32_t nq = min(cnt - h, MP_LAZY);
-        if (PF) {
-            if (h + MP_LAZY < cnt) mp_load<NT>(f, order, u0 + h + MP_LAZY, min(cnt - h - MP_LAZY, MP_LAZY), N, k, w, qw);
-        } else {
-            mp_load<NT>(f, order, u0 + h, nq, N, k, v, qi);
-        }
-        const f29<P29> r = mp_block(v, qi, nq, rp);
+        const uint32_t nq = min(cnt - h, LZ);
+        mp_load<NT, LZ>(f, order, u0 + h, nq, N, k, v, qi);
+        const f29<P29> r = mp_block<LZ>(v, qi, nq, rp);
         total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
-        if (PF) {
-#pragma unroll
-            for (uint32_t j = 0; j < MP_LAZY; j++) {
-                v[j][0] = w[j][0];
-                v[j][1] = w[j][1];
-                qi[j] = qw[j];
-            }
-        }
     }
     total = csub29<P29>(carry29<P29>(total));
     pack29<P29>(total, partial[(size_t)c * N + k].v);
@@ -1360,6 +1352,11 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
         if (z[i] >= N || row_of[z[i]] == 0xffffffffu) return VC_E_DOMAIN;
         row[i] = row_of[z[i]];
     }
+    // block / chunk shape of k_mp_chunk (VKZG_MP_SHAPE: 0 = 3 x 16, 1 = 4 x 16, 2 = 4 x 32, 3 = 6 x 24)
+    static const int shape_env = getenv("VKZG_MP_SHAPE") ? atoi(getenv("VKZG_MP_SHAPE")) : 0;
+    static const MpShape shapes[4] = {{3, 16}, {4, 16}, {4, 32}, {6, 24}};
+    const MpShape shp = shapes[shape_env >= 0 && shape_env < 4 ? shape_env : 0];
+    const uint32_t MP_CHUNK = shp.ch;
     // counting sort of the shard's queries by row, then chunks of <= MP_CHUNK queries
     std::vector<uint32_t> cnt(Z + 1, 0), order(Qs);
     for (size_t i = 0; i < Qs; i++) cnt[row[i] + 1]++;
@@ -1390,11 +1387,14 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     VK_CHECK_HIP(hipMemcpyAsync(d_be.p, be.data(), be.size() * 4, hipMemcpyHostToDevice, st));
     VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
     const uint32_t kblk = (uint32_t)((N + 255) / 256);
-    static const int pf_env = getenv("VKZG_MP_PREFETCH") ? atoi(getenv("VKZG_MP_PREFETCH")) : 0;  // A/B probes
     // non-temporal loads by default: 0.119-0.121 ms (4.43-4.51 TB/s) against 0.125-0.127 at 2^16 x 256
     // (profiles/r04/mp_nt_ab.txt)
     static const int nt_env = getenv("VKZG_MP_NT") ? atoi(getenv("VKZG_MP_NT")) : 1;
-    auto kern = pf_env ? (nt_env ? k_mp_chunk<1, 1> : k_mp_chunk<1, 0>) : (nt_env ? k_mp_chunk<0, 1> : k_mp_chunk<0, 0>);
+    using KFn = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, size_t, uint32_t, Fr*);
+    static const KFn kerns[2][4] = {
+        {k_mp_chunk<0, 3, 16>, k_mp_chunk<0, 4, 16>, k_mp_chunk<0, 4, 32>, k_mp_chunk<0, 6, 24>},
+        {k_mp_chunk<1, 3, 16>, k_mp_chunk<1, 4, 16>, k_mp_chunk<1, 4, 32>, k_mp_chunk<1, 6, 24>}};
+    const KFn kern = kerns[nt_env ? 1 : 0][shape_env >= 0 && shape_env < 4 ? shape_env : 0];
     VK_LAUNCH(ctx, "mp_chunk", kern, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
               d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
     VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,
