@@ -73,9 +73,13 @@ int vc_ctx_set_stream(vc_ctx* ctx, void* hip_stream);
  *     copies (~0.1 s at 2^20) on every switch, so keep one table on one path.
  *     0: plain variable-base Pippenger, no copies.
  *   VC_OPT_MSM_CHUNK_POINTS [2^27]: MSMs of more points run as summed chunks of this many
- *     (keeps the u32 entry space of the bucket sort from wrapping). */
+ *     (keeps the u32 entry space of the bucket sort from wrapping).
+ *   VC_OPT_MSM_HOST_CHUNKS [2]: vc_msm (host scalars) on the radix shared-window path copies the
+ *     scalars in this many chunks (1..4) on a second stream, each chunk's sort + accumulate under
+ *     the next chunk's copy, one reduction at the end; 1 = one copy, then the MSM. */
 #define VC_OPT_MSM_SHARED_WINDOWS 1
 #define VC_OPT_MSM_CHUNK_POINTS 2
+#define VC_OPT_MSM_HOST_CHUNKS 3
 int vc_ctx_set_option(vc_ctx* ctx, int option, int64_t value);
 int vc_ctx_get_option(vc_ctx* ctx, int option, int64_t* value);
 /* Per-kernel device timing (HIP events around each launch on the ctx stream). */

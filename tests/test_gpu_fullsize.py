@@ -125,8 +125,43 @@ def test_msm_radix_shared_edges(bls, case):
     d_k = torch.from_numpy(np.ascontiguousarray(k).view(np.int64).copy()).cuda()
     got = e.msm_device(tid, d_k.data_ptr(), n)
     assert _pt("bls12_381", *got) == want
-    got = e.msm(tid, k)
-    assert _pt("bls12_381", *got) == want
+    # host scalars: copied in 2 and 4 chunks, each chunk's sort + accumulate into one bucket set
+    # (all_equal: a chunk's fix-up chains exceed the walk, the unchunked MSM runs instead)
+    try:
+        for chunks in (2, 4):
+            e.set_option(e.OPT_MSM_HOST_CHUNKS, chunks)
+            got = e.msm(tid, k)
+            assert _pt("bls12_381", *got) == want, chunks
+    finally:
+        e.set_option(e.OPT_MSM_HOST_CHUNKS, 2)
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 3, 4])
+def test_msm_host_scalars_chunked_2e20(bls, chunks):
+    """vc_msm (host scalars) at 2^20: the scalars cross PCIe in `chunks` copies on a second stream,
+    chunk j's GLV split, sort, accumulate and fix-up run under chunk j+1's copy and add into one
+    bucket set (k_bucket_merge), one reduction -- equal to the device-scalar MSM and to the
+    linearity-pinned point; also over a point range of the table (offset) and ragged chunks."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    n = 1 << 20
+    e = bls
+    tid = e.random_bases(n, seed=2024)
+    s = vkzg.random_base_scalars("bls12_381", 2024, n)
+    k = vkzg.random_scalars("bls12_381", n, np.random.default_rng(99 + chunks))
+    e.set_option(e.OPT_MSM_HOST_CHUNKS, chunks)
+    try:
+        got = e.msm(tid, k)
+        assert _pt("bls12_381", *got) == C.mul(C.g, vkzg.dot_mod(k, s, C.r))
+        d_k = torch.from_numpy(k.view(np.int64).copy()).cuda()
+        assert np.array_equal(e.msm_device(tid, d_k.data_ptr(), n)[0], got[0])
+        # a ragged point range: [off, off + m) with m not a multiple of the 8192-scalar sort block
+        off, m = 12_345, 700_001
+        got = e.msm(tid, k[:m], offset=off)
+        assert _pt("bls12_381", *got) == C.mul(C.g, vkzg.dot_mod(k[:m], s[off:off + m], C.r))
+    finally:
+        e.set_option(e.OPT_MSM_HOST_CHUNKS, 2)
 
 
 def test_msm_2e20_window_parts_sum(bls):

@@ -259,6 +259,10 @@ int vc_ctx_set_option(vc_ctx* ctx, int option, int64_t value) {
             if (value < 1 || value > (int64_t(1) << 27)) return VC_E_INVALID;
             ctx->opt_msm_chunk = (size_t)value;
             return VC_OK;
+        case VC_OPT_MSM_HOST_CHUNKS:
+            if (value < 1 || value > 4) return VC_E_INVALID;
+            ctx->opt_host_chunks = (int)value;
+            return VC_OK;
     }
     return VC_E_INVALID;
 }
@@ -269,6 +273,7 @@ int vc_ctx_get_option(vc_ctx* ctx, int option, int64_t* value) {
     switch (option) {
         case VC_OPT_MSM_SHARED_WINDOWS: *value = ctx->opt_shared_windows; return VC_OK;
         case VC_OPT_MSM_CHUNK_POINTS: *value = (int64_t)ctx->opt_msm_chunk; return VC_OK;
+        case VC_OPT_MSM_HOST_CHUNKS: *value = ctx->opt_host_chunks; return VC_OK;
     }
     return VC_E_INVALID;
 }
@@ -398,13 +403,11 @@ int vc_msm(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n
            uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || !out_xy || !out_inf || (n > 0 && !scalars)) return VC_E_INVALID;
     Guard g(ctx);
-    if (n > 0) {
-        VK_TRY(ctx->ws[vk::WS_SCALARS].ensure(n * 32));
-        VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[vk::WS_SCALARS].p, scalars, n * 32, hipMemcpyHostToDevice,
-                                    ctx->stream));
-    }
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    if (offset > t->n || n > t->n - offset) return VC_E_RANGE;
     std::vector<uint32_t> acc(vk::point_words(ctx->curve));
-    VK_TRY(msm_device_acc(ctx, id, offset, ctx->ws[vk::WS_SCALARS].p, n, mont, acc.data()));
+    VK_TRY(vk::msm_run_host(ctx, t, offset, scalars, n, mont, acc.data()));
     return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
 }
 

@@ -187,6 +187,7 @@ struct vc_ctx {
     // vc_ctx_set_option knobs (include/vc_msm.h VC_OPT_*)
     int opt_shared_windows = 1;           // GLV MSMs over a whole table: one bucket set via Table::win
     size_t opt_msm_chunk = size_t(1) << 27;  // MSMs above this many points run as summed chunks
+    int opt_host_chunks = 2;                 // vc_msm: scalar copies in this many chunks (msm_run_host)
     uint32_t fb_lanes = 0;                // resident lanes of k_fb_commit_cm (cached per context)
     // geometry of the last MSM (vc_msm_last_plan): window bits c, windows W (of the whole MSM),
     // terms per point (2 with the GLV split), radix multiplier m (radix m 2^c; 1 = 2^c), shared
@@ -234,6 +235,9 @@ namespace vk {
 // implemented per translation unit with explicit instantiations
 int device_mad_rate(vc_ctx* ctx, double* tera_per_s);
 int msm_windows(int curve, size_t n, int* c, int* W, int* terms);
+// vc_msm: scalars in host memory (chunked copies under the previous chunk's kernels where the
+// geometry allows, msm.hip msm_run_host_chunks_t)
+int msm_run_host(vc_ctx* ctx, Table* t, size_t offset, const uint64_t* host_sc, size_t n, int mont, uint32_t* out_acc);
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,
             uint32_t* out_acc, int part = 0, int parts = 1);
 // K MSMs over the whole table t (scalar set k at d_scalars[k], Montgomery flag mont[k]) -> K

@@ -408,13 +408,38 @@ struct is_affp : std::false_type {};
 template <class FC, class BT>
 struct is_affp<FC, BT, std::void_t<typename FC::AffP>> : std::is_same<BT, typename FC::AffP> {};
 
+// straddle merge inside the accumulate (A/B knob VKZG_ACC_MERGE). Off by default: measured slower
+// (accumulate +0.087 ms, the remaining fix-up 0.083 -> 0.158 ms; profiles/r04/merge_ab/)
+static uint32_t acc_merge() {
+    static const uint32_t v = getenv("VKZG_ACC_MERGE") ? (uint32_t)atoi(getenv("VKZG_ACC_MERGE")) : 0u;
+    return v;
+}
+
+// one lane's value from lane + 1 of the wave (word by word through ds_bpermute)
+template <class T>
+__device__ __forceinline__ T shfl_down1(const T& v) {
+    static_assert(sizeof(T) % 4 == 0, "");
+    constexpr int NW = (int)(sizeof(T) / 4);
+    uint32_t w[NW];
+    __builtin_memcpy(w, &v, sizeof w);
+#pragma unroll
+    for (int k = 0; k < NW; k++) w[k] = (uint32_t)__shfl_down((int)w[k], 1);
+    T r;
+    __builtin_memcpy(&r, w, sizeof w);
+    return r;
+}
+
+// merge: the owner piece of a straddling bucket whose only carry piece is in the next lane of the
+// same wave is added here, after the loop (one general add per lane, all lanes together), and its
+// bucket written: owner_bucket[t] is cleared so the fix-up kernels skip it. Left for the fix-up:
+// lane 63's straddles (the next lane is in another wave) and chains over three or more threads.
 template <class C, class BT = typename C::Aff>
 __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     const BT* __restrict__ bases, const BT* __restrict__ phi, uint32_t nphi,
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename Fast29<C>::type::Acc* __restrict__ buckets, typename Fast29<C>::type::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename Fast29<C>::type::Acc* __restrict__ owner_piece,
-    uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max) {
+    uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max, uint32_t merge) {
     using FC = typename Fast29<C>::type;
     using Aff = BT;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -463,6 +488,7 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     };
     uint32_t idx = sorted[k];
     Pre P = fetch(idx);
+    uint32_t my_through = 0, own_b = NONE;  // for the merge after the loop
     while (true) {
         uint32_t cur = idx;
         typename FC::Aff Q;
@@ -480,7 +506,8 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
                 buckets[b] = acc;
             } else if (left_open) {
                 carry_in[t] = acc;
-                through[t] = right_open ? 2 : 1;  // 1: carry piece ending here, 2: bucket continues
+                my_through = right_open ? 2 : 1;
+                through[t] = (uint8_t)my_through;  // 1: carry piece ending here, 2: bucket continues
                 if (!right_open) {  // chain end: chain length = carry threads of this bucket
                     const uint32_t L = t - offsets[b] / M;
                     if (L >= 2) atomicMax(chain_max, L);
@@ -488,6 +515,7 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
             } else {
                 owner_piece[t] = acc;
                 owner_bucket[t] = b;
+                own_b = b;  // acc keeps the owner piece: it is the thread's last bucket
             }
             if (k == e) break;
             left_open = false;
@@ -496,6 +524,16 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
                 b++;
                 bend = offsets[b + 1];
             } while (bend <= k);
+        }
+    }
+    if (merge) {  // uniform
+        // the next lane's carry piece (its own store, read back by the thread that wrote it)
+        const typename FC::Acc mine = my_through == 1 ? carry_in[t] : FC::zero();
+        const typename FC::Acc nxt = shfl_down1(mine);
+        const uint32_t nth = (uint32_t)__shfl_down((int)my_through, 1);
+        if (own_b != NONE && (threadIdx.x & 63u) != 63u && nth == 1) {
+            buckets[own_b] = FC::add(acc, nxt);
+            owner_bucket[t] = NONE;
         }
     }
 }
@@ -1162,6 +1200,11 @@ struct MsmSlice {
     Acc* tail = nullptr;
     std::vector<Acc> ht;
     uint32_t Lmax = 0;
+    // chunked MSMs (msm_run_host_chunks_t): the accumulate writes these buckets instead of the
+    // workspace's, the chain word is this one, and the reduction is left to the caller
+    FAcc<C>* bucket_dst = nullptr;
+    uint32_t* chain_dst = nullptr;
+    bool skip_reduce = false;
     // BLS12-381 radix digits still to be made (msm_run_t leaves the GLV split to slice_enqueue,
     // which fuses the sort histogram into it when the geometry allows): sc == nullptr otherwise
     struct {
@@ -1306,10 +1349,10 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.nU = nU;
     sl.offsets = ws[WS_OFFSETS].as<uint32_t>();
     sl.tail_bytes = tail_bytes;
-    sl.chain_max = reinterpret_cast<uint32_t*>(ws[WS_TAIL].as<uint8_t>() + tail_bytes);
+    sl.chain_max = sl.chain_dst ? sl.chain_dst : reinterpret_cast<uint32_t*>(ws[WS_TAIL].as<uint8_t>() + tail_bytes);
     sl.through = ws[WS_THROUGH].as<uint8_t>();
     sl.owner_b = ws[WS_OWNER_B].as<uint32_t>();
-    sl.buckets = ws[WS_BUCKETS].as<RAcc>();
+    sl.buckets = sl.bucket_dst ? sl.bucket_dst : ws[WS_BUCKETS].as<RAcc>();
     sl.carry = ws[WS_CARRY].as<RAcc>();
     sl.owner = ws[WS_OWNER].as<RAcc>();
     sl.seg = ws[WS_SEG].as<RAcc>();
@@ -1351,7 +1394,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
     VK_LAUNCH_ON(ctx, st, "msm_accumulate", (k_msm_accumulate<C, BT>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi,
                  ws[WS_SORTED].as<uint32_t>(), sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
-                 sl.owner_b, sl.chain_max);
+                 sl.owner_b, sl.chain_max, acc_merge());
     if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
     // chains up to 2^guard carry pieces are walked serially by their owners; longer ones
     // (adversarial scalars) take the pointer-jumping path in slice_finish
@@ -1366,6 +1409,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     else
         VK_TRY(msm_tail_fixup_walk<C>(ctx, L, sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.owner, 1u << sl.guard,
                                       sl.owner_b, sl.through, Tmax));
+    if (sl.skip_reduce) return VC_OK;
     VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, Wr, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
                               sl.tail, nU > 1));
     return VC_OK;
@@ -2007,7 +2051,7 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_TRY(d_raw.ensure(nch * sizeof(RAcc)));
         VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C, FA>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
                   d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
-                  d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max);
+                  d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max, acc_merge());
         // straddling chunks merged by the serial walk of their owners, no chain limit: a chunk holds at
         // most CHNZ x W entries, so it spans at most CHNZ W / M + 2 threads. (The pointer-jumping rounds
         // used before read the longest chain back first -- a host sync per level -- and ran ~3 guarded
@@ -2075,6 +2119,170 @@ static int msm_run_chunked(vc_ctx* ctx, Table* t, size_t offset, const uint32_t*
     }
     memcpy(out_acc, &res, sizeof(Acc));
     return VC_OK;
+}
+
+// chunked host-scalar MSM: chunk j's buckets added into the running set (first: empty buckets
+// set to the identity, so the one reduction after the last chunk reads every bucket as live)
+template <class A>
+__global__ void __launch_bounds__(256) k_bucket_merge(typename A::Acc* __restrict__ acc,
+                                                     const typename A::Acc* __restrict__ add,
+                                                     const uint32_t* __restrict__ offsets, uint32_t NBtot,
+                                                     uint32_t first) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= NBtot) return;
+    const bool ne = offsets[b + 1] > offsets[b];
+    if (first) {
+        if (!ne) acc[b] = A::zero();
+    } else if (ne) {
+        acc[b] = A::add(acc[b], add[b]);
+    }
+}
+__global__ void k_iota(uint32_t* __restrict__ o, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) o[i] = i;
+}
+
+// vc_msm with host scalars (the drop-in `commit` of INTEGRATION.md over utils.rs:16-19): the
+// 32 n bytes cross PCIe in K chunks on the side stream while the context's stream runs the
+// previous chunk -- each chunk a point-range MSM on the table's radix shared-window copies (GLV
+// split + histogram, sort, accumulate, fix-up) whose buckets add into one set -- and ONE
+// reduction + host fold finish it. Only for that geometry (BLS12-381, GLV, radix copies);
+// *done = false otherwise (the caller copies and runs msm_run). A chunk whose fix-up chains
+// exceed its walk (adversarial scalars) sends the whole MSM to msm_run_t once the scalars are in.
+template <class C, class Fr>
+static int msm_run_host_chunks_t(vc_ctx* ctx, Table* t, size_t offset, const uint64_t* host_sc, size_t n, int mont,
+                                 int K, uint32_t* out_acc, bool* done) {
+    *done = false;
+    if constexpr (!std::is_same<C, BLS381G1>::value) {
+        return VC_OK;
+    } else {
+        using Acc = typename C::Acc;
+        using A = typename Fast29<C>::type;
+        using RAcc = FAcc<C>;
+        static const int radix_env = getenv("VKZG_MSM_RADIX") ? atoi(getenv("VKZG_MSM_RADIX")) : 5;
+        static const int range_env = getenv("VKZG_MSM_RANGE") ? atoi(getenv("VKZG_MSM_RANGE")) : 1;
+        if (K < 2 || K > 4 || n >= (1u << 30) || !ctx->opt_shared_windows || radix_env != 5 || !range_env ||
+            getenv("VKZG_MSM_C") || getenv("VKZG_WIN_PACKED") || 2 * (size_t)t->n < (1u << 19))
+            return VC_OK;
+        // chunks of whole 8192-scalar sort blocks, each >= 2^16 points (a point range on the copies)
+        const size_t blk = 8192, nb = (n + blk - 1) / blk;
+        if (nb < (size_t)K || n / K < (1u << 16)) return VC_OK;
+        bool glv = false;
+        VK_TRY(glv_table_ok(ctx, t, &glv));
+        if (!glv) return VC_OK;
+        VK_TRY(fast_tables<C>(ctx, t, true));
+        {
+            const size_t win_bytes = (size_t)7 * 2 * t->n *
+                                     (win_pair_on() ? 2 * sizeof(typename A::AffP) : sizeof(typename A::AffN));
+            if (win_bytes > (8ull << 30)) return VC_OK;
+            const int st = win_tables<C>(ctx, t, 16, 7, 0, 5, win_pair_on());
+            if (st == VC_E_OOM) {
+                t->win.release();
+                return VC_OK;
+            }
+            VK_TRY(st);
+        }
+        ctx->plan = {16, 7, 2, 5, 1};
+        const uint32_t NB = 5u << 15;
+        std::vector<size_t> lo(K + 1);
+        for (int j = 0; j <= K; j++) lo[j] = std::min(n, (nb * j / K) * blk);
+        size_t nmax = 0;
+        for (int j = 0; j < K; j++) nmax = std::max(nmax, lo[j + 1] - lo[j]);
+        VK_TRY(ctx->ws[WS_SCALARS].ensure(n * 32));
+        VK_TRY(ctx->ws[WS_GLV_SC].ensure(2 * nmax * 4 * 7));
+        VK_TRY(ctx->ws[WS_BUCKETS].ensure((size_t)NB * sizeof(RAcc)));
+        VK_TRY(ctx->ws2[WS_BUCKETS].ensure((size_t)NB * sizeof(RAcc)));
+        VK_TRY(ctx->ws2[WS_CHAIN].ensure(16));
+        VK_TRY(ctx->ws2[WS_OFFSETS].ensure(((size_t)NB + 1) * 4));
+        uint8_t* d_sc = ctx->ws[WS_SCALARS].as<uint8_t>();
+        RAcc* bA = ctx->ws[WS_BUCKETS].as<RAcc>();
+        RAcc* bB = ctx->ws2[WS_BUCKETS].as<RAcc>();
+        uint32_t* chain = ctx->ws2[WS_CHAIN].as<uint32_t>();
+        std::vector<hipEvent_t> ev(K);
+        for (int j = 0; j < K; j++) ev[j] = ctx->get_event();
+        MsmSlice<C> sl;
+        std::vector<uint32_t> guard(K);
+        for (int j = 0; j < K; j++) {
+            const size_t nj = lo[j + 1] - lo[j];
+            // chunk j's scalars on the side stream, issued after chunk j - 1's kernels are queued (a
+            // pageable copy can block the host until its data is staged)
+            VK_CHECK_HIP(hipMemcpyAsync(d_sc + lo[j] * 32, host_sc + lo[j] * 4, nj * 32, hipMemcpyHostToDevice,
+                                        ctx->side_stream));
+            VK_CHECK_HIP(hipEventRecord(ev[j], ctx->side_stream));
+            VK_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ev[j], 0));
+            sl = MsmSlice<C>();
+            sl.L = ctx->lane(0);
+            sl.c = 16;
+            sl.wb = 0;
+            sl.we = 7;
+            sl.W = 7;
+            sl.shared = true;
+            sl.m = 5;
+            sl.wps = 7;
+            sl.bucket_dst = j == 0 ? bA : bB;
+            sl.chain_dst = chain + j;
+            sl.skip_reduce = true;
+            sl.radix.sc = {reinterpret_cast<const uint32_t*>(d_sc + lo[j] * 32)};
+            sl.radix.mont = {mont};
+            sl.radix.inf = t->inf.as<uint8_t>() + offset + lo[j];
+            sl.radix.n = (uint32_t)nj;
+            sl.radix.dig = ctx->ws[WS_GLV_SC].as<int32_t>();
+            RadixDigits rd{ctx->ws[WS_GLV_SC].as<int32_t>(), (uint32_t)(2 * nj)};
+            rd.off = (uint32_t)(offset + lo[j]);
+            rd.half = (uint32_t)nj;
+            rd.gap = (uint32_t)(t->n - nj);
+            sl.stride = (uint32_t)(2 * t->n);
+            if (t->win_pair) {
+                const auto* wp = t->win.as<typename A::AffP>();
+                VK_TRY(slice_enqueue<C>(ctx, sl, rd, 2 * nj, wp, wp, 0xffffffffu, nullptr, nullptr));
+            } else {
+                const auto* wn = t->win.as<typename A::AffN>();
+                VK_TRY(slice_enqueue<C>(ctx, sl, rd, 2 * nj, wn, wn, 0xffffffffu, nullptr, nullptr));
+            }
+            guard[j] = sl.guard;
+            VK_LAUNCH(ctx, "msm_merge", (k_bucket_merge<A>), (NB + 255) / 256, 256, 0, bA, bB, sl.offsets, NB,
+                      j == 0 ? 1u : 0u);
+        }
+        // one reduction over the merged set: every bucket live (empty ones hold the identity)
+        uint32_t* iota = ctx->ws2[WS_OFFSETS].as<uint32_t>();
+        VK_LAUNCH(ctx, "msm_iota", k_iota, (NB + 1 + 255) / 256, 256, 0, iota, NB);
+        VK_TRY(msm_tail_reduce<C>(ctx, sl.L, bA, iota, sl.NB, sl.Wr, sl.Lseg, sl.S, sl.J, sl.seg, sl.rs, sl.bsum_part,
+                                  sl.tail, sl.nU > 1));
+        // the tail buffer's own chain word (read by slice_finish) was not used by the chunks
+        VK_CHECK_HIP(hipMemsetAsync(reinterpret_cast<uint8_t*>(sl.tail) + sl.tail_bytes, 0, 4, ctx->stream));
+        VK_TRY(slice_fetch<C>(sl));
+        uint32_t hchain[4] = {0, 0, 0, 0};
+        VK_CHECK_HIP(hipMemcpyAsync(hchain, chain, 4 * K, hipMemcpyDeviceToHost, ctx->stream));
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        for (int j = 0; j < K; j++) ctx->event_pool.push_back(ev[j]);
+        for (int j = 0; j < K; j++)
+            if (hchain[j] > (1u << guard[j])) {  // long chains: the unchunked MSM over the copied scalars
+                *done = true;
+                return msm_run_t<C, Fr>(ctx, t, offset, reinterpret_cast<const uint32_t*>(d_sc), n, mont, 0, 1,
+                                        out_acc);
+            }
+        Acc res;
+        VK_TRY(slice_finish<C>(ctx, sl, &res));
+        memcpy(out_acc, &res, sizeof(Acc));
+        *done = true;
+        return VC_OK;
+    }
+}
+
+// vc_msm: host scalars
+int msm_run_host(vc_ctx* ctx, Table* t, size_t offset, const uint64_t* host_sc, size_t n, int mont,
+                 uint32_t* out_acc) {
+    if (t->curve == VC_CURVE_BLS12_381 && ctx->opt_host_chunks > 1 && ctx->opt_msm_chunk >= n) {
+        bool done = false;
+        VK_TRY((msm_run_host_chunks_t<BLS381G1, BLS381Fr>(ctx, t, offset, host_sc, n, mont, ctx->opt_host_chunks,
+                                                          out_acc, &done)));
+        if (done) return VC_OK;
+    }
+    if (n > 0) {
+        VK_TRY(ctx->ws[WS_SCALARS].ensure(n * 32));
+        VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_SCALARS].p, host_sc, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    }
+    return msm_run(ctx, t, offset, ctx->ws[WS_SCALARS].p, n, mont, out_acc, 0, 1);
 }
 
 int msm_run(vc_ctx* ctx, Table* t, size_t offset, const void* d_scalars, size_t n, int mont,

@@ -84,13 +84,14 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk(typename A::Acc* __restr
                                                        const typename A::Acc* __restrict__ carry,
                                                        const typename A::Acc* __restrict__ owner_piece,
                                                        const uint32_t* __restrict__ offsets, uint32_t NBtot,
-                                                       uint32_t M, uint32_t limit) {
+                                                       uint32_t M, uint32_t limit, const uint32_t* __restrict__ owner_b) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= NBtot) return;
     const uint32_t lo = offsets[b], hi = offsets[b + 1];
     if (hi <= lo) return;  // empty
     const uint32_t t0 = lo / M, t1 = (hi - 1) / M;
     if (t0 == t1 || t1 - t0 > limit) return;  // inside one thread (written) / long chain (host path)
+    if (owner_b && owner_b[t0] == NONE_T) return;  // merged inside the accumulate (written)
     typename A::Acc acc = owner_piece[t0];
     for (uint32_t u = t0 + 1; u <= t1; u++) acc = A::add(acc, carry[u]);
     buckets[b] = acc;
@@ -103,13 +104,14 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk_q(typename A::Acc* __res
                                                          const typename A::Acc* __restrict__ carry,
                                                          const typename A::Acc* __restrict__ owner_piece,
                                                          const uint32_t* __restrict__ offsets, uint32_t NBtot,
-                                                         uint32_t M, uint32_t limit) {
+                                                         uint32_t M, uint32_t limit, const uint32_t* __restrict__ owner_b) {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, b = gid >> 2, role = gid & 3;
     if (b >= NBtot) return;  // whole quads (NBtot * 4 threads)
     const uint32_t lo = offsets[b], hi = offsets[b + 1];
     if (hi <= lo) return;
     const uint32_t t0 = lo / M, t1 = (hi - 1) / M;
     if (t0 == t1 || t1 - t0 > limit) return;  // uniform over the quad
+    if (owner_b && owner_b[t0] == NONE_T) return;  // merged inside the accumulate (written)
     typename A::Acc acc = owner_piece[t0];
     for (uint32_t u = t0 + 1; u <= t1; u++) {
         const typename A::Acc o = carry[u];
@@ -577,12 +579,12 @@ int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t N
     if constexpr (A::quad) {
         if ((quad_env && NBtot <= 65536) || quad_env == 2) {
             VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk_q<A>), (uint32_t)(((size_t)NBtot * 4 + 255) / 256), 256,
-                         0, buckets, carry, owner, offsets, NBtot, M, limit);
+                         0, buckets, carry, owner, offsets, NBtot, M, limit, owner_b);
             return VC_OK;
         }
     }
     VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_walk<A>), (NBtot + 255) / 256, 256, 0, buckets, carry, owner,
-                 offsets, NBtot, M, limit);
+                 offsets, NBtot, M, limit, owner_b);
     return VC_OK;
 }
 

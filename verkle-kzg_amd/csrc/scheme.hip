@@ -1300,7 +1300,9 @@ __device__ __forceinline__ void mp_load(const uint32_t* __restrict__ f, const ui
     }
 }
 
-template <int NT, uint32_t LZ, uint32_t CH>
+// PF = 1: the next block's loads are issued before the current block's arithmetic, so every lane
+// keeps LZ x 32 B in flight while it multiplies (A/B knob VKZG_MP_PF)
+template <int NT, uint32_t LZ, uint32_t CH, int PF = 0>
 __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f, const uint32_t* __restrict__ rp,
                                                  const uint32_t* __restrict__ order, const uint32_t* __restrict__ be,
                                                  size_t N, uint32_t kblk, Fr* __restrict__ partial) {
@@ -1311,13 +1313,30 @@ __global__ void __launch_bounds__(256) k_mp_chunk(const uint32_t* __restrict__ f
     f29<P29> total = zero29<P29>();
     uint4 v[LZ][2];
     uint32_t qi[LZ];
+    if constexpr (PF) {
+        if (cnt > 0) mp_load<NT, LZ>(f, order, u0, min(cnt, LZ), N, k, v, qi);
+    }
 #pragma unroll
     for (uint32_t h = 0; h < CH; h += LZ) {
         if (h >= cnt) break;
         const uint32_t nq = min(cnt - h, LZ);
-        mp_load<NT, LZ>(f, order, u0 + h, nq, N, k, v, qi);
-        const f29<P29> r = mp_block<LZ>(v, qi, nq, rp);
-        total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
+        if constexpr (PF) {
+            uint4 w[LZ][2];
+            uint32_t qw[LZ];
+            if (h + LZ < cnt) mp_load<NT, LZ>(f, order, u0 + h + LZ, min(cnt - h - LZ, LZ), N, k, w, qw);
+            const f29<P29> r = mp_block<LZ>(v, qi, nq, rp);
+            total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
+#pragma unroll
+            for (uint32_t j = 0; j < LZ; j++) {
+                v[j][0] = w[j][0];
+                v[j][1] = w[j][1];
+                qi[j] = qw[j];
+            }
+        } else {
+            mp_load<NT, LZ>(f, order, u0 + h, nq, N, k, v, qi);
+            const f29<P29> r = mp_block<LZ>(v, qi, nq, rp);
+            total = csub29<P29>(carry29<P29>(add29_raw<P29>(total, r)));
+        }
     }
     total = csub29<P29>(carry29<P29>(total));
     pack29<P29>(total, partial[(size_t)c * N + k].v);
@@ -1353,9 +1372,10 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
         row[i] = row_of[z[i]];
     }
     // block / chunk shape of k_mp_chunk (VKZG_MP_SHAPE: 0 = 3 x 16, 1 = 4 x 16, 2 = 4 x 32, 3 = 6 x 24)
-    static const int shape_env = getenv("VKZG_MP_SHAPE") ? atoi(getenv("VKZG_MP_SHAPE")) : 0;
+    // 4 x 16 by default: 0.125-0.129 ms against 0.128-0.131 for 3 x 16 (profiles/r04/mp_shape_ab.txt)
+    static const int shape_env = getenv("VKZG_MP_SHAPE") ? atoi(getenv("VKZG_MP_SHAPE")) : 1;
     static const MpShape shapes[4] = {{3, 16}, {4, 16}, {4, 32}, {6, 24}};
-    const MpShape shp = shapes[shape_env >= 0 && shape_env < 4 ? shape_env : 0];
+    const MpShape shp = shapes[shape_env >= 0 && shape_env < 4 ? shape_env : 1];
     const uint32_t MP_CHUNK = shp.ch;
     // counting sort of the shard's queries by row, then chunks of <= MP_CHUNK queries
     std::vector<uint32_t> cnt(Z + 1, 0), order(Qs);
@@ -1391,10 +1411,12 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
     // (profiles/r04/mp_nt_ab.txt)
     static const int nt_env = getenv("VKZG_MP_NT") ? atoi(getenv("VKZG_MP_NT")) : 1;
     using KFn = void (*)(const uint32_t*, const uint32_t*, const uint32_t*, const uint32_t*, size_t, uint32_t, Fr*);
-    static const KFn kerns[2][4] = {
+    static const int pf_env = getenv("VKZG_MP_PF") ? atoi(getenv("VKZG_MP_PF")) : 0;
+    static const KFn kerns[3][4] = {
         {k_mp_chunk<0, 3, 16>, k_mp_chunk<0, 4, 16>, k_mp_chunk<0, 4, 32>, k_mp_chunk<0, 6, 24>},
-        {k_mp_chunk<1, 3, 16>, k_mp_chunk<1, 4, 16>, k_mp_chunk<1, 4, 32>, k_mp_chunk<1, 6, 24>}};
-    const KFn kern = kerns[nt_env ? 1 : 0][shape_env >= 0 && shape_env < 4 ? shape_env : 0];
+        {k_mp_chunk<1, 3, 16>, k_mp_chunk<1, 4, 16>, k_mp_chunk<1, 4, 32>, k_mp_chunk<1, 6, 24>},
+        {k_mp_chunk<1, 3, 16, 1>, k_mp_chunk<1, 4, 16, 1>, k_mp_chunk<1, 4, 32, 1>, k_mp_chunk<1, 6, 24, 1>}};
+    const KFn kern = kerns[pf_env ? 2 : nt_env ? 1 : 0][shape_env >= 0 && shape_env < 4 ? shape_env : 1];
     VK_LAUNCH(ctx, "mp_chunk", kern, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
               d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
     VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,

@@ -154,6 +154,7 @@ class Engine:
     # vc_ctx_set_option knobs (include/vc_msm.h)
     OPT_MSM_SHARED_WINDOWS = 1
     OPT_MSM_CHUNK_POINTS = 2
+    OPT_MSM_HOST_CHUNKS = 3
 
     def set_option(self, option, value):
         check(lib().vc_ctx_set_option(self.h, option, int(value)), "vc_ctx_set_option")
