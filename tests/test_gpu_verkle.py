@@ -49,11 +49,16 @@ def _schemes(eng):
     return {"kzg": (kzg.table, kzg_commit), "ipa": (ipa.table, ipa_commit)}
 
 
+@pytest.mark.parametrize("dense", ["auto", "0", "1"])
 @pytest.mark.parametrize("scheme_name", ["kzg", "ipa"])
 @pytest.mark.parametrize("N,arity,n", [(3, 255, 120), (3, 6, 60), (4, 4, 50), (5, 3, 40)])
-def test_verkle_commitment_matches_oracle(eng, oracle_c, scheme_name, N, arity, n):
+def test_verkle_commitment_matches_oracle(eng, oracle_c, scheme_name, N, arity, n, dense, monkeypatch):
+    """dense: the level commits' path (VKZG_VERKLE_DENSE, read per call) -- auto (dense rows where
+    B x width is small or half full, sparse otherwise), 0 = every level sparse, 1 = every level dense."""
     from pyoracle import verkle as ov
     from vkzg.verkle import VerkleTree
+    if dense != "auto":
+        monkeypatch.setenv("VKZG_VERKLE_DENSE", dense)
     table, commit = _schemes(eng)[scheme_name]
     rng = random.Random(7 * N + arity)
     t, o = VerkleTree(N), ov.VerkleTree(N)

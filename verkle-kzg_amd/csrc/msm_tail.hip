@@ -136,17 +136,32 @@ __global__ void __launch_bounds__(256) k_msm_fixup_own(typename A::Acc* __restri
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t T = (*Lp + M - 1) / M;
     if (t >= T || t >= Tmax) return;
+    // the owner's piece, the next thread's carry piece and its through flag are loaded with the
+    // owner word, not after it: one memory latency instead of a chain of three (the kernel waited
+    // on loads 37 % of its wave cycles: profiles/r04/tail_pmc/). Threads t < T - 1 have a slot
+    // t + 1 in the through / carry arrays (written or zeroed by the accumulate's threads < T).
+    const bool nx = t + 1 < T;
     const uint32_t b = owner_bucket[t];
+    const uint8_t th1 = nx ? through[t + 1] : (uint8_t)0;
+    typename A::Acc acc = owner_piece[t];
+    typename A::Acc c1 = nx ? carry[t + 1] : A::zero();
     if (b == NONE_T) return;
     // an owner piece exists only when the bucket continues into t + 1, so the chain ends in a
     // thread u1 < T with through[u1] == 1
     uint32_t u1 = t + 1;
-    while (through[u1] == 2) {
-        if (u1 - t >= limit) return;  // longer than the walk takes: host path
+    if (th1 == 2) {  // longer chains (rare)
         u1++;
+        while (through[u1] == 2) {
+            if (u1 - t >= limit) return;  // longer than the walk takes: host path
+            u1++;
+        }
     }
-    typename A::Acc acc = owner_piece[t];
-    for (uint32_t u = t + 1; u <= u1; u++) acc = A::add(acc, carry[u]);
+    // one add call site (an inlined add is ~34 KB of code: two would not share the I-cache)
+    for (uint32_t u = t + 1;; u++) {
+        acc = A::add(acc, c1);
+        if (u == u1) break;
+        c1 = carry[u + 1];
+    }
     buckets[b] = acc;
 }
 

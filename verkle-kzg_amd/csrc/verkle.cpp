@@ -361,7 +361,11 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     auto build_rows = [&](size_t lo, size_t hi, size_t nnz_per, auto fn) {
         Rows out;
         const size_t count = hi - lo;
-        const unsigned T = count >= 4096 ? pool.size() : 1;
+        // by work, not rows: the 256 depth-1 nodes of a 65,536-key tree hold ~41K children (a
+        // serial walk of their maps took 0.84 ms: profiles/r04/verkle/laps_before.txt)
+        const unsigned T = (count >= 64 && count * nnz_per >= 16384)
+                               ? (unsigned)std::min<size_t>(pool.size(), std::max<size_t>(1, count / 16))
+                               : 1;
         if (T == 1) {
             out.reserve(count, count * nnz_per);
             for (size_t i = lo; i < hi; i++) fn(i, out);
@@ -405,13 +409,37 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     };
     lap("collect dirty");
     // outputs are written in full by the two calls (uninitialised staging, host/pool.hpp uvec)
-    auto commit_rows = [&](const Rows& r, uvec<uint64_t>& xy, uvec<uint8_t>& inf, uvec<uint64_t>& items) -> int {
+    // dense rows (vc_msm_batch: the fixed-base batched commit over the first `width` bases) for
+    // levels of <= 64 rows (its latency path: the root's one commit 0.44 -> 0.11 ms) -- the sparse
+    // path's ~10 latency-bound launches and host round trips cost ~0.35 ms even for one row;
+    // larger levels stay sparse (dense measured slower at 65 rows, equal at 65,536 x 4:
+    // profiles/r04/verkle/). VKZG_VERKLE_DENSE (read per call) forces one path:
+    // 0 = sparse, 1 = dense
+    const char* dense_env = getenv("VKZG_VERKLE_DENSE");
+    const int dense_mode = dense_env ? atoi(dense_env) : -1;
+    uvec<uint64_t> dense;
+    auto commit_rows = [&](const Rows& r, size_t width, uvec<uint64_t>& xy, uvec<uint8_t>& inf,
+                           uvec<uint64_t>& items) -> int {
         const size_t B = r.n();
         xy.resize(B * 8);
         inf.resize(B);
         items.resize(B * 4);
         if (B == 0) return VC_OK;
         lap("build rows");
+        const bool use_dense = !mu && (dense_mode == 1 || (dense_mode != 0 && B <= 64 && B * width <= 16384));
+        if (use_dense) {
+            dense.resize(B * width * 4);
+            for_each(B, [&](size_t b) {
+                uint64_t* row = &dense[b * width * 4];
+                memset(row, 0, width * 32);
+                for (uint64_t e = r.ptr[b]; e < r.ptr[b + 1]; e++) memcpy(row + 4 * (size_t)r.cols[e], &r.vals[4 * e], 32);
+            });
+            VK_TRY(vc_msm_batch(ctx, table, width, dense.data(), B, 0, xy.data(), inf.data()));
+            lap("dense commit");
+            const int st = vc_to_data_item_batch(ctx, xy.data(), inf.data(), B, items.data());
+            lap("to_data_item");
+            return st;
+        }
         if (mu) {  // member k commits rows [B k / G, B (k + 1) / G) of the level on its own device
             const int G = (int)mu->ctx.size();
             std::vector<int> st(G, VC_OK);
@@ -529,7 +557,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                 r.end_row();
             }
         });
-        int st = commit_rows(r12, xy, inf, items);
+        int st = commit_rows(r12, (size_t)N, xy, inf, items);
         Rows rx;
         if (st == VC_OK) rx = build_rows(lo, hi, 4, [&](size_t e, Rows& r) {
             const VNode& n = t->nodes[exts[e]];
@@ -541,7 +569,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             r.add(3, &items[(2 * (e - lo) + 1) * 4]);
             r.end_row();
         });
-        if (st == VC_OK) st = commit_rows(rx, xy2, inf2, items2);
+        if (st == VC_OK) st = commit_rows(rx, 4, xy2, inf2, items2);
         VK_TRY(store_level(exts, lo, hi, xy2, inf2, items2, st));
     }
     // internal nodes, deepest level first (HACK in the reference: width hard-coded 256); a
@@ -550,11 +578,13 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         const std::vector<int>& lv = internals[depth];
         size_t lo, hi;
         slice(lv.size(), &lo, &hi);
-        Rows ri = build_rows(lo, hi, 4, [&](size_t b, Rows& r) {
+        size_t kids = 0;  // children of the slice (the rows' non-zero bound)
+        for (size_t b = lo; b < hi; b++) kids += t->nodes[lv[b]].children.v.size();
+        Rows ri = build_rows(lo, hi, hi > lo ? (kids + hi - lo - 1) / (hi - lo) : 1, [&](size_t b, Rows& r) {
             for (auto& kv : t->nodes[lv[b]].children) r.add(kv.first, t->nodes[kv.second].item);
             r.end_row();
         });
-        const int st = commit_rows(ri, xy, inf, items);
+        const int st = commit_rows(ri, 256, xy, inf, items);
         VK_TRY(store_level(lv, lo, hi, xy, inf, items, st));
     }
     memcpy(out_xy, t->nodes[0].cxy, 64);
