@@ -2200,6 +2200,15 @@ static int msm_run_host_chunks_t(vc_ctx* ctx, Table* t, size_t offset, const uin
         uint32_t* chain = ctx->ws2[WS_CHAIN].as<uint32_t>();
         std::vector<hipEvent_t> ev(K);
         for (int j = 0; j < K; j++) ev[j] = ctx->get_event();
+        // on every exit (errors included): no copy still reading the caller's buffer, events back
+        struct Done {
+            vc_ctx* ctx;
+            std::vector<hipEvent_t>& ev;
+            ~Done() {
+                (void)hipStreamSynchronize(ctx->side_stream);
+                for (hipEvent_t e : ev) ctx->event_pool.push_back(e);
+            }
+        } done_guard{ctx, ev};
         MsmSlice<C> sl;
         std::vector<uint32_t> guard(K);
         for (int j = 0; j < K; j++) {
@@ -2254,7 +2263,6 @@ static int msm_run_host_chunks_t(vc_ctx* ctx, Table* t, size_t offset, const uin
         uint32_t hchain[4] = {0, 0, 0, 0};
         VK_CHECK_HIP(hipMemcpyAsync(hchain, chain, 4 * K, hipMemcpyDeviceToHost, ctx->stream));
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-        for (int j = 0; j < K; j++) ctx->event_pool.push_back(ev[j]);
         for (int j = 0; j < K; j++)
             if (hchain[j] > (1u << guard[j])) {  // long chains: the unchunked MSM over the copied scalars
                 *done = true;
