@@ -432,11 +432,12 @@ def mp_reference_shapes(ipa, N, cxy, cinf, z, y, d_all, dev, reps=5, cpu=None):
             break
         cq, ciq, zq, yq = (np.ascontiguousarray(v[:q]) for v in (cxy, cinf, z, y))
 
-        def prove():
-            tr, r, rows = scheme.multiproof_begin(N, cq, ciq, zq, yq)
+        def prove():  # phases 1 + 2 in one call: the transcript overlapped with the planning
+            rows = scheme.multiproof_rows(N, zq)
             S = torch.empty((rows, N, 4), dtype=torch.int64, device=dev)
             torch.cuda.current_stream(dev).synchronize()
-            scheme.multiproof_accumulate(ipa.engine, N, zq, 0, q, d_all.data_ptr(), r, S.data_ptr())
+            tr, _r = scheme.multiproof_begin_accumulate(ipa.engine, N, cq, ciq, zq, yq, 0, q, d_all.data_ptr(),
+                                                        S.data_ptr())
             return scheme.multiproof_finish(ipa, zq, S.data_ptr(), 1, tr)
 
         def verify(mp):

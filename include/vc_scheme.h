@@ -149,6 +149,14 @@ int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_
  *   rows x N x 4 u64 (canonical, device). z = ALL Q points (it fixes the rows). */
 int vc_multiproof_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* z, size_t first, size_t Qs,
                              const void* d_data, const uint64_t* r, void* d_S);
+/* phases 1 + 2 in one call, the host transcript on a helper thread while the calling thread sorts
+ *   this shard's queries by point and uploads the plan (only the per-point sums wait for r): the
+ *   same transcript, r and S as vc_multiproof_begin + vc_multiproof_accumulate. rows (the size of
+ *   d_S) from vc_multiproof_rows. On error no transcript is returned. */
+int vc_multiproof_rows(size_t N, size_t Q, const uint64_t* z, size_t* rows);
+int vc_multiproof_begin_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                                   const uint64_t* z, const uint64_t* y, size_t first, size_t Qs, const void* d_data,
+                                   void* d_S, vc_transcript** transcript, uint64_t* r);
 /* phase 3: G shards' S matrices (device, contiguous, e.g. an all-gather) are summed; then
  *   quotients, g, D, t, h, E and the inner proof (:129-175). Advances `transcript`. */
 int vc_multiproof_finish(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, const uint64_t* z,

@@ -183,3 +183,32 @@ def test_multiproof_n256_kzg_vs_oracle(eng):
     want = mpcheck.multiproof(okz, N, data, cxy, cinf, z, nthreads=NT)
     assert got["d"] == want["d"]
     assert got["proof"]["proof"] == want["proof"]["proof"] and got["proof"]["y"] == want["proof"]["y"]
+
+
+def test_multiproof_begin_accumulate_equals_phases(eng, crs):
+    """vc_multiproof_begin_accumulate (the transcript on a helper thread while the shard is planned)
+    gives the r and the per-point sums S of vc_multiproof_begin + vc_multiproof_accumulate, for
+    the whole query set and for a shard; the transcripts then finish to the same proof."""
+    import torch
+    from vkzg import scheme
+    N, Q = 256, 4096
+    data, z = _inputs(Q, N, seed=9)
+    ipa = scheme.IPA(eng, N, crs)
+    d_all, cxy, cinf = _commit_device(eng, ipa.table, N, data)
+    y = np.ascontiguousarray(data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)])
+    rows = scheme.multiproof_rows(N, z)
+    assert rows == N
+    for lo, hi in ((0, Q), (1000, 2500)):
+        tr_a, r_a, rows_a = scheme.multiproof_begin(N, cxy, cinf, z, y)
+        S_a = torch.zeros((rows, N, 4), dtype=torch.int64, device="cuda")
+        d_slice = d_all[lo * N:hi * N]
+        scheme.multiproof_accumulate(eng, N, z, lo, hi - lo, d_slice.data_ptr(), r_a, S_a.data_ptr())
+        S_b = torch.zeros((rows, N, 4), dtype=torch.int64, device="cuda")
+        tr_b, r_b = scheme.multiproof_begin_accumulate(eng, N, cxy, cinf, z, y, lo, hi - lo, d_slice.data_ptr(),
+                                                       S_b.data_ptr())
+        torch.cuda.synchronize()
+        assert rows_a == rows and np.array_equal(r_a, r_b)
+        assert torch.equal(S_a, S_b)
+        pa = scheme.multiproof_finish(ipa, z, S_a.data_ptr(), 1, tr_a)
+        pb = scheme.multiproof_finish(ipa, z, S_b.data_ptr(), 1, tr_b)
+        assert pa["d"] == pb["d"] and pa["proof"].l == pb["proof"].l and pa["proof"].tip == pb["proof"].tip

@@ -79,3 +79,30 @@ def test_verkle_commitment_matches_oracle(eng, oracle_c, scheme_name, N, arity, 
     assert t.stats()["dirty"] > 0
     assert t.commitment(eng, table) == o.commitment(commit)
     assert t.stats()["dirty"] == 0
+
+
+def test_verkle_update_equals_fresh_tree(eng):
+    """A 40,000-key tree (32-unit keys) committed, 1 % of the keys rewritten, committed again
+    (only the dirty nodes: levels of a few hundred rows with ~150 children each, whose rows are
+    built on part of the host pool) == a fresh tree of the final contents committed in full."""
+    import numpy as np
+    from vkzg import scheme
+    from vkzg.verkle import VerkleTree
+    kzg = scheme.KZG(eng, 256)
+    rng = np.random.default_rng(5)
+    nk = 40_000
+    keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    t = VerkleTree(32)
+    for i in range(nk):
+        t.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    t.commitment(eng, kzg.table)
+    for i in rng.choice(nk, size=nk // 100, replace=False):
+        vals[i] = rng.integers(0, 256, size=32, dtype=np.uint8)
+        t.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    assert t.stats()["dirty"] > 0
+    got = t.commitment(eng, kzg.table)
+    f = VerkleTree(32)
+    for i in range(nk):
+        f.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    assert got == f.commitment(eng, kzg.table)

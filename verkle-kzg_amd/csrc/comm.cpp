@@ -14,6 +14,7 @@
 
 #include "../../include/vc_comm.h"
 #include "comm.hpp"
+#include "scheme_internal.hpp"
 #include "ctx.hpp"
 
 namespace {
@@ -344,7 +345,8 @@ int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int tabl
     vk::shard_range(Q, comm->rank, comm->world, &lo, &hi);
     // this rank's share up to the exchange; its status is agreed on before the device all-gather
     // (a rank without its S buffer cannot enter that collective)
-    int st = vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows);
+    // rows of S = the distinct z (validated here, as the begin call would)
+    int st = vk::mp_rows(N, Q, z, &rows);
     const size_t sbytes = rows * N * 32;
     uint8_t* dS = nullptr;
     if (st == VC_OK) {
@@ -353,7 +355,8 @@ int vc_multiproof_prove_sharded(vc_ctx* ctx, vc_comm* comm, int scheme, int tabl
         st = comm->work.ensure(sbytes * (comm->world + 1));
         if (st == VC_OK) {
             dS = reinterpret_cast<uint8_t*>(comm->work.p);
-            st = vc_multiproof_accumulate(ctx, N, Q, z, lo, hi - lo, d_data_slice, r, dS);
+            // the host transcript overlapped with the shard's plan (scheme.hip mp_begin_accumulate)
+            st = vk::mp_begin_accumulate(ctx, N, Q, com_xy, com_inf, z, y, lo, hi - lo, d_data_slice, dS, &tr, r);
         }
     }
     st = agree(comm, ctx, st);

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -1354,16 +1355,31 @@ __global__ void k_mp_chunk_reduce(const Fr* __restrict__ partial, const uint32_t
 }
 
 // rows of S are the distinct query points zval (sorted, over ALL queries -- every shard
-// uses the same rows so the shards' S add up); Z = zval.size()
-static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, const uint64_t* z, const Fr& r,
-                         size_t first, const std::vector<uint32_t>& zval, void* d_S) {
+// uses the same rows so the shards' S add up); Z = zval.size().
+// The shard's plan depends on z alone (not on the challenge r): rows, the counting sort of the
+// queries by row, chunks of <= CH queries inside a row, and their uploads -- so mp_begin_accumulate
+// builds it while the host transcript that yields r runs on another thread.
+struct MpPlan {
+    size_t Qs = 0, first = 0, Z = 0;
+    uint32_t nch = 0;
+    std::vector<uint32_t> order, be, zc;  // alive until mp_run's sync (async uploads)
+    DevBuf d_rp, d_order, d_be, d_zc, d_part;
+    explicit MpPlan(vc_ctx* ctx) : d_rp(ctx), d_order(ctx), d_be(ctx), d_zc(ctx), d_part(ctx) {}
+};
+// block / chunk shape of k_mp_chunk (VKZG_MP_SHAPE: 0 = 3 x 16, 1 = 4 x 16, 2 = 4 x 32, 3 = 6 x 24);
+// 4 x 16 by default: 0.125-0.129 ms against 0.128-0.131 for 3 x 16 (profiles/r04/mp_shape_ab.txt)
+static int mp_shape_index() {
+    static const int shape_env = getenv("VKZG_MP_SHAPE") ? atoi(getenv("VKZG_MP_SHAPE")) : 1;
+    return shape_env >= 0 && shape_env < 4 ? shape_env : 1;
+}
+static int mp_plan(vc_ctx* ctx, size_t N, size_t Qs, const uint64_t* z, size_t first, const std::vector<uint32_t>& zval,
+                   MpPlan* pl) {
     hipStream_t st = ctx->stream;
     const size_t Z = zval.size();
-    if (Qs == 0) {  // an empty shard contributes zero sums (synchronous like every ABI call)
-        VK_CHECK_HIP(hipMemsetAsync(d_S, 0, Z * N * 32, st));
-        VK_CHECK_HIP(hipStreamSynchronize(st));
-        return VC_OK;
-    }
+    pl->Qs = Qs;
+    pl->first = first;
+    pl->Z = Z;
+    if (Qs == 0) return VC_OK;
     // row of each query: a table over the domain (z < N, checked by mp_points over all queries)
     std::vector<uint32_t> row_of(N, 0xffffffffu), row(Qs);
     for (size_t k = 0; k < Z; k++) row_of[zval[k]] = (uint32_t)k;
@@ -1371,41 +1387,48 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
         if (z[i] >= N || row_of[z[i]] == 0xffffffffu) return VC_E_DOMAIN;
         row[i] = row_of[z[i]];
     }
-    // block / chunk shape of k_mp_chunk (VKZG_MP_SHAPE: 0 = 3 x 16, 1 = 4 x 16, 2 = 4 x 32, 3 = 6 x 24)
-    // 4 x 16 by default: 0.125-0.129 ms against 0.128-0.131 for 3 x 16 (profiles/r04/mp_shape_ab.txt)
-    static const int shape_env = getenv("VKZG_MP_SHAPE") ? atoi(getenv("VKZG_MP_SHAPE")) : 1;
     static const MpShape shapes[4] = {{3, 16}, {4, 16}, {4, 32}, {6, 24}};
-    const MpShape shp = shapes[shape_env >= 0 && shape_env < 4 ? shape_env : 1];
-    const uint32_t MP_CHUNK = shp.ch;
+    const uint32_t MP_CHUNK = shapes[mp_shape_index()].ch;
     // counting sort of the shard's queries by row, then chunks of <= MP_CHUNK queries
-    std::vector<uint32_t> cnt(Z + 1, 0), order(Qs);
+    std::vector<uint32_t> cnt(Z + 1, 0);
+    pl->order.resize(Qs);
     for (size_t i = 0; i < Qs; i++) cnt[row[i] + 1]++;
     for (size_t k = 0; k < Z; k++) cnt[k + 1] += cnt[k];
     {
         std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
-        for (size_t i = 0; i < Qs; i++) order[pos[row[i]]++] = (uint32_t)i;
+        for (size_t i = 0; i < Qs; i++) pl->order[pos[row[i]]++] = (uint32_t)i;
     }
     // chunks of <= MP_CHUNK queries inside one row; zc[row] = first chunk of the row
-    std::vector<uint32_t> be, zc(Z + 1, 0);
+    pl->be.clear();
+    pl->zc.assign(Z + 1, 0);
     for (size_t k = 0; k < Z; k++) {
-        zc[k] = (uint32_t)(be.size() / 2);
+        pl->zc[k] = (uint32_t)(pl->be.size() / 2);
         for (uint32_t u = cnt[k]; u < cnt[k + 1]; u += MP_CHUNK) {
-            be.push_back(u);
-            be.push_back(std::min<uint32_t>(u + MP_CHUNK, cnt[k + 1]));
+            pl->be.push_back(u);
+            pl->be.push_back(std::min<uint32_t>(u + MP_CHUNK, cnt[k + 1]));
         }
     }
-    const uint32_t nch = (uint32_t)(be.size() / 2);
-    zc[Z] = nch;
-    DevBuf d_rp(ctx), d_order(ctx), d_be(ctx), d_zc(ctx), d_part(ctx);
-    VK_TRY(d_rp.ensure(Qs * MP_RP_WORDS * 4));
-    VK_TRY(d_order.ensure(Qs * 4));
-    VK_TRY(d_be.ensure(be.size() * 4));
-    VK_TRY(d_zc.ensure((Z + 1) * 4));
-    VK_TRY(d_part.ensure(std::max<size_t>(nch, 1) * N * 32));
-    VK_LAUNCH(ctx, "mp_rpow", k_mp_rpow, (Qs + 255) / 256, 256, 0, r, first, Qs, d_rp.as<uint32_t>());
-    VK_CHECK_HIP(hipMemcpyAsync(d_order.p, order.data(), Qs * 4, hipMemcpyHostToDevice, st));
-    VK_CHECK_HIP(hipMemcpyAsync(d_be.p, be.data(), be.size() * 4, hipMemcpyHostToDevice, st));
-    VK_CHECK_HIP(hipMemcpyAsync(d_zc.p, zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
+    pl->nch = (uint32_t)(pl->be.size() / 2);
+    pl->zc[Z] = pl->nch;
+    VK_TRY(pl->d_rp.ensure(Qs * MP_RP_WORDS * 4));
+    VK_TRY(pl->d_order.ensure(Qs * 4));
+    VK_TRY(pl->d_be.ensure(pl->be.size() * 4));
+    VK_TRY(pl->d_zc.ensure((Z + 1) * 4));
+    VK_TRY(pl->d_part.ensure(std::max<size_t>(pl->nch, 1) * N * 32));
+    VK_CHECK_HIP(hipMemcpyAsync(pl->d_order.p, pl->order.data(), Qs * 4, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(pl->d_be.p, pl->be.data(), pl->be.size() * 4, hipMemcpyHostToDevice, st));
+    VK_CHECK_HIP(hipMemcpyAsync(pl->d_zc.p, pl->zc.data(), (Z + 1) * 4, hipMemcpyHostToDevice, st));
+    return VC_OK;
+}
+static int mp_run(vc_ctx* ctx, size_t N, const void* d_data, const Fr& r, MpPlan& pl, void* d_S) {
+    hipStream_t st = ctx->stream;
+    const size_t Qs = pl.Qs, Z = pl.Z;
+    if (Qs == 0) {  // an empty shard contributes zero sums (synchronous like every ABI call)
+        VK_CHECK_HIP(hipMemsetAsync(d_S, 0, Z * N * 32, st));
+        VK_CHECK_HIP(hipStreamSynchronize(st));
+        return VC_OK;
+    }
+    VK_LAUNCH(ctx, "mp_rpow", k_mp_rpow, (Qs + 255) / 256, 256, 0, r, pl.first, Qs, pl.d_rp.as<uint32_t>());
     const uint32_t kblk = (uint32_t)((N + 255) / 256);
     // non-temporal loads by default: 0.119-0.121 ms (4.43-4.51 TB/s) against 0.125-0.127 at 2^16 x 256
     // (profiles/r04/mp_nt_ab.txt)
@@ -1416,13 +1439,84 @@ static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, c
         {k_mp_chunk<0, 3, 16>, k_mp_chunk<0, 4, 16>, k_mp_chunk<0, 4, 32>, k_mp_chunk<0, 6, 24>},
         {k_mp_chunk<1, 3, 16>, k_mp_chunk<1, 4, 16>, k_mp_chunk<1, 4, 32>, k_mp_chunk<1, 6, 24>},
         {k_mp_chunk<1, 3, 16, 1>, k_mp_chunk<1, 4, 16, 1>, k_mp_chunk<1, 4, 32, 1>, k_mp_chunk<1, 6, 24, 1>}};
-    const KFn kern = kerns[pf_env ? 2 : nt_env ? 1 : 0][shape_env >= 0 && shape_env < 4 ? shape_env : 1];
-    VK_LAUNCH(ctx, "mp_chunk", kern, (size_t)nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
-              d_rp.as<uint32_t>(), d_order.as<uint32_t>(), d_be.as<uint32_t>(), N, kblk, d_part.as<Fr>());
-    VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, d_part.as<Fr>(), d_zc.as<uint32_t>(), N,
-              kblk, reinterpret_cast<Fr*>(d_S));
-    VK_CHECK_HIP(hipStreamSynchronize(st));  // host vectors above die on return
+    const KFn kern = kerns[pf_env ? 2 : nt_env ? 1 : 0][mp_shape_index()];
+    VK_LAUNCH(ctx, "mp_chunk", kern, (size_t)pl.nch * kblk, 256, 0, reinterpret_cast<const uint32_t*>(d_data),
+              pl.d_rp.as<uint32_t>(), pl.d_order.as<uint32_t>(), pl.d_be.as<uint32_t>(), N, kblk, pl.d_part.as<Fr>());
+    VK_LAUNCH(ctx, "mp_chunk_reduce", k_mp_chunk_reduce, Z * kblk, 256, 0, pl.d_part.as<Fr>(), pl.d_zc.as<uint32_t>(),
+              N, kblk, reinterpret_cast<Fr*>(d_S));
+    VK_CHECK_HIP(hipStreamSynchronize(st));  // the plan's host vectors may die after this
     return VC_OK;
+}
+static int mp_accumulate(vc_ctx* ctx, size_t N, size_t Qs, const void* d_data, const uint64_t* z, const Fr& r,
+                         size_t first, const std::vector<uint32_t>& zval, void* d_S) {
+    MpPlan pl(ctx);
+    const int st = mp_plan(ctx, N, Qs, z, first, zval, &pl);
+    if (st != VC_OK) {
+        (void)hipStreamSynchronize(ctx->stream);  // uploads from the plan's vectors may be queued
+        return st;
+    }
+    return mp_run(ctx, N, d_data, r, pl, d_S);
+}
+
+// mp_begin on a helper thread while this thread runs `overlap` (the shard's plan; mp_prove also
+// the evaluations' upload): the serial SHA-256 transcript is the longest host step of a multiproof
+// (2.6 ms at Q = 2^16), and neither the plan nor the upload needs its challenge. Falls back to
+// running both in turn if no thread can be started.
+template <class Fn>
+static int mp_begin_overlapped(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
+                               const uint64_t* y, vc_transcript** tr_out, Fr* r_out, Fn overlap) {
+    int st_b = VC_E_INVALID, st_o = VC_OK;
+    *tr_out = nullptr;
+    try {
+        std::thread th([&] { st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out); });
+        st_o = overlap();
+        th.join();
+    } catch (const std::system_error&) {
+        st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out);
+        if (st_b == VC_OK) st_o = overlap();
+    }
+    if (st_b != VC_OK || st_o != VC_OK) {
+        if (*tr_out) vc_transcript_free(*tr_out);
+        *tr_out = nullptr;
+        return st_b != VC_OK ? st_b : st_o;
+    }
+    return VC_OK;
+}
+
+int mp_rows(size_t N, size_t Q, const uint64_t* z, size_t* rows) {
+    if (!z || !rows || !is_pow2(N) || Q == 0) return VC_E_INVALID;
+    std::vector<uint32_t> zval;
+    VK_TRY(mp_points(N, Q, z, &zval));
+    *rows = zval.size();
+    return VC_OK;
+}
+
+// begin + accumulate of one query shard [first, first + Qs) with the transcript overlapped (the
+// single-proof paths: mp_prove, vc_multiproof_prove_sharded)
+int mp_begin_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                        const uint64_t* z, const uint64_t* y, size_t first, size_t Qs, const void* d_data, void* d_S,
+                        vc_transcript** tr_out, uint64_t* r_out) {
+    if (!ctx || !com_xy || !com_inf || !z || !y || !d_S || !tr_out || !r_out || (Qs && !d_data) || first > Q ||
+        Qs > Q - first || ctx->curve != VC_CURVE_BN254 || !is_pow2(N) || Q == 0)
+        return VC_E_INVALID;
+    std::vector<uint32_t> zval;
+    VK_TRY(mp_points(N, Q, z, &zval));
+    Guard g(ctx);
+    MpPlan pl(ctx);
+    Fr r;
+    const int st = mp_begin_overlapped(N, Q, com_xy, com_inf, z, y, tr_out, &r,
+                                       [&] { return mp_plan(ctx, N, Qs, z + first, first, zval, &pl); });
+    if (st != VC_OK) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return st;
+    }
+    canon_of(r, r_out);
+    const int st2 = mp_run(ctx, N, d_data, r, pl, d_S);
+    if (st2 != VC_OK) {
+        vc_transcript_free(*tr_out);
+        *tr_out = nullptr;
+    }
+    return st2;
 }
 
 // S = sum over G shards (canonical) -> Montgomery
@@ -1501,19 +1595,23 @@ static int mp_prove(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, const
                     vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
     vc_transcript* tr = nullptr;
     Fr r;
-    VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
     std::vector<uint32_t> zval;
-    int zst = mp_points(N, Q, z, &zval);  // z itself was validated by mp_begin
-    if (zst != VC_OK) {
-        vc_transcript_free(tr);
-        return zst;
-    }
+    if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
+    VK_TRY(mp_points(N, Q, z, &zval));
     DevBuf d_data(ctx), d_S(ctx);
-    int st = d_data.ensure(Q * N * 32);
-    if (st == VC_OK) st = d_S.ensure(zval.size() * N * 32);
-    if (st == VC_OK && hipMemcpyAsync(d_data.p, data, Q * N * 32, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
-        st = VC_E_HIP;
-    if (st == VC_OK) st = mp_accumulate(ctx, N, Q, d_data.p, z, r, 0, zval, d_S.p);
+    MpPlan pl(ctx);
+    // the 32 Q N bytes of evaluations cross PCIe and the shard is planned under the transcript
+    int st = mp_begin_overlapped(N, Q, com_xy, com_inf, z, y, &tr, &r, [&]() -> int {
+        VK_TRY(d_data.ensure(Q * N * 32));
+        VK_TRY(d_S.ensure(zval.size() * N * 32));
+        VK_CHECK_HIP(hipMemcpyAsync(d_data.p, data, Q * N * 32, hipMemcpyHostToDevice, ctx->stream));
+        return mp_plan(ctx, N, Q, z, 0, zval, &pl);
+    });
+    if (st != VC_OK) {
+        (void)hipStreamSynchronize(ctx->stream);
+        return st;
+    }
+    st = mp_run(ctx, N, d_data.p, r, pl, d_S.p);
     if (st == VC_OK)
         st = mp_finish(ctx, scheme, t, N, zval, d_S.p, 1, tr, d_xy, d_inf, ipa_proof, kzg_xy, kzg_inf, kzg_y);
     vc_transcript_free(tr);
@@ -1771,6 +1869,14 @@ int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_
     *rows = zval.size();
     *tr_out = tr;
     return VC_OK;
+}
+
+int vc_multiproof_rows(size_t N, size_t Q, const uint64_t* z, size_t* rows) { return mp_rows(N, Q, z, rows); }
+
+int vc_multiproof_begin_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                                   const uint64_t* z, const uint64_t* y, size_t first, size_t Qs, const void* d_data,
+                                   void* d_S, vc_transcript** transcript, uint64_t* r) {
+    return mp_begin_accumulate(ctx, N, Q, com_xy, com_inf, z, y, first, Qs, d_data, d_S, transcript, r);
 }
 
 int vc_multiproof_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* z, size_t first, size_t Qs,

@@ -16,5 +16,12 @@ void compress_g1(const uint64_t* xy, bool inf, uint8_t out[32]);
 // serialise many records on several threads)
 uint8_t* transcript_extend(vc_transcript* t, size_t n);
 Fr to_data_item_host(const uint64_t* xy, bool inf);
+// vc_multiproof_begin + vc_multiproof_accumulate of the query shard [first, first + Qs), the host
+// transcript on a helper thread while this thread plans the shard (scheme.hip); r_out canonical
+// the number of distinct z (rows of the per-point sums); VC_E_DOMAIN for z >= N
+int mp_rows(size_t N, size_t Q, const uint64_t* z, size_t* rows);
+int mp_begin_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
+                        const uint64_t* z, const uint64_t* y, size_t first, size_t Qs, const void* d_data, void* d_S,
+                        vc_transcript** tr_out, uint64_t* r_out);
 
 }  // namespace vk

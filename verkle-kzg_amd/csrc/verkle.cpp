@@ -372,7 +372,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             return out;
         }
         std::vector<Rows> part(T);
-        pool.run([&](unsigned k) {
+        pool.run([&](unsigned k) {  // the pool runs k < pool.size(): workers past T have no part
+            if (k >= T) return;
             const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
             part[k].reserve(b - a, (b - a) * nnz_per);
             for (size_t i = a; i < b; i++) fn(i, part[k]);
@@ -387,6 +388,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         out.cols.resize(noff[T]);
         out.vals.resize(4 * noff[T]);
         pool.run([&](unsigned k) {
+            if (k >= T) return;
             const Rows& r = part[k];
             for (size_t i = 1; i < r.ptr.size(); i++) out.ptr[roff[k] + i] = noff[k] + r.ptr[i];
             if (!r.cols.empty()) {

@@ -91,6 +91,9 @@ SIGNATURES = {
     "vc_multiproof_prove_many": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, c_size_t, c_void_p, P, P, P, P,
                                          P, P, P, P, P, P]),
     "vc_multiproof_accumulate": (c_int, [c_void_p, c_size_t, c_size_t, P, c_size_t, c_size_t, P, P, P]),
+    "vc_multiproof_rows": (c_int, [c_size_t, c_size_t, P, P]),
+    "vc_multiproof_begin_accumulate": (c_int, [c_void_p, c_size_t, c_size_t, P, P, P, P, c_size_t, c_size_t, P, P, P,
+                                               P]),
     "vc_multiproof_finish": (c_int, [c_void_p, c_int, c_int, c_size_t, c_size_t, P, P, c_int, c_void_p, P, P, P, P,
                                      P, P]),
     "vc_multiproof_verify_ipa": (c_int, [c_void_p, c_int, c_size_t, c_size_t, P, P, P, P, P, ctypes.c_uint8, P,

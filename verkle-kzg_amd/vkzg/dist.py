@@ -150,15 +150,16 @@ def multiproof_prove_sharded(vc, cxy, cinf, z, y, d_data_ptr, rank, world, devic
     from . import scheme
     from ._lib import lib
     N = vc.N if isinstance(vc, scheme.IPA) else vc.size
-    tr, r, rows = scheme.multiproof_begin(N, cxy, cinf, z, y)
+    rows = scheme.multiproof_rows(N, z)
     lo, hi = shard_range(len(z), rank, world)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    # every element of S is written by the accumulate (on the engine's stream, which is
+    # synchronised before it returns): no fill on torch's stream that could race with it
+    S = torch.empty((rows, N, 4), dtype=torch.int64, device=dev)
+    torch.cuda.current_stream(dev).synchronize()
+    # the host transcript (phase 1) overlapped with this shard's planning (phase 2)
+    tr, r = scheme.multiproof_begin_accumulate(vc.engine, N, cxy, cinf, z, y, lo, hi - lo, d_data_ptr, S.data_ptr())
     try:
-        # every element of S is written by vc_multiproof_accumulate (on the engine's stream, which
-        # is synchronised before it returns): no fill on torch's stream that could race with it
-        S = torch.empty((rows, N, 4), dtype=torch.int64, device=dev)
-        torch.cuda.current_stream(dev).synchronize()
-        scheme.multiproof_accumulate(vc.engine, N, z, lo, hi - lo, d_data_ptr, r, S.data_ptr())
         if world > 1:
             outs = [torch.empty_like(S) for _ in range(world)]
             dist.all_gather(outs, S)

@@ -456,6 +456,24 @@ def multiproof_accumulate(engine, N, z, first, count, d_data_ptr, r, d_S_ptr):
                                          _p(r), ctypes.c_void_p(d_S_ptr)), "multiproof_accumulate")
 
 
+def multiproof_rows(N, z):
+    """The number of distinct query points (rows of the per-point sums S)."""
+    rows = ctypes.c_size_t()
+    check(lib().vc_multiproof_rows(N, len(z), _p(z), ctypes.byref(rows)), "multiproof_rows")
+    return rows.value
+
+
+def multiproof_begin_accumulate(engine, N, cxy, cinf, z, y, first, count, d_data_ptr, d_S_ptr):
+    """Phases 1 + 2 in one call (the transcript overlapped with the shard's planning and uploads)
+    -> (transcript handle, r limbs); S of the shard into d_S (multiproof_rows(N, z) x N x 4 u64)."""
+    tr = ctypes.c_void_p()
+    r = np.zeros(4, dtype=np.uint64)
+    check(lib().vc_multiproof_begin_accumulate(engine.h, N, len(z), _p(cxy), _p(cinf), _p(z), _p(y), first, count,
+                                               ctypes.c_void_p(d_data_ptr), ctypes.c_void_p(d_S_ptr),
+                                               ctypes.byref(tr), _p(r)), "multiproof_begin_accumulate")
+    return tr, r
+
+
 def multiproof_finish(vc, z, d_S_parts_ptr, G, tr):
     """Phase 3: sum the G shards' S, then D, t, E and the inner proof -- an IPA proof or the KZG
     (proof, y) of prove_point at t (multiproof.rs:129-175). Frees `tr`."""
