@@ -408,8 +408,9 @@ struct is_affp : std::false_type {};
 template <class FC, class BT>
 struct is_affp<FC, BT, std::void_t<typename FC::AffP>> : std::is_same<BT, typename FC::AffP> {};
 
-// straddle merge inside the accumulate (A/B knob VKZG_ACC_MERGE). Off by default: measured slower
-// (accumulate +0.087 ms, the remaining fix-up 0.083 -> 0.158 ms; profiles/r04/merge_ab/)
+// straddle merge inside the accumulate (A/B knob VKZG_ACC_MERGE in a -DVKZG_ACC_MERGE_BUILD build;
+// the default build leaves the code out: it grew the kernel to 237 VGPRs and 18,441 instructions).
+// Measured slower: accumulate +0.087 ms, the remaining fix-up 0.083 -> 0.158 ms (profiles/r04/merge_ab/)
 static uint32_t acc_merge() {
     static const uint32_t v = getenv("VKZG_ACC_MERGE") ? (uint32_t)atoi(getenv("VKZG_ACC_MERGE")) : 0u;
     return v;
@@ -526,6 +527,7 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
             } while (bend <= k);
         }
     }
+#ifdef VKZG_ACC_MERGE_BUILD
     if (merge) {  // uniform
         // the next lane's carry piece (its own store, read back by the thread that wrote it)
         const typename FC::Acc mine = my_through == 1 ? carry_in[t] : FC::zero();
@@ -536,6 +538,11 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
             owner_bucket[t] = NONE;
         }
     }
+#else
+    (void)merge;
+    (void)my_through;
+    (void)own_b;
+#endif
 }
 
 // radix-29 bucket accumulators -> ec.hpp form, non-empty buckets only (empty ones keep what the
