@@ -87,3 +87,20 @@ def test_ipa_crs_golden():
     assert scheme.ipa_crs(257, max_=512) == want
     with pytest.raises(vkzg.VCError):          # OutOfBounds: default max 256 < 257
         scheme.ipa_crs(257)
+
+
+def test_multiproof_rows_host():
+    """vc_multiproof_rows (host only): the distinct query points, VC_E_DOMAIN for z >= N (the
+    reference indexes the Lagrange evaluations with z and panics), VC_E_INVALID for a width that is
+    not a power of two -- the checks vc_multiproof_begin_accumulate runs before anything else."""
+    import numpy as np
+    from vkzg import scheme
+    from vkzg._lib import lib
+    VC_E_INVALID, VC_E_DOMAIN = -1, -8  # include/vc_msm.h
+    z = np.array([3, 3, 0, 255, 7, 3], dtype=np.uint64)
+    assert scheme.multiproof_rows(256, z) == 4
+    import ctypes
+    rows = ctypes.c_size_t()
+    bad = np.array([1, 256], dtype=np.uint64)
+    assert lib().vc_multiproof_rows(256, 2, scheme._p(bad), ctypes.byref(rows)) == VC_E_DOMAIN
+    assert lib().vc_multiproof_rows(255, 2, scheme._p(z), ctypes.byref(rows)) == VC_E_INVALID
