@@ -56,20 +56,22 @@ def main(d, out):
                                                   + e["WRITE_SIZE_KB_per_launch"])
         ns = per_launch.get(k, {}).get("ns", [])
         def classes(xs):
-            lo = min(xs)
+            # in units of the median launch (the headline MSM's, the most frequent), to halves: the
+            # chunked host-scalar MSM's half-size launches are class 0.5, the KZG two-set ones 2
+            unit = sorted(xs)[len(xs) // 2]
             out = defaultdict(list)
             for x in xs:
-                out[str(max(1, round(x / lo)))].append(x)
+                out[f"{max(0.5, round(2 * x / unit) / 2):g}"].append(x)
             return out
         if ("k_msm_accumulate" in k and len(ns) > 1 and min(ns) > 0 and max(ns) / min(ns) >= 1.6
-                and len(classes(ns)) <= 3):  # a few clean classes (K = 1, 2 bucket sets), not a size sweep
+                and len(classes(ns)) <= 4):  # a few clean classes (K = 1, 2 bucket sets), not a size sweep
             cls = {}
             for c, xs in classes(ns).items():
                 cls[c] = {"calls": len(xs), "avg_ns": sum(xs) / len(xs)}
             for ctr, name in (("SQ_INSTS_VALU", "SQ_INSTS_VALU_per_launch"), ("FETCH_SIZE", "FETCH_SIZE_KB_per_launch_raw"),
                               ("WRITE_SIZE", "WRITE_SIZE_KB_per_launch")):
                 xs_all = p.get(ctr, [])
-                if xs_all and min(xs_all) > 0 and len(classes(xs_all)) <= 3:
+                if xs_all and min(xs_all) > 0 and len(classes(xs_all)) <= 4:
                     for c, xs in classes(xs_all).items():
                         cls.setdefault(c, {})[name] = sum(xs) / len(xs)
             for c, ce in cls.items():
