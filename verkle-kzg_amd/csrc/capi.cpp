@@ -467,6 +467,22 @@ int vc_msm_batch_sparse(vc_ctx* ctx, int id, size_t batch, const uint64_t* row_p
     return vk::msm_batch_sparse(ctx, t, batch, row_ptr, cols, scalars, mont, out_xy, out_inf);
 }
 
+}  // extern "C"
+
+namespace vk {
+int msm_batch_sparse_items_guarded(vc_ctx* ctx, int id, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                                   const uint64_t* scalars, uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_items) {
+    if (!ctx || (batch > 0 && (!row_ptr || !out_xy || !out_inf || !out_items))) return VC_E_INVALID;
+    if (batch > 0 && row_ptr[batch] > 0 && (!cols || !scalars)) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    return vk::msm_batch_sparse_items(ctx, t, batch, row_ptr, cols, scalars, 0, out_xy, out_inf, out_items);
+}
+}  // namespace vk
+
+extern "C" {
+
 int vc_msm_batch(vc_ctx* ctx, int id, size_t width, const uint64_t* scalars, size_t batch, int mont,
                  uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || (batch > 0 && (!scalars || !out_xy || !out_inf)) || width == 0) return VC_E_INVALID;

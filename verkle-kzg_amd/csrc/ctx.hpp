@@ -145,6 +145,7 @@ enum WsSlot {
     WS_GLV_SC,
     WS_GLV_FLAG,
     WS_RAW_B,  // radix-29 row sums of the sparse accumulate (converted by k_fast_store)
+    WS_SP_ITEMS,  // to_data_item of the sparse commits' rows (msm_batch_sparse_items)
     WS_COUNT_
 };
 
@@ -258,6 +259,16 @@ int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows = 0);
 int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void* d_out_xy, uint8_t* d_out_inf);
 int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                      const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
+// the same with the rows' to_data_item values too (BN254; lib.rs:56-67), computed on the device from
+// the normalised points and read back with them (the verkle levels: no second round trip)
+int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                           const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_items);
+// the same behind the ctx lock, by table id (what vc_msm_batch_sparse does for the plain call)
+int msm_batch_sparse_items_guarded(vc_ctx* ctx, int table, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                                   const uint64_t* scalars, uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_items);
+// k_to_data_item over device points (canonical affine u64 x 8 + flags) into device items, on the
+// ctx stream (scheme.hip)
+int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, size_t n, void* d_items);
 int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 // h_out_xy / h_out_inf (optional): host destinations -- when the small-batch latency path ran,
 // the results are written there instead of d_out_* and *on_host is set

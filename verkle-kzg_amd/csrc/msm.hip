@@ -1923,7 +1923,8 @@ __global__ void __launch_bounds__(64) k_sparse_combine(const typename C::Acc* __
 
 template <class C, class Fr>
 static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
-                              const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf) {
+                              const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf,
+                              uint64_t* out_items = nullptr) {
     using Acc = typename C::Acc;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
@@ -2076,9 +2077,22 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     lap("normalise");
     VK_CHECK_HIP(hipMemcpyAsync(out_xy, d_xy.p, batch * 2 * C::F::N * 4, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipMemcpyAsync(out_inf, d_inf.p, batch, hipMemcpyDeviceToHost, st));
+    if (out_items) {  // to_data_item of the rows' points, from the device copies
+        DevBuf& d_it = ctx->ws[WS_SP_ITEMS];
+        VK_TRY(d_it.ensure(batch * 32));
+        VK_TRY(to_data_item_device(ctx, d_xy.p, d_inf.as<uint8_t>(), batch, d_it.p));
+        VK_CHECK_HIP(hipMemcpyAsync(out_items, d_it.p, batch * 32, hipMemcpyDeviceToHost, st));
+    }
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host staging vectors die on return
     lap("D2H");
     return VC_OK;
+}
+
+int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                           const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_items) {
+    if (t->curve != VC_CURVE_BN254 || (batch && !out_items)) return VC_E_INVALID;
+    return msm_batch_sparse_t<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, cols, scalars, mont, out_xy, out_inf,
+                                                 out_items);
 }
 
 int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,

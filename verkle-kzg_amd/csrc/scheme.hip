@@ -794,6 +794,14 @@ struct Guard {
 bool proof_ok(const vc_ipa_proof* p) { return p && p->l_xy && p->r_xy && p->l_inf && p->r_inf; }
 }  // namespace
 
+namespace vk {
+int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, size_t n, void* d_items) {
+    if (n == 0) return VC_OK;
+    VK_LAUNCH(ctx, "to_data_item", k_to_data_item, (n + 255) / 256, 256, 0, static_cast<const fe<BN254Fq>*>(d_xy),
+              d_inf, n, static_cast<fe<F>*>(d_items));
+    return VC_OK;
+}
+}  // namespace vk
 extern "C" {
 
 int vc_to_data_item_batch(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, size_t n, uint64_t* out) {

@@ -18,6 +18,7 @@
 #include "comm.hpp"
 #include "host/pool.hpp"
 #include "host/fr.hpp"
+#include "scheme_internal.hpp"
 
 namespace {
 
@@ -272,6 +273,12 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
 
 namespace vk {
 
+// vc_msm_batch_sparse + vc_to_data_item_batch in one call (capi.cpp vc_msm_batch_sparse_items)
+static int sparse_items(vc_ctx* ctx, int table, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                        const uint64_t* vals, uint64_t* xy, uint8_t* inf, uint64_t* items) {
+    return msm_batch_sparse_items_guarded(ctx, table, batch, row_ptr, cols, vals, xy, inf, items);
+}
+
 int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh,
                       const Multi* mu) {
     if (!ctx || !t || !out_xy || !out_inf || (sh && mu)) return VC_E_INVALID;
@@ -437,10 +444,13 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                 for (uint64_t e = r.ptr[b]; e < r.ptr[b + 1]; e++) memcpy(row + 4 * (size_t)r.cols[e], &r.vals[4 * e], 32);
             });
             VK_TRY(vc_msm_batch(ctx, table, width, dense.data(), B, 0, xy.data(), inf.data()));
-            lap("dense commit");
-            const int st = vc_to_data_item_batch(ctx, xy.data(), inf.data(), B, items.data());
-            lap("to_data_item");
-            return st;
+            // <= 64 points: to_data_item on the host (compress + mod r, no inversion: already affine)
+            for (size_t b = 0; b < B; b++) {
+                const Fr it = to_data_item_host(&xy[8 * b], inf[b] != 0);
+                mont_to_canon<BN254Fr>(it, &items[4 * b]);
+            }
+            lap("dense commit + to_data_item");
+            return VC_OK;
         }
         if (mu) {  // member k commits rows [B k / G, B (k + 1) / G) of the level on its own device
             const int G = (int)mu->ctx.size();
@@ -454,21 +464,20 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                 for (size_t i = 0; i <= e - a; i++) rp[i] = r.ptr[a + i] - base;
                 const uint32_t* cols = r.cols.size() ? r.cols.data() + base : nullptr;
                 const uint64_t* vals = r.vals.size() ? r.vals.data() + 4 * base : nullptr;
-                st[k] = vc_msm_batch_sparse(mu->ctx[k], mu->table[k], e - a, rp.data(), cols, vals, 0, xy.data() + 8 * a,
-                                            inf.data() + a);
-                if (st[k] == VC_OK)
-                    st[k] = vc_to_data_item_batch(mu->ctx[k], xy.data() + 8 * a, inf.data() + a, e - a, items.data() + 4 * a);
+                st[k] = sparse_items(mu->ctx[k], mu->table[k], e - a, rp.data(), cols, vals, xy.data() + 8 * a,
+                                     inf.data() + a, items.data() + 4 * a);
             });
             for (int s : st)
                 if (s != VC_OK) return s;
             lap("sparse commit + to_data_item (members)");
             return VC_OK;
         }
-        VK_TRY(vc_msm_batch_sparse(ctx, table, B, r.ptr.data(), r.cols.data(), r.vals.data(), 0, xy.data(), inf.data()));
-        lap("sparse commit");
-        int st = vc_to_data_item_batch(ctx, xy.data(), inf.data(), B, items.data());
-        lap("to_data_item");
-        return st;
+        // the rows' commitments and their to_data_item values in one call (items computed on the
+        // device from the normalised points: no second upload / read-back per level)
+        VK_TRY(sparse_items(ctx, table, B, r.ptr.data(), r.cols.data(), r.vals.data(), xy.data(), inf.data(),
+                            items.data()));
+        lap("sparse commit + to_data_item");
+        return VC_OK;
     };
     // the nodes nodes[lo, hi) of a level got (xy, inf, items) here: store them; with a shard,
     // first all-gather every rank's slice (records of 8 + 4 + 1 u64: xy, item, inf), so every
