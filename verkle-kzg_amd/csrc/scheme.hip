@@ -1475,13 +1475,29 @@ static int mp_begin_overlapped(size_t N, size_t Q, const uint64_t* com_xy, const
                                const uint64_t* y, vc_transcript** tr_out, Fr* r_out, Fn overlap) {
     int st_b = VC_E_INVALID, st_o = VC_OK;
     *tr_out = nullptr;
+    auto guarded = [&]() -> int {  // the helper must be joined whatever the overlap does
+        try {
+            return overlap();
+        } catch (...) {
+            return VC_E_OOM;
+        }
+    };
+    std::thread th;
     try {
-        std::thread th([&] { st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out); });
-        st_o = overlap();
-        th.join();
-    } catch (const std::system_error&) {
+        th = std::thread([&] {
+            try {
+                st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out);
+            } catch (...) {  // nothing may leave a thread function
+                st_b = VC_E_OOM;
+            }
+        });
+    } catch (const std::system_error&) {  // no thread: one after the other
         st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out);
-        if (st_b == VC_OK) st_o = overlap();
+        if (st_b == VC_OK) st_o = guarded();
+    }
+    if (th.joinable()) {
+        st_o = guarded();
+        th.join();
     }
     if (st_b != VC_OK || st_o != VC_OK) {
         if (*tr_out) vc_transcript_free(*tr_out);
