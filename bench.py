@@ -518,7 +518,7 @@ def mp_proof_parallel(ipa, N, cxy, cinf, z, y, d_all, dev, rank, world, comm, wa
             else "one GPU: vc_multiproof_prove_many"}
 
 
-def mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, want, P=6):
+def mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, want, P=9):
     """A stream of P multiproofs through the three-phase ABI: phase 1 (the host transcript over all
     queries, vc_multiproof_begin -- pure host code, ctypes drops the GIL) of proof k + 1 runs on a
     second host thread while proof k's accumulate and finish (GPU, then the IPA rounds) run: what a
@@ -536,22 +536,31 @@ def mp_pipelined(ipa, N, cxy, cinf, z, y, d_all, dev, want, P=6):
         scheme.multiproof_accumulate(ipa.engine, N, z, 0, Q, d_all.data_ptr(), r, S.data_ptr())
         return scheme.multiproof_finish(ipa, z, S.data_ptr(), 1, tr)
 
-    with ThreadPoolExecutor(1) as pool:
-        back(pool.submit(scheme.multiproof_begin, N, cxy, cinf, z, y).result())  # warm
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        fut = pool.submit(scheme.multiproof_begin, N, cxy, cinf, z, y)
-        ok = True
-        for k in range(P):
-            begun = fut.result()
-            if k + 1 < P:
-                fut = pool.submit(scheme.multiproof_begin, N, cxy, cinf, z, y)
-            got = back(begun)
-            ok = ok and got["d"] == want["d"] and got["proof"].as_dict() == want["proof"].as_dict()
-        torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t0) / P
-    return {"proofs": P, "ms_per_multiproof": dt * 1e3, "multiproofs_per_s": 1.0 / dt, "same_proofs": ok,
-            "note": "phase 1 (host transcript) of proof k+1 overlapped with proof k's GPU phases and IPA rounds"}
+    def run(depth):
+        # up to `depth` transcripts in flight on host threads (the serial SHA-256 of one transcript
+        # is longer than one proof's GPU phases) while the main thread runs proof k's phases 2 + 3
+        with ThreadPoolExecutor(depth) as pool:
+            back(pool.submit(scheme.multiproof_begin, N, cxy, cinf, z, y).result())  # warm
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            futs = [pool.submit(scheme.multiproof_begin, N, cxy, cinf, z, y) for _ in range(min(depth, P))]
+            ok = True
+            for k in range(P):
+                begun = futs.pop(0).result()
+                if k + depth < P:
+                    futs.append(pool.submit(scheme.multiproof_begin, N, cxy, cinf, z, y))
+                got = back(begun)
+                ok = ok and got["d"] == want["d"] and got["proof"].as_dict() == want["proof"].as_dict()
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t0) / P, ok
+
+    depths = {d: run(d) for d in (1, 2, 3)}
+    dt = depths[3][0]
+    return {"proofs": P, "ms_per_multiproof": dt * 1e3, "multiproofs_per_s": 1.0 / dt,
+            "same_proofs": all(ok for _, ok in depths.values()),
+            "ms_per_multiproof_by_transcripts_in_flight": {str(d): v[0] * 1e3 for d, v in depths.items()},
+            "note": "phase 1 (host transcript) of proofs k+1 .. k+3 on three host threads, overlapped with proof "
+                    "k's GPU phases and IPA rounds (by_transcripts_in_flight: 1, 2, 3 threads)"}
 
 
 BN254_P = 21888242871839275222246405745257275088696311157297823662689037894645226208583  # base field
