@@ -160,6 +160,11 @@ def test_msm_host_scalars_chunked_2e20(bls, chunks):
         off, m = 12_345, 700_001
         got = e.msm(tid, k[:m], offset=off)
         assert _pt("bls12_381", *got) == C.mul(C.g, vkzg.dot_mod(k[:m], s[off:off + m], C.r))
+        if chunks == 2:  # Montgomery-form scalars (arkworks' in-memory form) through the chunks
+            m2 = 1 << 17
+            km = vkzg.ints_to_limbs([(vkzg.limbs_to_int(x) << 256) % C.r for x in k[:m2]])
+            got = e.msm(tid, km, mont=True)
+            assert _pt("bls12_381", *got) == C.mul(C.g, vkzg.dot_mod(k[:m2], s[:m2], C.r))
     finally:
         e.set_option(e.OPT_MSM_HOST_CHUNKS, 2)
 
