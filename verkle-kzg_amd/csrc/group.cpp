@@ -9,6 +9,7 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -313,34 +314,64 @@ int vc_group_multiproof_prove(vc_group* g, int scheme, int id, size_t N, size_t 
     if (G == 1)
         return vc_multiproof_prove(g->ctx[0], scheme, g->tables[id][0], N, Q, data, com_xy, com_inf, z, y, d_xy, d_inf,
                                    ipa_proof, kzg_proof_xy, kzg_proof_inf, kzg_y);
-    // phase 1 once (the serial transcript over all queries, multiproof.rs:106-115)
+    // phase 1 once (the serial transcript over all queries, multiproof.rs:106-115) on a helper
+    // thread while the members upload their slices of the evaluations: the transcript needs none
+    // of them, and the accumulate needs its challenge r
+    size_t rows = 0;
+    VK_TRY(vc_multiproof_rows(N, Q, z, &rows));
+    const size_t sbytes = rows * N * 32;
     vc_transcript* tr = nullptr;
     uint64_t r[4];
-    size_t rows = 0;
-    VK_TRY(vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows));
-    const size_t sbytes = rows * N * 32;
+    size_t rows_b = 0;
+    int st_b = VC_E_INVALID;
+    auto begin = [&] {
+        try {
+            st_b = vc_multiproof_begin(N, Q, com_xy, com_inf, z, y, &tr, r, &rows_b);
+        } catch (...) {  // nothing may leave a thread function
+            st_b = VC_E_OOM;
+        }
+    };
+    std::thread th;
+    try {
+        th = std::thread(begin);
+    } catch (const std::system_error&) {
+        begin();  // no thread: the transcript first
+    }
     // member 0 holds every member's sums contiguously (vc_multiproof_finish adds G parts)
     int st0 = g->sums[0].ensure(sbytes * G);
     std::vector<int> st(G, st0);
     if (st0 == VC_OK)
         g->team->run([&](int k) {
+            auto upload = [&]() -> int {
+                size_t lo, hi;
+                vk::shard_range(Q, k, G, &lo, &hi);
+                if (hi == lo) return VC_OK;
+                VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+                VK_TRY(g->data[k].ensure((hi - lo) * N * 32));
+                VK_CHECK_HIP(hipMemcpy(g->data[k].p, data + lo * N * 4, (hi - lo) * N * 32, hipMemcpyHostToDevice));
+                if (k != 0) VK_TRY(g->sums[k].ensure(sbytes));
+                return VC_OK;
+            };
+            st[k] = upload();
+        });
+    if (th.joinable()) th.join();
+    if (st_b != VC_OK) {
+        if (tr) vc_transcript_free(tr);
+        return st_b;
+    }
+    if (first_error(st) == VC_OK)
+        g->team->run([&](int k) {
             auto share = [&]() -> int {
                 size_t lo, hi;
                 vk::shard_range(Q, k, G, &lo, &hi);
                 uint8_t* dst0 = static_cast<uint8_t*>(g->sums[0].p) + (size_t)k * sbytes;
-                VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
                 if (hi == lo) {  // an empty slice contributes zero sums
                     VK_CHECK_HIP(hipSetDevice(g->ctx[0]->device));
                     VK_CHECK_HIP(hipMemset(dst0, 0, sbytes));
                     return VC_OK;
                 }
-                VK_TRY(g->data[k].ensure((hi - lo) * N * 32));
-                VK_CHECK_HIP(hipMemcpy(g->data[k].p, data + lo * N * 4, (hi - lo) * N * 32, hipMemcpyHostToDevice));
-                void* dS = dst0;
-                if (k != 0) {
-                    VK_TRY(g->sums[k].ensure(sbytes));
-                    dS = g->sums[k].p;
-                }
+                VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+                void* dS = k != 0 ? g->sums[k].p : static_cast<void*>(dst0);
                 VK_TRY(vc_multiproof_accumulate(g->ctx[k], N, Q, z, lo, hi - lo, g->data[k].p, r, dS));
                 if (k != 0)
                     VK_CHECK_HIP(hipMemcpyPeer(dst0, g->ctx[0]->device, dS, g->ctx[k]->device, sbytes));
