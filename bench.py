@@ -750,7 +750,12 @@ def kzg_reference_shapes(local, stream, cpu=True):
     rng = np.random.default_rng(12)
     data = scheme.LagrangeBasis([int(v) for v in rng.integers(0, 1 << 62, size=20)], 32)
     com = kz.commit(data)
+    out["commit_ms_pippenger"] = med(lambda: kz.commit(data))
+    # the SRS's fixed-base windows (setup, untimed -- a fixed CRS): vc_msm's small commits then take
+    # the fixed-base latency path
+    e.fixed_base_precompute(kz.table, 8)
     out["commit_ms"] = med(lambda: kz.commit(data))
+    out["commit_same_result"] = kz.commit(data) == com
     out["single_proof_ms"] = med(lambda: kz.prove(com, 7, data))
     e.close()
     if cpu:

@@ -368,3 +368,34 @@ def test_batch_commit_sparse(engines, oracle_c, curve):
     mont = [v * R % C.r for v in vals]
     m_xy, m_inf = e.msm_batch_sparse(tid, ptr, cols, vkzg.ints_to_limbs(mont), mont=True)
     assert np.array_equal(m_xy, got_xy) and np.array_equal(m_inf, got_inf)
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_msm_small_on_precomputed_table(engines, oracle_c, curve):
+    """vc_msm of <= 1024 host scalars from the start of a table with precomputed fixed-base
+    windows takes the fixed-base latency path (capi.cpp vc_msm): == the oracle and == the
+    Pippenger pipeline (vc_msm_device) on the same table, for 1, 37 and 256 scalars, a point
+    range (offset > 0: Pippenger) and Montgomery-form scalars."""
+    import torch
+    import vkzg
+    e = engines[curve]
+    rng = np.random.default_rng(77)
+    tid = e.random_bases(300, seed=300)
+    xy, inf = e.download_bases(tid)
+    e.fixed_base_precompute(tid, 8)
+    r = vkzg.SCALAR_R[curve]
+    for n in (1, 37, 256):
+        sc = vkzg.random_scalars(curve, n, rng)
+        want = _oracle(oracle_c, curve, xy, inf, sc)
+        got = e.msm(tid, sc)
+        assert got[1] == want[1] and (want[1] or np.array_equal(got[0], want[0])), n
+        d = torch.from_numpy(sc.view(np.int64).copy()).cuda()
+        dev = e.msm_device(tid, d.data_ptr(), n)
+        assert dev[1] == got[1] and np.array_equal(dev[0], got[0]), n
+        mont = vkzg.ints_to_limbs([(vkzg.limbs_to_int(x) << 256) % r for x in sc])
+        gm = e.msm(tid, mont, mont=True)
+        assert gm[1] == got[1] and np.array_equal(gm[0], got[0]), n
+    sc = vkzg.random_scalars(curve, 40, rng)
+    want = _oracle(oracle_c, curve, xy[5:45], inf[5:45], sc)
+    got = e.msm(tid, sc, offset=5)
+    assert got[1] == want[1] and (want[1] or np.array_equal(got[0], want[0]))

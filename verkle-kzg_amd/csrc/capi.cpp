@@ -399,6 +399,28 @@ int vc_msm_device_many(vc_ctx* ctx, int id, const void* const* d_scalars, const 
     return VC_OK;
 }
 
+// batched fixed-base commits of host scalars over bases [0, width) (vc_msm_batch; the caller holds
+// the ctx lock)
+static int batch_commit_host(vc_ctx* ctx, vk::Table* t, size_t width, const uint64_t* scalars, size_t batch, int mont,
+                             uint64_t* out_xy, uint8_t* out_inf) {
+    if (batch == 0) return VC_OK;
+    const size_t nl = (size_t)vk::aff_limbs64(ctx->curve);
+    VK_TRY(ctx->ws[vk::WS_SCALARS].ensure(batch * width * 32));
+    VK_TRY(ctx->ws[vk::WS_MISC].ensure(batch * (2 * nl * 8 + 1)));
+    uint8_t* dxy = ctx->ws[vk::WS_MISC].as<uint8_t>();
+    uint8_t* dinf = dxy + batch * 2 * nl * 8;
+    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[vk::WS_SCALARS].p, scalars, batch * width * 32,
+                                hipMemcpyHostToDevice, ctx->stream));
+    bool on_host = false;
+    VK_TRY(vk::msm_batch_run(ctx, t, width, ctx->ws[vk::WS_SCALARS].p, batch, mont, dxy, dinf, out_xy, out_inf,
+                             &on_host));
+    if (on_host) return VC_OK;
+    VK_CHECK_HIP(hipMemcpyAsync(out_xy, dxy, batch * 2 * nl * 8, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipMemcpyAsync(out_inf, dinf, batch, hipMemcpyDeviceToHost, ctx->stream));
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VC_OK;
+}
+
 int vc_msm(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n, int mont,
            uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || !out_xy || !out_inf || (n > 0 && !scalars)) return VC_E_INVALID;
@@ -406,6 +428,12 @@ int vc_msm(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n
     vk::Table* t = ctx->table(id);
     if (!t) return VC_E_TABLE;
     if (offset > t->n || n > t->n - offset) return VC_E_RANGE;
+    // a small MSM from the start of a table whose fixed-base windows the caller precomputed
+    // (vc_fixed_base_precompute over a CRS at setup): the fixed-base latency path -- one (base,
+    // window) point per thread, quad-add block sums -- instead of the Pippenger pipeline's fixed
+    // ~0.25 ms (IPA::commit at width 256 through vc_msm: the reference's commit)
+    if (n > 0 && n <= 1024 && offset == 0 && t->fb_c != 0)
+        return batch_commit_host(ctx, t, n, scalars, 1, mont, out_xy, out_inf);
     std::vector<uint32_t> acc(vk::point_words(ctx->curve));
     VK_TRY(vk::msm_run_host(ctx, t, offset, scalars, n, mont, acc.data()));
     return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
@@ -489,22 +517,7 @@ int vc_msm_batch(vc_ctx* ctx, int id, size_t width, const uint64_t* scalars, siz
     Guard g(ctx);
     vk::Table* t = ctx->table(id);
     if (!t) return VC_E_TABLE;
-    if (batch == 0) return VC_OK;
-    const size_t nl = (size_t)vk::aff_limbs64(ctx->curve);
-    VK_TRY(ctx->ws[vk::WS_SCALARS].ensure(batch * width * 32));
-    VK_TRY(ctx->ws[vk::WS_MISC].ensure(batch * (2 * nl * 8 + 1)));
-    uint8_t* dxy = ctx->ws[vk::WS_MISC].as<uint8_t>();
-    uint8_t* dinf = dxy + batch * 2 * nl * 8;
-    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[vk::WS_SCALARS].p, scalars, batch * width * 32,
-                                hipMemcpyHostToDevice, ctx->stream));
-    bool on_host = false;
-    VK_TRY(vk::msm_batch_run(ctx, t, width, ctx->ws[vk::WS_SCALARS].p, batch, mont, dxy, dinf, out_xy, out_inf,
-                             &on_host));
-    if (on_host) return VC_OK;
-    VK_CHECK_HIP(hipMemcpyAsync(out_xy, dxy, batch * 2 * nl * 8, hipMemcpyDeviceToHost, ctx->stream));
-    VK_CHECK_HIP(hipMemcpyAsync(out_inf, dinf, batch, hipMemcpyDeviceToHost, ctx->stream));
-    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    return VC_OK;
+    return batch_commit_host(ctx, t, width, scalars, batch, mont, out_xy, out_inf);
 }
 
 }  // extern "C"
