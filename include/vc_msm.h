@@ -101,7 +101,10 @@ int vc_bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* table_id);
 int vc_bases_download(vc_ctx* ctx, int table_id, uint64_t* affine_xy, uint8_t* inf);
 
 /* MSM: out = sum_i scalars[i] * bases[offset + i]  (utils::inner_product, utils.rs:16-19).
- * `zip` truncation of the reference (Appendix B.9) is the caller's n. */
+ * `zip` truncation of the reference (Appendix B.9) is the caller's n. Host scalars: n <= 1024 from
+ * offset 0 of a table with precomputed fixed-base windows (vc_fixed_base_precompute) runs as one
+ * fixed-base commit (the latency path); large BLS12-381 MSMs copy the scalars in
+ * VC_OPT_MSM_HOST_CHUNKS chunks under the previous chunk's work. Same result either way. */
 int vc_msm(vc_ctx* ctx, int table_id, size_t offset, const uint64_t* scalars, size_t n, int mont,
            uint64_t* out_xy, uint8_t* out_inf);
 /* Same with scalars already resident in device memory (4 u64 per scalar). */
