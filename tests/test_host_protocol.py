@@ -67,9 +67,21 @@ def test_multiproof_transcript_matches_oracle():
     want = a.digest("r")
     cxy, cinf = vkzg.points_to_arrays("bn254", pts)
     tr, r, rows = scheme.multiproof_begin(N, cxy, cinf, z, vkzg.ints_to_limbs(ys))
-    lib().vc_transcript_free(tr)
-    assert sum(int(v) << (64 * k) for k, v in enumerate(r)) == want
-    assert rows == len(set(int(v) for v in z))
+    try:
+        assert sum(int(v) << (64 * k) for k, v in enumerate(r)) == want
+        assert rows == len(set(int(v) for v in z))
+        # the state after the digest (the records stream into the hash, never stored): the next
+        # challenge t after D (multiproof.rs:152-155) agrees with the oracle's
+        d = gold[3]
+        a.append_point(d, "D")
+        want_t = a.digest("t")
+        dxy, dinf = vkzg.points_to_arrays("bn254", [d])
+        lib().vc_transcript_append_point(tr, scheme._p(dxy), int(dinf[0]), b"D")
+        t = np.zeros(4, dtype=np.uint64)
+        assert lib().vc_transcript_digest(tr, b"t", scheme._p(t)) == 0
+        assert sum(int(v) << (64 * k) for k, v in enumerate(t)) == want_t
+    finally:
+        lib().vc_transcript_free(tr)
 
 
 def test_compress_and_to_data_item_golden():

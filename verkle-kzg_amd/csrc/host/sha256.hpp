@@ -34,8 +34,12 @@ __attribute__((target("sha,sse4.1"))) static inline void sha256_blocks_shani(uin
     while (nblocks--) {
         const __m128i A0 = S0, C0 = S1;
         __m128i M[4];
+        // fully unrolled (M[] stays in registers): without the pragma, hipcc's host pass kept the
+        // 16 groups as a loop over a stack array -- 2x slower on the multiproof transcript
+#pragma unroll
         for (int k = 0; k < 4; k++)
             M[k] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(data + 16 * k)), MASK);
+#pragma unroll
         for (int g = 0; g < 16; g++) {
             const __m128i cur = M[g & 3];
             __m128i MSG = _mm_add_epi32(cur, _mm_loadu_si128(reinterpret_cast<const __m128i*>(&kSha256K[4 * g])));

@@ -1142,31 +1142,21 @@ struct MpPrep {
 // host threads (the point compression is the costly part); the SHA-256 over them stays serial.
 // pool_ok = false: fill serially on the calling thread (mp_prove_many's transcript workers already
 // run one proof each; nesting the shared host pool there serialised them on its one-loop lock)
-static vc_transcript* mp_transcript(size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
-                                    const uint64_t* y, bool pool_ok = true) {
+// the multiproof transcript's records "C" ++ compressed(C_i) ++ "z" ++ le64(z_i) ++ "y" ++ le(y_i)
+// (multiproof.rs:109-113) for queries [lo, hi) into out
+static void mp_records(const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
+                       size_t lo, size_t hi, uint8_t* out) {
     constexpr size_t REC = 75;
-    vc_transcript* tr = vc_transcript_new("multiproof");
-    vc_transcript_reserve(tr, Q * REC + 64);
-    uint8_t* out = transcript_extend(tr, Q * REC);
-    auto fill = [&](size_t lo, size_t hi) {
-        static const uint64_t zero[8] = {0};
-        for (size_t i = lo; i < hi; i++) {
-            uint8_t* o = out + REC * i;
-            o[0] = 'C';
-            compress_g1(com_inf[i] ? zero : com_xy + 8 * i, com_inf[i] != 0, o + 1);
-            o[33] = 'z';
-            for (int k = 0; k < 8; k++) o[34 + k] = (uint8_t)(z[i] >> (8 * k));
-            o[42] = 'y';
-            memcpy(o + 43, y + 4 * i, 32);
-        }
-    };
-    if (!pool_ok || Q < 8192 || host_pool().size() == 1) {
-        fill(0, Q);
-    } else {
-        const unsigned T = host_pool().size();
-        host_pool().run([&](unsigned k) { fill(Q * k / T, Q * (k + 1) / T); });
+    static const uint64_t zero[8] = {0};
+    for (size_t i = lo; i < hi; i++) {
+        uint8_t* o = out + REC * (i - lo);
+        o[0] = 'C';
+        compress_g1(com_inf[i] ? zero : com_xy + 8 * i, com_inf[i] != 0, o + 1);
+        o[33] = 'z';
+        for (int k = 0; k < 8; k++) o[34 + k] = (uint8_t)(z[i] >> (8 * k));
+        o[42] = 'y';
+        memcpy(o + 43, y + 4 * i, 32);
     }
-    return tr;
 }
 
 static std::vector<Fr> invert_domain_at(const Fr& t, size_t N) {  // utils.rs:57-62 (integer i)
@@ -1189,8 +1179,11 @@ static int mp_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* c
     if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
-    vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y, pool_ok);
-    *r_out = transcript_digest(tr, "r");
+    // the records stream into the hash (never stored whole: transcript_digest_records)
+    vc_transcript* tr = vc_transcript_new("multiproof");
+    *r_out = transcript_digest_records(
+        tr, Q, 75, [&](size_t lo, size_t hi, uint8_t* out) { mp_records(com_xy, com_inf, z, y, lo, hi, out); }, "r",
+        pool_ok && Q >= 8192);
     *tr_out = tr;
     return VC_OK;
 }
@@ -1804,8 +1797,14 @@ static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, con
     if (!is_pow2(N) || N > (size_t(1) << 28)) return VC_E_INVALID;  // tables below are sized by N
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
-    vc_transcript* tr = mp_transcript(Q, com_xy, com_inf, z, y);
-    Fr r = transcript_digest(tr, "r");
+    vc_transcript* tr = nullptr;
+    Fr r;
+    if (Q == 0) {  // no queries: the transcript of the labels alone (mp_begin wants Q > 0)
+        tr = vc_transcript_new("multiproof");
+        r = transcript_digest(tr, "r");
+    } else {
+        VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
+    }
     vc_transcript_append_point(tr, d_xy, d_inf, "D");
     Fr tt = transcript_digest(tr, "t");
     std::vector<Fr> invs = invert_domain_at(tt, N);

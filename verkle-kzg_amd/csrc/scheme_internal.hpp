@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
+
 #include "../../include/vc_scheme.h"
 #include "host/fr.hpp"
 
@@ -15,6 +17,11 @@ void compress_g1(const uint64_t* xy, bool inf, uint8_t out[32]);
 // grow the transcript state by n bytes and return the start of the new region (callers that
 // serialise many records on several threads)
 uint8_t* transcript_extend(vc_transcript* t, size_t n);
+// transcript_digest of the state followed by nrec records of rec bytes (made by fill(lo, hi, out)
+// chunk by chunk, never stored whole) and the label; pool_ok: make them on the host pool
+using RecordFill = std::function<void(size_t lo, size_t hi, uint8_t* out)>;
+Fr transcript_digest_records(vc_transcript* t, size_t nrec, size_t rec, const RecordFill& fill, const char* label,
+                             bool pool_ok);
 Fr to_data_item_host(const uint64_t* xy, bool inf);
 // vc_multiproof_begin + vc_multiproof_accumulate of the query shard [first, first + Qs), the host
 // transcript on a helper thread while this thread plans the shard (scheme.hip); r_out canonical
