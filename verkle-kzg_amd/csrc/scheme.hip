@@ -740,17 +740,34 @@ __global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, co
 }
 
 // g[k] = sum_z Q[z][k] ; h[k] = sum_z invt[z] S[z][k] ; hmg = h - g
-__global__ void k_mp_combine(const fe<F>* __restrict__ S, const fe<F>* __restrict__ Q, const fe<F>* __restrict__ invt_z,
-                             size_t N, uint32_t Z, fe<F>* __restrict__ g, fe<F>* __restrict__ h) {
-    size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= N) return;
+// g[k] = sum_z Q[z][k], h[k] = sum_z invt_z[z] S[z][k]: a block per MP_CB_K columns, its 256
+// threads split the Z rows MP_CB_R ways (row-groups strided by MP_CB_R), partials added in LDS --
+// the one-thread-per-column form ran 256 dependent multiplies per thread on 4 waves (~0.15 ms of
+// the multiproof finish at N = 256)
+constexpr uint32_t MP_CB_K = 16, MP_CB_R = 16;
+__global__ void __launch_bounds__(256) k_mp_combine(const fe<F>* __restrict__ S, const fe<F>* __restrict__ Q,
+                                                    const fe<F>* __restrict__ invt_z, size_t N, uint32_t Z,
+                                                    fe<F>* __restrict__ g, fe<F>* __restrict__ h) {
+    __shared__ fe<F> pg[MP_CB_R][MP_CB_K], ph[MP_CB_R][MP_CB_K];
+    const uint32_t kc = threadIdx.x % MP_CB_K, rg = threadIdx.x / MP_CB_K;
+    const size_t k = (size_t)blockIdx.x * MP_CB_K + kc;
     fe<F> gg = fe_zero<F>(), hh = fe_zero<F>();
-    for (uint32_t zi = 0; zi < Z; zi++) {
-        gg = fe_add<F>(gg, Q[(size_t)zi * N + k]);
-        if (invt_z) hh = fe_add<F>(hh, fe_mul<F>(invt_z[zi], S[(size_t)zi * N + k]));
+    if (k < N)
+        for (uint32_t zi = rg; zi < Z; zi += MP_CB_R) {
+            gg = fe_add<F>(gg, Q[(size_t)zi * N + k]);
+            if (invt_z) hh = fe_add<F>(hh, fe_mul<F>(invt_z[zi], S[(size_t)zi * N + k]));
+        }
+    pg[rg][kc] = gg;
+    ph[rg][kc] = hh;
+    __syncthreads();
+    if (rg == 0 && k < N) {
+        for (uint32_t j = 1; j < MP_CB_R; j++) {
+            gg = fe_add<F>(gg, pg[j][kc]);
+            if (invt_z) hh = fe_add<F>(hh, ph[j][kc]);
+        }
+        g[k] = gg;
+        if (invt_z) h[k] = hh;
     }
-    g[k] = gg;
-    if (invt_z) h[k] = hh;
 }
 
 // ---------------------------------------------------------------- to_data_item (a13)
@@ -1550,6 +1567,16 @@ static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vec
                      vc_ipa_proof* ipa_proof, uint64_t* kzg_xy, uint8_t* kzg_inf, uint64_t* kzg_y) {
     if (!is_pow2(N) || G < 1 || zval.empty()) return VC_E_INVALID;
     hipStream_t st = ctx->stream;
+    // VKZG_VERBOSE: phase laps on stderr (with a stream sync at each: diagnostics only)
+    static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
+    auto tic = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!verbose) return;
+        (void)hipStreamSynchronize(st);
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[mp_finish] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tic).count());
+        tic = now;
+    };
     const uint32_t Z = (uint32_t)zval.size();
     DevBuf d_zv(ctx), d_S(ctx), d_Q(ctx), d_g(ctx), d_h(ctx), d_it(ctx);
     VK_TRY(d_zv.ensure(Z * 4));
@@ -1565,28 +1592,32 @@ static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vec
     VK_TRY(domain_tables<F>(ctx, bn254_group_gen(N), N, &pw, &pwi, &inv1));
     VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, d_S.as<fe<F>>(), inv1, pw, pwi, d_zv.as<uint32_t>(), N,
               d_Q.as<fe<F>>());
-    VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
+    VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
               (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
     std::vector<Fr> g(N), h(N);
     VK_CHECK_HIP(hipMemcpyAsync(g.data(), d_g.p, N * 32, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));
+    lap("sums, quotients, g");
     // D = commit(g)
     uint64_t dxy[8];
     uint8_t dinf;
     VK_TRY(commit_batch(ctx, t, N, g.data(), 1, dxy, &dinf));
+    lap("D");
     transcript_append_point(tr, dxy, dinf, "D");
     Fr tt = transcript_digest(tr, "t");
     std::vector<Fr> invs = invert_domain_at(tt, N);  // 1/(t - z), z an integer (utils.rs:57-62)
     std::vector<Fr> invz(Z);
     for (uint32_t k = 0; k < Z; k++) invz[k] = invs[zval[k]];
     VK_CHECK_HIP(hipMemcpyAsync(d_it.p, invz.data(), Z * 32, hipMemcpyHostToDevice, st));
-    VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
+    VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
               d_it.as<fe<F>>(), N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
     VK_CHECK_HIP(hipMemcpyAsync(h.data(), d_h.p, N * 32, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));
+    lap("t, h");
     uint64_t exy[8];
     uint8_t einf;
     VK_TRY(commit_batch(ctx, t, N, h.data(), 1, exy, &einf));
+    lap("E");
     transcript_append_point(tr, exy, einf, "E");
     std::vector<Fr> hmg(N);
     for (size_t k = 0; k < N; k++) hmg[k] = fe_sub<F>(h[k], g[k]);
@@ -1598,7 +1629,9 @@ static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vec
         std::vector<Acc> cs(1, mc);
         std::vector<Fr> ps(1, tt);
         vc_transcript* trs[1] = {tr};
-        return ipa_prove_impl(ctx, t, N, dd, cs, ps, trs, ipa_proof);
+        const int s = ipa_prove_impl(ctx, t, N, dd, cs, ps, trs, ipa_proof);
+        lap("inner IPA proof");
+        return s;
     }
     std::vector<uint64_t> ev(N * 4);
     for (size_t k = 0; k < N; k++) canon_of(hmg[k], &ev[4 * k]);
@@ -1727,7 +1760,7 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
                       (size_t)Z * N, Sm[p]->as<Fr>());
             VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, Sm[p]->as<fe<F>>(), inv1, pw, pwi, zv[p]->as<uint32_t>(), N,
                       Qb[p]->as<fe<F>>());
-            VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
+            VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
                       (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N);
             return VC_OK;
         };
@@ -1753,7 +1786,7 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
             break;
         }
         auto launch = [&]() -> int {
-            VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + 255) / 256, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
+            VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
                       it[p]->as<fe<F>>(), N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N);
             return VC_OK;
         };
