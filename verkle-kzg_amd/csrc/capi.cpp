@@ -73,10 +73,12 @@ int PinBuf::ensure(size_t bytes) {
     if (bytes <= cap && p) return VC_OK;
     release();
     if (bytes == 0) bytes = 16;
-    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, bytes, flags ? flags : hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
     if (e != hipSuccess) {
         last_hip_error() = e;
-        p = nullptr;
+        if (p) (void)hipHostFree(p);
+        p = dp = nullptr;
         cap = 0;
         return VC_E_OOM;
     }
@@ -86,7 +88,7 @@ int PinBuf::ensure(size_t bytes) {
 
 void PinBuf::release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dp = nullptr;
     cap = 0;
 }
 
@@ -187,6 +189,7 @@ int vc_ctx_create(int curve, int device, vc_ctx** out) {
     vc_ctx* c = new vc_ctx();
     c->curve = curve;
     c->device = device;
+    c->pin_small.flags = hipHostMallocCoherent;
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         vk::last_hip_error() = e;

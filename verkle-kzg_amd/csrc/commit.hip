@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -580,7 +582,8 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
 
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
-                       void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host) {
+                       void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
+                       const PinBuf* pin_sc) {
     using Acc = typename C::Acc;
     if (width > t->n) return VC_E_RANGE;
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8, 0));
@@ -594,21 +597,46 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     const int W = fg.W;
     const int wpt = fb_wpt();
     const size_t WG = (size_t)(W + wpt - 1) / wpt;
-    if (items * WG <= lanes && batch <= 64) {  // small batch: latency path
+    const bool small = items * WG <= lanes && batch <= 64;
+    // zero-copy on the latency path (VKZG_ZERO_COPY, A/B probe: bit 0 partials, bit 1 scalars):
+    // the kernel reads host-pinned scalars and writes its block partials to fine-grained host
+    // memory over PCIe instead of a copy engine moving them before / after it
+    static const int zc = getenv("VKZG_ZERO_COPY") ? atoi(getenv("VKZG_ZERO_COPY")) : 3;
+    if (pin_sc) {
+        if (small && (zc & 2)) {
+            d_sc = pin_sc->dp;
+        } else {
+            VK_TRY(ctx->ws[WS_SCALARS].ensure(items * 32));
+            VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_SCALARS].p, pin_sc->p, items * 32, hipMemcpyHostToDevice,
+                                        ctx->stream));
+            d_sc = ctx->ws[WS_SCALARS].p;
+        }
+    }
+    if (small) {  // small batch: latency path
         const uint32_t bpc = (uint32_t)((width * WG + 255) / 256);
-        VK_TRY(ctx->ws[WS_PIECE].ensure((size_t)batch * bpc * sizeof(Acc)));
+        // VKZG_HOST_TIMING=1: launch-to-readback, host adds and normalisation on stderr (probe)
+        static const bool timing = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+        auto now_us = [] {
+            return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        };
+        const double t0 = timing ? now_us() : 0.0;
+        const size_t part_bytes = (size_t)batch * bpc * sizeof(Acc);
+        VK_TRY(ctx->pin_small.ensure(part_bytes));
+        if (!(zc & 1)) VK_TRY(ctx->ws[WS_PIECE].ensure(part_bytes));
+        Acc* d_part = (zc & 1) ? static_cast<Acc*>(ctx->pin_small.dp) : ctx->ws[WS_PIECE].as<Acc>();
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
                   t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
-                  bpc, wpt, ctx->ws[WS_PIECE].as<Acc>());
+                  bpc, wpt, d_part);
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
         // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the
         // upload / second read-back round trip)
-        VK_TRY(ctx->pin_small.ensure((size_t)batch * bpc * sizeof(Acc)));
         const Acc* parts = ctx->pin_small.as<Acc>();
-        VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_small.p, ctx->ws[WS_PIECE].p, (size_t)batch * bpc * sizeof(Acc),
-                                    hipMemcpyDeviceToHost, ctx->stream));
+        if (!(zc & 1))
+            VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_small.p, ctx->ws[WS_PIECE].p, part_bytes, hipMemcpyDeviceToHost,
+                                        ctx->stream));
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        const double t1 = timing ? now_us() : 0.0;
         const int nl = (int)(C::F::N / 2);
         std::vector<uint64_t> oxy(h_out_xy ? 0 : (size_t)batch * 2 * nl);
         std::vector<uint8_t> oinf(h_out_xy ? 0 : batch);
@@ -622,7 +650,11 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
             for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
             sums[g] = a;
         }
+        const double t2 = timing ? now_us() : 0.0;
         VK_TRY(acc_to_affine_batch(ctx->curve, reinterpret_cast<const uint32_t*>(sums.data()), batch, rxy, rinf));
+        if (timing)
+            fprintf(stderr, "[fb_small] %zu x %u partials: launch..readback %.1f us, adds %.1f us, affine %.1f us\n",
+                    batch, bpc, t1 - t0, t2 - t1, now_us() - t2);
         if (h_out_xy) {
             *on_host = true;
             return VC_OK;
@@ -725,7 +757,8 @@ int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows) {
 }
 
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
-                  void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host) {
+                  void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
+                  const PinBuf* pin_sc) {
     bool dummy = false;
     if (!on_host) on_host = &dummy;
     *on_host = false;
@@ -733,13 +766,13 @@ int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t 
     switch (t->curve) {
         case VC_CURVE_BN254:
             return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                 h_out_inf, on_host);
+                                                 h_out_inf, on_host, pin_sc);
         case VC_CURVE_BLS12_381:
             return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                   h_out_inf, on_host);
+                                                   h_out_inf, on_host, pin_sc);
         case VC_CURVE_BANDERSNATCH:
             return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                     h_out_inf, on_host);
+                                                     h_out_inf, on_host, pin_sc);
     }
     return VC_E_INVALID;
 }

@@ -55,7 +55,9 @@ struct DevBuf {
 // bounce buffer and start late (measured ~25 us before the MSM's second small read-back)
 struct PinBuf {
     void* p = nullptr;
+    void* dp = nullptr;     // the device's address of p (kernels read / write it over PCIe)
     size_t cap = 0;
+    unsigned flags = 0;     // hipHostMalloc flags (0 = default; hipHostMallocCoherent: fine-grained)
     int ensure(size_t bytes);
     void release();
     template <class T>
@@ -176,7 +178,8 @@ struct vc_ctx {
     vk::DevBuf ws2[vk::WS_COUNT_];  // workspace of lane 1 (side_stream)
     vk::PinBuf pin[2];              // read-back staging of lanes 0 / 1
     vk::PinBuf pin_io;              // host <-> device staging of the scheme paths (commit_batch)
-    vk::PinBuf pin_small;           // block partials of the small-batch commit path
+    vk::PinBuf pin_small;           // block partials of the small-batch commit path (fine-grained:
+                                    // the kernel writes them straight to host memory)
     vk::PinBuf pin_norm;            // block products / inverses of the split normalisation
     vk::PinBuf pin_y;               // the KZG opening's y, copied back asynchronously
     // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
@@ -272,7 +275,9 @@ int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, siz
 int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 // h_out_xy / h_out_inf (optional): host destinations -- when the small-batch latency path ran,
 // the results are written there instead of d_out_* and *on_host is set
+// pin_sc: the scalars in ctx->pin_io (host, page-locked) instead of d_scalars (nullptr): uploaded
+// to WS_SCALARS here, or read in place over PCIe by the latency path
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
-                  uint8_t* h_out_inf = nullptr, bool* on_host = nullptr);
+                  uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr);
 }  // namespace vk

@@ -126,17 +126,16 @@ static bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
 static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
                         uint8_t* out_inf) {
     const size_t in_bytes = batch * width * 32, out_bytes = batch * 65;
-    VK_TRY(ctx->ws[WS_SCALARS].ensure(in_bytes));
     VK_TRY(ctx->ws[WS_MISC].ensure(out_bytes));
     uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
     uint8_t* dinf = dxy + batch * 64;
     // pinned staging both ways (the IPA rounds call this 8 times per proof: pageable copies went
-    // through bounce buffers), points and flags read back in one copy
+    // through bounce buffers), points and flags read back in one copy; the scalars are uploaded by
+    // msm_batch_run, or read in place by its latency path
     VK_TRY(ctx->pin_io.ensure(std::max(in_bytes, out_bytes)));
     memcpy(ctx->pin_io.p, sc, in_bytes);
-    VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_SCALARS].p, ctx->pin_io.p, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     bool on_host = false;
-    VK_TRY(msm_batch_run(ctx, t, width, ctx->ws[WS_SCALARS].p, batch, 1, dxy, dinf, out_xy, out_inf, &on_host));
+    VK_TRY(msm_batch_run(ctx, t, width, nullptr, batch, 1, dxy, dinf, out_xy, out_inf, &on_host, &ctx->pin_io));
     if (on_host) return VC_OK;
     VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_io.p, dxy, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
@@ -217,6 +216,14 @@ static int msm_points(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, const
 }
 
 // ---------------------------------------------------------------- IPA prove (a8/a9)
+// VKZG_HOST_TIMING=1: the IPA prover's / verifier's host and GPU phases on stderr (probe)
+static double verify_clock_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool verify_timing() {
+    static const bool on = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+    return on;
+}
 struct IpaState {
     std::vector<Fr> a, b, coeff;
     Fr eval, w;
@@ -261,8 +268,10 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     std::vector<Fr> sc(2 * B * W);
     std::vector<uint64_t> oxy(2 * B * 8);
     std::vector<uint8_t> oinf(2 * B);
+    double lap_fill = 0, lap_commit = 0, lap_fold = 0;
     for (size_t r = 0; r < K; r++) {
         const size_t m = N >> r, half = m / 2;
+        const double c0 = verify_timing() ? verify_clock_us() : 0.0;
         par_for([&](size_t p) {
             IpaState& s = st[p];
             Fr* sL = &sc[(2 * p) * W];
@@ -281,7 +290,9 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
             sL[N] = fe_mul<F>(s.w, inner(&s.a[0], &s.b[half], half));
             sR[N] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
         });
+        const double c1 = verify_timing() ? verify_clock_us() : 0.0;
         VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data()));
+        const double c2 = verify_timing() ? verify_clock_us() : 0.0;
         par_for([&](size_t p) {
             IpaState& s = st[p];
             const uint64_t* Lxy = &oxy[(2 * p) * 8];
@@ -303,7 +314,14 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
             for (size_t i = 0; i < N; i++)
                 if ((i % m) < half) s.coeff[i] = fe_mul<F>(s.coeff[i], x);
         });
+        if (verify_timing()) {
+            const double c3 = verify_clock_us();
+            lap_fill += c1 - c0, lap_commit += c2 - c1, lap_fold += c3 - c2;
+        }
     }
+    if (verify_timing())
+        fprintf(stderr, "[ipa_prove] %zu proofs x %zu rounds: rows %.1f us, L/R commits %.1f us, transcript + folds %.1f us\n",
+                B, K, lap_fill, lap_commit, lap_fold);
     for (size_t p = 0; p < B; p++) {
         proofs[p].rounds = K;
         canon_of(st[p].a[0], proofs[p].tip);
@@ -314,14 +332,6 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
 }
 
 // ---------------------------------------------------------------- IPA verify (a10)
-// VKZG_HOST_TIMING=1: the verifier's host / GPU phases on stderr (probe)
-static double verify_clock_us() {
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-static bool verify_timing() {
-    static const bool on = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
-    return on;
-}
 int ipa_verify_impl(vc_ctx* ctx, Table* t, size_t N, const Acc& com, const Fr& point, const vc_ipa_proof* pr,
                     vc_transcript* tr_in, int* result) {
     if (!is_pow2(N) || t->n < N + 1) return VC_E_INVALID;
