@@ -122,6 +122,15 @@ static Fr inner(const Fr* a, const Fr* b, size_t n) {
 
 static bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
 
+// VKZG_HOST_TIMING=1: the IPA prover's / verifier's and the multiproof verifier's host and GPU phases on stderr (probe)
+static double verify_clock_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static bool verify_timing() {
+    static const bool on = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+    return on;
+}
+
 // width-w fixed-base commitments of Montgomery scalars (host) -> canonical affine (host)
 static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
                         uint8_t* out_inf) {
@@ -207,7 +216,12 @@ static int host_msm(const uint64_t* xy, const uint8_t* inf, const Fr* sc, size_t
 static int msm_points(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, const std::vector<Fr>& sc, Acc* out) {
     size_t n = sc.size();
     if (n <= HOST_MSM_MAX) return host_msm(xy, inf, sc.data(), n, out);
+    const double c0 = verify_timing() ? verify_clock_us() : 0.0;
     VK_TRY(bases_fill(ctx, &ctx->scratch, xy, inf, n));
+    if (verify_timing()) {
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        fprintf(stderr, "msm_points n=%zu bases_fill_us=%.1f\n", n, verify_clock_us() - c0);
+    }
     DevBuf d(ctx);
     VK_TRY(d.ensure(std::max<size_t>(n, 1) * 32));
     VK_CHECK_HIP(hipMemcpyAsync(d.p, sc.data(), n * 32, hipMemcpyHostToDevice, ctx->stream));
@@ -216,14 +230,6 @@ static int msm_points(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, const
 }
 
 // ---------------------------------------------------------------- IPA prove (a8/a9)
-// VKZG_HOST_TIMING=1: the IPA prover's / verifier's host and GPU phases on stderr (probe)
-static double verify_clock_us() {
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-static bool verify_timing() {
-    static const bool on = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
-    return on;
-}
 struct IpaState {
     std::vector<Fr> a, b, coeff;
     Fr eval, w;
@@ -1840,6 +1846,7 @@ static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, con
     if (!is_pow2(N) || N > (size_t(1) << 28)) return VC_E_INVALID;  // tables below are sized by N
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
+    const double c0 = verify_timing() ? verify_clock_us() : 0.0;
     vc_transcript* tr = nullptr;
     Fr r;
     if (Q == 0) {  // no queries: the transcript of the labels alone (mp_begin wants Q > 0)
@@ -1867,12 +1874,15 @@ static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, con
         const unsigned T = host_pool().size();
         host_pool().run([&](unsigned k) { fill(Q * k / T, Q * (k + 1) / T); });
     }
+    const double c1 = verify_timing() ? verify_clock_us() : 0.0;
     Acc e;
     int st = msm_points(ctx, com_xy, com_inf, coef, &e);
     if (st != VC_OK) {
         vc_transcript_free(tr);
         return st;
     }
+    if (verify_timing())
+        fprintf(stderr, "mp_claim Q=%zu transcript+coef_us=%.1f e_msm_us=%.1f\n", Q, c1 - c0, verify_clock_us() - c1);
     uint64_t exy[8];
     uint8_t einf;
     aff_of(e, exy, &einf);
