@@ -33,11 +33,31 @@ def glv_split(k, r):
     return rem, q
 
 
-def choose_window(n):
+def top_shortfall(c, total):
+    """bits the top window of `total` digit bits in c-bit windows lacks (msm.hip top_shortfall)"""
+    W = (total + c - 1) // c
+    return c - (total - c * (W - 1))
+
+
+def choose_window(n, total):
+    """msm.hip choose_window: the size rule, unless its top window is short by more than 2 bits;
+    then the cheapest c in c0 - 5 .. c0 + 2 (W n + 2 W 2^(c-1)) whose top window is not."""
+    c0 = 5
     for lim, c in ((1 << 19, 16), (1 << 17, 15), (1 << 15, 13), (1 << 12, 11), (1 << 9, 9), (64, 7)):
         if n >= lim:
-            return c
-    return 5
+            c0 = c
+            break
+    if top_shortfall(c0, total) <= 2:
+        return c0
+    best, best_cost = c0, None
+    for c in range(max(4, c0 - 5), min(16, c0 + 2) + 1):
+        if top_shortfall(c, total) > 2:
+            continue
+        W = (total + c - 1) // c
+        cost = W * n + 2 * W * (1 << (c - 1))
+        if best_cost is None or cost < best_cost:
+            best, best_cost = c, cost
+    return best
 
 
 def signed_digits(s, c, W):
@@ -64,7 +84,7 @@ def window_slice(curve, n, part, parts):
         c = glv_window(2 * n)
         W = (GLV_BITS + c - 1) // c
     else:
-        c = choose_window(n)
+        c = choose_window(n, SCALAR_BITS[curve] + 1)
         W = (SCALAR_BITS[curve] + 1 + c - 1) // c
     return c, W, part * W // parts, (part + 1) * W // parts
 

@@ -46,7 +46,8 @@ def test_glv_window_parts_sum_to_scalar():
                 tot[i] += v
         assert all((t - s) % C.r == 0 for t, s in zip(tot, sc))
     assert pippenger.window_slice("bls12_381", 1 << 20, 0, 1)[:2] == (16, 8)
-    assert pippenger.window_slice("bls12_381", 4095, 0, 1)[:2] == (9, 29)      # below GLV_MIN_N
+    # below GLV_MIN_N: 256 digit bits; the size rule's c = 9 leaves a 4-bit top window, so 8 x 32
+    assert pippenger.window_slice("bls12_381", 4095, 0, 1)[:2] == (8, 32)
 
 
 def _mulraw(C, P, k):
@@ -148,3 +149,20 @@ def test_bit_sums_marginal_row_total():
                     continue
                 T, U = pippenger.bit_sums_marginal_urow(R, h, pL)
                 assert T == want and U == sum(R)
+
+
+def test_window_choice_top_window_full():
+    """vc_msm_windows (host only) for per-window MSMs: the top window is short by at most 2 bits --
+    a short top window piles its digits into a few buckets (BN254 at the old c = 11: 2 of 1,024,
+    every call then redid its fix-up) -- and the oracle's window_slice follows the same rule."""
+    from pyoracle import pippenger
+    from vkzg import dist
+    for curve in ("bn254", "bls12_381", "bandersnatch"):
+        total = pippenger.SCALAR_BITS[curve] + 1
+        for lg in range(1, 22):
+            for n in (1 << lg, (1 << lg) + (1 << lg) // 2):
+                c, W, terms = dist.window_count(curve, n, with_terms=True)
+                if terms != 1:
+                    continue
+                assert (c, W) == pippenger.window_slice(curve, n, 0, 1)[:2]
+                assert c - (total - c * (W - 1)) <= 2, (curve, n, c, W)

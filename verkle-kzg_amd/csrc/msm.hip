@@ -1165,14 +1165,38 @@ static int glv_window_shared(size_t nv) {
     if (env >= 8 && env <= 20) return env;
     return glv_window(nv);
 }
-static int choose_window(size_t n) {
-    if (n >= (1u << 19)) return 16;
-    if (n >= (1u << 17)) return 15;
-    if (n >= (1u << 15)) return 13;
-    if (n >= (1u << 12)) return 11;
-    if (n >= (1u << 9)) return 9;
-    if (n >= 64) return 7;
-    return 5;
+// bits of the top window of `total` digit bits cut into c-bit windows, as a shortfall: the top
+// window's digits fall into 2^-(shortfall) of its bucket set
+static int top_shortfall(int c, int total) {
+    const int W = (total + c - 1) / c;
+    return c - (total - c * (W - 1));
+}
+// window bits of a per-window (non-GLV) MSM of n terms whose signed digits cover `total` bits
+// (scalar bits + 1). The size rule alone gave BN254 (255 bits) top windows of 2 bits at c = 11
+// and 8 of 13 at c = 13: a 4096-term MSM piled all its top digits into 2 of 1,024 buckets,
+// chains of ~256 pieces, so every call redid its fix-up by pointer jumping and the reduction
+// (+0.37 ms of a 0.7 ms MSM, the multiproof verifier's). A size whose top window is short by more
+// than 2 bits is replaced by the cheapest of c - 5 .. c + 2 (W n mixed adds + 2 W 2^(c-1)
+// reduction adds) that is not.
+static int choose_window(size_t n, int total) {
+    int c0 = 5;
+    if (n >= (1u << 19)) c0 = 16;
+    else if (n >= (1u << 17)) c0 = 15;
+    else if (n >= (1u << 15)) c0 = 13;
+    else if (n >= (1u << 12)) c0 = 11;
+    else if (n >= (1u << 9)) c0 = 9;
+    else if (n >= 64) c0 = 7;
+    static const int env = getenv("VKZG_MSM_TOPFIT") ? atoi(getenv("VKZG_MSM_TOPFIT")) : 1;  // A/B probe
+    if (!env || top_shortfall(c0, total) <= 2) return c0;
+    int best = c0;
+    double best_cost = 0.0;
+    for (int c = std::max(4, c0 - 5); c <= std::min(16, c0 + 2); c++) {
+        if (top_shortfall(c, total) > 2) continue;
+        const double W = (total + c - 1) / c;
+        const double cost = W * (double)n + 2.0 * W * (double)(1u << (c - 1));
+        if (best == c0 || cost < best_cost) best = c, best_cost = cost;
+    }
+    return best;
 }
 
 // One window slice [wb, we) of an MSM enqueued on a lane: sort, accumulate, fix-up, reduction and
@@ -1186,6 +1210,7 @@ struct MsmSlice {
     Lane L{};
     int c = 0, wb = 0, we = 0, W = 0;
     bool shared = false;  // all windows into one bucket set (Table::win copies)
+    int top_f = 0;        // per-window buckets: the top window's shortfall (top_shortfall), if in the slice
     uint32_t m = 1;       // > 1: radix m 2^c digits (RadixDigits), m 2^(c-1) buckets
     int sets = 1;         // shared windows: bucket sets = MSMs over the table in this slice
     uint32_t wps = 0;     // shared windows: windows per set (the window copies' count)
@@ -1405,7 +1430,8 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
     // chains up to 2^guard carry pieces are walked serially by their owners; longer ones
     // (adversarial scalars) take the pointer-jumping path in slice_finish
-    sl.guard = msm_fixup_guard_rounds(load, NB, M);
+    // (a top window short by f bits loads its buckets 2^f times the mean)
+    sl.guard = msm_fixup_guard_rounds(sl.shared ? load : load << sl.top_f, NB, M);
     // shared windows: a short top window's digits load 2^-tb of the buckets several times the
     // mean (c = 19: ~310 entries vs 56), so the walk takes chains of up to 16 pieces
     if (sl.shared) sl.guard = std::max<uint32_t>(sl.guard, 4);
@@ -1555,7 +1581,7 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
     bool shared = false;
     int top_shift = 0;
     uint32_t radix_m = 1;  // > 1: radix-B shared windows, B = radix_m 2^c
-    int c = glv ? glv_window(nv) : choose_window(nv);
+    int c = glv ? glv_window(nv) : choose_window(nv, Fr::BITS + 1);
     if constexpr (std::is_same<C, BLS381G1>::value) {
         const bool shared_env = ctx->opt_shared_windows != 0;  // vc_ctx_set_option(VC_OPT_MSM_SHARED_WINDOWS)
         // Radix-B shared windows (B = 5 x 2^16 ~ 2^18.3, one MSM on one GPU): 7 uniformly loaded
@@ -1642,6 +1668,8 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         sl[k].shared = shared;
         sl[k].m = radix_m;
         sl[k].wps = (uint32_t)Wfull;
+        if (!shared && radix_m == 1 && sl[k].we == Wfull)
+            sl[k].top_f = top_shortfall(c, glv ? GLV_BITS : Fr::BITS + 1);
     }
     hipEvent_t fork = nullptr, join = nullptr, acc0 = nullptr;
     if (nsl == 2) acc0 = ctx->get_event();
@@ -2115,7 +2143,7 @@ int msm_windows(int curve, size_t n, int* c, int* W, int* terms) {
     // BLS12-381 tables of subgroup points take the GLV split (2n terms of 127-bit scalars)
     const bool glv = curve == VC_CURVE_BLS12_381 && n >= GLV_MIN_N && n < (1u << 30);
     // (a GLV MSM over a whole table takes the shared-window size, msm_run_t)
-    *c = glv ? glv_window_shared(2 * n) : choose_window(n);
+    *c = glv ? glv_window_shared(2 * n) : choose_window(n, bits + 1);
     *W = glv ? (GLV_BITS + *c - 1) / *c : (bits + 1 + *c - 1) / *c;
     if (terms) *terms = glv ? 2 : 1;
     return VC_OK;
