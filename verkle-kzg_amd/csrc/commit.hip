@@ -583,11 +583,14 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                       const PinBuf* pin_sc) {
+                       const PinBuf* pin_sc, const std::function<void()>* overlap) {
     using Acc = typename C::Acc;
     if (width > t->n) return VC_E_RANGE;
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8, 0));
-    if (batch == 0) return VC_OK;
+    if (batch == 0) {
+        if (overlap && *overlap) (*overlap)();
+        return VC_OK;
+    }
     VK_TRY(ctx->ws[WS_OUT].ensure(batch * sizeof(Acc)));
     // resident lanes of this context's device (cached per ctx: the Guard's mutex serialises it)
     if (!ctx->fb_lanes) ctx->fb_lanes = resident_lanes(k_fb_commit_cm<C, Fr>, 256);
@@ -635,6 +638,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         if (!(zc & 1))
             VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_small.p, ctx->ws[WS_PIECE].p, part_bytes, hipMemcpyDeviceToHost,
                                         ctx->stream));
+        if (overlap && *overlap) (*overlap)();
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         const double t1 = timing ? now_us() : 0.0;
         const int nl = (int)(C::F::N / 2);
@@ -703,6 +707,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         VK_LAUNCH(ctx, "fb_combine", (k_fb_combine_wave<C>), batch, 64, 0,
                   ctx->ws[WS_PIECE].as<typename Fast29<C>::type::Acc>(), (uint32_t)nch, (uint32_t)batch,
                   ctx->ws[WS_OUT].as<Acc>());
+    if (overlap && *overlap) (*overlap)();
     return normalize_split<C>(ctx, ctx->ws[WS_OUT].as<Acc>(), batch, (typename C::Aff*)nullptr,
                               reinterpret_cast<uint32_t*>(d_out_xy), d_out_inf);
 }
@@ -758,7 +763,7 @@ int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows) {
 
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                   void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                  const PinBuf* pin_sc) {
+                  const PinBuf* pin_sc, const std::function<void()>* overlap) {
     bool dummy = false;
     if (!on_host) on_host = &dummy;
     *on_host = false;
@@ -766,13 +771,13 @@ int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t 
     switch (t->curve) {
         case VC_CURVE_BN254:
             return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                 h_out_inf, on_host, pin_sc);
+                                                 h_out_inf, on_host, pin_sc, overlap);
         case VC_CURVE_BLS12_381:
             return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                   h_out_inf, on_host, pin_sc);
+                                                   h_out_inf, on_host, pin_sc, overlap);
         case VC_CURVE_BANDERSNATCH:
             return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                     h_out_inf, on_host, pin_sc);
+                                                     h_out_inf, on_host, pin_sc, overlap);
     }
     return VC_E_INVALID;
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -276,8 +277,10 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 // h_out_xy / h_out_inf (optional): host destinations -- when the small-batch latency path ran,
 // the results are written there instead of d_out_* and *on_host is set
 // pin_sc: the scalars in ctx->pin_io (host, page-locked) instead of d_scalars (nullptr): uploaded
-// to WS_SCALARS here, or read in place over PCIe by the latency path
+// to WS_SCALARS here, or read in place over PCIe by the latency path. overlap: host work run once
+// the commit kernel is enqueued, before the call waits for it
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
-                  uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr);
+                  uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr,
+                  const std::function<void()>* overlap = nullptr);
 }  // namespace vk
