@@ -312,7 +312,10 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             }
             if ((int)in.size() <= depth) in.resize(depth + 1);
             in[depth].push_back(id);
-            for (auto& kv : n.children) stack.push_back({kv.second, depth + 1});
+            for (auto& kv : n.children) {  // (popped in reverse: fetch their lines meanwhile)
+                __builtin_prefetch(&t->nodes[kv.second]);
+                stack.push_back({kv.second, depth + 1});
+            }
         }
     };
     {
@@ -365,9 +368,21 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     // walks are pointer-chasing code: ~100-200 ns per node on one thread); every worker builds
     // the rows of its item range, then copies them into place in parallel
     HostPool& pool = host_pool();
-    auto build_rows = [&](size_t lo, size_t hi, size_t nnz_per, auto fn) {
+    // pf(i, stage): software prefetch of item i's node data ahead of the walk (stage 0 at 16 items
+    // ahead: the node; stage 1 at 8 ahead: what the node points to, its line now cached) -- the
+    // walks are chains of dependent DRAM misses (~360 ns per extension node on 16 threads)
+    auto build_rows = [&](size_t lo, size_t hi, size_t nnz_per, auto fn, auto pf) {
         Rows out;
         const size_t count = hi - lo;
+        auto walk_range = [&](size_t a, size_t b, Rows& r) {
+            for (size_t i = a; i < std::min(b, a + 16); i++) pf(i, 0);
+            for (size_t i = a; i < std::min(b, a + 8); i++) pf(i, 1);
+            for (size_t i = a; i < b; i++) {
+                if (i + 16 < b) pf(i + 16, 0);
+                if (i + 8 < b) pf(i + 8, 1);
+                fn(i, r);
+            }
+        };
         // by work, not rows: the 256 depth-1 nodes of a 65,536-key tree hold ~41K children (a
         // serial walk of their maps took 0.84 ms: profiles/r04/verkle/laps_before.txt)
         const unsigned T = (count >= 64 && count * nnz_per >= 16384)
@@ -375,7 +390,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                                : 1;
         if (T == 1) {
             out.reserve(count, count * nnz_per);
-            for (size_t i = lo; i < hi; i++) fn(i, out);
+            walk_range(lo, hi, out);
             return out;
         }
         std::vector<Rows> part(T);
@@ -383,7 +398,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             if (k >= T) return;
             const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
             part[k].reserve(b - a, (b - a) * nnz_per);
-            for (size_t i = a; i < b; i++) fn(i, part[k]);
+            walk_range(a, b, part[k]);
         });
         std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0);
         for (unsigned k = 0; k < T; k++) {
@@ -567,6 +582,14 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
                 for (int k = 0; k < cnt[h]; k++) r.add(half[h][k].pos, half[h][k].v);
                 r.end_row();
             }
+        }, [&](size_t e, int stage) {
+            const VNode& n = t->nodes[exts[e]];
+            if (stage == 0) {
+                __builtin_prefetch(&n);
+                __builtin_prefetch(reinterpret_cast<const char*>(&n) + 64);
+            } else if (!n.leaves.v.empty()) {
+                __builtin_prefetch(n.leaves.v.data());
+            }
         });
         int st = commit_rows(r12, (size_t)N, xy, inf, items);
         Rows rx;
@@ -579,6 +602,8 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
             r.add(2, &items[(2 * (e - lo)) * 4]);
             r.add(3, &items[(2 * (e - lo) + 1) * 4]);
             r.end_row();
+        }, [&](size_t e, int stage) {
+            if (stage == 0) __builtin_prefetch(t->nodes[exts[e]].stem.data());
         });
         if (st == VC_OK) st = commit_rows(rx, 4, xy2, inf2, items2);
         VK_TRY(store_level(exts, lo, hi, xy2, inf2, items2, st));
@@ -594,6 +619,14 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         Rows ri = build_rows(lo, hi, hi > lo ? (kids + hi - lo - 1) / (hi - lo) : 1, [&](size_t b, Rows& r) {
             for (auto& kv : t->nodes[lv[b]].children) r.add(kv.first, t->nodes[kv.second].item);
             r.end_row();
+        }, [&](size_t b, int stage) {
+            const VNode& n = t->nodes[lv[b]];
+            if (stage == 0) {
+                __builtin_prefetch(&n);
+                __builtin_prefetch(reinterpret_cast<const char*>(&n) + 64);
+            } else if (!n.children.v.empty()) {
+                __builtin_prefetch(n.children.v.data());
+            }
         });
         const int st = commit_rows(ri, 256, xy, inf, items);
         VK_TRY(store_level(lv, lo, hi, xy, inf, items, st));
