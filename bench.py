@@ -752,12 +752,15 @@ def kzg_reference_shapes(local, stream, cpu=True):
     data = scheme.LagrangeBasis([int(v) for v in rng.integers(0, 1 << 62, size=20)], 32)
     com = kz.commit(data)
     out["commit_ms_pippenger"] = med(lambda: kz.commit(data))
+    out["single_proof_ms_pippenger"] = med(lambda: kz.prove(com, 7, data))
+    prf = kz.prove(com, 7, data)
     # the SRS's fixed-base windows (setup, untimed -- a fixed CRS): vc_msm's small commits then take
     # the fixed-base latency path
     e.fixed_base_precompute(kz.table, 8)
     out["commit_ms"] = med(lambda: kz.commit(data))
     out["commit_same_result"] = kz.commit(data) == com
     out["single_proof_ms"] = med(lambda: kz.prove(com, 7, data))
+    out["single_proof_same_result"] = kz.prove(com, 7, data) == prf
     e.close()
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

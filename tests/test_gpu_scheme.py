@@ -181,6 +181,54 @@ def test_kzg_256_golden(eng):
         assert pr["proof"] == P(op["proof"]) and hex(pr["y"]) == op["y"]
 
 
+@pytest.mark.parametrize("curve", ["bn254", "bls12_381"])
+def test_kzg_prove_on_fixed_base_tables(curve):
+    """A KZG table with fixed-base window tables (vc_fixed_base_precompute) proves a <= 1024-term
+    opening on the batched commit's latency path instead of Pippenger: the proof and y equal the
+    Pippenger ones (and, on BN254, the golden openings), in and out of the domain, sizes 32 / 256."""
+    import ctypes
+    import numpy as np
+    import vkzg
+    from vkzg import scheme
+    from vkzg._lib import check, lib
+    e = vkzg.Engine(curve)
+    try:
+        if curve == "bn254":
+            g = load("kzg_256.json")
+            kz = scheme.KZG(e, 256, secret=100)
+            data = scheme.LagrangeBasis([H(x) for x in g["evals"]], 256)
+            com = kz.commit(data)
+            ops = [op for op in g["openings"] if "error" not in op]
+            e.fixed_base_precompute(kz.table, 8)
+            for op in ops:
+                pr = kz.prove(com, op["point"], data)
+                assert pr["proof"] == P(op["proof"]) and hex(pr["y"]) == op["y"], op["point"]
+        rng = random.Random(11)
+        nl = 8 if curve == "bn254" else 12
+        from vkzg import dist
+        r = scheme.R_BN254 if curve == "bn254" else dist.BASE_P["bandersnatch"]  # Bandersnatch's base = BLS12-381 r
+        for size in (32, 256):
+            tid = e.random_bases(size, seed=size)
+            ev = vkzg.ints_to_limbs([rng.randrange(r) for _ in range(size - 3)])
+
+            def prove(point):
+                pxy = np.zeros(nl, dtype=np.uint64)
+                pinf = np.zeros(1, dtype=np.uint8)
+                y = np.zeros(4, dtype=np.uint64)
+                pt = np.array([(point >> (64 * j)) & (2**64 - 1) for j in range(4)], dtype=np.uint64)
+                check(lib().vc_kzg_prove(e.h, tid, size, scheme._p(ev), size - 3, scheme._p(pt), scheme._p(pxy),
+                                         scheme._p(pinf), scheme._p(y)), "kzg_prove")
+                return pxy.tolist(), int(pinf[0]), y.tolist()
+
+            points = (0, 5, size - 1, size + 7, rng.randrange(r))
+            want = [prove(z) for z in points]       # Pippenger
+            e.fixed_base_precompute(tid, 8)
+            got = [prove(z) for z in points]        # fixed-base latency path
+            assert got == want, (curve, size)
+    finally:
+        e.close()
+
+
 def test_scratch_pool_reuse_and_stream_switch():
     """Per-call scratch comes from the context's stream-ordered pool (ctx.hpp DevBuf(ctx)):
     repeated KZG opens of different sizes, interleaved IPA proofs, and a switch to another

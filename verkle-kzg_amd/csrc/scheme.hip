@@ -497,6 +497,20 @@ static int kzg_prove_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals
         VK_TRY(acc_to_affine(ctx->curve, acc.data() + words, proof_xy, proof_inf));
     } else if (t && out_acc) {
         VK_TRY(msm_run(ctx, t, 0, d_q.p, size, 1, out_acc, part, parts));
+    } else if (t && t->fb_c != 0 && size <= 1024) {
+        // a small proof MSM over a table that has fixed-base window tables (vc_fixed_base_precompute):
+        // the batched commit's latency path -- one launch, the block partials added on the host --
+        // instead of a Pippenger pipeline of ~12 latency-bound launches (benches/kzg.rs: 32 terms)
+        const size_t xyb = (size_t)C_::F::N * 8;  // canonical affine x, y
+        VK_TRY(ctx->ws[WS_MISC].ensure(xyb + 1));
+        uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
+        bool on_host = false;
+        VK_TRY(msm_batch_run(ctx, t, size, d_q.p, 1, 1, dxy, dxy + xyb, proof_xy, proof_inf, &on_host));
+        if (!on_host) {
+            VK_CHECK_HIP(hipMemcpyAsync(proof_xy, dxy, xyb, hipMemcpyDeviceToHost, ctx->stream));
+            VK_CHECK_HIP(hipMemcpyAsync(proof_inf, dxy + xyb, 1, hipMemcpyDeviceToHost, ctx->stream));
+            VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        }
     } else if (t) {
         std::vector<uint32_t> acc(point_words(ctx->curve));
         VK_TRY(msm_run(ctx, t, 0, d_q.p, size, 1, acc.data()));
