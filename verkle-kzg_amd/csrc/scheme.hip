@@ -1202,8 +1202,9 @@ struct MpPrep {
 // multiproof.rs:106-112: per query "C" || compress(C) || "z" || z (u64 LE) || "y" || y -- 75
 // bytes at offset 75 i, so the records are written straight into the transcript on up to 16
 // host threads (the point compression is the costly part); the SHA-256 over them stays serial.
-// pool_ok = false: fill serially on the calling thread (mp_prove_many's transcript workers already
-// run one proof each; nesting the shared host pool there serialised them on its one-loop lock)
+// pool_ok = false: the call's own filler thread feeds the hash (scheme_host.cpp
+// transcript_digest_records) -- mp_prove_many's transcript workers and vc_multiproof_begin, whose
+// callers run several transcripts at once: on the shared host pool they queued on its one-loop lock
 // the multiproof transcript's records "C" ++ compressed(C_i) ++ "z" ++ le64(z_i) ++ "y" ++ le(y_i)
 // (multiproof.rs:109-113) for queries [lo, hi) into out
 static void mp_records(const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
@@ -1963,7 +1964,7 @@ int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_
     if (!com_xy || !com_inf || !z || !y || !tr_out || !r_out || !rows) return VC_E_INVALID;
     vc_transcript* tr = nullptr;
     Fr r;
-    VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
+    VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r, false));  // (callers overlap several)
     canon_of(r, r_out);
     std::vector<uint32_t> zval;
     const int zst = mp_points(N, Q, z, &zval);  // z itself was validated by mp_begin

@@ -1,7 +1,13 @@
 // Host-side protocol pieces (serial by nature): Fiat-Shamir transcript, hash_to_field,
 // arkworks compressed encoding, IPA CRS generation. Exported through include/vc_scheme.h.
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "../../include/vc_scheme.h"
@@ -238,7 +244,11 @@ Fr transcript_digest_records(vc_transcript* t, size_t nrec, size_t rec, const Re
                              bool pool_ok) {
     constexpr size_t CH = 4096;  // records per chunk (~300 KB)
     HostPool& P = host_pool();
+    // pool_ok: the shared host pool fills the next chunk while its worker 0 hashes; otherwise a
+    // filler thread of the call's own does (concurrent transcripts -- a stream of multiproofs,
+    // mp_prove_many's workers -- then run side by side instead of queueing on the one pool)
     const unsigned T = pool_ok ? P.size() : 1;
+    const bool helper_ok = !pool_ok;
     std::vector<uint8_t> buf[2];
     buf[0].resize(std::min(nrec, CH) * rec);
     buf[1].resize(std::min(nrec, CH) * rec);
@@ -250,12 +260,62 @@ Fr transcript_digest_records(vc_transcript* t, size_t nrec, size_t rec, const Re
     };
     auto feed = [&](Sha256& h) {
         h.update(t->state.data(), t->state.size());
+        auto serial = [&] {
+            for (size_t k = 0; k < nch; k++) {
+                chunk_fill(k, 0, 1);
+                h.update(buf[k & 1].data(), (std::min(nrec, (k + 1) * CH) - k * CH) * rec);
+            }
+        };
         if (nch > 0) {
-            if (T == 1) {
-                for (size_t k = 0; k < nch; k++) {
-                    chunk_fill(k, 0, 1);
-                    h.update(buf[k & 1].data(), (std::min(nrec, (k + 1) * CH) - k * CH) * rec);
+            if (T == 1 && nch >= 2 && helper_ok) {
+                // one filler thread of this call's own, a chunk ahead of the hash (double buffer;
+                // both sides block rather than spin: spinning threads ate the CPU quota the host
+                // pool's workers needed beside them)
+                std::mutex mu;
+                std::condition_variable cv;
+                size_t filled = 0, hashed = 0;  // under mu; filled = nch + 1: the filler failed
+                std::exception_ptr err;
+                std::thread filler;
+                bool threaded = true;
+                try {
+                    filler = std::thread([&] {
+                        try {
+                            for (size_t k = 0; k < nch; k++) {
+                                {
+                                    std::unique_lock<std::mutex> lk(mu);
+                                    cv.wait(lk, [&] { return k < hashed + 2; });
+                                }
+                                chunk_fill(k, 0, 1);
+                                std::lock_guard<std::mutex> lk(mu);
+                                filled = k + 1;
+                                cv.notify_all();
+                            }
+                        } catch (...) {
+                            std::lock_guard<std::mutex> lk(mu);
+                            err = std::current_exception();
+                            filled = nch + 1;
+                            cv.notify_all();
+                        }
+                    });
+                } catch (const std::system_error&) {  // no thread to be had: fill in line
+                    threaded = false;
+                    serial();
                 }
+                for (size_t k = 0; threaded && k < nch; k++) {
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return filled > k; });
+                        if (filled > nch) break;  // the filler failed
+                    }
+                    h.update(buf[k & 1].data(), (std::min(nrec, (k + 1) * CH) - k * CH) * rec);
+                    std::lock_guard<std::mutex> lk(mu);
+                    hashed = k + 1;
+                    cv.notify_all();
+                }
+                if (threaded) filler.join();
+                if (err) std::rethrow_exception(err);
+            } else if (T == 1) {
+                serial();
             } else {
                 P.run([&](unsigned w) { chunk_fill(0, w, T); });
                 for (size_t k = 0; k < nch; k++) {
