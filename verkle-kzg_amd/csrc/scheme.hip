@@ -216,11 +216,13 @@ static int host_msm(const uint64_t* xy, const uint8_t* inf, const Fr* sc, size_t
 }
 
 // variable-base MSM over host points (ctx scratch table) with Montgomery scalars -> Acc
-static int msm_points(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, const std::vector<Fr>& sc, Acc* out) {
+// filled: the points are in ctx->scratch already (bases_fill run by the caller)
+static int msm_points(vc_ctx* ctx, const uint64_t* xy, const uint8_t* inf, const std::vector<Fr>& sc, Acc* out,
+                      bool filled = false) {
     size_t n = sc.size();
     if (n <= HOST_MSM_MAX) return host_msm(xy, inf, sc.data(), n, out);
     const double c0 = verify_timing() ? verify_clock_us() : 0.0;
-    VK_TRY(bases_fill(ctx, &ctx->scratch, xy, inf, n));
+    if (!filled) VK_TRY(bases_fill(ctx, &ctx->scratch, xy, inf, n));
     if (verify_timing()) {
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         fprintf(stderr, "msm_points n=%zu bases_fill_us=%.1f\n", n, verify_clock_us() - c0);
@@ -1879,9 +1881,16 @@ static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, con
     const double c0 = verify_timing() ? verify_clock_us() : 0.0;
     vc_transcript* tr = nullptr;
     Fr r;
+    // the e-coefficient MSM's points (the Q commitments) are uploaded and checked on the GPU while
+    // the host transcript runs (mp_begin_overlapped) once the transcript is long enough to pay for
+    // the helper thread (Q = 32768: verify 2.37-2.52 -> 2.28 ms; neutral at 4096)
+    const bool filled = Q >= 8192;
     if (Q == 0) {  // no queries: the transcript of the labels alone (mp_begin wants Q > 0)
         tr = vc_transcript_new("multiproof");
         r = transcript_digest(tr, "r");
+    } else if (filled) {
+        VK_TRY(mp_begin_overlapped(N, Q, com_xy, com_inf, z, y, &tr, &r,
+                                   [&] { return bases_fill(ctx, &ctx->scratch, com_xy, com_inf, Q); }));
     } else {
         VK_TRY(mp_begin(N, Q, com_xy, com_inf, z, y, &tr, &r));
     }
@@ -1906,7 +1915,7 @@ static int mp_claim(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, con
     }
     const double c1 = verify_timing() ? verify_clock_us() : 0.0;
     Acc e;
-    int st = msm_points(ctx, com_xy, com_inf, coef, &e);
+    int st = msm_points(ctx, com_xy, com_inf, coef, &e, filled);
     if (st != VC_OK) {
         vc_transcript_free(tr);
         return st;
