@@ -1540,11 +1540,15 @@ static int mp_begin_overlapped(size_t N, size_t Q, const uint64_t* com_xy, const
             return VC_E_OOM;
         }
     };
+    // the overlapped transcript fills its records on its own filler thread, not the host pool the
+    // overlapped planning uses: single proof 3.99-4.15 -> 3.84-3.89 ms (`profiles/r04/mp_begin_pool/`;
+    // VKZG_MP_BEGIN_POOL=1 restores the pool, A/B probe)
+    static const bool pool = getenv("VKZG_MP_BEGIN_POOL") && atoi(getenv("VKZG_MP_BEGIN_POOL")) != 0;
     std::thread th;
     try {
         th = std::thread([&] {
             try {
-                st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out);
+                st_b = mp_begin(N, Q, com_xy, com_inf, z, y, tr_out, r_out, pool);
             } catch (...) {  // nothing may leave a thread function
                 st_b = VC_E_OOM;
             }
