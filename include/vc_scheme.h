@@ -141,7 +141,10 @@ int vc_multiproof_prove(vc_ctx* ctx, int scheme, int table, size_t N, size_t Q, 
 /* The same prover in three phases, so the Q x N field phase shards over GPUs with one
  * exchange. vc_multiproof_prove == begin + accumulate(all Q) + finish(G=1).
  * phase 1 (host, every rank): transcript over all (C, z, y) (:106-114), challenge r
- *   (canonical), and the number of distinct query points `rows` (the rows of S). */
+ *   (canonical), and the number of distinct query points `rows` (the rows of S). Pure host code,
+ *   safe to call from several threads at once: above 4096 queries each call runs one filler
+ *   thread of its own beside its SHA-256 (not the shared host pool), so concurrent transcripts
+ *   proceed side by side. */
 int vc_multiproof_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                         const uint64_t* y, vc_transcript** transcript, uint64_t* r, size_t* rows);
 /* phase 2 (device, per shard): S[row][k] = sum r^i f_i[k] over queries i in [first, first + Qs)
