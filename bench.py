@@ -153,6 +153,30 @@ def cpu_baseline(curve, n_full, sample, reps=3):
             "ms_per_msm": per_msm_s * 1e3, "host_cpus": os.cpu_count()}
 
 
+def provenance():
+    """What ran the line: the host CPU model, the SHA-256 rounds the host
+    transcript used, and the hash of the libvkzg.so this process loaded."""
+    import hashlib
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        so = open(vkzg.LIB_PATH, "rb").read()
+        lib_sha = hashlib.sha256(so).hexdigest()
+    except OSError:
+        lib_sha = None
+    sha = vkzg.lib().vc_host_sha256_path()
+    return {"host_cpu": model, "host_cpus": host_cpu_share(),
+            "sha256_path": "SHA-NI" if sha == 1 else "portable",
+            "libvkzg_sha256": lib_sha, "libvkzg": os.path.relpath(vkzg.LIB_PATH, ROOT),
+            "device": torch.cuda.get_device_name(torch.cuda.current_device())}
+
+
 def host_cpu_share():
     """What the process may actually run on: the CPUs it reports, its affinity mask and the cgroup
     v2 CPU quota (cpu.max "quota period"; None when unlimited or unreadable). On the GPU boxes the
@@ -327,13 +351,32 @@ def kzg_line(a, rank, world, local, dev, stream):
             "achieved_GBps_in_domain": fused_bytes / (res["in_domain"]["ms_per_commit_open"] * 1e-3) / 1e9}
 
 
+def rj_plus_i(rng, Q, N):
+    """Q datasets of N evaluations f_j[i] = r_j + i (benches/ipa.rs gen_data, :54-62), r_j random
+    BN254 Fr: (Q * N, 4) canonical u64 limbs. r_j's top limb is drawn below r's, so r_j + i < r
+    for every i < 2^64 (no reduction)."""
+    from vkzg import scheme
+    r3 = scheme.R_BN254 >> 192
+    rj = rng.integers(0, 1 << 63, size=(Q, 4), dtype=np.uint64) * np.uint64(2) + \
+        rng.integers(0, 2, size=(Q, 4), dtype=np.uint64)
+    rj[:, 3] = rng.integers(0, r3, size=Q, dtype=np.uint64)
+    i = np.arange(N, dtype=np.uint64)
+    out = np.empty((Q, N, 4), dtype=np.uint64)
+    out[:, :, 0] = rj[:, None, 0] + i[None, :]
+    carry = (out[:, :, 0] < rj[:, None, 0]).astype(np.uint64)
+    for k in (1, 2, 3):
+        out[:, :, k] = rj[:, None, k] + carry
+        carry = carry & (out[:, :, k] == 0).astype(np.uint64)
+    return out.reshape(Q * N, 4)
+
+
 def mp_line(a, rank, world, local, dev, stream, comm=None):
     """configs[4]: IPA multiproof (multiproof.rs:99-176) over Q = 2^mp_log_q width-256 queries
     on BN254 (the reference's curve), the query set sharded over the ranks (vkzg.dist
     .multiproof_prove_sharded: host transcript on every rank, per-point sums of the local
-    slice on the GPU, one all-gather of the 256 x 256 sums, finish on every rank). Inputs:
-    random evaluations (< 2^252), their commitments (batched fixed-base commits, untimed),
-    uniform points z in [0, 256), y = f(z)."""
+    slice on the GPU, one all-gather of the 256 x 256 sums, finish on every rank). Inputs: the
+    reference bench's datasets f_j[i] = r_j + i (benches/ipa.rs:38-62, rj_plus_i), their
+    commitments (batched fixed-base commits, untimed), uniform points z in [0, 256), y = f(z)."""
     from vkzg import scheme
     N, Q = 256, 1 << a.mp_log_q
     meng = vkzg.Engine("bn254", local)
@@ -342,8 +385,7 @@ def mp_line(a, rank, world, local, dev, stream, comm=None):
     ipa = scheme.IPA(meng, N, crs)
     rng = np.random.default_rng(77)
     lo, hi = vdist.shard_range(Q, rank, world)
-    data = rng.integers(0, 1 << 63, size=(Q * N, 4), dtype=np.uint64)
-    data[:, 3] &= np.uint64((1 << 60) - 1)          # < 2^252 < r
+    data = rj_plus_i(rng, Q, N)
     z = rng.integers(0, N, size=Q, dtype=np.uint64)
     y = data.reshape(Q, N, 4)[np.arange(Q), z.astype(np.int64)].copy()
     # commitments of all queries (every rank needs all of them for the transcript), untimed
@@ -994,8 +1036,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    eng.enable_timing(True)
-    eng.reset_timing()
+    # the timed region runs WITHOUT per-kernel HIP events: an event recorded between two kernels
+    # of one stream holds the next dispatch ~10 us (profiles/r05/event_gaps/), i.e. ~0.1 ms of the
+    # ~11-kernel pipeline; the kernel durations come from a second pass below
     step_ms = []  # every step returns its host result (the call is synchronous): per-step times
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -1006,8 +1049,23 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    eng.enable_timing(False)
     plan = eng.msm_last_plan()  # the geometry the timed MSMs ran (before the 1-term result check)
+    # kernel-timing pass: the same K steps with HIP events around every launch (on the stream the
+    # kernels run on); its wall time is reported beside the headline as ms_per_step_with_events
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.enable_timing(True)
+    eng.reset_timing()
+    t0e = time.perf_counter()
+    for _ in range(a.steps):
+        res_e = step()
+    torch.cuda.synchronize(dev)
+    dt_events = time.perf_counter() - t0e
+    eng.enable_timing(False)
+    if not (int(res_e[1]) == int(res[1]) and np.array_equal(np.asarray(res_e[0]), np.asarray(res[0]))):
+        raise SystemExit("bench: the kernel-timing pass gave a different MSM result")
+    acc_mhz, acc_clk_n = eng.accumulate_clock()
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -1140,6 +1198,7 @@ def main():
         "ms_per_step": ms_per_step,
         "ms_per_step_median": float(np.median(step_ms)),
         "ms_per_step_min": float(np.min(step_ms)),
+        "ms_per_step_with_events": dt_events / a.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -1154,8 +1213,9 @@ def main():
                    "window_bits": c_bits, "windows": w_total, "radix": plan["radix_mul"] << c_bits,
                    "radix_form": f"{plan['radix_mul']} * 2^{c_bits}", "terms_per_point": terms,
                    "precomputed_bases": (f"{w_total} x 2n window copies B^w P_i, B^w phi(P_i) with B = "
-                                         f"{plan['radix_mul']} * 2^{c_bits}, each x, y, -y in radix-2^29 limbs "
-                                         f"({w_total * 2 * n * 168 / 1e9:.2f} GB), built once per base table "
+                                         f"{plan['radix_mul']} * 2^{c_bits}, each signed copy (+-) one aligned "
+                                         f"128-B record of signed radix-2^30 limbs (x, y) "
+                                         f"({w_total * 2 * n * 2 * 128 / 1e9:.2f} GB), built once per base table "
                                          "(a fixed CRS), untimed; `variable_base` is the same MSM without them")
                    if plan["shared_windows"] else None},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1169,6 +1229,12 @@ def main():
                              "frac are the algorithmic-HBM figures BASELINE.json's metric asks for; the "
                              "valu object is the binding roofline"},
         "kernel_ms": kernels,
+        "kernel_timing": ("a second pass of the same K steps with HIP events around every launch on the "
+                          "launch stream (ms_per_step_with_events); the headline pass runs without them"),
+        "accumulate_clock_mhz": acc_mhz or None,
+        "accumulate_clock_source": (f"s_memtime / s_memrealtime stamps around one lane's loop, {acc_clk_n} "
+                                    "timed launches (vc_ctx_accumulate_clock)") if acc_clk_n else None,
+        "provenance": provenance(),
         "result_inf": int(res[1]),
         "result_check": check,
         "variable_base": variable,

@@ -35,6 +35,13 @@ void vc_group_destroy(vc_group* g);
 int vc_group_size(const vc_group* g);
 /* member k's context (its knobs, timing, stream); owned by the group */
 vc_ctx* vc_group_member(vc_group* g, int k);
+/* How device-to-device copies from member `from` to member `to` travel (the multiproof sums to
+ * member 0): VC_GROUP_PEER_SAME (one device), VC_GROUP_PEER_DIRECT (peer access enabled at
+ * vc_group_create: xGMI), VC_GROUP_PEER_STAGED (no peer access: HIP stages through host memory). */
+#define VC_GROUP_PEER_SAME 0
+#define VC_GROUP_PEER_DIRECT 1
+#define VC_GROUP_PEER_STAGED 2
+int vc_group_peer_path(const vc_group* g, int from, int to);
 
 /* Tables: a group table id names one copy per member (uploaded to every member concurrently). */
 int vc_group_bases_upload(vc_group* g, const uint64_t* affine_xy, const uint8_t* inf, size_t n, int* table_id);

@@ -87,6 +87,10 @@ int vc_ctx_enable_timing(vc_ctx* ctx, int on);
 /* name: "msm_accumulate", "msm_digits", ... ; returns total ms and launch count */
 int vc_ctx_kernel_time(vc_ctx* ctx, const char* name, double* total_ms, long* launches);
 int vc_ctx_reset_timing(vc_ctx* ctx);
+/* With timing on, each bucket-accumulate launch also stamps the shader clock (s_memtime) against
+ * the 100 MHz constant clock (s_memrealtime) around one lane's loop: the mean effective shader clock
+ * (MHz) over the launches since the last reset -- the DVFS state the accumulate ran at. */
+int vc_ctx_accumulate_clock(vc_ctx* ctx, double* mhz, long* launches);
 
 /* Base tables ---------------------------------------------------------------
  * Upload n affine bases once (validated on the device: VC_E_NOT_ON_CURVE).
@@ -122,6 +126,11 @@ int vc_msm_device_many(vc_ctx* ctx, int table_id, const void* const* d_scalars, 
 int vc_point_words(int curve);
 int vc_msm_device_partial(vc_ctx* ctx, int table_id, size_t offset, const void* d_scalars,
                           size_t n, int mont, uint32_t* out_acc);
+/* The same from host scalars (vc_msm's chunked copy: a large BLS12-381 range copies its scalars in
+ * VC_OPT_MSM_HOST_CHUNKS chunks under the previous chunk's work) -- one GPU's share of a
+ * point-split MSM whose scalars live in host memory (vc_group_msm, vc_msm_sharded callers). */
+int vc_msm_partial(vc_ctx* ctx, int table_id, size_t offset, const uint64_t* scalars, size_t n, int mont,
+                   uint32_t* out_acc);
 /* Window-sliced partial MSM (the other way to shard one MSM across GPUs): part k of `parts`
  * covers Pippenger windows [k*W/parts, (k+1)*W/parts) of ALL n terms, including their 2^(c*w)
  * weights, so the parts' accumulators sum (vc_partials_sum) to the whole MSM. Each part
@@ -155,7 +164,7 @@ int vc_msm_batch_device(vc_ctx* ctx, int table_id, size_t width, const void* d_s
 int vc_msm_batch_sparse(vc_ctx* ctx, int table_id, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                         const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
 /* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 20]
- * (n x ceil(bits/c) x 2^(c-1) affine points: 167 GB for 256 Bandersnatch bases at c = 20). */
+ * (n x ceil(bits/c) x 2^(c-1) entries of 108 B: 188 GB for 256 Bandersnatch bases at c = 20). */
 int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
 /* The same with `windows` signed-digit windows of window_bits or window_bits + 1 bits (the
  * last bits + 1 - window_bits * windows windows are the wider ones; window_bits in [4, 19]).

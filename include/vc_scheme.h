@@ -29,6 +29,9 @@ extern "C" {
  * creation; then state = ser(out) || label. */
 typedef struct vc_transcript vc_transcript;
 vc_transcript* vc_transcript_new(const char* label);
+/* which SHA-256 rounds the host transcript runs on this machine: 1 = x86 SHA extensions (SHA-NI),
+ * 0 = the portable rounds (same digests; a machine-dependent speed, reported by bench.py) */
+int vc_host_sha256_path(void);
 vc_transcript* vc_transcript_clone(const vc_transcript* t);
 void vc_transcript_free(vc_transcript* t);
 void vc_transcript_reserve(vc_transcript* t, size_t bytes); /* capacity hint for long transcripts */

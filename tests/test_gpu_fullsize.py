@@ -6,8 +6,9 @@ properties that are exact for these inputs:
               s_i are re-derived on the host and 64 sampled P_i are checked against the oracle's
               s_i G), so sum k_i P_i = (sum k_i s_i mod r) G exactly -- on the shared-window
               path the bench times, on the plain variable-base path, and in point chunks;
-  configs[2]  10k x width-256 Bandersnatch commits on the c = 20 fixed-base table (the bench's),
-              16 sampled commits against the C oracle (utils.rs:16-19 restated);
+  configs[2]  10k x width-256 Bandersnatch commits on the uniform c = 20 fixed-base table and on
+              the mixed tables (the bench's is 13 windows of 19 / 20 bits), sampled commits
+              against the C oracle (utils.rs:16-19 restated);
   configs[3]  KZG commit + open at d = 2^20 on BLS12-381: the trapdoor identity
               pi (s - z) = C - y G (s = 100, kzg/mod.rs:115-154) in and outside the domain;
   configs[4]  IPA multiproof over Q = 2^16 width-256 queries: verify_multiproof accepts, D / y

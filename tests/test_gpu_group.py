@@ -206,3 +206,77 @@ def test_group_errors():
         assert inf == 1
     finally:
         g.close()
+
+
+def test_group_multiproof_fewer_queries_than_members():
+    """Q < G: the empty slices contribute zero sums (cleared on member 0's stream before the
+    finish reads them); the proof equals the one-member group's (vc_multiproof_prove)."""
+    want_g, data, cxy, cinf, z, y = _golden_mp("ipa")
+    Q = 2
+    data, cxy, cinf = data[:Q * 256], cxy[:Q], cinf[:Q]
+    z, y = z[:Q], y[:Q]
+    out = []
+    for G in (1, 3):
+        g = _group("bn254", G)
+        try:
+            tid = g.upload_points([P(h) for h in load("ipa_crs_bn254.json")["points"]])
+            out.append(g.multiproof_prove(0, tid, 256, data, cxy, cinf, z, y))
+        finally:
+            g.close()
+    a, b = out
+    assert a["d"] == b["d"]
+    assert a["proof"].l == b["proof"].l and a["proof"].r == b["proof"].r
+    assert a["proof"].tip == b["proof"].tip and a["proof"].y == b["proof"].y
+
+
+def test_group_peer_path():
+    """members on one device copy within it (VC_GROUP_PEER_SAME); distinct devices report direct
+    peer access or staged copies -- never an error."""
+    import torch
+    g = _group("bn254", 2)
+    try:
+        assert g.peer_path(0, 1) == 0 and g.peer_path(1, 0) == 0 and g.peer_path(0, 0) == 0
+    finally:
+        g.close()
+    if torch.cuda.device_count() > 1:
+        from vkzg.group import Group
+        g = Group("bn254", [0, 1])
+        try:
+            assert g.peer_path(0, 1) in (1, 2) and g.peer_path(1, 0) in (1, 2)
+        finally:
+            g.close()
+
+
+def test_group_msm_2e20_chunked_point_split():
+    """configs[1] through vc_group_msm's point split on G = 2 members: each member's 2^19-point
+    share copies its host scalars in chunks under its own MSM (vc_msm_partial, the chunked
+    point-range path on the radix copies); the sum == (sum k_i s_i) G over P_i = s_i G; and
+    vc_msm_partial == vc_msm_device_partial on one member."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    n = 1 << 20
+    g = _group("bls12_381", 2)
+    try:
+        tid = g.random_bases(n, seed=2024)
+        s = vkzg.random_base_scalars("bls12_381", 2024, n)
+        k = vkzg.random_scalars("bls12_381", n, np.random.default_rng(1234))
+        want = C.mul(C.g, vkzg.dot_mod(k, s, C.r))
+        from vkzg import group as vgroup
+        g.set_msm_split(vgroup.SPLIT_POINTS)
+        got = g.msm(tid, k)
+        assert vkzg.arrays_to_points("bls12_381", np.asarray(got[0])[None, :],
+                                     np.array([got[1]], dtype=np.uint8))[0] == want
+        eng = vkzg.Engine.__new__(vkzg.Engine)  # member 0's context, not owned
+        eng.h, eng.curve, eng.cid, eng.nl = g.member(0), "bls12_381", vkzg.engine.CURVE_IDS["bls12_381"], 6
+        mt = g.member_table(tid, 0)
+        half = n // 2
+        a = eng.msm_partial(mt, k[half:], offset=half)
+        d_k = torch.from_numpy(k[half:].view(np.int64).copy()).cuda()
+        b = eng.msm_device_partial(mt, d_k.data_ptr(), half, offset=half)
+        from vkzg.engine import partials_sum
+        pa, pb = partials_sum("bls12_381", [a]), partials_sum("bls12_381", [b])
+        assert pa[1] == pb[1] and np.array_equal(pa[0], pb[0])
+        eng.h = None
+    finally:
+        g.close()

@@ -123,7 +123,29 @@ void vc_ctx::timer_end(const char* name, hipEvent_t a, hipStream_t s) {
     pending.push_back({a, b, name});
 }
 
+uint64_t* vc_ctx::clk_slot() {
+    constexpr uint32_t SLOTS = 256;
+    if (!timing || clk.ensure(SLOTS * 4 * sizeof(uint64_t)) != VC_OK) return nullptr;
+    if (clk_pending.size() >= SLOTS) return nullptr;  // uncollected slots would be overwritten
+    const uint32_t s = clk_next++ % SLOTS;
+    clk_pending.push_back(s);
+    return clk.as<uint64_t>() + 4 * (size_t)s;
+}
+
 void vc_ctx::collect_timers() {
+    if (!clk_pending.empty()) {
+        std::vector<uint64_t> h(clk.cap / sizeof(uint64_t));
+        if (hipMemcpy(h.data(), clk.p, clk.cap, hipMemcpyDeviceToHost) == hipSuccess)
+            for (uint32_t s : clk_pending) {
+                const uint64_t* v = &h[4 * (size_t)s];
+                if (v[2] > v[0] && v[3] > v[1]) {
+                    clk_cycles += (double)(v[2] - v[0]);
+                    clk_ticks += (double)(v[3] - v[1]);
+                    clk_n++;
+                }
+            }
+        clk_pending.clear();
+    }
     for (auto& p : pending) {
         float ms = 0.f;
         if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
@@ -297,10 +319,20 @@ int vc_ctx_kernel_time(vc_ctx* ctx, const char* name, double* total_ms, long* la
     return VC_OK;
 }
 
+int vc_ctx_accumulate_clock(vc_ctx* ctx, double* mhz, long* launches) {
+    if (!ctx || !mhz) return VC_E_INVALID;
+    Guard g(ctx);
+    *mhz = ctx->clk_ticks > 0 ? ctx->clk_cycles / ctx->clk_ticks * 100.0 : 0.0;
+    if (launches) *launches = ctx->clk_n;
+    return VC_OK;
+}
+
 int vc_ctx_reset_timing(vc_ctx* ctx) {
     if (!ctx) return VC_E_INVALID;
     Guard g(ctx);
     ctx->ktime.clear();
+    ctx->clk_cycles = ctx->clk_ticks = 0.0;
+    ctx->clk_n = 0;
     return VC_OK;
 }
 
@@ -440,6 +472,16 @@ int vc_msm(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n
     std::vector<uint32_t> acc(vk::point_words(ctx->curve));
     VK_TRY(vk::msm_run_host(ctx, t, offset, scalars, n, mont, acc.data()));
     return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
+}
+
+int vc_msm_partial(vc_ctx* ctx, int id, size_t offset, const uint64_t* scalars, size_t n, int mont,
+                   uint32_t* out_acc) {
+    if (!ctx || !out_acc || (n > 0 && !scalars)) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    if (offset > t->n || n > t->n - offset) return VC_E_RANGE;
+    return vk::msm_run_host(ctx, t, offset, scalars, n, mont, out_acc);
 }
 
 int vc_partials_sum(int curve, const uint32_t* accs, size_t k, uint64_t* out_xy, uint8_t* out_inf) {

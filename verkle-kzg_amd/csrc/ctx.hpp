@@ -202,6 +202,15 @@ struct vc_ctx {
     std::vector<vk::PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
     std::map<std::string, std::pair<double, long>> ktime;
+    // effective shader clock of timed accumulate launches: with timing on, the first lane of the
+    // grid stamps s_memtime (shader cycles) and s_memrealtime (100 MHz) around its loop into a slot
+    // of `clk` (4 u64); collect_timers adds the deltas (vc_ctx_accumulate_clock)
+    vk::DevBuf clk;
+    std::vector<uint32_t> clk_pending;  // slots written by launches not yet collected
+    uint32_t clk_next = 0;
+    double clk_cycles = 0.0, clk_ticks = 0.0;
+    long clk_n = 0;
+    uint64_t* clk_slot();  // nullptr unless timing (and the buffer exists)
     vk::Table scratch;  // variable-base points of verifiers (grow-only)
     // per-domain constant tables (domain powers, 1/(w^k - 1)), keyed by field and size
     std::map<std::string, std::unique_ptr<vk::DevBuf>> dcache;

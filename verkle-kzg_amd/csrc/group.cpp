@@ -20,10 +20,13 @@
 namespace {
 
 // G workers; run(f) calls f(k) for every member k concurrently (k = 0 on the caller's thread) and
-// returns when all have finished. Threads live as long as the group.
+// returns when all have finished. Threads live as long as the group. An exception out of f(k)
+// (std::bad_alloc from a vc_* call's host vectors) is caught on whichever thread ran it and
+// reported through failed(k) after every member has finished: the caller's f outlives every
+// worker that still runs it.
 class Team {
 public:
-    explicit Team(int n) : n_(n) {
+    explicit Team(int n) : n_(n), failed_(n, 0) {
         for (int k = 1; k < n; k++) th_.emplace_back([this, k] { loop(k); });
     }
     ~Team() {
@@ -36,8 +39,9 @@ public:
         for (auto& t : th_) t.join();
     }
     void run(const std::function<void(int)>& f) {
+        for (auto& x : failed_) x = 0;
         if (n_ == 1) {
-            f(0);
+            guarded(f, 0);
             return;
         }
         {
@@ -47,10 +51,21 @@ public:
             gen_++;
         }
         cv_.notify_all();
-        f(0);
+        guarded(f, 0);
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [&] { return pending_ == 0; });
         job_ = nullptr;
+    }
+    // member k's share threw in the last run (its status slot may not have been written)
+    bool failed(int k) const { return failed_[k] != 0; }
+
+private:
+    void guarded(const std::function<void(int)>& f, int k) {
+        try {
+            f(k);
+        } catch (...) {
+            failed_[k] = 1;
+        }
     }
 
 private:
@@ -65,12 +80,13 @@ private:
                 if (quit_) return;
                 f = job_;
             }
-            (*f)(k);
+            guarded(*f, k);
             std::lock_guard<std::mutex> lk(mu_);
             if (--pending_ == 0) done_.notify_one();
         }
     }
     int n_;
+    std::vector<char> failed_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
@@ -117,11 +133,19 @@ struct vc_group {
     std::vector<vc_ctx*> ctx;
     std::vector<std::vector<int>> tables;  // [group table id][member] -> member table id
     std::vector<MemBuf> data, sums;        // per member: input staging, multiproof sums
+    std::vector<int> peer;                 // [from * G + to]: VC_GROUP_PEER_* (vc_group_peer_path)
     int split = VC_GROUP_SPLIT_AUTO;
     std::mutex mu;  // one group call at a time
     Team* team = nullptr;
     int size() const { return (int)ctx.size(); }
     bool table_ok(int id) const { return id >= 0 && id < (int)tables.size(); }
+    // f(k) on every member; a share that threw reports VC_E_OOM in st[k]. Returns the first error.
+    int run(std::vector<int>& st, const std::function<void(int)>& f) {
+        team->run(f);
+        for (int k = 0; k < size(); k++)
+            if (team->failed(k)) st[k] = VC_E_OOM;
+        return first_error(st);
+    }
 };
 
 extern "C" {
@@ -144,6 +168,23 @@ int vc_group_create(int curve, int ndev, const int* devices, vc_group** out) {
     g->data.resize(ndev);
     g->sums.resize(ndev);
     for (int k = 0; k < ndev; k++) g->data[k].dev = g->sums[k].dev = g->ctx[k]->device;
+    // direct peer access (xGMI) for every member pair whose devices allow it; otherwise the
+    // device-to-device copies (multiproof sums to member 0) are staged through host memory by HIP
+    g->peer.assign((size_t)ndev * ndev, VC_GROUP_PEER_SAME);
+    for (int a = 0; a < ndev; a++)
+        for (int b = 0; b < ndev; b++) {
+            const int da = g->ctx[a]->device, db = g->ctx[b]->device;
+            if (da == db) continue;
+            int can = 0;
+            int path = VC_GROUP_PEER_STAGED;
+            if (hipDeviceCanAccessPeer(&can, da, db) == hipSuccess && can) {
+                (void)hipSetDevice(da);
+                const hipError_t e = hipDeviceEnablePeerAccess(db, 0);
+                if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) path = VC_GROUP_PEER_DIRECT;
+                (void)hipGetLastError();  // an already-enabled pair is not an error for later calls
+            }
+            g->peer[(size_t)a * ndev + b] = path;
+        }
     g->team = new Team(ndev);
     *out = g;
     return VC_OK;
@@ -159,6 +200,11 @@ void vc_group_destroy(vc_group* g) {
 }
 
 int vc_group_size(const vc_group* g) { return g ? g->size() : VC_E_INVALID; }
+
+int vc_group_peer_path(const vc_group* g, int from, int to) {
+    if (!g || from < 0 || to < 0 || from >= g->size() || to >= g->size()) return VC_E_INVALID;
+    return g->peer[(size_t)from * g->size() + to];
+}
 
 vc_ctx* vc_group_member(vc_group* g, int k) { return (g && k >= 0 && k < g->size()) ? g->ctx[k] : nullptr; }
 
@@ -184,8 +230,7 @@ namespace {
 int new_table(vc_group* g, const std::function<int(int k, int* id)>& make, int* table_id) {
     const int G = g->size();
     std::vector<int> ids(G, -1), st(G, VC_OK);
-    g->team->run([&](int k) { st[k] = make(k, &ids[k]); });
-    VK_TRY(first_error(st));
+    VK_TRY(g->run(st, [&](int k) { st[k] = make(k, &ids[k]); }));
     g->tables.push_back(ids);
     *table_id = (int)g->tables.size() - 1;
     return VC_OK;
@@ -222,10 +267,9 @@ int vc_group_fixed_base_precompute(vc_group* g, int id, int window_bits, int win
     std::lock_guard<std::mutex> lk(g->mu);
     if (!g->table_ok(id)) return VC_E_TABLE;
     std::vector<int> st(g->size(), VC_OK);
-    g->team->run([&](int k) {
+    return g->run(st, [&](int k) {
         st[k] = vc_fixed_base_precompute_windows(g->ctx[k], g->tables[id][k], window_bits, windows);
     });
-    return first_error(st);
 }
 
 int vc_group_msm(vc_group* g, int id, size_t offset, const uint64_t* scalars, size_t n, int mont, uint64_t* out_xy,
@@ -240,21 +284,21 @@ int vc_group_msm(vc_group* g, int id, size_t offset, const uint64_t* scalars, si
     const int words = vc_point_words(g->curve);
     std::vector<uint32_t> accs((size_t)words * G, 0);
     std::vector<int> st(G, VC_OK);
-    g->team->run([&](int k) {
+    VK_TRY(g->run(st, [&](int k) {
         auto share = [&]() -> int {
-            size_t lo = 0, hi = n;
-            if (!windows) vk::shard_range(n, k, G, &lo, &hi);  // n >= G: no empty share
-            VK_TRY(g->data[k].ensure((hi - lo) * 32));
-            VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
-            VK_CHECK_HIP(hipMemcpy(g->data[k].p, scalars + lo * 4, (hi - lo) * 32, hipMemcpyHostToDevice));
             uint32_t* acc = accs.data() + (size_t)k * words;
-            if (windows)
-                return vc_msm_device_window_part(g->ctx[k], g->tables[id][k], offset, g->data[k].p, n, mont, k, G, acc);
-            return vc_msm_device_partial(g->ctx[k], g->tables[id][k], offset + lo, g->data[k].p, hi - lo, mont, acc);
+            if (!windows) {  // its own scalars only, copied in chunks under its own MSM (vc_msm_partial)
+                size_t lo, hi;
+                vk::shard_range(n, k, G, &lo, &hi);  // n >= G: no empty share
+                return vc_msm_partial(g->ctx[k], g->tables[id][k], offset + lo, scalars + lo * 4, hi - lo, mont, acc);
+            }
+            VK_TRY(g->data[k].ensure(n * 32));
+            VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+            VK_CHECK_HIP(hipMemcpy(g->data[k].p, scalars, n * 32, hipMemcpyHostToDevice));
+            return vc_msm_device_window_part(g->ctx[k], g->tables[id][k], offset, g->data[k].p, n, mont, k, G, acc);
         };
         st[k] = share();
-    });
-    VK_TRY(first_error(st));
+    }));
     return vc_partials_sum(g->curve, accs.data(), G, out_xy, out_inf);
 }
 
@@ -266,14 +310,13 @@ int vc_group_msm_batch(vc_group* g, int id, size_t width, const uint64_t* scalar
     const int G = g->size();
     const size_t W2 = 2 * (size_t)vk::aff_limbs64(g->curve);
     std::vector<int> st(G, VC_OK);
-    g->team->run([&](int k) {
+    return g->run(st, [&](int k) {
         size_t lo, hi;
         vk::shard_range(batch, k, G, &lo, &hi);
         if (hi > lo)
             st[k] = vc_msm_batch(g->ctx[k], g->tables[id][k], width, scalars + lo * width * 4, hi - lo, mont,
                                  out_xy + lo * W2, out_inf + lo);
     });
-    return first_error(st);
 }
 
 int vc_group_kzg_prove(vc_group* g, int id, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
@@ -287,7 +330,7 @@ int vc_group_kzg_prove(vc_group* g, int id, size_t size, const uint64_t* evals, 
     std::vector<uint32_t> accs((size_t)words * G, 0);
     std::vector<uint64_t> ys((size_t)4 * G, 0);
     std::vector<int> st(G, VC_OK);
-    g->team->run([&](int k) {
+    VK_TRY(g->run(st, [&](int k) {
         auto share = [&]() -> int {
             VK_TRY(g->data[k].ensure(max * 32));
             VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
@@ -296,8 +339,7 @@ int vc_group_kzg_prove(vc_group* g, int id, size_t size, const uint64_t* evals, 
                                             accs.data() + (size_t)k * words, &ys[(size_t)4 * k]);
         };
         st[k] = share();
-    });
-    VK_TRY(first_error(st));
+    }));
     memcpy(y, ys.data(), 32);
     return vc_partials_sum(g->curve, accs.data(), G, proof_xy, proof_inf);
 }
@@ -341,7 +383,7 @@ int vc_group_multiproof_prove(vc_group* g, int scheme, int id, size_t N, size_t 
     int st0 = g->sums[0].ensure(sbytes * G);
     std::vector<int> st(G, st0);
     if (st0 == VC_OK)
-        g->team->run([&](int k) {
+        g->run(st, [&](int k) {
             auto upload = [&]() -> int {
                 size_t lo, hi;
                 vk::shard_range(Q, k, G, &lo, &hi);
@@ -360,14 +402,16 @@ int vc_group_multiproof_prove(vc_group* g, int scheme, int id, size_t N, size_t 
         return st_b;
     }
     if (first_error(st) == VC_OK)
-        g->team->run([&](int k) {
+        g->run(st, [&](int k) {
             auto share = [&]() -> int {
                 size_t lo, hi;
                 vk::shard_range(Q, k, G, &lo, &hi);
                 uint8_t* dst0 = static_cast<uint8_t*>(g->sums[0].p) + (size_t)k * sbytes;
-                if (hi == lo) {  // an empty slice contributes zero sums
+                if (hi == lo) {  // an empty slice (Q < G) contributes zero sums, cleared on the stream
+                    // vc_multiproof_finish reads them on
                     VK_CHECK_HIP(hipSetDevice(g->ctx[0]->device));
-                    VK_CHECK_HIP(hipMemset(dst0, 0, sbytes));
+                    VK_CHECK_HIP(hipMemsetAsync(dst0, 0, sbytes, g->ctx[0]->stream));
+                    VK_CHECK_HIP(hipStreamSynchronize(g->ctx[0]->stream));
                     return VC_OK;
                 }
                 VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
@@ -399,7 +443,7 @@ int vc_group_multiproof_prove_many(vc_group* g, int scheme, int id, size_t N, si
     if (!g->table_ok(id)) return VC_E_TABLE;
     const int G = g->size();
     std::vector<int> st(G, VC_OK);
-    g->team->run([&](int k) {
+    return g->run(st, [&](int k) {
         auto share = [&]() -> int {
             size_t lo, hi;
             vk::shard_range(P, k, G, &lo, &hi);
@@ -416,7 +460,6 @@ int vc_group_multiproof_prove_many(vc_group* g, int scheme, int id, size_t N, si
         };
         st[k] = share();
     });
-    return first_error(st);
 }
 
 int vc_group_verkle_commitment(vc_group* g, int id, vc_verkle* tree, uint64_t* out_xy, uint8_t* out_inf) {
@@ -426,8 +469,16 @@ int vc_group_verkle_commitment(vc_group* g, int id, vc_verkle* tree, uint64_t* o
     vk::Multi mu;
     mu.ctx = g->ctx;
     mu.table = g->tables[id];
-    mu.run = [&](const std::function<void(int)>& f) { g->team->run(f); };
-    return vk::verkle_commitment(g->ctx[0], g->tables[id][0], tree, out_xy, out_inf, nullptr, &mu);
+    // a member share that threw fails the level: rethrown here, after every member has finished
+    mu.run = [&](const std::function<void(int)>& f) {
+        std::vector<int> st(g->size(), VC_OK);
+        if (g->run(st, f) != VC_OK) throw std::bad_alloc();
+    };
+    try {
+        return vk::verkle_commitment(g->ctx[0], g->tables[id][0], tree, out_xy, out_inf, nullptr, &mu);
+    } catch (const std::bad_alloc&) {
+        return VC_E_OOM;
+    }
 }
 
 }  // extern "C"

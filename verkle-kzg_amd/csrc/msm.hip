@@ -440,13 +440,20 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ offsets, uint32_t NBtot, uint32_t M,
     typename Fast29<C>::type::Acc* __restrict__ buckets, typename Fast29<C>::type::Acc* __restrict__ carry_in,
     uint8_t* __restrict__ through, typename Fast29<C>::type::Acc* __restrict__ owner_piece,
-    uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max, uint32_t merge) {
+    uint32_t* __restrict__ owner_bucket, uint32_t* __restrict__ chain_max, uint32_t merge,
+    unsigned long long* __restrict__ clk) {
     using FC = typename Fast29<C>::type;
     using Aff = BT;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t L = offsets[NBtot];  // entry count, read on the device: no host round trip
     uint32_t k = t * M;                 // grid sized for the n*W upper bound
     if (k >= L) return;
+    // clock stamp (timing passes only: clk is null otherwise): shader cycles and 100 MHz ticks
+    const bool stamp = clk != nullptr && t == 0;
+    if (stamp) {
+        clk[0] = __builtin_amdgcn_s_memtime();
+        clk[1] = __builtin_amdgcn_s_memrealtime();
+    }
     uint32_t e = min(k + M, L);
     owner_bucket[t] = NONE;
     through[t] = 0;
@@ -526,6 +533,10 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
                 bend = offsets[b + 1];
             } while (bend <= k);
         }
+    }
+    if (stamp) {
+        clk[2] = __builtin_amdgcn_s_memtime();
+        clk[3] = __builtin_amdgcn_s_memrealtime();
     }
 #ifdef VKZG_ACC_MERGE_BUILD
     if (merge) {  // uniform
@@ -1426,7 +1437,7 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     if (acc_wait) VK_CHECK_HIP(hipStreamWaitEvent(st, acc_wait, 0));
     VK_LAUNCH_ON(ctx, st, "msm_accumulate", (k_msm_accumulate<C, BT>), (Tmax + 255) / 256, 256, 0, bases, phi, nphi,
                  ws[WS_SORTED].as<uint32_t>(), sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.through, sl.owner,
-                 sl.owner_b, sl.chain_max, acc_merge());
+                 sl.owner_b, sl.chain_max, acc_merge(), (unsigned long long*)ctx->clk_slot());
     if (acc_done) VK_CHECK_HIP(hipEventRecord(acc_done, st));
     // chains up to 2^guard carry pieces are walked serially by their owners; longer ones
     // (adversarial scalars) take the pointer-jumping path in slice_finish
@@ -2087,7 +2098,8 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         VK_TRY(d_raw.ensure(nch * sizeof(RAcc)));
         VK_LAUNCH(ctx, "sparse_accumulate", (k_msm_accumulate<C, FA>), (Tmax + 255) / 256, 256, 0, tab, tab, 0xffffffffu,
                   d_ent.as<uint32_t>(), d_off.as<uint32_t>(), (uint32_t)nch, M, d_raw.as<RAcc>(), d_carry.as<RAcc>(),
-                  d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max, acc_merge());
+                  d_thr.as<uint8_t>(), d_own.as<RAcc>(), d_ownb.as<uint32_t>(), chain_max, acc_merge(),
+                  (unsigned long long*)nullptr);
         // straddling chunks merged by the serial walk of their owners, no chain limit: a chunk holds at
         // most CHNZ x W entries, so it spans at most CHNZ W / M + 2 threads. (The pointer-jumping rounds
         // used before read the longest chain back first -- a host sync per level -- and ran ~3 guarded

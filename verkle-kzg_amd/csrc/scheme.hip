@@ -1201,14 +1201,10 @@ struct MpPrep {
     std::vector<Fr> rpow;
 };
 
-// multiproof.rs:106-112: per query "C" || compress(C) || "z" || z (u64 LE) || "y" || y -- 75
-// bytes at offset 75 i, so the records are written straight into the transcript on up to 16
-// host threads (the point compression is the costly part); the SHA-256 over them stays serial.
-// pool_ok = false: the call's own filler thread feeds the hash (scheme_host.cpp
-// transcript_digest_records) -- mp_prove_many's transcript workers and vc_multiproof_begin, whose
-// callers run several transcripts at once: on the shared host pool they queued on its one-loop lock
 // the multiproof transcript's records "C" ++ compressed(C_i) ++ "z" ++ le64(z_i) ++ "y" ++ le(y_i)
-// (multiproof.rs:109-113) for queries [lo, hi) into out
+// (multiproof.rs:106-113) for queries [lo, hi) into out: 75 bytes at offset 75 i, so the records
+// are written straight into the transcript on up to 16 host threads (the point compression is the
+// costly part); the SHA-256 over them stays serial
 static void mp_records(const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z, const uint64_t* y,
                        size_t lo, size_t hi, uint8_t* out) {
     constexpr size_t REC = 75;
@@ -1239,21 +1235,30 @@ static std::vector<Fr> invert_domain_at(const Fr& t, size_t N) {  // utils.rs:57
 //                  inner proof                                                     (:129-175)
 // Grouping queries by z and summing per group first is the same field arithmetic as the
 // reference's per-group LagrangeBasis sums; rows of z with no query are zero and add nothing.
+// pool_ok = false: the call's own filler thread feeds the hash (scheme_host.cpp
+// transcript_digest_records) -- mp_prove_many's transcript workers and vc_multiproof_begin, whose
+// callers run several transcripts at once: on the shared host pool their record filling queued
+// on the pool's one-loop lock. No transcript is returned on error (VC_E_OOM if the hashing threw).
 static int mp_begin(size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf, const uint64_t* z,
                     const uint64_t* y, vc_transcript** tr_out, Fr* r_out, bool pool_ok = true) {
+    *tr_out = nullptr;
     if (!is_pow2(N) || Q == 0) return VC_E_INVALID;
     for (size_t i = 0; i < Q; i++)
         if (z[i] >= N) return VC_E_DOMAIN;
     // the records stream into the hash (never stored whole: transcript_digest_records)
     vc_transcript* tr = vc_transcript_new("multiproof");
-    *r_out = transcript_digest_records(
-        tr, Q, 75, [&](size_t lo, size_t hi, uint8_t* out) { mp_records(com_xy, com_inf, z, y, lo, hi, out); }, "r",
-        pool_ok && Q >= 8192);
+    try {
+        *r_out = transcript_digest_records(
+            tr, Q, 75, [&](size_t lo, size_t hi, uint8_t* out) { mp_records(com_xy, com_inf, z, y, lo, hi, out); },
+            "r", pool_ok && Q >= 8192);
+    } catch (...) {  // the filler thread's failure, rethrown by the digest
+        vc_transcript_free(tr);
+        return VC_E_OOM;
+    }
     *tr_out = tr;
     return VC_OK;
 }
 
-// distinct query points, sorted (the rows of S)
 // distinct query points, sorted; VC_E_DOMAIN for a z outside the domain (the reference indexes
 // the Lagrange evaluations with it and panics). The accumulate / finish entry points take z
 // from the caller again, so every path validates here (a bitmap of N, not of max z).
@@ -1582,6 +1587,7 @@ int mp_rows(size_t N, size_t Q, const uint64_t* z, size_t* rows) {
 int mp_begin_accumulate(vc_ctx* ctx, size_t N, size_t Q, const uint64_t* com_xy, const uint8_t* com_inf,
                         const uint64_t* z, const uint64_t* y, size_t first, size_t Qs, const void* d_data, void* d_S,
                         vc_transcript** tr_out, uint64_t* r_out) {
+    if (tr_out) *tr_out = nullptr;  // no transcript on any error return (vc_scheme.h)
     if (!ctx || !com_xy || !com_inf || !z || !y || !d_S || !tr_out || !r_out || (Qs && !d_data) || first > Q ||
         Qs > Q - first || ctx->curve != VC_CURVE_BN254 || !is_pow2(N) || Q == 0)
         return VC_E_INVALID;
@@ -1753,9 +1759,13 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
         workers.emplace_back([&] {
             for (size_t p; !cancel.load(std::memory_order_relaxed) && (p = next.fetch_add(1)) < P;) {
                 Begun b;
-                b.st = mp_begin(N, Q, com_xy + p * Q * 8, com_inf + p * Q, z + p * Q, y + p * Q * 4, &b.tr, &b.r,
-                                false);
-                if (b.st == VC_OK) b.st = mp_points(N, Q, z + p * Q, &b.zval);
+                try {  // nothing may leave a thread function
+                    b.st = mp_begin(N, Q, com_xy + p * Q * 8, com_inf + p * Q, z + p * Q, y + p * Q * 4, &b.tr,
+                                    &b.r, false);
+                    if (b.st == VC_OK) b.st = mp_points(N, Q, z + p * Q, &b.zval);
+                } catch (...) {
+                    b.st = VC_E_OOM;
+                }
                 std::lock_guard<std::mutex> lk(mu);
                 B[p] = std::move(b);
                 B[p].done = true;

@@ -150,6 +150,8 @@ struct vc_transcript {
 
 extern "C" {
 
+int vc_host_sha256_path(void) { return vk::sha256_have_shani() ? 1 : 0; }
+
 vc_transcript* vc_transcript_new(const char* label) {
     vc_transcript* t = new vc_transcript();
     t->dst = label ? label : "";

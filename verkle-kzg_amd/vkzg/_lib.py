@@ -31,6 +31,8 @@ SIGNATURES = {
     "vc_ctx_enable_timing": (c_int, [c_void_p, c_int]),
     "vc_ctx_kernel_time": (c_int, [c_void_p, c_char_p, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
     "vc_ctx_reset_timing": (c_int, [c_void_p]),
+    "vc_ctx_accumulate_clock": (c_int, [c_void_p, P, P]),
+    "vc_host_sha256_path": (c_int, []),
     "vc_bases_upload": (c_int, [c_void_p, P, P, c_size_t, ctypes.POINTER(c_int)]),
     "vc_bases_count": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
     "vc_bases_random": (c_int, [c_void_p, c_uint64, c_size_t, ctypes.POINTER(c_int)]),
@@ -39,6 +41,7 @@ SIGNATURES = {
     "vc_msm_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
     "vc_point_words": (c_int, [c_int]),
     "vc_msm_device_partial": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P]),
+    "vc_msm_partial": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P]),
     "vc_device_mad_rate": (c_int, [c_void_p, P]),
     "vc_msm_batch_sparse": (c_int, [c_void_p, c_int, c_size_t, P, P, P, c_int, P, P]),
     "vc_verkle_new": (c_void_p, [c_int]),
@@ -122,6 +125,7 @@ SIGNATURES = {
     "vc_group_create": (c_int, [c_int, c_int, P, ctypes.POINTER(c_void_p)]),
     "vc_group_destroy": (None, [c_void_p]),
     "vc_group_size": (c_int, [c_void_p]),
+    "vc_group_peer_path": (c_int, [c_void_p, c_int, c_int]),
     "vc_group_member": (c_void_p, [c_void_p, c_int]),
     "vc_group_bases_upload": (c_int, [c_void_p, P, P, c_size_t, ctypes.POINTER(c_int)]),
     "vc_group_bases_random": (c_int, [c_void_p, c_uint64, c_size_t, ctypes.POINTER(c_int)]),

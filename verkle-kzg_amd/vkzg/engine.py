@@ -170,6 +170,14 @@ class Engine:
     def reset_timing(self):
         check(lib().vc_ctx_reset_timing(self.h), "vc_ctx_reset_timing")
 
+    def accumulate_clock(self):
+        """mean effective shader clock (MHz) of the accumulate launches timed since the last reset,
+        and their count (vc_ctx_accumulate_clock: s_memtime / s_memrealtime stamps)"""
+        mhz = ctypes.c_double()
+        cnt = ctypes.c_long()
+        check(lib().vc_ctx_accumulate_clock(self.h, ctypes.byref(mhz), ctypes.byref(cnt)), "vc_ctx_accumulate_clock")
+        return mhz.value, cnt.value
+
     def kernel_time(self, name):
         ms = ctypes.c_double()
         cnt = ctypes.c_long()
@@ -273,6 +281,14 @@ class Engine:
         acc = np.zeros(self.point_words(), dtype=np.uint32)
         check(lib().vc_msm_device_partial(self.h, table, offset, ctypes.c_void_p(d_scalars_ptr), n,
                                           1 if mont else 0, _ptr(acc)), "vc_msm_device_partial")
+        return acc
+
+    def msm_partial(self, table, scalars, offset=0, mont=False):
+        """un-normalised accumulator of the MSM over table[offset, offset + n) from host scalars"""
+        sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+        acc = np.zeros(self.point_words(), dtype=np.uint32)
+        check(lib().vc_msm_partial(self.h, table, offset, _ptr(sc), len(sc), 1 if mont else 0, _ptr(acc)),
+              "vc_msm_partial")
         return acc
 
     def msm_last_plan(self):

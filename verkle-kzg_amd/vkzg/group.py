@@ -39,6 +39,12 @@ class Group:
     def size(self):
         return lib().vc_group_size(self.h)
 
+    def peer_path(self, a, b):
+        """how copies from member a to member b travel: 0 one device, 1 peer access (xGMI), 2 staged"""
+        r = lib().vc_group_peer_path(self.h, a, b)
+        check(min(r, 0), "vc_group_peer_path")
+        return r
+
     def member(self, k):
         """member k's vc_ctx handle (ctypes.c_void_p)"""
         return ctypes.c_void_p(lib().vc_group_member(self.h, k))
