@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--commit-batch", type=int, default=10000)
     ap.add_argument("--commit-window", type=int, default=19,
                     help="fixed-base window bits of the config-3 table (19 with --commit-windows 13: 13 windows of "
-                         "19 / 20 bits, 145 GB, the speed of the 188 GB c = 20 table; falls back to 16)")
+                         "19 / 20 bits, 172 GB of 128-B entries, the speed of a c = 20 table; falls back to 16)")
     ap.add_argument("--commit-windows", type=int, default=13,
                     help="windows of the config-3 table (0: uniform c-bit windows)")
     ap.add_argument("--no-secondary", action="store_true")
@@ -937,25 +937,32 @@ def verkle_line(a, local, stream):
         w.insert_single(keys[i].tobytes(), vals[i].tobytes())
     w.commitment(veng, kzg.table)
     del w
+    # the kernel totals of a full commitment: an identical tree committed with per-kernel events
+    k = VerkleTree(32)
+    for i in range(nk):
+        k.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    veng.enable_timing(True)
+    veng.reset_timing()
+    k.commitment(veng, kzg.table)
+    veng.enable_timing(False)
+    del k
     t = VerkleTree(32)
     t0 = time.perf_counter()
     for i in range(nk):
         t.insert_single(keys[i].tobytes(), vals[i].tobytes())
     t_ins = time.perf_counter() - t0
     st = t.stats()
-    veng.enable_timing(True)
-    veng.reset_timing()
-    t0 = time.perf_counter()
+    t0 = time.perf_counter()  # timed without per-kernel events
     t.commitment(veng, kzg.table)
     t_full = time.perf_counter() - t0
     kms = {}
     for k in ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup_init", "msm_fixup_jump",
               "msm_fixup", "sparse_store", "sparse_combine", "norm_prep", "norm_finish", "fb_normalize",
-              "fb_commit", "fb_combine", "fb_commit_small", "to_data_item"):
+              "fb_commit", "fb_combine", "fb_commit_small", "to_data_item", "sparse_iota", "verkle_widen",
+              "verkle_ext_rows4", "verkle_gather", "verkle_dense", "verkle_scatter"):
         ms, cnt = veng.kernel_time(k)
         if cnt:
             kms[k] = round(ms, 3)
-    veng.enable_timing(False)
     gpu_ms = sum(kms.values())
     upd = max(1, nk // 100)
     for i in rng.integers(0, nk, size=upd):
@@ -1244,7 +1251,8 @@ def main():
     progress("variable-base / host-scalar lines done")
     if not a.no_secondary:
         # config 3: batched width-256 commits (fixed-base tables), batch split across ranks; timed
-        # on the commit_window / commit_windows table (145 GB at 19 / 13) and on the deployable c = 16 one (14.5 GB)
+        # on the commit_window / commit_windows table (172 GB at 19 / 13), the c = 16 one (17.2 GB), the c = 18 x 14
+        # one (68.7 GB) and the deployable c = 17 one (32.2 GB)
         cstate = {}
 
         def cengine():  # (re)create: closing the engine frees a table a peer rank could not fit
@@ -1289,16 +1297,18 @@ def main():
             torch.cuda.synchronize(dev)
             if world > 1:
                 dist.barrier()
-            ceng.reset_timing()
-            ceng.enable_timing(True)
             t0 = time.perf_counter()
             reps = 5
-            for _ in range(reps):
+            for _ in range(reps):  # no per-kernel events in the timed passes
                 cstep()
             torch.cuda.synchronize(dev)
             if world > 1:
                 dist.barrier()
             cdt = (time.perf_counter() - t0) / reps
+            ceng.reset_timing()
+            ceng.enable_timing(True)  # one more pass for the kernel time
+            cstep()
+            torch.cuda.synchronize(dev)
             ceng.enable_timing(False)
             if world > 1:
                 tt = torch.tensor([cdt], dtype=torch.float64, device=dev)
@@ -1310,12 +1320,14 @@ def main():
                     "ms_per_batch": cdt * 1e3,
                     "fb_commit_kernel_ms": fb_ms / fb_n if fb_n else None,
                     "achieved_GBps": (Bl * 8256) / (fb_ms / fb_n * 1e-3) / 1e9 if fb_n else None,
-                    "table_bytes": 256 * (gw + gbig) * (1 << (gc - 1)) * 108}  # FbE: 3 x 9 limbs
+                    "table_bytes": ceng.fixed_base_table_bytes(ctab)}
 
         big = ctime(a.commit_window, a.commit_windows if a.commit_window != 16 else 0)
         small = ctime(16) if a.commit_window != 16 else big
-        # the <= 60 GB table: 14 windows (12 of 18 bits, 2 of 19), 58 GB
+        # the <= 70 GB table: 14 windows (12 of 18 bits, 2 of 19), 68.7 GB
         mixed = ctime(18, 14)
+        # the deployable <= 32 GB table: 15 windows of 17 bits, 32.2 GB (30 GiB)
+        deploy = ctime(17)
         head = big or small
         if head is None:  # neither table fits beside the rest on every rank
             out["secondary"] = {"workload": f"{B} batched width-256 Bandersnatch commits (configs[2])",
@@ -1328,6 +1340,7 @@ def main():
                 **head,
                 "c16": small,
                 "mixed_c18_w14": mixed,
+                "c17_w15_deployable": deploy,
             }
         cstate["eng"].close()
 

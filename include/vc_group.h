@@ -56,8 +56,8 @@ int vc_group_member_table(const vc_group* g, int table_id, int member, int* memb
  *     (vc_msm_device_window_part) -- every member receives all n scalars;
  *   VC_GROUP_SPLIT_POINTS: member k computes the MSM of its contiguous 1/G of the points
  *     (vc_msm_device_partial) -- every member receives only its scalars;
- *   VC_GROUP_SPLIT_AUTO (default): POINTS for vc_group_msm (host scalars: the PCIe copy is split
- *     too), WINDOWS for vc_group_kzg_prove. */
+ *   VC_GROUP_SPLIT_AUTO (default): POINTS (host scalars: the PCIe copy is split too); for
+ *     vc_group_kzg_prove index ranges of the domain (the quotient split too). */
 #define VC_GROUP_SPLIT_AUTO 0
 #define VC_GROUP_SPLIT_WINDOWS 1
 #define VC_GROUP_SPLIT_POINTS 2
@@ -70,8 +70,11 @@ int vc_group_msm(vc_group* g, int table_id, size_t offset, const uint64_t* scala
  * slices per member. */
 int vc_group_msm_batch(vc_group* g, int table_id, size_t width, const uint64_t* scalars, size_t batch, int mont,
                        uint64_t* out_xy, uint8_t* out_inf);
-/* KZG::prove_point (kzg/mod.rs:136-154): the quotient on every member, the proof MSM split by
- * windows (vc_kzg_prove_device_part). Same arguments as vc_kzg_prove. */
+/* KZG::prove_point (kzg/mod.rs:136-154), same arguments as vc_kzg_prove. Default: split by index
+ * range -- member k uploads only f on its 1/G of the domain, computes the quotient there and the
+ * proof MSM over SRS points of that range; the in-domain q_m (outside: y) needs one exchange of G
+ * field partials between the two phases. VC_GROUP_SPLIT_WINDOWS: every member the whole quotient
+ * and a window slice of the MSM (vc_kzg_prove_device_part). */
 int vc_group_kzg_prove(vc_group* g, int table_id, size_t size, const uint64_t* evals, size_t max,
                        const uint64_t* point, uint64_t* proof_xy, uint8_t* proof_inf, uint64_t* y);
 /* prove_multiproof (multiproof.rs:99-176), arguments as vc_multiproof_prove (host data Q x N):

@@ -175,6 +175,8 @@ int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
 int vc_fixed_base_precompute_windows(vc_ctx* ctx, int table_id, int window_bits, int windows);
 /* Geometry of a table's fixed-base tables (0s if none yet): window bits c, windows, wide windows */
 int vc_fixed_base_geometry(vc_ctx* ctx, int table_id, int* window_bits, int* windows, int* wide_windows);
+/* bytes of the table's fixed-base window tables in HBM (0 when none are built) */
+int vc_fixed_base_table_bytes(vc_ctx* ctx, int table_id, size_t* bytes);
 
 #ifdef __cplusplus
 }

@@ -81,13 +81,20 @@ def test_group_msm_batch(oracle_c, G):
         g.close()
 
 
-def test_group_kzg_prove_golden():
-    """vc_group_kzg_prove (window-split proof MSM over 2 members) == the golden KZG d = 256 openings."""
+@pytest.mark.parametrize("G", [2, 3])
+@pytest.mark.parametrize("split", ["ranges", "windows"])
+def test_group_kzg_prove_golden(G, split):
+    """vc_group_kzg_prove == the golden KZG d = 256 openings (in the domain, at its boundary, outside,
+    and the reference's error case), with the default index-range shards (each member its slice of
+    the quotient and of the SRS points, one exchange of G field partials) and the window split."""
     import vkzg
+    from vkzg import group as vgroup
     from vkzg import scheme
     gd = load("kzg_256.json")
-    g = _group("bn254", 2)
+    g = _group("bn254", G)
     try:
+        if split == "windows":
+            g.set_msm_split(vgroup.SPLIT_WINDOWS)
         tid, size = g.kzg_setup(256)
         ev = vkzg.ints_to_limbs([int(x, 16) for x in gd["evals"]])
         for op in gd["openings"]:
@@ -280,3 +287,59 @@ def test_group_msm_2e20_chunked_point_split():
         eng.h = None
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("where", ["in_domain", "beyond_max", "outside"])
+@pytest.mark.parametrize("G", [2, 3])
+def test_group_kzg_prove_ranges_2e20_trapdoor(where, G):
+    """configs[3]'s open at d = 2^20 on BLS12-381 through index-range shards (each member its 1/G
+    of the quotient and a point range of the SRS on its radix copies), with max < size so the last
+    member's slice lies partly beyond max: the same proof and y as the one-context vc_kzg_prove on
+    member 0's context, and pi (s - z) = C - y G (s = 100, kzg/mod.rs:115-154) with C from the
+    group MSM. beyond_max opens in the domain at m >= max (y = 0)."""
+    import ctypes
+    import vkzg
+    from pyoracle.curves import BLS12_381 as C
+    from vkzg._lib import check, lib
+    n = 1 << 20
+    g = _group("bls12_381", G)
+    try:
+        tid, size = g.kzg_setup(n)
+        mx = n - 12345
+        rng = np.random.default_rng(31 + G)
+        ev = vkzg.random_scalars("bls12_381", mx, rng)
+        if where == "in_domain":
+            point_int = n // 3
+            zval = pow(pow(7, (C.r - 1) // n, C.r), point_int, C.r)
+        elif where == "beyond_max":
+            point_int = n - 100
+            zval = pow(pow(7, (C.r - 1) // n, C.r), point_int, C.r)
+        else:
+            point_int = n + 987654321
+            zval = point_int
+        xy, inf, y = g.kzg_prove(tid, size, ev, point_int)
+        if where == "in_domain":
+            assert y == vkzg.limbs_to_int(ev[point_int])
+        if where == "beyond_max":
+            assert y == 0
+        # the one-context open on member 0's context and table
+        h0, t0 = g.member(0), g.member_table(tid, 0)
+        pt = vkzg.ints_to_limbs([point_int])[0].copy()
+        pxy = np.zeros(12, dtype=np.uint64)
+        pinf = np.zeros(1, dtype=np.uint8)
+        y1 = np.zeros(4, dtype=np.uint64)
+        Pp = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+        check(lib().vc_kzg_prove(h0, t0, size, Pp(ev), mx, Pp(pt), Pp(pxy), Pp(pinf), Pp(y1)), "vc_kzg_prove")
+        assert np.array_equal(xy, pxy) and inf == pinf[0] and y == vkzg.limbs_to_int(y1)
+        full = np.zeros((n, 4), dtype=np.uint64)
+        full[:mx] = ev
+        com = _pt_bls(*g.msm(tid, full))
+        proof = _pt_bls(xy, inf)
+        assert C.mul(proof, (100 - zval) % C.r) == C.add(com, C.neg(C.mul(C.g, y)))
+    finally:
+        g.close()
+
+
+def _pt_bls(xy, inf):
+    import vkzg
+    return vkzg.arrays_to_points("bls12_381", np.asarray(xy)[None, :], np.array([inf], dtype=np.uint8))[0]

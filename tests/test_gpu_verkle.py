@@ -49,16 +49,22 @@ def _schemes(eng):
     return {"kzg": (kzg.table, kzg_commit), "ipa": (ipa.table, ipa_commit)}
 
 
+@pytest.mark.parametrize("path", ["dev", "host"])
 @pytest.mark.parametrize("dense", ["auto", "0", "1"])
 @pytest.mark.parametrize("scheme_name", ["kzg", "ipa"])
 @pytest.mark.parametrize("N,arity,n", [(3, 255, 120), (3, 6, 60), (4, 4, 50), (5, 3, 40)])
-def test_verkle_commitment_matches_oracle(eng, oracle_c, scheme_name, N, arity, n, dense, monkeypatch):
-    """dense: the level commits' path (VKZG_VERKLE_DENSE, read per call) -- auto (dense rows where
-    B x width is small or half full, sparse otherwise), 0 = every level sparse, 1 = every level dense."""
+def test_verkle_commitment_matches_oracle(eng, oracle_c, scheme_name, N, arity, n, dense, path, monkeypatch):
+    """path: dev = the device-resident levels (vc_verkle_commitment's default: items stay in a
+    device mirror between levels), host = the host-built rows (VKZG_VERKLE_DEV=0, the sharded /
+    group paths' code). dense: the level commits' path (VKZG_VERKLE_DENSE, read per call) -- auto
+    (dense rows for small levels, sparse otherwise), 0 = every level sparse, 1 = every level dense
+    (internal levels on the dev path)."""
     from pyoracle import verkle as ov
     from vkzg.verkle import VerkleTree
     if dense != "auto":
         monkeypatch.setenv("VKZG_VERKLE_DENSE", dense)
+    if path == "host":
+        monkeypatch.setenv("VKZG_VERKLE_DEV", "0")
     table, commit = _schemes(eng)[scheme_name]
     rng = random.Random(7 * N + arity)
     t, o = VerkleTree(N), ov.VerkleTree(N)
@@ -106,3 +112,39 @@ def test_verkle_update_equals_fresh_tree(eng):
     for i in range(nk):
         f.insert_single(keys[i].tobytes(), vals[i].tobytes())
     assert got == f.commitment(eng, kzg.table)
+
+
+def test_verkle_paths_and_contexts_interleave(oracle_c):
+    """One tree committed alternately on the device path of two contexts and on the host path
+    (the mirror moves between devices' contexts, is dropped by a host-path commitment and rebuilt
+    from the host arrays): every commitment == the oracle's."""
+    import vkzg
+    from pyoracle import verkle as ov
+    from vkzg.verkle import VerkleTree
+    e1, e2 = vkzg.Engine("bn254"), vkzg.Engine("bn254")
+    try:
+        s1, s2 = _schemes(e1)["kzg"], _schemes(e2)["kzg"]
+        rng = random.Random(99)
+        N = 4
+        t, o = VerkleTree(N), ov.VerkleTree(N)
+        for step, (eng_, (table, commit), env) in enumerate([(e1, s1, None), (e2, s2, None), (e1, s1, "0"),
+                                                             (e1, s1, None), (e2, s2, "0"), (e2, s2, None)]):
+            for _ in range(30):
+                k, v = _key(rng, N, 8), _val(rng)
+                try:
+                    o.insert_single(k, v)
+                except ov.VerklePanic:
+                    continue
+                t.insert_single(k, v)
+            if env is None:
+                os.environ.pop("VKZG_VERKLE_DEV", None)
+            else:
+                os.environ["VKZG_VERKLE_DEV"] = env
+            try:
+                assert t.commitment(eng_, table) == o.commitment(commit), step
+                assert t.commitment(eng_, table) == o.commitment(commit), step  # nothing dirty
+            finally:
+                os.environ.pop("VKZG_VERKLE_DEV", None)
+    finally:
+        e1.close()
+        e2.close()

@@ -1,4 +1,5 @@
 // extern "C" entry points of libvkzg.so (declared in include/vc_msm.h).
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -209,6 +210,8 @@ int vc_ctx_create(int curve, int device, vc_ctx** out) {
     if (device < 0 || device >= ndev) return VC_E_INVALID;
     VK_CHECK_HIP(hipSetDevice(device));
     vc_ctx* c = new vc_ctx();
+    static std::atomic<uint64_t> next_uid{1};
+    c->uid = next_uid.fetch_add(1);
     c->curve = curve;
     c->device = device;
     c->pin_small.flags = hipHostMallocCoherent;
@@ -505,6 +508,15 @@ int vc_fixed_base_precompute_windows(vc_ctx* ctx, int id, int window_bits, int w
     vk::Table* t = ctx->table(id);
     if (!t) return VC_E_TABLE;
     return vk::fixed_base_precompute(ctx, t, window_bits, windows);
+}
+
+int vc_fixed_base_table_bytes(vc_ctx* ctx, int id, size_t* bytes) {
+    if (!ctx || !bytes) return VC_E_INVALID;
+    Guard g(ctx);
+    vk::Table* t = ctx->table(id);
+    if (!t) return VC_E_TABLE;
+    *bytes = (t->fb_c != 0 && t->fb.p) ? t->fb.cap : 0;
+    return VC_OK;
 }
 
 int vc_fixed_base_geometry(vc_ctx* ctx, int id, int* window_bits, int* windows, int* wide_windows) {

@@ -36,5 +36,17 @@ struct Multi {
 // members write into the one tree's level records directly)
 int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf, const Shard* sh,
                       const Multi* mu = nullptr);
+// KZG::prove_point split by index range (scheme.hip): share [lo, hi) of the domain uploads only
+// its evaluations, phase 1 returns its partial of the one global sum (4 u64: Montgomery Fr words),
+// phase 2 takes the members' total (kzg_share_sum) and returns the MSM accumulator over SRS points
+// [lo, hi) and y (canonical)
+struct KzgShare;
+int kzg_share_begin(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                    size_t lo, size_t hi, KzgShare** out, uint64_t* partial);
+int kzg_share_finish(KzgShare* s, const uint64_t* total, uint32_t* out_acc, uint64_t* y);
+void kzg_share_free(KzgShare* s);
+int kzg_share_sum(int curve, const uint64_t* parts, int G, uint64_t* total);
+// one context, every level device-resident (verkle.cpp; vc_verkle_commitment's default)
+int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf);
 
 }  // namespace vk

@@ -170,6 +170,7 @@ struct PendingTimer {
 struct vc_ctx {
     int curve = 0;
     int device = 0;
+    uint64_t uid = 0;  // unique per context ever created (a freed context's address can come back)
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     hipStream_t side_stream = nullptr;  // second queue for latency-bound tails
@@ -279,6 +280,12 @@ int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* 
 // the same behind the ctx lock, by table id (what vc_msm_batch_sparse does for the plain call)
 int msm_batch_sparse_items_guarded(vc_ctx* ctx, int table, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                                    const uint64_t* scalars, uint64_t* out_xy, uint8_t* out_inf, uint64_t* out_items);
+// the same on the device (BN254): CSR columns / canonical scalars already in device memory, the row
+// structure row_ptr on the host (rows_fit: every row has 1..4 non-zeros -- the chunks are the rows);
+// affine rows, flags and items written to device memory, enqueued on ctx->stream (verkle.cpp's
+// device-resident levels)
+int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
+                            const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items);
 // k_to_data_item over device points (canonical affine u64 x 8 + flags) into device items, on the
 // ctx stream (scheme.hip)
 int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, size_t n, void* d_items);

@@ -330,15 +330,41 @@ int vc_group_kzg_prove(vc_group* g, int id, size_t size, const uint64_t* evals, 
     std::vector<uint32_t> accs((size_t)words * G, 0);
     std::vector<uint64_t> ys((size_t)4 * G, 0);
     std::vector<int> st(G, VC_OK);
+    if (g->split == VC_GROUP_SPLIT_WINDOWS) {  // every member the whole quotient, a window slice of the MSM
+        VK_TRY(g->run(st, [&](int k) {
+            auto share = [&]() -> int {
+                VK_TRY(g->data[k].ensure(max * 32));
+                VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
+                if (max) VK_CHECK_HIP(hipMemcpy(g->data[k].p, evals, max * 32, hipMemcpyHostToDevice));
+                return vc_kzg_prove_device_part(g->ctx[k], g->tables[id][k], size, g->data[k].p, max, point, k, G,
+                                                accs.data() + (size_t)k * words, &ys[(size_t)4 * k]);
+            };
+            st[k] = share();
+        }));
+        memcpy(y, ys.data(), 32);
+        return vc_partials_sum(g->curve, accs.data(), G, proof_xy, proof_inf);
+    }
+    // index ranges: member k uploads f on its 1/G of the domain, computes q there
+    // and the MSM over SRS points [lo, hi); the in-domain q_m (or the out-of-domain y) needs one
+    // exchange of G field partials between the two phases
+    std::vector<vk::KzgShare*> sh(G, nullptr);
+    std::vector<uint64_t> parts((size_t)4 * G, 0);
+    struct Free {
+        std::vector<vk::KzgShare*>& s;
+        ~Free() {
+            for (auto* x : s) vk::kzg_share_free(x);
+        }
+    } free_shares{sh};
     VK_TRY(g->run(st, [&](int k) {
-        auto share = [&]() -> int {
-            VK_TRY(g->data[k].ensure(max * 32));
-            VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
-            if (max) VK_CHECK_HIP(hipMemcpy(g->data[k].p, evals, max * 32, hipMemcpyHostToDevice));
-            return vc_kzg_prove_device_part(g->ctx[k], g->tables[id][k], size, g->data[k].p, max, point, k, G,
-                                            accs.data() + (size_t)k * words, &ys[(size_t)4 * k]);
-        };
-        st[k] = share();
+        size_t lo, hi;
+        vk::shard_range(size, k, G, &lo, &hi);
+        st[k] = vk::kzg_share_begin(g->ctx[k], g->tables[id][k], size, evals, max, point, lo, hi, &sh[k],
+                                    &parts[(size_t)4 * k]);
+    }));
+    uint64_t total[4];
+    VK_TRY(vk::kzg_share_sum(g->curve, parts.data(), G, total));
+    VK_TRY(g->run(st, [&](int k) {
+        st[k] = vk::kzg_share_finish(sh[k], total, accs.data() + (size_t)k * words, &ys[(size_t)4 * k]);
     }));
     memcpy(y, ys.data(), 32);
     return vc_partials_sum(g->curve, accs.data(), G, proof_xy, proof_inf);

@@ -1960,47 +1960,30 @@ __global__ void __launch_bounds__(64) k_sparse_combine(const typename C::Acc* __
     if (lane == 0) rows[g] = v;
 }
 
-template <class C, class Fr>
-static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
-                              const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf,
-                              uint64_t* out_items = nullptr) {
-    using Acc = typename C::Acc;
-    if (batch == 0) return VC_OK;
-    const size_t nnz = row_ptr[batch];
-    // VKZG_VERBOSE: per-phase wall times (with a stream sync at each lap: diagnostics only)
-    static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
-    auto tic = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!verbose) return;
-        (void)hipStreamSynchronize(ctx->stream);
-        auto now = std::chrono::steady_clock::now();
-        fprintf(stderr, "[sparse %zu rows %zu nnz] %s %.3f ms\n", batch, nnz, what,
-                std::chrono::duration<double, std::milli>(now - tic).count());
-        tic = now;
-    };
-    // argument checks and the chunk lists on the host pool (verkle levels: 10^5 rows / non-zeros)
-    std::vector<uint8_t> bad_part(host_pool().size(), 0);
-    host_pool().run([&](unsigned k) {
-        const unsigned T = host_pool().size();
-        uint8_t b = 0;
-        for (size_t g = batch * k / T; g < batch * (k + 1) / T; g++) b |= row_ptr[g + 1] < row_ptr[g] ? 1 : 0;
-        for (size_t j = nnz * k / T; j < nnz * (k + 1) / T; j++) b |= cols[j] >= t->n ? 2 : 0;
-        bad_part[k] = b;
-    });
-    uint8_t bad = 0;
-    for (uint8_t b : bad_part) bad |= b;
-    if (bad & 1) return VC_E_INVALID;
-    if (bad & 2) return VC_E_RANGE;
-    if (t->fb_c == 0) VK_TRY(fixed_base_precompute(ctx, t, 8));
-    const FbGeom fg = t->fb_geom();
-    const int W = fg.W;
-    // rows are cut into chunks of <= CHNZ non-zeros (the accumulate's buckets), so a long row
-    // (e.g. a verkle root: 256 children x W windows) does not become one bucket straddling
-    // hundreds of threads -- whose pieces the fix-up would add serially; chunk sums are folded
-    // per row by k_sparse_combine
-    const size_t CHNZ = 4;
-    // rc[g] = first chunk of row g (an empty row gets one empty chunk); cptr = chunk ends
-    uvec<uint32_t> rc(batch + 1);
+__global__ void k_iota(uint32_t* __restrict__ o, uint32_t n);
+
+// Chunk lists of a CSR row structure (host): rows are cut into chunks of <= CHNZ non-zeros (the
+// accumulate's buckets), so a long row (e.g. a verkle root: 256 children x W windows) does not
+// become one bucket straddling hundreds of threads -- whose pieces the fix-up would add serially;
+// chunk sums are folded per row by k_sparse_combine. rc[g] = first chunk of row g (an empty row
+// gets one empty chunk), cptr = chunk ends. When every row has 1..CHNZ non-zeros the chunks are
+// the rows (identity: rc = 0..batch, cptr = row_ptr; nothing is built).
+constexpr size_t SPARSE_CHNZ = 4;
+struct SparseChunks {
+    uvec<uint32_t> rc;
+    uvec<uint64_t> cptr;
+    size_t nch = 0;
+    bool identity = false;
+};
+static void sparse_chunks(const uint64_t* row_ptr, size_t batch, bool rows_fit, SparseChunks* out) {
+    const size_t CHNZ = SPARSE_CHNZ;
+    if (rows_fit) {  // the caller knows every row has 1..CHNZ non-zeros
+        out->identity = true;
+        out->nch = batch;
+        return;
+    }
+    auto& rc = out->rc;
+    rc.resize(batch + 1);
     pool_for(0, batch, 4096, [&](size_t g) {
         const uint64_t len = row_ptr[g + 1] - row_ptr[g];
         rc[g] = (uint32_t)(len == 0 ? 1 : (len + CHNZ - 1) / CHNZ);
@@ -2011,17 +1994,48 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
         rc[g] = run;
         run += c;
     }
-    const size_t nch = run;
-    uvec<uint64_t> cptr(nch + 1);
+    out->nch = run;
+    auto& cptr = out->cptr;
+    cptr.resize(out->nch + 1);
     cptr[0] = 0;
     pool_for(0, batch, 4096, [&](size_t g) {
-        uint64_t* out = &cptr[rc[g] + 1];
+        uint64_t* o = &cptr[rc[g] + 1];
         if (row_ptr[g + 1] == row_ptr[g]) {
-            out[0] = row_ptr[g];
+            o[0] = row_ptr[g];
             return;
         }
-        for (uint64_t j = row_ptr[g]; j < row_ptr[g + 1]; j += CHNZ) *out++ = std::min<uint64_t>(j + CHNZ, row_ptr[g + 1]);
+        for (uint64_t j = row_ptr[g]; j < row_ptr[g + 1]; j += CHNZ) *o++ = std::min<uint64_t>(j + CHNZ, row_ptr[g + 1]);
     });
+}
+
+// The sparse commit on the device: columns d_cols (u32) and scalars d_sc (4 u64, canonical unless
+// mont) already in device memory, the row structure row_ptr on the host (the chunk lists; rows_fit:
+// every row has 1..CHNZ non-zeros). Outputs on the device: canonical affine rows d_xy / d_inf and,
+// with d_items (BN254), their to_data_item values. Enqueued on ctx->stream; the normalisation's
+// host step synchronises it once (normalize_split), nothing else waits.
+template <class C, class Fr>
+static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
+                             const uint32_t* d_cols_in, const void* d_sc_in, int mont, void* d_xy, uint8_t* d_inf,
+                             void* d_items) {
+    using Acc = typename C::Acc;
+    if (batch == 0) return VC_OK;
+    const size_t nnz = row_ptr[batch];
+    static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
+    auto tic = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!verbose) return;
+        (void)hipStreamSynchronize(ctx->stream);
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[sparse %zu rows %zu nnz] %s %.3f ms\n", batch, nnz, what,
+                std::chrono::duration<double, std::milli>(now - tic).count());
+        tic = now;
+    };
+    if (t->fb_c == 0) VK_TRY(fixed_base_precompute(ctx, t, 8));
+    const FbGeom fg = t->fb_geom();
+    const int W = fg.W;
+    SparseChunks ch;
+    sparse_chunks(row_ptr, batch, rows_fit, &ch);
+    const size_t nch = ch.nch;
     if ((uint64_t)t->n * fg.stride() >= (1ull << 31)) return VC_E_RANGE;  // entry index + sign bit
     const size_t maxL = nnz * (size_t)W;
     if (maxL >= 0xffffffffull) return VC_E_RANGE;
@@ -2029,8 +2043,6 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     // grow-only ctx workspaces (the MSM's own slots for entries / carries / scan scratch: the
     // two paths never run concurrently on one ctx)
     DevBuf& d_rp = ctx->ws[WS_SP_RP];
-    DevBuf& d_cols = ctx->ws[WS_SP_COLS];
-    DevBuf& d_sc = ctx->ws[WS_SP_SC];
     DevBuf& d_cnt = ctx->ws[WS_SP_CNT];
     DevBuf& d_eoff = ctx->ws[WS_SP_EOFF];
     DevBuf& d_ent = ctx->ws[WS_SORTED];
@@ -2041,8 +2053,6 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     DevBuf& d_own = ctx->ws[WS_OWNER];
     DevBuf& d_ownb = ctx->ws[WS_OWNER_B];
     DevBuf& d_tmp = ctx->ws[WS_SCAN_TMP];
-    DevBuf& d_xy = ctx->ws[WS_SP_XY];
-    DevBuf& d_inf = ctx->ws[WS_SP_INF];
     const uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     DevBuf& d_rc = ctx->ws[WS_SP_RC];
@@ -2050,8 +2060,6 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_TRY(d_rp.ensure((nch + 1) * 8));
     VK_TRY(d_rc.ensure((batch + 1) * 4));
     VK_TRY(d_chunks.ensure(nch * sizeof(Acc)));
-    VK_TRY(d_cols.ensure(std::max<size_t>(nnz, 1) * 4));
-    VK_TRY(d_sc.ensure(std::max<size_t>(nnz, 1) * 32));
     VK_TRY(d_cnt.ensure((nnz + 1) * 4));
     VK_TRY(d_eoff.ensure((nnz + 1) * 4));
     VK_TRY(d_ent.ensure(std::max<size_t>(maxL, 1) * 4));
@@ -2061,20 +2069,21 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_TRY(d_thr.ensure((size_t)(Tmax + 8)));
     VK_TRY(d_own.ensure((size_t)(Tmax + 8) * sizeof(FAcc<C>)));
     VK_TRY(d_ownb.ensure((size_t)(Tmax + 8) * 4));
-    VK_TRY(d_xy.ensure(batch * 2 * C::F::N * 4));
-    VK_TRY(d_inf.ensure(batch));
     lap("host chunk lists");
-    VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, cptr.data(), (nch + 1) * 8, hipMemcpyHostToDevice, st));
-    VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, rc.data(), (batch + 1) * 4, hipMemcpyHostToDevice, st));
-    if (nnz) {
-        VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, cols, nnz * 4, hipMemcpyHostToDevice, st));
-        VK_CHECK_HIP(hipMemcpyAsync(d_sc.p, scalars, nnz * 32, hipMemcpyHostToDevice, st));
+    if (ch.identity) {
+        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, row_ptr, (batch + 1) * 8, hipMemcpyHostToDevice, st));
+        VK_LAUNCH(ctx, "sparse_iota", k_iota, (uint32_t)((batch + 1 + 255) / 256), 256, 0, d_rc.as<uint32_t>(),
+                  (uint32_t)batch);
+    } else {
+        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, ch.cptr.data(), (nch + 1) * 8, hipMemcpyHostToDevice, st));
+        VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, ch.rc.data(), (batch + 1) * 4, hipMemcpyHostToDevice, st));
     }
-    lap("H2D");
+    const uint32_t* d_cols = d_cols_in;
+    const uint32_t* d_sc = static_cast<const uint32_t*>(d_sc_in);
     VK_CHECK_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + nnz, 0, 4, st));
     if (nnz)
-        VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(), nnz, mont,
-                  fg, d_cnt.as<uint32_t>());
+        VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc, nnz, mont, fg,
+                  d_cnt.as<uint32_t>());
     size_t tmp_bytes = 0;
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
                                                   nnz + 1, st));
@@ -2082,8 +2091,8 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp.p, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
                                                   nnz + 1, st));
     if (nnz)
-        VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc.as<uint32_t>(),
-                  d_cols.as<uint32_t>(), nnz, mont, fg, d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
+        VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc, d_cols, nnz, mont, fg,
+                  d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
     VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, d_rp.as<uint64_t>(),
               d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
     // the fixed-base tables hold radix-2^29 limbs (commit.hip FbE): k_msm_accumulate<C, FA>
@@ -2113,19 +2122,60 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
               d_rc.as<uint32_t>(), d_rows.as<Acc>());
     lap("kernels");
-    VK_TRY(normalize_to_canon(ctx, ctx->curve, d_rows.p, batch, d_xy.p, d_inf.as<uint8_t>()));
+    VK_TRY(normalize_to_canon(ctx, ctx->curve, d_rows.p, batch, d_xy, d_inf));
     lap("normalise");
+    if (d_items) VK_TRY(to_data_item_device(ctx, d_xy, d_inf, batch, d_items));
+    return VC_OK;
+}
+
+template <class C, class Fr>
+static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
+                              const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf,
+                              uint64_t* out_items = nullptr) {
+    if (batch == 0) return VC_OK;
+    const size_t nnz = row_ptr[batch];
+    // argument checks on the host pool (verkle levels: 10^5 rows / non-zeros)
+    std::vector<uint8_t> bad_part(host_pool().size(), 0);
+    host_pool().run([&](unsigned k) {
+        const unsigned T = host_pool().size();
+        uint8_t b = 0;
+        for (size_t g = batch * k / T; g < batch * (k + 1) / T; g++) b |= row_ptr[g + 1] < row_ptr[g] ? 1 : 0;
+        for (size_t j = nnz * k / T; j < nnz * (k + 1) / T; j++) b |= cols[j] >= t->n ? 2 : 0;
+        bad_part[k] = b;
+    });
+    uint8_t bad = 0;
+    for (uint8_t b : bad_part) bad |= b;
+    if (bad & 1) return VC_E_INVALID;
+    if (bad & 2) return VC_E_RANGE;
+    hipStream_t st = ctx->stream;
+    DevBuf& d_cols = ctx->ws[WS_SP_COLS];
+    DevBuf& d_sc = ctx->ws[WS_SP_SC];
+    DevBuf& d_xy = ctx->ws[WS_SP_XY];
+    DevBuf& d_inf = ctx->ws[WS_SP_INF];
+    DevBuf& d_it = ctx->ws[WS_SP_ITEMS];
+    VK_TRY(d_cols.ensure(std::max<size_t>(nnz, 1) * 4));
+    VK_TRY(d_sc.ensure(std::max<size_t>(nnz, 1) * 32));
+    VK_TRY(d_xy.ensure(batch * 2 * C::F::N * 4));
+    VK_TRY(d_inf.ensure(batch));
+    if (out_items) VK_TRY(d_it.ensure(batch * 32));
+    if (nnz) {
+        VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, cols, nnz * 4, hipMemcpyHostToDevice, st));
+        VK_CHECK_HIP(hipMemcpyAsync(d_sc.p, scalars, nnz * 32, hipMemcpyHostToDevice, st));
+    }
+    VK_TRY((sparse_commit_dev<C, Fr>(ctx, t, batch, row_ptr, false, d_cols.as<uint32_t>(), d_sc.p, mont, d_xy.p,
+                                     d_inf.as<uint8_t>(), out_items ? d_it.p : nullptr)));
     VK_CHECK_HIP(hipMemcpyAsync(out_xy, d_xy.p, batch * 2 * C::F::N * 4, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipMemcpyAsync(out_inf, d_inf.p, batch, hipMemcpyDeviceToHost, st));
-    if (out_items) {  // to_data_item of the rows' points, from the device copies
-        DevBuf& d_it = ctx->ws[WS_SP_ITEMS];
-        VK_TRY(d_it.ensure(batch * 32));
-        VK_TRY(to_data_item_device(ctx, d_xy.p, d_inf.as<uint8_t>(), batch, d_it.p));
-        VK_CHECK_HIP(hipMemcpyAsync(out_items, d_it.p, batch * 32, hipMemcpyDeviceToHost, st));
-    }
+    if (out_items) VK_CHECK_HIP(hipMemcpyAsync(out_items, d_it.p, batch * 32, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host staging vectors die on return
-    lap("D2H");
     return VC_OK;
+}
+
+// BN254 sparse commits with device inputs and outputs (the verkle tree's device-resident levels)
+int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
+                            const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items) {
+    if (t->curve != VC_CURVE_BN254) return VC_E_INVALID;
+    return sparse_commit_dev<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, rows_fit, d_cols, d_sc, 0, d_xy, d_inf, d_items);
 }
 
 int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,

@@ -417,6 +417,105 @@ int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const 
     return VC_OK;
 }
 
+// ---- index-range shards of the quotient (vc_group_kzg_prove): a member holds f
+// and q on [lo, lo + L) of the domain; the one global sum each case needs (in the domain q_m's
+// sum of q_i w^i, outside the barycentric sum of f_i w^i inv_i) leaves as one field partial per
+// member, and the finish gets the members' total back.
+// in domain at m (lagrange_basis.rs:91-119): q_i = (f_i - f_m) / (w^i - w^m), block partials of
+// q_i w^i; f_m by value (it may lie in another member's slice)
+template <class F>
+__global__ void __launch_bounds__(256) k_q_in_range(const fe<F>* __restrict__ f, size_t nvalid,
+                                                   const fe<F>* __restrict__ inv1, const fe<F>* __restrict__ pw,
+                                                   size_t n, size_t lo, size_t L, size_t m, fe<F> wminv, fe<F> fm,
+                                                   fe<F>* __restrict__ q, fe<F>* __restrict__ partial) {
+    __shared__ fe<F> sh[256];
+    size_t i0 = (size_t)blockIdx.x * 256 * 8 + threadIdx.x;
+    fe<F> acc = fe_zero<F>();
+    for (int k = 0; k < 8; k++) {
+        const size_t i = i0 + (size_t)k * 256;  // local index; global lo + i
+        if (i >= L) break;
+        const size_t gi = lo + i;
+        if (gi == m) {
+            q[i] = fe_zero<F>();
+            continue;
+        }
+        const fe<F> fi = i < nvalid ? f[i] : fe_zero<F>();
+        const fe<F> inv = fe_mul<F>(wminv, inv1[(gi + n - m) & (n - 1)]);  // 1 / (w^gi - w^m)
+        const fe<F> qi = fe_mul<F>(fe_sub<F>(fi, fm), inv);
+        q[i] = qi;
+        acc = fe_add<F>(acc, fe_mul<F>(qi, pw[gi]));
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) sh[threadIdx.x] = fe_add<F>(sh[threadIdx.x], sh[threadIdx.x + h]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+// outside: q_i = (f_i - y) inv_i with y by value
+template <class F>
+__global__ void k_q_out_v(const fe<F>* __restrict__ f, size_t nvalid, const fe<F>* __restrict__ inv, size_t L, fe<F> y,
+                          fe<F>* __restrict__ q) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L) return;
+    const fe<F> fi = i < nvalid ? f[i] : fe_zero<F>();
+    q[i] = fe_mul<F>(fe_sub<F>(fi, y), inv[i]);
+}
+
+// phase 1 of a range share: d_f = f on [lo, lo + L) (Montgomery; entries >= nvalid are zero), q
+// on the slice (in domain) or the inverses inv_i = 1 / (w^(lo+i) - z) (outside) into d_inv, and
+// this share's partial of the global sum into *partial (host; the stream is synchronised)
+template <class F>
+int kzg_range_part(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t nvalid, size_t lo, size_t L, const fe<F>& point,
+                   const fe<F>& omega, bool in_domain, size_t m, const fe<F>& fm, fe<F>* d_q, fe<F>* d_inv,
+                   DevBuf& part, fe<F>* partial) {
+    hipStream_t st = ctx->stream;
+    const size_t nblk = std::max<size_t>(1, (L + 2047) / 2048);
+    VK_TRY(part.ensure((nblk + 1) * sizeof(fe<F>)));
+    fe<F>* d_sum = part.as<fe<F>>() + nblk;
+    fe<F>* pwp = nullptr;
+    VK_TRY(cached_powers<F>(ctx, omega, n, &pwp));
+    if (in_domain) {
+        const fe<F> wminv = host_pow<F>(omega, (n - m) & (n - 1));
+        fe<F>* inv1 = nullptr;
+        VK_TRY(cached_inv1<F>(ctx, pwp, n, &inv1));
+        VK_LAUNCH(ctx, "kzg_q_in", (k_q_in_range<F>), nblk, 256, 0, d_f, nvalid, inv1, pwp, n, lo, L, m, wminv, fm,
+                  d_q, part.as<fe<F>>());
+    } else {
+        VK_LAUNCH(ctx, "kzg_den", (k_den<F>), (L + 255) / 256, 256, 0, pwp + lo, L, point, (long long)-1, d_q);
+        VK_TRY(batch_inverse<F>(ctx, d_q, d_inv, L));
+        VK_LAUNCH(ctx, "kzg_bary", (k_bary_partial<F>), nblk, 256, 0, d_f, nvalid, pwp + lo, d_inv, L, part.as<fe<F>>());
+    }
+    VK_LAUNCH(ctx, "kzg_fold", (k_fold_partials<F>), 1, 256, 0, part.as<fe<F>>(), nblk, fe_one<F>(), d_sum);
+    VK_TRY(ctx->pin_y.ensure(sizeof(fe<F>)));
+    VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_y.p, d_sum, sizeof(fe<F>), hipMemcpyDeviceToHost, st));
+    VK_CHECK_HIP(hipStreamSynchronize(st));
+    *partial = *ctx->pin_y.as<fe<F>>();
+    return VC_OK;
+}
+// phase 2: with the members' total, in domain q_m = -w^-m total (written by the share holding
+// m), outside y = -t total ((z^n - 1) / n) and q_i = (f_i - y) inv_i; *y_mont = y outside
+template <class F>
+int kzg_range_finish(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t nvalid, size_t lo, size_t L, const fe<F>& point,
+                     const fe<F>& omega, bool in_domain, size_t m, const fe<F>& total, fe<F>* d_q, const fe<F>* d_inv,
+                     fe<F>* y_mont) {
+    if (in_domain) {
+        const fe<F> wminv = host_pow<F>(omega, (n - m) & (n - 1));
+        if (m >= lo && m < lo + L)
+            VK_LAUNCH(ctx, "kzg_set", (k_set<F>), 1, 64, 0, d_q, m - lo, fe_mul<F>(fe_neg<F>(wminv), total));
+        return VC_OK;
+    }
+    fe<F> nn = fe_zero<F>();
+    nn.v[0] = (uint32_t)n;
+    nn.v[1] = (uint32_t)((uint64_t)n >> 32);
+    const fe<F> t = fe_mul<F>(fe_sub<F>(host_pow<F>(point, n), fe_one<F>()), fe_inv_bin<F>(fe_to_mont<F>(nn)));
+    const fe<F> y = fe_mul<F>(fe_neg<F>(t), total);
+    *y_mont = y;
+    if (L) VK_LAUNCH(ctx, "kzg_q_out", (k_q_out_v<F>), (L + 255) / 256, 256, 0, d_f, nvalid, d_inv, L, y, d_q);
+    return VC_OK;
+}
+
 template <class F>
 int canon_to_mont_dev(vc_ctx* ctx, const void* d_in, size_t n, size_t n_valid, fe<F>* d_out) {
     VK_LAUNCH(ctx, "to_mont", (k_canon_to_mont<F>), (n + 255) / 256, 256, 0, reinterpret_cast<const fe<F>*>(d_in), n,
@@ -460,7 +559,11 @@ int kzg_srs_dev(vc_ctx* ctx, size_t max_items, size_t n, const fe<Fr>& s_mont, c
     template int kzg_quotient_dev<F>(vc_ctx*, size_t, const fe<F>*, size_t, const fe<F>&, const fe<F>&, \
                                      fe<F>*, fe<F>*, DevBuf&, DevBuf&, DevBuf&);                       \
     template int canon_to_mont_dev<F>(vc_ctx*, const void*, size_t, size_t, fe<F>*);                  \
-    template int mont_to_canon_dev<F>(vc_ctx*, const fe<F>*, size_t, void*);
+    template int mont_to_canon_dev<F>(vc_ctx*, const fe<F>*, size_t, void*);                           \
+    template int kzg_range_part<F>(vc_ctx*, size_t, const fe<F>*, size_t, size_t, size_t, const fe<F>&, \
+                                   const fe<F>&, bool, size_t, const fe<F>&, fe<F>*, fe<F>*, DevBuf&, fe<F>*); \
+    template int kzg_range_finish<F>(vc_ctx*, size_t, const fe<F>*, size_t, size_t, size_t, const fe<F>&, \
+                                     const fe<F>&, bool, size_t, const fe<F>&, fe<F>*, const fe<F>*, fe<F>*);
 VK_INST_F(BN254Fr)
 VK_INST_F(BLS381Fr)
 template int kzg_srs_dev<BN254G1, BN254Fr>(vc_ctx*, size_t, size_t, const fe<BN254Fr>&, const fe<BN254Fr>&,

@@ -15,6 +15,17 @@ int domain_tables(vc_ctx* ctx, const fe<F>& w, size_t n, const fe<F>** pw, const
 template <class F>
 int kzg_quotient_dev(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t max, const fe<F>& point, const fe<F>& omega,
                      fe<F>* d_q, fe<F>* y_out, DevBuf& pw, DevBuf& tmp, DevBuf& part);
+// index-range shards of the quotient (vc_group_kzg_prove): phase 1 writes q (in domain) or the
+// slice's inverses (outside) and returns this share's partial of the global sum; phase 2 takes
+// the members' total (poly.hip)
+template <class F>
+int kzg_range_part(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t nvalid, size_t lo, size_t L, const fe<F>& point,
+                   const fe<F>& omega, bool in_domain, size_t m, const fe<F>& fm, fe<F>* d_q, fe<F>* d_inv,
+                   DevBuf& part, fe<F>* partial);
+template <class F>
+int kzg_range_finish(vc_ctx* ctx, size_t n, const fe<F>* d_f, size_t nvalid, size_t lo, size_t L, const fe<F>& point,
+                     const fe<F>& omega, bool in_domain, size_t m, const fe<F>& total, fe<F>* d_q, const fe<F>* d_inv,
+                     fe<F>* y_mont);
 template <class F>
 int canon_to_mont_dev(vc_ctx* ctx, const void* d_in, size_t n, size_t n_valid, fe<F>* d_out);
 template <class F>

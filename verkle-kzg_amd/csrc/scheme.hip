@@ -1193,6 +1193,153 @@ int vc_kzg_quotient(vc_ctx* ctx, size_t size, const uint64_t* evals, size_t max,
 
 }  // extern "C"
 
+namespace vk {
+// ---------------------------------------------------------------- range-sharded KZG open
+// One member's share of KZG::prove_point (kzg/mod.rs:136-154) split by index range (SURVEY 8(e)
+// C4): the member uploads only f on [lo, hi), computes q there, and its MSM covers the SRS points
+// [lo, hi) (a point range on the table's radix copies). The global sum of each case leaves as one
+// field partial (phase 1), the members' total comes back (phase 2). vc_group_kzg_prove drives it.
+struct KzgShare {
+    vc_ctx* ctx = nullptr;
+    Table* t = nullptr;
+    size_t n = 0, lo = 0, L = 0, nvalid = 0, m = 0;
+    bool in_domain = false;
+    uint32_t point[8] = {0}, omega[8] = {0};  // Montgomery Fr words
+    uint64_t y_in[4] = {0};                   // in domain: y = f_m (canonical)
+    DevBuf f, q, inv, part;
+    explicit KzgShare(vc_ctx* c) : ctx(c), f(c), q(c), inv(c), part(c) {}
+};
+
+template <class C_, class Fr_>
+static int kzg_share_begin_t(vc_ctx* ctx, Table* t, size_t size, const uint64_t* evals, size_t max,
+                             const uint64_t* point, size_t lo, size_t hi, KzgShare* s, uint64_t* partial) {
+    using Fe = fe<Fr_>;
+    if (!is_pow2(size) || max > size || lo > hi || hi > size) return VC_E_INVALID;
+    if (t->n < size) return VC_E_RANGE;
+    s->ctx = ctx;
+    s->t = t;
+    s->n = size;
+    s->lo = lo;
+    s->L = hi - lo;
+    s->nvalid = max > lo ? std::min(max, hi) - lo : 0;
+    const Fe pm = canon_to_mont<Fr_>(point);
+    const Fe omega = group_gen_t<Fr_>(size, fr_generator<Fr_>());
+    memcpy(s->point, pm.v, 32);
+    memcpy(s->omega, omega.v, 32);
+    // prove_point: `point <= size` -> the in-domain branch with index to_usize(point)
+    const Fe pc = fe_from_mont<Fr_>(pm);
+    bool small = true;
+    for (int i = 2; i < Fr_::N; i++) small &= pc.v[i] == 0;
+    const uint64_t pv = (uint64_t)pc.v[0] | ((uint64_t)pc.v[1] << 32);
+    s->in_domain = small && pv <= size;
+    if (s->in_domain && pv == size) return VC_E_DOMAIN;  // vanishing_at(size) out of bounds
+    s->m = s->in_domain ? (size_t)pv : 0;
+    Fe fm = fe_zero<Fr_>();
+    if (s->in_domain && s->m < max) {  // y = evaluate(point): the stored value, or 0 in [max, size]
+        memcpy(s->y_in, evals + 4 * s->m, 32);
+        fm = canon_to_mont<Fr_>(evals + 4 * s->m);
+    }
+    const size_t L = std::max<size_t>(s->L, 1);
+    VK_TRY(s->f.ensure(L * 32));
+    VK_TRY(s->q.ensure(L * 32));
+    VK_TRY(s->inv.ensure(L * 32));
+    if (s->nvalid)
+        VK_CHECK_HIP(hipMemcpyAsync(s->q.p, evals + 4 * lo, s->nvalid * 32, hipMemcpyHostToDevice, ctx->stream));
+    VK_TRY(canon_to_mont_dev<Fr_>(ctx, s->q.p, s->L, s->nvalid, s->f.as<Fe>()));
+    Fe part;
+    VK_TRY(kzg_range_part<Fr_>(ctx, size, s->f.as<Fe>(), s->nvalid, lo, s->L, pm, omega, s->in_domain, s->m, fm,
+                               s->q.as<Fe>(), s->inv.as<Fe>(), s->part, &part));
+    memcpy(partial, part.v, 32);
+    return VC_OK;
+}
+
+template <class C_, class Fr_>
+static int kzg_share_finish_t(KzgShare* s, const uint64_t* total, uint32_t* out_acc, uint64_t* y) {
+    using Fe = fe<Fr_>;
+    vc_ctx* ctx = s->ctx;
+    Fe tot, pm, omega, ym = fe_zero<Fr_>();
+    memcpy(tot.v, total, 32);
+    memcpy(pm.v, s->point, 32);
+    memcpy(omega.v, s->omega, 32);
+    VK_TRY(kzg_range_finish<Fr_>(ctx, s->n, s->f.as<Fe>(), s->nvalid, s->lo, s->L, pm, omega, s->in_domain, s->m, tot,
+                                 s->q.as<Fe>(), s->inv.as<Fe>(), &ym));
+    if (s->in_domain) memcpy(y, s->y_in, 32);
+    else mont_to_canon<Fr_>(ym, y);
+    if (s->L == 0) {  // an empty share adds the identity
+        typename C_::Acc z = C_::zero();
+        memcpy(out_acc, &z, sizeof z);
+        return VC_OK;
+    }
+    return msm_run(ctx, s->t, s->lo, s->q.p, s->L, 1, out_acc);
+}
+
+int kzg_share_begin(vc_ctx* ctx, int table, size_t size, const uint64_t* evals, size_t max, const uint64_t* point,
+                    size_t lo, size_t hi, KzgShare** out, uint64_t* partial) {
+    if (!ctx || !out || !point || !partial || (max && !evals)) return VC_E_INVALID;
+    *out = nullptr;
+    Guard g(ctx);
+    Table* t = ctx->table(table);
+    if (!t) return VC_E_TABLE;
+    KzgShare* s = new KzgShare(ctx);
+    int st = VC_E_INVALID;
+    if (ctx->curve == VC_CURVE_BN254)
+        st = kzg_share_begin_t<BN254G1, BN254Fr>(ctx, t, size, evals, max, point, lo, hi, s, partial);
+    else if (ctx->curve == VC_CURVE_BLS12_381)
+        st = kzg_share_begin_t<BLS381G1, BLS381Fr>(ctx, t, size, evals, max, point, lo, hi, s, partial);
+    if (st != VC_OK) {
+        (void)hipStreamSynchronize(ctx->stream);
+        delete s;  // (the pooled buffers return to the pool under the lock held here)
+        return st;
+    }
+    *out = s;
+    return VC_OK;
+}
+
+int kzg_share_finish(KzgShare* s, const uint64_t* total, uint32_t* out_acc, uint64_t* y) {
+    if (!s || !total || !out_acc || !y) return VC_E_INVALID;
+    Guard g(s->ctx);
+    if (s->ctx->curve == VC_CURVE_BN254) return kzg_share_finish_t<BN254G1, BN254Fr>(s, total, out_acc, y);
+    return kzg_share_finish_t<BLS381G1, BLS381Fr>(s, total, out_acc, y);
+}
+
+void kzg_share_free(KzgShare* s) {
+    if (!s) return;
+    {
+        Guard g(s->ctx);  // the pooled buffers go back to their context's pool under its lock
+        (void)hipStreamSynchronize(s->ctx->stream);
+        s->f.release();
+        s->q.release();
+        s->inv.release();
+        s->part.release();
+    }
+    delete s;
+}
+
+// sum of G range partials (Montgomery Fr words of the context's scalar field)
+int kzg_share_sum(int curve, const uint64_t* parts, int G, uint64_t* total) {
+    if (curve == VC_CURVE_BN254) {
+        fe<BN254Fr> a = fe_zero<BN254Fr>(), b;
+        for (int k = 0; k < G; k++) {
+            memcpy(b.v, parts + 4 * (size_t)k, 32);
+            a = fe_add<BN254Fr>(a, b);
+        }
+        memcpy(total, a.v, 32);
+        return VC_OK;
+    }
+    if (curve == VC_CURVE_BLS12_381) {
+        fe<BLS381Fr> a = fe_zero<BLS381Fr>(), b;
+        for (int k = 0; k < G; k++) {
+            memcpy(b.v, parts + 4 * (size_t)k, 32);
+            a = fe_add<BLS381Fr>(a, b);
+        }
+        memcpy(total, a.v, 32);
+        return VC_OK;
+    }
+    return VC_E_INVALID;
+}
+
+}  // namespace vk
+
 // ---------------------------------------------------------------- multiproof (a11)
 namespace vk {
 

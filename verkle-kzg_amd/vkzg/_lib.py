@@ -62,6 +62,7 @@ SIGNATURES = {
     "vc_msm_batch_device": (c_int, [c_void_p, c_int, c_size_t, P, c_size_t, c_int, P, P]),
     "vc_fixed_base_precompute": (c_int, [c_void_p, c_int, c_int]),
     "vc_fixed_base_precompute_windows": (c_int, [c_void_p, c_int, c_int, c_int]),
+    "vc_fixed_base_table_bytes": (c_int, [c_void_p, c_int, P]),
     "vc_fixed_base_geometry": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                        ctypes.POINTER(c_int)]),
     # vc_scheme.h

@@ -226,6 +226,12 @@ class Engine:
         else:
             check(lib().vc_fixed_base_precompute(self.h, table, window_bits), "vc_fixed_base_precompute")
 
+    def fixed_base_table_bytes(self, table):
+        """HBM bytes of the table's fixed-base window tables (vc_fixed_base_table_bytes)"""
+        b = ctypes.c_size_t()
+        check(lib().vc_fixed_base_table_bytes(self.h, table, ctypes.byref(b)), "vc_fixed_base_table_bytes")
+        return b.value
+
     def fixed_base_geometry(self, table):
         """(window_bits, windows, wide_windows) of the table's fixed-base tables (0s if none)."""
         c, w, b = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
