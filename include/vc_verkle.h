@@ -46,6 +46,9 @@ int vc_verkle_get(const vc_verkle* t, const uint8_t* key, uint8_t* value32, int*
 int vc_verkle_path(const vc_verkle* t, const uint8_t* key, size_t max_len, uint8_t* units, size_t* len);
 /* commitment (lib.rs:127-129): root commitment, canonical affine BN254 G1 (x, y: 4 u64 each) */
 int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf);
+/* diagnostics: per node id (up to max) its type (0 internal, 1 extension), level and committed
+ * to_data_item (4 u64, canonical); *n = the node count */
+int vc_verkle_debug_nodes(vc_verkle* t, size_t max, uint8_t* type, int32_t* level, uint64_t* items, size_t* n);
 /* node counts (diagnostics): internal, extension, dirty */
 int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, size_t* dirty);
 

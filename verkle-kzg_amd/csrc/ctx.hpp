@@ -184,6 +184,7 @@ struct vc_ctx {
                                     // the kernel writes them straight to host memory)
     vk::PinBuf pin_norm;            // block products / inverses of the split normalisation
     vk::PinBuf pin_y;               // the KZG opening's y, copied back asynchronously
+    vk::PinBuf pin_verkle;          // the verkle extension rows, merged straight into page-locked memory
     // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
     // (or are synchronised), so a block freed by one call is safely reused by the next in
     // stream order; vc_ctx_set_stream drains the old stream first
@@ -284,8 +285,12 @@ int msm_batch_sparse_items_guarded(vc_ctx* ctx, int table, size_t batch, const u
 // structure row_ptr on the host (rows_fit: every row has 1..4 non-zeros -- the chunks are the rows);
 // affine rows, flags and items written to device memory, enqueued on ctx->stream (verkle.cpp's
 // device-resident levels)
+// d_add_ids (optional): row g also adds the canonical affine point (d_add_xy, d_add_inf)[d_add_ids[g]]
+// before the normalisation (0xffffffff: nothing) -- a verkle row that updates its old commitment
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
-                            const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items);
+                            const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items,
+                            const uint32_t* d_add_ids = nullptr, const uint64_t* d_add_xy = nullptr,
+                            const uint8_t* d_add_inf = nullptr);
 // k_to_data_item over device points (canonical affine u64 x 8 + flags) into device items, on the
 // ctx stream (scheme.hip)
 int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, size_t n, void* d_items);

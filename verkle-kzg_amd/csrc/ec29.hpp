@@ -371,4 +371,24 @@ struct Fast29<Bandersnatch> {
     using type = TE29<Bandersnatch, F29BLS381Fr>;
 };
 
+// Fixed-base window table entry (commit.hip; read by the sparse commits' accumulate, msm.hip).
+// Table entry (kept as a type so the layout can change in one place): the radix-2^29 limbs the
+// mixed add consumes (ec29.hpp Aff, 4 B per 29-bit limb: 108 B for Bandersnatch's x, y, d x y),
+// so the loop reads operands with no unpacking (~53 of 2,250 instructions per Edwards add).
+// (Padding the packed 96-B form -- unpacked in the loop -- to 128 B was measured slower, round 2.)
+// Every entry is padded to a whole 128-B line (round 5), so a gather reads one line instead of
+// straddling two: Bandersnatch's 108-B entries mostly spanned two lines (33.3M gathers per 10k
+// commits at c = 19 x 13 moved 8-9.5 GB by the counters). Measured on one MI355X, 10k width-256
+// commits: c = 16 3.08-3.11 -> 3.19-3.25 M/s, c = 17 (15 windows) 3.27-3.31 -> 3.40-3.41, c = 18 x 14
+// 3.53 -> 3.66-3.68 (profiles/r05/commit_pad128/). -DVKZG_FB_PACKED keeps the 108-B entries (A/B).
+template <class C>
+struct FbEntryLimbs {
+    typename Fast29<C>::type::Aff u;
+#ifndef VKZG_FB_PACKED
+    uint32_t pad[(128 - sizeof(typename Fast29<C>::type::Aff) % 128) % 128 / 4];
+#endif
+};
+template <class C>
+using FbE = FbEntryLimbs<C>;
+
 }  // namespace vk

@@ -289,16 +289,43 @@ __global__ void __launch_bounds__(1024) k_sort_coarse_st(Src src, uint32_t n, in
     __syncthreads();
     const uint32_t fmask = (1u << FB) - 1;
     const uint32_t lo = blockIdx.x * chunk, hi = min(lo + chunk, n);
-    for (uint32_t i = lo + t; i < hi; i += blockDim.x) {
-        src(i, c, we, [&](int w, int32_t d) {
-            if (d != 0 && w >= wb) {
-                const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-                const uint32_t p = atomicAdd(
-                    &lcur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB) - bin0], 1u);
-                stage[p] = sort_pack<uint32_t>(b & fmask, stride ? src.pt(i) + ((uint32_t)w % wps) * stride : i, d < 0,
-                                               FB);
+    auto put = [&](uint32_t i, int w, int32_t d) {
+        if (d != 0 && w >= wb) {
+            const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+            const uint32_t p = atomicAdd(
+                &lcur[(stride ? (uint32_t)w / wps : (uint32_t)(w - wb)) * NBC + (b >> FB) - bin0], 1u);
+            stage[p] = sort_pack<uint32_t>(b & fmask, stride ? src.pt(i) + ((uint32_t)w % wps) * stride : i, d < 0, FB);
+        }
+    };
+    if constexpr (std::is_same<Src, RadixDigits>::value) {
+        // radix digits: the digits of PRE iterations (<= 8 windows each) loaded before their LDS
+        // atomics (one load, one atomic at a time left the waves waiting on memory 71 % of their
+        // cycles: profiles/r04/tail_pmc/sq_summary.txt)
+        constexpr int PRE = 4, WMAX = 8;
+        if (we - src.w0 <= WMAX) {
+            for (uint32_t i0 = lo + t; i0 < hi; i0 += PRE * blockDim.x) {
+                int32_t dg[PRE][WMAX];
+#pragma unroll
+                for (int k = 0; k < PRE; k++) {
+                    const uint32_t i = i0 + (uint32_t)k * blockDim.x;
+#pragma unroll
+                    for (int j = 0; j < WMAX; j++)
+                        dg[k][j] = (i < hi && src.w0 + j < we) ? src.dig[(size_t)(src.w0 + j) * src.nv + i] : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < PRE; k++) {
+                    const uint32_t i = i0 + (uint32_t)k * blockDim.x;
+                    if (i >= hi) break;
+#pragma unroll
+                    for (int j = 0; j < WMAX; j++)
+                        if (src.w0 + j < we) put(i, src.w0 + j, dg[k][j]);
+                }
             }
-        });
+        } else {
+            for (uint32_t i = lo + t; i < hi; i += blockDim.x) src(i, c, we, [&](int w, int32_t d) { put(i, w, d); });
+        }
+    } else {
+        for (uint32_t i = lo + t; i < hi; i += blockDim.x) src(i, c, we, [&](int w, int32_t d) { put(i, w, d); });
     }
     __syncthreads();
     // every bin's run in one burst: 16 lanes per bin (runs are ~10-25 entries: a whole wave per bin
@@ -332,7 +359,20 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
     const uint32_t end = base[(size_t)(g + 1) * nblk];  // base has bins*nblk + 1 entries
     if (cnt_lane) h[t] = 0;
     __syncthreads();
-    for (uint32_t p = start + t; p < end; p += blockDim.x) atomicAdd(&h[sort_fine_of<T>(tmp[p], FB)], 1u);
+    {  // RH loads in flight per thread before their counter atomics
+        constexpr uint32_t RH = 4;
+        for (uint32_t p0 = start + t; p0 < end; p0 += RH * blockDim.x) {
+            T e[RH];
+#pragma unroll
+            for (uint32_t k = 0; k < RH; k++) {
+                const uint32_t p = p0 + k * blockDim.x;
+                e[k] = p < end ? tmp[p] : T(0);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < RH; k++)
+                if (p0 + k * blockDim.x < end) atomicAdd(&h[sort_fine_of<T>(e[k], FB)], 1u);
+        }
+    }
     __syncthreads();
     // inclusive Hillis-Steele scan over 256 counters
     const uint32_t v = cnt_lane ? h[t] : 0u;
@@ -397,7 +437,7 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
 // to the ec.hpp form at the three store sites (4 multiplies each) put ~50 KB of rarely-run code
 // into the loop and cost 7 % of the kernel.
 // BT: the base entry type -- packed-29 C::Aff (tables), the limb form of the fixed-base tables
-// the sparse commits read (Fast29<C>::type::Aff, commit.hip FbE), or the signed limb form of the
+// the sparse commits read (ec29.hpp FbE: the limbs in a 128-B entry), or the signed limb form of the
 // shared-window copies (SW29::AffN: x, y, -y -- the entry's sign picks the y to load)
 template <class FC, class BT, class = void>
 struct is_affn : std::false_type {};
@@ -407,6 +447,9 @@ template <class FC, class BT, class = void>
 struct is_affp : std::false_type {};
 template <class FC, class BT>
 struct is_affp<FC, BT, std::void_t<typename FC::AffP>> : std::is_same<BT, typename FC::AffP> {};
+// a fixed-base table entry (FbE: the limbs in .u, padded to a 128-B line)
+template <class C, class BT>
+struct is_fbe : std::is_same<BT, FbE<C>> {};
 
 // straddle merge inside the accumulate (A/B knob VKZG_ACC_MERGE in a -DVKZG_ACC_MERGE_BUILD build;
 // the default build leaves the code out: it grew the kernel to 237 VGPRs and 18,441 instructions).
@@ -472,9 +515,12 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     auto base_of = [&](uint32_t j) -> const Aff* { return j < nphi ? bases + j : phi + (j - nphi); };
     constexpr bool SN = is_affn<FC, BT>::value;
     constexpr bool SP = is_affp<FC, BT>::value;  // pair layout: the sign picks the record
-    using Pre = std::conditional_t<SN || SP, typename FC::Aff, Aff>;  // the prefetched entry
+    constexpr bool FBE = is_fbe<C, BT>::value;   // fixed-base entries: the limbs, not the padding
+    using Pre = std::conditional_t<SN || SP || FBE, typename FC::Aff, Aff>;  // the prefetched entry
     auto fetch = [&](uint32_t id) -> Pre {
-        if constexpr (SP) {
+        if constexpr (FBE) {
+            return base_of(id & 0x7fffffffu)->u;
+        } else if constexpr (SP) {
             const Aff* r = bases + 2 * (size_t)(id & 0x7fffffffu) + (id >> 31);
             typename FC::Aff a;
             a.x = r->x;
@@ -500,7 +546,7 @@ __global__ void __launch_bounds__(256) VK_ACC_OCC k_msm_accumulate(
     while (true) {
         uint32_t cur = idx;
         typename FC::Aff Q;
-        if constexpr (SN || SP) Q = P;
+        if constexpr (SN || SP || FBE) Q = P;
         else Q = FC::load(&P);
         if (k + 1 < e) {  // prefetch next base
             idx = sorted[k + 1];
@@ -855,24 +901,42 @@ __global__ void __launch_bounds__(1024) k_glv_radix_hist(const uint32_t* __restr
     __syncthreads();
     const size_t nv = 2 * (size_t)n;
     const uint32_t lo = blockIdx.x * chunk, hi = lo + chunk;
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        if (inf != nullptr && inf[i]) {
-            for (int w = 0; w < W; w++) dig[(size_t)w * nv + i] = dig[(size_t)w * nv + n + i] = 0;
-            continue;
+    // a thread's scalars are loaded up front, PRE at a time (the loads of one scalar after the
+    // previous one's digits left the waves waiting on memory 52 % of their cycles:
+    // profiles/r04/tail_pmc/sq_summary.txt)
+    constexpr int PRE = 4;
+    for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += PRE * blockDim.x) {
+        fe<Fr> f[PRE];
+        bool skip[PRE];
+#pragma unroll
+        for (int k = 0; k < PRE; k++) {
+            const uint32_t i = i0 + (uint32_t)k * blockDim.x;
+            skip[k] = i >= hi || (inf != nullptr && inf[i]);
+            f[k] = i < hi ? load_scalar<Fr>(sc, i) : fe_zero<Fr>();
         }
-        uint64_t s[4];
-        glv_load<Fr>(sc, i, mont, s);
-        u128 rem, q;
-        bool nr, nq;
-        glv_decompose(s, K, rem, nr, q, nq);
-        radix_digits<MUL, C0>(rem, nr, W, [&](int w, int32_t d) {
-            dig[(size_t)w * nv + i] = d;
-            if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1) >> FB], 1u);
-        });
-        radix_digits<MUL, C0>(q, nq, W, [&](int w, int32_t d) {
-            dig[(size_t)w * nv + n + i] = d;
-            if (d != 0) atomicAdd(&hist[NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
-        });
+        for (int k = 0; k < PRE; k++) {
+            const uint32_t i = i0 + (uint32_t)k * blockDim.x;
+            if (i >= hi) break;
+            if (skip[k]) {
+                for (int w = 0; w < W; w++) dig[(size_t)w * nv + i] = dig[(size_t)w * nv + n + i] = 0;
+                continue;
+            }
+            if (mont) f[k] = fe_from_mont<Fr>(f[k]);
+            uint64_t s[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[j] = (uint64_t)f[k].v[2 * j] | ((uint64_t)f[k].v[2 * j + 1] << 32);
+            u128 rem, q;
+            bool nr, nq;
+            glv_decompose(s, K, rem, nr, q, nq);
+            radix_digits<MUL, C0>(rem, nr, W, [&](int w, int32_t d) {
+                dig[(size_t)w * nv + i] = d;
+                if (d != 0) atomicAdd(&hist[((uint32_t)(d < 0 ? -d : d) - 1) >> FB], 1u);
+            });
+            radix_digits<MUL, C0>(q, nq, W, [&](int w, int32_t d) {
+                dig[(size_t)w * nv + n + i] = d;
+                if (d != 0) atomicAdd(&hist[NBC + (((uint32_t)(d < 0 ? -d : d) - 1) >> FB)], 1u);
+            });
+        }
     }
     __syncthreads();
     const uint32_t s1 = sort_slot(blockIdx.x, nblk), s2 = sort_slot(blockIdx.x + n / chunk, nblk);
@@ -2013,10 +2077,28 @@ static void sparse_chunks(const uint64_t* row_ptr, size_t batch, bool rows_fit, 
 // every row has 1..CHNZ non-zeros). Outputs on the device: canonical affine rows d_xy / d_inf and,
 // with d_items (BN254), their to_data_item values. Enqueued on ctx->stream; the normalisation's
 // host step synchronises it once (normalize_split), nothing else waits.
+// row g += the canonical affine point (cxy[id], cinf[id]) of id = add_ids[g] (none: 0xffffffff)
+template <class C>
+__global__ void k_rows_add_base(typename C::Acc* __restrict__ rows, size_t batch, const uint32_t* __restrict__ add_ids,
+                                const uint64_t* __restrict__ cxy, const uint8_t* __restrict__ cinf) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= batch) return;
+    const uint32_t id = add_ids[g];
+    if (id == 0xffffffffu || cinf[id]) return;
+    using F = typename C::F;
+    typename C::Aff a;
+    memcpy(a.x.v, cxy + (size_t)id * 2 * (F::N / 2), F::N * 4);
+    memcpy(a.y.v, cxy + (size_t)id * 2 * (F::N / 2) + F::N / 2, F::N * 4);
+    a.x = fe_to_mont<F>(a.x);
+    a.y = fe_to_mont<F>(a.y);
+    rows[g] = C::madd(rows[g], a, false);
+}
+
 template <class C, class Fr>
 static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
                              const uint32_t* d_cols_in, const void* d_sc_in, int mont, void* d_xy, uint8_t* d_inf,
-                             void* d_items) {
+                             void* d_items, const uint32_t* d_add_ids = nullptr, const uint64_t* d_add_xy = nullptr,
+                             const uint8_t* d_add_inf = nullptr) {
     using Acc = typename C::Acc;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
@@ -2095,8 +2177,9 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
                   d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
     VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, d_rp.as<uint64_t>(),
               d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
-    // the fixed-base tables hold radix-2^29 limbs (commit.hip FbE): k_msm_accumulate<C, FA>
-    using FA = typename Fast29<C>::type::Aff;
+    // the fixed-base tables hold radix-2^29 limbs in 128-B entries (ec29.hpp FbE): the accumulate
+    // reads the entries' limbs (is_fbe)
+    using FA = FbE<C>;
     const FA* tab = t->fb.as<FA>();
     if (Tmax > 0) {  // all-zero rows only: k_sparse_rows already set every chunk to the identity
         VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
@@ -2121,6 +2204,9 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     }
     VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
               d_rc.as<uint32_t>(), d_rows.as<Acc>());
+    if (d_add_ids)  // rows that update a previous commitment: C_old + sum (delta_k) L_k
+        VK_LAUNCH(ctx, "sparse_add_base", (k_rows_add_base<C>), (unsigned)((batch + 255) / 256), 256, 0,
+                  d_rows.as<Acc>(), batch, d_add_ids, d_add_xy, d_add_inf);
     lap("kernels");
     VK_TRY(normalize_to_canon(ctx, ctx->curve, d_rows.p, batch, d_xy, d_inf));
     lap("normalise");
@@ -2173,9 +2259,11 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
 
 // BN254 sparse commits with device inputs and outputs (the verkle tree's device-resident levels)
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
-                            const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items) {
+                            const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items,
+                            const uint32_t* d_add_ids, const uint64_t* d_add_xy, const uint8_t* d_add_inf) {
     if (t->curve != VC_CURVE_BN254) return VC_E_INVALID;
-    return sparse_commit_dev<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, rows_fit, d_cols, d_sc, 0, d_xy, d_inf, d_items);
+    return sparse_commit_dev<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, rows_fit, d_cols, d_sc, 0, d_xy, d_inf, d_items,
+                                               d_add_ids, d_add_xy, d_add_inf);
 }
 
 int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,

@@ -135,14 +135,13 @@ static void item_of_bytes(const uint8_t* b, size_t len, uint64_t out[4]) {
 struct VerkleDev {
     uint64_t ctx_uid = 0;  // the context whose device holds it (0: none)
     int dev = -1;
-    void* item = nullptr;  // [cap] x 4 u64
+    void* item = nullptr;  // [cap] x 4 u64 (the start of the one allocation)
     void* cxy = nullptr;   // [cap] x 8 u64
     void* inf = nullptr;   // [cap] u8
     size_t cap = 0;
     void release() {
         if (dev >= 0) (void)hipSetDevice(dev);
-        for (void* p : {item, cxy, inf})
-            if (p) (void)hipFree(p);
+        if (item) (void)hipFree(item);  // one block: item, then cxy, then inf
         item = cxy = inf = nullptr;
         cap = 0;
         ctx_uid = 0;
@@ -349,6 +348,21 @@ int vc_verkle_path(const vc_verkle* t, const uint8_t* key, size_t max_len, uint8
     return VC_OK;
 }
 
+// diagnostics (tools/verkle_nodes.py): per node id, type (0 internal, 1 extension), level and the
+// committed item (the device mirror's values brought to the host first)
+int vc_verkle_debug_nodes(vc_verkle* t, size_t max, uint8_t* type, int32_t* level, uint64_t* items, size_t* n) {
+    if (!t || !n) return VC_E_INVALID;
+    VK_TRY(vk::verkle_pull_host(t));
+    const size_t m = std::min(max, t->nodes.size());
+    for (size_t i = 0; i < m; i++) {
+        if (type) type[i] = t->nodes[i].ext ? 1 : 0;
+        if (level) level[i] = t->nodes[i].level;
+        if (items) memcpy(items + 4 * i, &t->item[4 * i], 32);
+    }
+    *n = t->nodes.size();
+    return VC_OK;
+}
+
 int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, size_t* dirty) {
     if (!t) return VC_E_INVALID;
     size_t a = 0, b = 0, c = 0;
@@ -399,6 +413,34 @@ struct Rows {
 // i's node data ahead of the walk (stage 0 at 16 items ahead: the node; stage 1 at 8 ahead: what
 // the node points to, its line now cached) -- the walks are chains of dependent DRAM misses
 // (~360 ns per extension node on 16 threads)
+// the per-worker parts of build_rows (one part when the range is small)
+template <class R, class Fn, class Pf>
+std::vector<R> build_parts(HostPool& pool, size_t lo, size_t hi, size_t nnz_per, Fn fn, Pf pf) {
+    const size_t count = hi - lo;
+    auto walk_range = [&](size_t a, size_t b, R& r) {
+        for (size_t i = a; i < std::min(b, a + 16); i++) pf(i, 0);
+        for (size_t i = a; i < std::min(b, a + 8); i++) pf(i, 1);
+        for (size_t i = a; i < b; i++) {
+            if (i + 16 < b) pf(i + 16, 0);
+            if (i + 8 < b) pf(i + 8, 1);
+            fn(i, r);
+        }
+    };
+    const unsigned T = (count >= 64 && count * nnz_per >= 16384)
+                           ? (unsigned)std::min<size_t>(pool.size(), std::max<size_t>(1, count / 16))
+                           : 1;
+    std::vector<R> part(T);
+    auto run = [&](unsigned k) {
+        if (k >= T) return;
+        const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
+        part[k].reserve(b - a, (b - a) * std::min<size_t>(nnz_per, 4));
+        walk_range(a, b, part[k]);
+    };
+    if (T == 1) run(0);
+    else pool.run(run);
+    return part;
+}
+
 template <class R = Rows, class Fn, class Pf>
 R build_rows(HostPool& pool, size_t lo, size_t hi, size_t nnz_per, Fn fn, Pf pf) {
     R out;
@@ -433,6 +475,7 @@ R build_rows(HostPool& pool, size_t lo, size_t hi, size_t nnz_per, Fn fn, Pf pf)
     for (unsigned k = 0; k < T; k++) {
         roff[k + 1] = roff[k] + part[k].n();
         noff[k + 1] = noff[k] + part[k].cols.size();
+        if constexpr (!std::is_same<R, Rows>::value) out.maxlen = std::max(out.maxlen, part[k].maxlen);
     }
     out.ptr.resize(roff[T] + 1);
     out.ptr[0] = 0;
@@ -494,14 +537,17 @@ struct ExtRows16 {
     uvec<uint64_t> ptr{0};
     uvec<uint32_t> cols;
     uvec<uint64_t> vals;  // 2 u64 per non-zero
+    uvec<uint64_t> stem;  // 4 u64 per extension node (its stem item)
+    uint32_t maxlen = 0;  // longest row (<= 4: the sparse commit's chunks are the rows)
     void reserve(size_t rows, size_t nnz) {
-        ptr.reserve(rows + 1);
+        ptr.reserve(2 * rows + 1);
         cols.reserve(nnz);
         vals.reserve(2 * nnz);
+        stem.reserve(4 * rows);
     }
     size_t n() const { return ptr.size() - 1; }
 };
-static void ext_rows16(const vc_verkle* t, int id, ExtRows16& r, uint64_t* stem_item) {
+static void ext_rows16(const vc_verkle* t, int id, ExtRows16& r) {
     const int N = t->N;
     struct PV {
         uint32_t pos;
@@ -537,9 +583,11 @@ static void ext_rows16(const vc_verkle* t, int id, ExtRows16& r, uint64_t* stem_
             r.vals.push_back(half[h][k].v[0]);
             r.vals.push_back(half[h][k].v[1]);
         }
+        r.maxlen = std::max<uint32_t>(r.maxlen, (uint32_t)(r.cols.size() - r.ptr.back()));
         r.ptr.push_back(r.cols.size());
     }
-    item_of_bytes(n.stem.data(), N, stem_item);  // bytes_to_item(stem.to_bytes())
+    r.stem.resize(r.stem.size() + 4);
+    item_of_bytes(n.stem.data(), N, r.stem.data() + r.stem.size() - 4);  // bytes_to_item(stem.to_bytes())
 }
 
 static void ext_prefetch(const vc_verkle* t, int id, int stage) {
@@ -574,6 +622,7 @@ static int mirror_pull(vc_verkle* t) {
     t->host_valid = true;
     return VC_OK;
 }
+int verkle_pull_host(vc_verkle* t) { return mirror_pull(t); }
 // a mirror on ctx's device holding every committed node's results, with room for every node
 static int mirror_prepare(vc_ctx* ctx, vc_verkle* t) {
     VerkleDev& D = t->dev;
@@ -585,23 +634,19 @@ static int mirror_prepare(vc_ctx* ctx, vc_verkle* t) {
     const bool fresh = D.ctx_uid == 0;
     if (D.cap < n) {  // (with room: a tree that grows by an update's splits keeps its buffers)
         const size_t cap = std::max<size_t>({n + n / 4, 2 * D.cap, 1024});
-        void* p[3] = {nullptr, nullptr, nullptr};
-        const size_t sz[3] = {cap * 32, cap * 64, cap};
-        for (int k = 0; k < 3; k++) {
-            if (hipMalloc(&p[k], sz[k]) != hipSuccess) {
-                for (int j = 0; j < k; j++) (void)hipFree(p[j]);
-                (void)hipGetLastError();
-                return VC_E_OOM;
-            }
+        void* blk = nullptr;  // one allocation: items, commitments, flags
+        if (hipMalloc(&blk, cap * (32 + 64 + 1)) != hipSuccess) {
+            (void)hipGetLastError();
+            return VC_E_OOM;
         }
+        void* p[3] = {blk, static_cast<uint8_t*>(blk) + cap * 32, static_cast<uint8_t*>(blk) + cap * 96};
         if (!fresh && D.cap) {  // keep the committed results (every id < the old capacity)
             VK_CHECK_HIP(hipMemcpyAsync(p[0], D.item, D.cap * 32, hipMemcpyDeviceToDevice, ctx->stream));
             VK_CHECK_HIP(hipMemcpyAsync(p[1], D.cxy, D.cap * 64, hipMemcpyDeviceToDevice, ctx->stream));
             VK_CHECK_HIP(hipMemcpyAsync(p[2], D.inf, D.cap, hipMemcpyDeviceToDevice, ctx->stream));
             VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         }
-        for (void* q : {D.item, D.cxy, D.inf})
-            if (q) (void)hipFree(q);
+        if (D.item) (void)hipFree(D.item);  // (the block's start)
         D.item = p[0];
         D.cxy = p[1];
         D.inf = p[2];
@@ -990,12 +1035,40 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     const std::vector<int>& exts = t->dirty_ext;
     const size_t E = exts.size();
     if (E) {
-        uvec<uint64_t> stem(E * 4);
-        ExtRows16 r12 = build_rows<ExtRows16>(
-            pool, 0, E, (size_t)N, [&](size_t e, ExtRows16& r) { ext_rows16(t, exts[e], r, &stem[4 * e]); },
+        // the rows are built in per-worker parts (with each node's stem item), then merged straight
+        // into page-locked memory: the uploads are plain DMA, and no fresh pageable buffer is touched
+        std::vector<ExtRows16> parts = build_parts<ExtRows16>(
+            pool, 0, E, (size_t)N, [&](size_t e, ExtRows16& r) { ext_rows16(t, exts[e], r); },
             [&](size_t e, int stage) { ext_prefetch(t, exts[e], stage); });
+        const size_t T = parts.size();
+        std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0), eoff(T + 1, 0);
+        uint32_t maxlen = 0;
+        for (size_t k = 0; k < T; k++) {
+            roff[k + 1] = roff[k] + parts[k].n();
+            noff[k + 1] = noff[k] + parts[k].cols.size();
+            eoff[k + 1] = eoff[k] + parts[k].stem.size() / 4;
+            maxlen = std::max(maxlen, parts[k].maxlen);
+        }
+        const size_t nnz = noff[T];
+        // page-locked layout: row_ptr (2E + 1 u64) | stem items (E x 4 u64) | values (nnz x 2 u64) | cols
+        const size_t o_stem = (2 * E + 1) * 8, o_vals = o_stem + E * 32, o_cols = o_vals + nnz * 16;
+        VK_TRY(ctx->pin_verkle.ensure(o_cols + nnz * 4));
+        uint8_t* pin = ctx->pin_verkle.as<uint8_t>();
+        uint64_t* rp = reinterpret_cast<uint64_t*>(pin);
+        rp[0] = 0;
+        auto merge = [&](unsigned k) {
+            if (k >= T) return;
+            const ExtRows16& r = parts[k];
+            for (size_t i = 1; i < r.ptr.size(); i++) rp[roff[k] + i] = noff[k] + r.ptr[i];
+            memcpy(pin + o_stem + eoff[k] * 32, r.stem.data(), r.stem.size() * 8);
+            if (!r.cols.empty()) {
+                memcpy(pin + o_vals + noff[k] * 16, r.vals.data(), r.vals.size() * 8);
+                memcpy(pin + o_cols + noff[k] * 4, r.cols.data(), r.cols.size() * 4);
+            }
+        };
+        if (T == 1) merge(0);
+        else pool.run(merge);
         lap("ext rows (host)");
-        const size_t nnz = r12.cols.size();
         DevBuf d_cols(ctx), d_v16(ctx), d_vals(ctx), d_stem(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
         VK_TRY(d_cols.ensure(std::max<size_t>(nnz, 1) * 4));
         VK_TRY(d_v16.ensure(std::max<size_t>(nnz, 1) * 16));
@@ -1005,14 +1078,16 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         VK_TRY(d_inf.ensure(2 * E));
         VK_TRY(d_it.ensure(2 * E * 32));
         if (nnz) {
-            VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, r12.cols.data(), nnz * 4, hipMemcpyHostToDevice, st));
-            VK_CHECK_HIP(hipMemcpyAsync(d_v16.p, r12.vals.data(), nnz * 16, hipMemcpyHostToDevice, st));
+            VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, pin + o_cols, nnz * 4, hipMemcpyHostToDevice, st));
+            VK_CHECK_HIP(hipMemcpyAsync(d_v16.p, pin + o_vals, nnz * 16, hipMemcpyHostToDevice, st));
             VK_LAUNCH(ctx, "verkle_widen", k_vk_widen16, grid(nnz), 256, 0, d_v16.as<uint64_t>(), nnz,
                       d_vals.as<uint64_t>());
         }
-        VK_CHECK_HIP(hipMemcpyAsync(d_stem.p, stem.data(), E * 32, hipMemcpyHostToDevice, st));
-        VK_TRY(sparse_commit_items_dev(ctx, tab, 2 * E, r12.ptr.data(), false, d_cols.as<uint32_t>(), d_vals.p,
-                                       d_xy.p, d_inf.as<uint8_t>(), d_it.p));
+        VK_CHECK_HIP(hipMemcpyAsync(d_stem.p, pin + o_stem, E * 32, hipMemcpyHostToDevice, st));
+        // rows of <= 4 non-zeros (random keys: one leaf per extension) are the sparse commit's chunks
+        // as they are (an empty row is an empty chunk: the identity), no chunk lists
+        VK_TRY(sparse_commit_items_dev(ctx, tab, 2 * E, rp, maxlen <= 4, d_cols.as<uint32_t>(), d_vals.p, d_xy.p,
+                                       d_inf.as<uint8_t>(), d_it.p));
         lap("ext c1 / c2 commits");
         DevBuf d_c4(ctx), d_v4(ctx), d_xy4(ctx), d_inf4(ctx), d_it4(ctx);
         VK_TRY(d_c4.ensure(4 * E * 4));

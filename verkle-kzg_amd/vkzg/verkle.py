@@ -53,6 +53,18 @@ class VerkleTree:
               "vc_verkle_path")
         return [(tuple(key[:d + 1]), key[d]) for d in range(n.value)]
 
+    def debug_nodes(self):
+        """per node id: (type 0 internal / 1 extension, level, committed item as int)"""
+        n = ctypes.c_size_t()
+        check(lib().vc_verkle_debug_nodes(self.h, 0, None, None, None, ctypes.byref(n)), "vc_verkle_debug_nodes")
+        m = n.value
+        ty = np.zeros(m, dtype=np.uint8)
+        lv = np.zeros(m, dtype=np.int32)
+        it = np.zeros((m, 4), dtype=np.uint64)
+        check(lib().vc_verkle_debug_nodes(self.h, m, ctypes.c_void_p(ty.ctypes.data), ctypes.c_void_p(lv.ctypes.data),
+                                          ctypes.c_void_p(it.ctypes.data), ctypes.byref(n)), "vc_verkle_debug_nodes")
+        return [(int(ty[i]), int(lv[i]), limbs_to_int(it[i])) for i in range(m)]
+
     def stats(self):
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         check(lib().vc_verkle_stats(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "vc_verkle_stats")
