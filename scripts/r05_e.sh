@@ -9,6 +9,7 @@ echo "tests rc=$rc"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 200 python -u verkle-kzg_amd/tools/verkle_nodes.py > $O/nodes.txt 2>&1 || exit $?
 timeout -k 10 200 python -u verkle-kzg_amd/tools/verkle_ab.py 65536 5 > $O/ab.txt 2>&1 || exit $?
+VKZG_VERKLE_DELTA=0 timeout -k 10 200 python -u verkle-kzg_amd/tools/verkle_ab.py 65536 5 >> $O/ab.txt 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/vtrace -o vt -- python3 -u verkle-kzg_amd/tools/verkle_ab.py 65536 2 > $O/vtrace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/msm -o msm -- python3 -u verkle-kzg_amd/tools/msm_once.py > $O/msm.log 2>&1 || exit $?
 timeout -k 10 300 python -u verkle-kzg_amd/tools/group_probe.py > $O/group.txt 2>&1 || exit $?

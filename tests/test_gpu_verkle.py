@@ -87,11 +87,53 @@ def test_verkle_commitment_matches_oracle(eng, oracle_c, scheme_name, N, arity, 
     assert t.stats()["dirty"] == 0
 
 
-def test_verkle_update_equals_fresh_tree(eng):
+@pytest.mark.parametrize("small", ["auto", "0"])
+@pytest.mark.parametrize("delta", ["1", "0"])
+@pytest.mark.parametrize("N,arity", [(3, 6), (4, 4), (3, 255)])
+def test_verkle_delta_rounds_match_oracle(eng, oracle_c, N, arity, delta, small, monkeypatch):
+    """Several update rounds on the device path: an updated internal node's row is its old
+    commitment plus the changed slots' item differences (delta rows, the insert-time slot log:
+    path slots, new extensions in empty slots, splits replacing an extension by an internal node,
+    several changes to one slot inside a round); VKZG_VERKLE_DELTA=0 recommits full rows. small:
+    the sparse commits' latency path (a wave per 64 pairs, the default for levels of <= 2^18
+    pairs) or, "0", the sort-based path for every level. Every round's commitment == the
+    oracle's recursive gen_commitment."""
+    from pyoracle import verkle as ov
+    from vkzg.verkle import VerkleTree
+    monkeypatch.setenv("VKZG_VERKLE_DELTA", delta)
+    if small != "auto":
+        monkeypatch.setenv("VKZG_SPARSE_SMALL_MAX", small)
+    table, commit = _schemes(eng)["kzg"]
+    rng = random.Random(1000 * N + arity)
+    t, o = VerkleTree(N), ov.VerkleTree(N)
+    inserted = []
+    for rnd, m in enumerate([60, 3, 1, 12, 25, 7]):
+        for _ in range(m):
+            if inserted and rng.random() < 0.4:
+                k = rng.choice(inserted)   # rewrite an existing key (its path's slots only)
+            else:
+                k = _key(rng, N, arity)
+            v = _val(rng)
+            try:
+                o.insert_single(k, v)
+            except ov.VerklePanic:
+                continue
+            t.insert_single(k, v)
+            inserted.append(k)
+        assert t.commitment(eng, table) == o.commitment(commit), rnd
+        assert t.stats()["dirty"] == 0
+
+
+@pytest.mark.parametrize("small", ["auto", "0", "1000000000"])
+def test_verkle_update_equals_fresh_tree(eng, small, monkeypatch):
     """A 40,000-key tree (32-unit keys) committed, 1 % of the keys rewritten, committed again
     (only the dirty nodes: levels of a few hundred rows with ~150 children each, whose rows are
-    built on part of the host pool) == a fresh tree of the final contents committed in full."""
+    built on part of the host pool; delta rows) == a fresh tree of the final contents committed in
+    full. small: the levels' path by size (auto), the sort-based path everywhere (0) or the
+    latency path everywhere (10^9 pairs: the 80,000-row extension levels too)."""
     import numpy as np
+    if small != "auto":
+        monkeypatch.setenv("VKZG_SPARSE_SMALL_MAX", small)
     from vkzg import scheme
     from vkzg.verkle import VerkleTree
     kzg = scheme.KZG(eng, 256)

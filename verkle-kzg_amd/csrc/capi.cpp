@@ -248,6 +248,10 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         ctx->pin_small.release();
         ctx->pin_norm.release();
         ctx->pin_y.release();
+        ctx->pin_verkle.release();
+        for (auto& b : ctx->pin_verkle_lv) b.release();
+        ctx->pin_norm_vk.release();
+        ctx->pin_sparse_ck.release();
         for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
         ctx->pool_free.clear();
         for (auto& p : ctx->pending) {

@@ -201,15 +201,13 @@ __global__ void __launch_bounds__(256) k_normalize(const typename C::Acc* __rest
 // (Montgomery's trick) and k_norm_finish scales. One pinned round trip (~20 us) replaces the
 // lane inversion: 10k Bandersnatch commits normalise in ~0.06 instead of 0.18 ms.
 template <class C>
-__global__ void __launch_bounds__(256) k_norm_prep(const typename C::Acc* __restrict__ in, size_t count,
-                                                  fe<typename C::F>* __restrict__ others,
-                                                  fe<typename C::F>* __restrict__ tot) {
+__device__ __forceinline__ void norm_prep_block(const typename C::Acc& a, size_t j, size_t count,
+                                                fe<typename C::F>* __restrict__ others,
+                                                fe<typename C::F>* __restrict__ tot) {
     using F = typename C::F;
     __shared__ fe<F> pre[256];
     __shared__ fe<F> suf[256];
-    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t tid = threadIdx.x;
-    const typename C::Acc a = j < count ? in[j] : C::zero();
     fe<F> z = (j < count && !norm_as_one<C>(a)) ? denom<C>(a) : fe_one<F>();
     pre[tid] = z;
     suf[tid] = z;
@@ -228,6 +226,37 @@ __global__ void __launch_bounds__(256) k_norm_prep(const typename C::Acc* __rest
     if (tid < 255) o = tid > 0 ? fe_mul<F>(o, suf[tid + 1]) : suf[tid + 1];
     if (j < count) others[j] = o;
     if (tid == 0) tot[blockIdx.x] = pre[255];
+}
+template <class C>
+__global__ void __launch_bounds__(256) k_norm_prep(const typename C::Acc* __restrict__ in, size_t count,
+                                                  fe<typename C::F>* __restrict__ others,
+                                                  fe<typename C::F>* __restrict__ tot) {
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    norm_prep_block<C>(j < count ? in[j] : C::zero(), j, count, others, tot);
+}
+// verkle rows (BN254): row j first takes the canonical affine point (add_xy, add_inf)[add_ids[j]]
+// (0xffffffff: none) -- the old commitment of a delta row -- and is written back with it
+__global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__ rows, size_t count,
+                                                     const uint32_t* __restrict__ add_ids,
+                                                     const uint64_t* __restrict__ add_xy,
+                                                     const uint8_t* __restrict__ add_inf,
+                                                     fe<BN254Fq>* __restrict__ others, fe<BN254Fq>* __restrict__ tot) {
+    using C = BN254G1;
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    C::Acc a = j < count ? rows[j] : C::zero();
+    if (add_ids && j < count) {
+        const uint32_t id = add_ids[j];
+        if (id != 0xffffffffu && !add_inf[id]) {
+            C::Aff q;
+            memcpy(q.x.v, add_xy + 8 * (size_t)id, 32);
+            memcpy(q.y.v, add_xy + 8 * (size_t)id + 4, 32);
+            q.x = fe_to_mont<BN254Fq>(q.x);
+            q.y = fe_to_mont<BN254Fq>(q.y);
+            a = C::madd(a, q, false);
+            rows[j] = a;
+        }
+    }
+    norm_prep_block<C>(a, j, count, others, tot);
 }
 
 template <class C>
@@ -272,6 +301,30 @@ __global__ void __launch_bounds__(256) k_norm_finish(const typename C::Acc* __re
         }
     }
     if (out_inf) out_inf[j] = ident ? 1 : 0;
+}
+
+// verkle rows (BN254): canonical affine point, identity flag and to_data_item of row j stored at
+// dst[j] (dst null: at j) -- straight into the tree's device mirror
+__global__ void __launch_bounds__(256) k_norm_finish_vk(const BN254G1::Acc* __restrict__ rows, size_t count,
+                                                       const fe<BN254Fq>* __restrict__ others,
+                                                       const fe<BN254Fq>* __restrict__ binv,
+                                                       const uint32_t* __restrict__ dst, uint64_t* __restrict__ out_xy,
+                                                       uint8_t* __restrict__ out_inf, uint64_t* __restrict__ out_item) {
+    using F = BN254Fq;
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= count) return;
+    const BN254G1::Acc a = rows[j];
+    const bool ident = BN254G1::is_zero(a);
+    const fe<F> iz = fe_mul<F>(binv[blockIdx.x], others[j]);
+    const fe<F> t = fe_mul<F>(iz, a.zz);  // 1/Z
+    fe<F> cx = fe_from_mont<F>(fe_mul<F>(a.x, fe_sqr<F>(t))), cy = fe_from_mont<F>(fe_mul<F>(a.y, iz));
+    if (ident) cx = cy = fe_zero<F>();
+    const size_t o = dst ? dst[j] : j;
+    memcpy(out_xy + 8 * o, cx.v, 32);
+    memcpy(out_xy + 8 * o + 4, cy.v, 32);
+    out_inf[o] = ident ? 1 : 0;
+    const fe<BN254Fr> it = to_data_item_canon(cx, cy, ident);
+    memcpy(out_item + 4 * o, it.v, 32);
 }
 
 // d_in (count accumulators) -> affine / canonical outputs; synchronises the stream once
@@ -421,80 +474,33 @@ __global__ void __launch_bounds__(64) k_fb_combine_wave(const typename Fast29<C>
 constexpr int FB_WPT = 1;
 static int fb_wpt() { return FB_WPT; }
 
-// xor butterfly over the wave on the radix-29 accumulators (the add the tails run too). The
-// shuffle moves sizeof(Acc) / 4 words (shfl_xor_pod): SW29::Acc is 4 L limbs of 29 bits plus the
-// `inf` flag -- 37 words at BN254 (L = 9), 57 at BLS12-381 -- not the 4 N words of the ec.hpp
-// accumulator (C::ACC_WORDS = 32 / 48). An earlier version shuffled C::ACC_WORDS words of the
-// radix-29 accumulator, which left zz / zzz partly and `inf` entirely lane-local: every commit
-// with more than one non-identity lane came out wrong (batched-commit parity failed at the first
-// non-zero commit on the GPU while the host tests of the add formulas passed).
-template <class FC>
-__device__ __forceinline__ typename FC::Acc fb_wave_sum29(typename FC::Acc v) {
-    for (uint32_t m = 1; m < 64; m <<= 1) v = FC::add(v, shfl_xor_pod(v, m));
-    return v;
-}
-
 template <class C, class Fr>
 __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
                                                         const uint8_t* __restrict__ inf, uint32_t width, FbGeom fg,
                                                         const uint32_t* __restrict__ sc, int mont,
-                                                        uint32_t bpc, int wpt, typename C::Acc* __restrict__ part) {
-    using Acc = typename C::Acc;
+                                                        uint32_t bpc, int wpt, const uint32_t* __restrict__ cols,
+                                                        typename C::Acc* __restrict__ part) {
     using FC = typename Fast29<C>::type;
-    __shared__ Acc wsum[4];
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
     const int W = fg.W;
     const uint32_t WG = (uint32_t)(W + wpt - 1) / wpt;
     const uint32_t j = blk * 256 + threadIdx.x;
     const uint32_t i = j / WG, wg = j % WG;
     typename FC::Acc fa = FC::zero();
-    if (i < width && !inf[i]) {
+    // cols (optional): commit g's item i is table base cols[g width + i] (compacted rows)
+    const uint32_t base = (i < width && cols) ? cols[(size_t)g * width + i] : i;
+    if (i < width && !inf[base]) {
         FbDigits<Fr> dg;
         dg.s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
         if (mont) dg.s = fe_from_mont<Fr>(dg.s);
-        const FbE<C>* ti = tab + (size_t)i * fg.stride();
+        const FbE<C>* ti = tab + (size_t)base * fg.stride();
         const int wb = (int)wg * wpt, we = min(W, wb + wpt);
         for (int w = 0; w < we; w++) {
             const int32_t d = dg.next(fg.width(w));
             if (w >= wb && d != 0) fa = FC::madd(fa, ti[fg.off(w) + (uint32_t)(d < 0 ? -d : d) - 1].u, d < 0);
         }
     }
-    if constexpr (FC::quad) {
-        // block sum on 4-lane cooperative adds (SW29::add_quad, ~half the latency of a full add):
-        // quad q first adds its own four lanes' points (3 rounds), then the 16 quads of the wave
-        // fold by xor (4), then wave 0 folds the 4 wave sums from LDS (2): 9 dependent adds of
-        // ~6 us instead of 6 full adds of ~13 us plus 3 more on one thread
-        __shared__ typename FC::Acc wq[4];
-        const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, role = lane & 3, q0 = lane & ~3u;
-        typename FC::Acc v = shfl_idx_pod(fa, q0);
-        for (uint32_t it = 0; it < 9; it++) {  // one add call site
-            typename FC::Acc o;
-            if (it < 3) {
-                o = shfl_idx_pod(fa, q0 + it + 1);
-            } else if (it < 7) {
-                o = shfl_xor_pod(v, 4u << (it - 3));
-            } else {
-                if (it == 7) {
-                    if (lane == 0) wq[wave] = v;
-                    __syncthreads();
-                    if (wave != 0) break;
-                    v = (lane >> 2) < 4 ? wq[lane >> 2] : FC::zero();
-                }
-                o = shfl_xor_pod(v, 4u << (it - 7));
-            }
-            v = FC::add_quad(v, o, role);
-        }
-        if (threadIdx.x == 0) part[blockIdx.x] = FC::store(v);
-    } else {
-        Acc acc = FC::store(fb_wave_sum29<FC>(fa));
-        const int wave = threadIdx.x / 64;
-        if ((threadIdx.x & 63) == 0) wsum[wave] = acc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            Acc t = C::add(C::add(wsum[0], wsum[1]), C::add(wsum[2], wsum[3]));
-            part[blockIdx.x] = t;
-        }
-    }
+    fb_block_sum_store<C>(fa, &part[blockIdx.x]);
 }
 
 template <class C>
@@ -574,9 +580,10 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                       const PinBuf* pin_sc, const std::function<void()>* overlap) {
+                       const PinBuf* pin_sc, const std::function<void()>* overlap, bool with_cols) {
     using Acc = typename C::Acc;
-    if (width > t->n) return VC_E_RANGE;
+    if (width > t->n && !with_cols) return VC_E_RANGE;
+    if (with_cols && !pin_sc) return VC_E_INVALID;
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8, 0));
     if (batch == 0) {
         if (overlap && *overlap) (*overlap)();
@@ -592,6 +599,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     const int wpt = fb_wpt();
     const size_t WG = (size_t)(W + wpt - 1) / wpt;
     const bool small = items * WG <= lanes && batch <= 64;
+    if (with_cols && !small) return VC_E_INVALID;  // compacted rows: the latency path only
     // zero-copy on the latency path (VKZG_ZERO_COPY, A/B probe: bit 0 partials, bit 1 scalars):
     // the kernel reads host-pinned scalars and writes its block partials to fine-grained host
     // memory over PCIe instead of a copy engine moving them before / after it
@@ -618,9 +626,22 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         VK_TRY(ctx->pin_small.ensure(part_bytes));
         if (!(zc & 1)) VK_TRY(ctx->ws[WS_PIECE].ensure(part_bytes));
         Acc* d_part = (zc & 1) ? static_cast<Acc*>(ctx->pin_small.dp) : ctx->ws[WS_PIECE].as<Acc>();
+        // compacted rows: the base indices follow the scalars in the pinned staging
+        const uint32_t* d_cols = nullptr;
+        if (with_cols) {
+            const size_t off = items * 32;
+            if (zc & 2) {
+                d_cols = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pin_sc->dp) + off);
+            } else {
+                VK_TRY(ctx->ws[WS_COLS].ensure(items * 4));
+                VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_COLS].p, static_cast<const uint8_t*>(pin_sc->p) + off,
+                                            items * 4, hipMemcpyHostToDevice, ctx->stream));
+                d_cols = ctx->ws[WS_COLS].as<uint32_t>();
+            }
+        }
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
                   t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
-                  bpc, wpt, d_part);
+                  bpc, wpt, d_cols, d_part);
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
         // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the
@@ -728,6 +749,47 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) {
     return VC_E_INVALID;
 }
 
+// verkle rows (BN254, device): optional old-commitment adds, then canonical affine points,
+// identity flags and to_data_item values at dst[j] (k_norm_prep_vk / k_norm_finish_vk). One
+// pinned round trip (the block products' inversion on the host) and no trailing synchronisation:
+// the finish kernel and its H2D copy stay queued (the next call synchronises the stream -- after
+// the D2H of its products -- before its host writes into pin_norm_vk, so the copy has left it).
+int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* add_ids, const uint64_t* add_xy,
+                         const uint8_t* add_inf, const uint32_t* dst, uint64_t* out_xy, uint8_t* out_inf,
+                         uint64_t* out_item, const std::function<void()>* overlap) {
+    using F = BN254Fq;
+    if (n == 0) return VC_OK;
+    const size_t nblk = (n + 255) / 256;
+    DevBuf others(ctx), tot(ctx);
+    VK_TRY(others.ensure(n * sizeof(fe<F>)));
+    VK_TRY(tot.ensure(nblk * sizeof(fe<F>)));
+    // its own pinned staging (the previous call's H2D may still be queued: grow it only after a sync)
+    if (ctx->pin_norm_vk.cap < 2 * nblk * sizeof(fe<F>)) {
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        VK_TRY(ctx->pin_norm_vk.ensure(std::max<size_t>(2 * nblk, 64) * sizeof(fe<F>)));
+    }
+    fe<F>* h = ctx->pin_norm_vk.as<fe<F>>();
+    VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids, add_xy,
+              add_inf, others.as<fe<F>>(), tot.as<fe<F>>());
+    VK_CHECK_HIP(hipMemcpyAsync(h, tot.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, ctx->stream));
+    if (overlap && *overlap) (*overlap)();
+    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    fe<F>* inv = h + nblk;
+    inv[0] = h[0];
+    for (size_t b = 1; b < nblk; b++) inv[b] = fe_mul<F>(inv[b - 1], h[b]);
+    fe<F> run = fe_inv_bin<F>(inv[nblk - 1]);
+    for (size_t b = nblk - 1; b > 0; b--) {
+        const fe<F> ib = fe_mul<F>(run, inv[b - 1]);
+        run = fe_mul<F>(run, h[b]);
+        inv[b] = ib;
+    }
+    inv[0] = run;
+    VK_CHECK_HIP(hipMemcpyAsync(tot.p, inv, nblk * sizeof(fe<F>), hipMemcpyHostToDevice, ctx->stream));
+    VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
+              others.as<fe<F>>(), tot.as<fe<F>>(), dst, out_xy, out_inf, out_item);
+    return VC_OK;
+}
+
 // normalise n device accumulators to canonical affine (device outputs)
 int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void* d_out_xy, uint8_t* d_out_inf) {
     if (n == 0) return VC_OK;
@@ -752,9 +814,24 @@ int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows) {
     return VC_E_INVALID;
 }
 
+bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch) {
+    if (t->curve != ctx->curve || batch == 0 || batch > 64) return false;
+    if (!ctx->fb_lanes) {
+        switch (t->curve) {
+            case VC_CURVE_BN254: ctx->fb_lanes = resident_lanes(k_fb_commit_cm<BN254G1, BN254Fr>, 256); break;
+            case VC_CURVE_BLS12_381: ctx->fb_lanes = resident_lanes(k_fb_commit_cm<BLS381G1, BLS381Fr>, 256); break;
+            default: ctx->fb_lanes = resident_lanes(k_fb_commit_cm<Bandersnatch, BandFr>, 256); break;
+        }
+    }
+    const size_t lanes = ctx->fb_lanes ? ctx->fb_lanes : 131072;
+    const int c = t->fb_c ? t->fb_c : 8;
+    const size_t W = t->fb_c ? (size_t)t->fb_W : (size_t)((255 + 1 + c - 1) / c);  // (before the default tables exist)
+    return batch * width * W <= lanes;
+}
+
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                   void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                  const PinBuf* pin_sc, const std::function<void()>* overlap) {
+                  const PinBuf* pin_sc, const std::function<void()>* overlap, bool with_cols) {
     bool dummy = false;
     if (!on_host) on_host = &dummy;
     *on_host = false;
@@ -762,13 +839,13 @@ int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t 
     switch (t->curve) {
         case VC_CURVE_BN254:
             return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                 h_out_inf, on_host, pin_sc, overlap);
+                                                 h_out_inf, on_host, pin_sc, overlap, with_cols);
         case VC_CURVE_BLS12_381:
             return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                   h_out_inf, on_host, pin_sc, overlap);
+                                                   h_out_inf, on_host, pin_sc, overlap, with_cols);
         case VC_CURVE_BANDERSNATCH:
             return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                     h_out_inf, on_host, pin_sc, overlap);
+                                                     h_out_inf, on_host, pin_sc, overlap, with_cols);
     }
     return VC_E_INVALID;
 }

@@ -127,6 +127,7 @@ enum WsSlot {
     WS_SCALARS,
     WS_OUT,
     WS_MISC,
+    WS_COLS,
     WS_TREE,
     WS_TAIL,
     WS_PIECE,
@@ -185,6 +186,10 @@ struct vc_ctx {
     vk::PinBuf pin_norm;            // block products / inverses of the split normalisation
     vk::PinBuf pin_y;               // the KZG opening's y, copied back asynchronously
     vk::PinBuf pin_verkle;          // the verkle extension rows, merged straight into page-locked memory
+    vk::PinBuf pin_verkle_lv[2];    // verkle levels' lists (one upload per level; the next level's are
+                                    // built into the other one while the current level runs)
+    vk::PinBuf pin_norm_vk;         // block products / inverses of the verkle rows' normalisation
+    vk::PinBuf pin_sparse_ck;       // chunk tables of the sparse commits' latency path
     // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
     // (or are synchronised), so a block freed by one call is safely reused by the next in
     // stream order; vc_ctx_set_stream drains the old stream first
@@ -285,6 +290,39 @@ int msm_batch_sparse_items_guarded(vc_ctx* ctx, int table, size_t batch, const u
 // structure row_ptr on the host (rows_fit: every row has 1..4 non-zeros -- the chunks are the rows);
 // affine rows, flags and items written to device memory, enqueued on ctx->stream (verkle.cpp's
 // device-resident levels)
+// the sparse commits' latency path (msm.hip k_fb_sparse_small, BN254): rows of (column, scalar)
+// non-zeros; mode 0: d_vals (4 canonical words per non-zero), 1: d_vals of 2 words (16-byte
+// values), 2: d_item[d_child[j]] - (d_sidx && d_sidx[j] >= 0 ? d_snap[d_sidx[j]] : 0). Row g
+// also adds the point (d_add_xy, d_add_inf)[d_add_ids[g]] if given (0xffffffff: none); its
+// canonical affine point, identity flag and to_data_item go to index d_dst[g] (null: g) of the
+// outputs. Enqueued on ctx->stream; one host round trip (the normalisation), no final sync.
+struct SmallRows {
+    size_t batch = 0;
+    const uint64_t* row_ptr = nullptr;  // host, batch + 1
+    int mode = 0;
+    const uint32_t* d_cols = nullptr;
+    const uint64_t* d_vals = nullptr;
+    const uint64_t* d_item = nullptr;
+    const uint32_t* d_child = nullptr;
+    const int32_t* d_sidx = nullptr;
+    const uint64_t* d_snap = nullptr;
+    const uint32_t* d_add_ids = nullptr;
+    const uint64_t* d_add_xy = nullptr;
+    const uint8_t* d_add_inf = nullptr;
+    const uint32_t* d_dst = nullptr;
+    uint64_t* d_out_xy = nullptr;
+    uint8_t* d_out_inf = nullptr;
+    uint64_t* d_out_item = nullptr;
+};
+// overlap (optional): host work run once the kernels and the read-back are queued, before the wait
+int sparse_small_items_dev(vc_ctx* ctx, Table* t, const SmallRows& in,
+                           const std::function<void()>* overlap = nullptr);
+size_t sparse_small_pairs(const Table* t, size_t nnz);  // (non-zero, window) pairs of nnz non-zeros
+// BN254 rows -> (optional old-commitment adds) canonical affine points, flags, to_data_item at
+// dst[j] (commit.hip); no final sync
+int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* add_ids, const uint64_t* add_xy,
+                         const uint8_t* add_inf, const uint32_t* dst, uint64_t* out_xy, uint8_t* out_inf,
+                         uint64_t* out_item, const std::function<void()>* overlap = nullptr);
 // d_add_ids (optional): row g also adds the canonical affine point (d_add_xy, d_add_inf)[d_add_ids[g]]
 // before the normalisation (0xffffffff: nothing) -- a verkle row that updates its old commitment
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
@@ -299,9 +337,13 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 // the results are written there instead of d_out_* and *on_host is set
 // pin_sc: the scalars in ctx->pin_io (host, page-locked) instead of d_scalars (nullptr): uploaded
 // to WS_SCALARS here, or read in place over PCIe by the latency path. overlap: host work run once
-// the commit kernel is enqueued, before the call waits for it
+// the commit kernel is enqueued, before the call waits for it. with_cols: compacted rows -- item i
+// of commit g is table base cols[g width + i], the u32 cols following the batch x width scalars in
+// pin_sc (latency path only: VC_E_INVALID otherwise; fb_small_path says whether it runs)
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
                   uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr,
-                  const std::function<void()>* overlap = nullptr);
+                  const std::function<void()>* overlap = nullptr, bool with_cols = false);
+// whether msm_batch_run of `batch` width-`width` commits takes the latency path
+bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch);
 }  // namespace vk

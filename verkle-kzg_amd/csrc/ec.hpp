@@ -287,5 +287,25 @@ using BN254G1 = SWCurve<BN254Fq, 3>;
 using BLS381G1 = SWCurve<BLS381Fq, 4>;
 using Bandersnatch = TECurve<BLS381Fr, BandD>;
 
+// to_data_item (reference lib.rs:56-67) of a canonical affine BN254 G1 point: its compressed
+// encoding (x, the top bit set when y > p - y) read as a little-endian integer mod r -- canonical
+// Fr words; the identity maps to 0
+VK_HD inline fe<BN254Fr> to_data_item_canon(const fe<BN254Fq>& x, const fe<BN254Fq>& y, bool inf) {
+    fe<BN254Fr> r = fe_zero<BN254Fr>();
+    if (inf) return r;
+    const fe<BN254Fq> ny = fe_sub<BN254Fq>(fe_zero<BN254Fq>(), y);
+    bool neg = false;  // y > p - y (canonical)
+    for (int k = 7; k >= 0; k--) {
+        if (y.v[k] != ny.v[k]) {
+            neg = y.v[k] > ny.v[k];
+            break;
+        }
+    }
+    for (int k = 0; k < 8; k++) r.v[k] = x.v[k];
+    if (neg) r.v[7] |= 0x80000000u;
+    for (int it = 0; it < 6; it++) r = fe_reduce_once<BN254Fr>(r);  // < 2^256 < 6r
+    return r;
+}
+
 
 }  // namespace vk

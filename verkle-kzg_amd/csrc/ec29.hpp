@@ -391,4 +391,65 @@ struct FbEntryLimbs {
 template <class C>
 using FbE = FbEntryLimbs<C>;
 
+// xor butterfly over the wave on the radix-29 accumulators (the add the tails run too). The
+// shuffle moves sizeof(Acc) / 4 words (shfl_xor_pod): SW29::Acc is 4 L limbs of 29 bits plus the
+// `inf` flag -- 37 words at BN254 (L = 9), 57 at BLS12-381 -- not the 4 N words of the ec.hpp
+// accumulator (C::ACC_WORDS = 32 / 48). An earlier version shuffled C::ACC_WORDS words of the
+// radix-29 accumulator, which left zz / zzz partly and `inf` entirely lane-local: every commit
+// with more than one non-identity lane came out wrong (batched-commit parity failed at the first
+// non-zero commit on the GPU while the host tests of the add formulas passed).
+template <class FC>
+__device__ __forceinline__ typename FC::Acc fb_wave_sum29(typename FC::Acc v) {
+    for (uint32_t m = 1; m < 64; m <<= 1) v = FC::add(v, shfl_xor_pod(v, m));
+    return v;
+}
+
+// The sum of a block's accumulators (one per thread, NT = 256 or 64 threads), stored by thread 0
+// at *out (the fixed-base latency paths: commit.hip k_fb_commit_small, msm.hip k_fb_sparse_small).
+// On 4-lane cooperative adds (SW29::add_quad, ~half the latency of a full add): quad q first adds
+// its own four lanes' points (3 rounds), then the 16 quads of the wave fold by xor (4), then (NT =
+// 256) wave 0 folds the 4 wave sums from LDS (2): 9 dependent adds of ~6 us instead of 6 full adds
+// of ~13 us plus 3 more on one thread. Every thread of the block must call it.
+template <class C, int NT = 256>
+__device__ __forceinline__ void fb_block_sum_store(typename Fast29<C>::type::Acc fa, typename C::Acc* out) {
+    static_assert(NT == 256 || NT == 64, "a wave or four");
+    using FC = typename Fast29<C>::type;
+    using Acc = typename C::Acc;
+    if constexpr (FC::quad) {
+        __shared__ typename FC::Acc wq[NT / 64];
+        const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, role = lane & 3, q0 = lane & ~3u;
+        constexpr uint32_t ITS = NT == 256 ? 9 : 7;
+        typename FC::Acc v = shfl_idx_pod(fa, q0);
+        for (uint32_t it = 0; it < ITS; it++) {  // one add call site
+            typename FC::Acc o;
+            if (it < 3) {
+                o = shfl_idx_pod(fa, q0 + it + 1);
+            } else if (it < 7) {
+                o = shfl_xor_pod(v, 4u << (it - 3));
+            } else {
+                if (it == 7) {
+                    if (lane == 0) wq[wave] = v;
+                    __syncthreads();
+                    if (wave != 0) break;
+                    v = (lane >> 2) < 4 ? wq[lane >> 2] : FC::zero();
+                }
+                o = shfl_xor_pod(v, 4u << (it - 7));
+            }
+            v = FC::add_quad(v, o, role);
+        }
+        if (threadIdx.x == 0) *out = FC::store(v);
+    } else {
+        Acc acc = FC::store(fb_wave_sum29<FC>(fa));
+        if constexpr (NT == 64) {
+            if (threadIdx.x == 0) *out = acc;
+        } else {
+            __shared__ Acc wsum[4];
+            const int wave = threadIdx.x / 64;
+            if ((threadIdx.x & 63) == 0) wsum[wave] = acc;
+            __syncthreads();
+            if (threadIdx.x == 0) *out = C::add(C::add(wsum[0], wsum[1]), C::add(wsum[2], wsum[3]));
+        }
+    }
+}
+
 }  // namespace vk

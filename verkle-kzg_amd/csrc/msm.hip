@@ -23,6 +23,7 @@
 #include <type_traits>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -2255,6 +2256,139 @@ static int msm_batch_sparse_t(vc_ctx* ctx, Table* t, size_t batch, const uint64_
     if (out_items) VK_CHECK_HIP(hipMemcpyAsync(out_items, d_it.p, batch * 32, hipMemcpyDeviceToHost, st));
     VK_CHECK_HIP(hipStreamSynchronize(st));  // host staging vectors die on return
     return VC_OK;
+}
+
+// ---- latency path of the sparse commits (verkle levels of a few thousand non-zeros). The
+// sort-based path above is a chain of ~10 launches whose accumulate runs M = 16 serial mixed adds
+// per thread and whose fix-up walks straddles serially: ~0.2 ms of kernels for a level of 1,000
+// non-zeros, whatever its size (profiles/r05/verkle/). Here a wave takes a chunk of <= 64 of a
+// row's (non-zero, window) pairs -- two non-zeros at W = 32 --, every lane adds its one table
+// point (a load: the accumulator starts at the identity) and the wave folds on quad-cooperative
+// adds (7 dependent ones); rows of several chunks are folded by k_sparse_combine.
+// MODE 0: scalars vals[j] (4 canonical words); 1: 16-byte values (2 words: the leaf halves of
+// an extension's c1 / c2 rows); 2: item[child[j]] - (sidx[j] < 0 ? 0 : snap[sidx[j]]) mod r (a
+// verkle level's children's items from the mirror, minus the old item of a delta row's slot).
+struct SmallChunk {
+    uint32_t j0, npairs, p0, pad;  // the row's first non-zero, its pair count, this chunk's first pair
+};
+template <class C, class Fr, int MODE, int NT>
+__global__ void __launch_bounds__(NT) k_fb_sparse_small(const FbE<C>* __restrict__ tab, const uint8_t* __restrict__ inf,
+                                                       FbGeom fg, const SmallChunk* __restrict__ ck,
+                                                       const uint32_t* __restrict__ cols, const uint64_t* __restrict__ vals,
+                                                       const uint64_t* __restrict__ item, const uint32_t* __restrict__ child,
+                                                       const int32_t* __restrict__ sidx, const uint64_t* __restrict__ snap,
+                                                       typename C::Acc* __restrict__ part) {
+    using FC = typename Fast29<C>::type;
+    const SmallChunk c = ck[blockIdx.x];
+    const uint32_t p = c.p0 + threadIdx.x, W = (uint32_t)fg.W;
+    typename FC::Acc fa = FC::zero();
+    if (p < c.npairs) {
+        const size_t j = (size_t)c.j0 + p / W;
+        const int w = (int)(p % W);
+        const uint32_t col = cols[j];
+        fe<Fr> s = fe_zero<Fr>();
+        if constexpr (MODE == 0) {
+            memcpy(s.v, vals + 4 * j, 32);
+        } else if constexpr (MODE == 1) {
+            memcpy(s.v, vals + 2 * j, 16);
+        } else {
+            memcpy(s.v, item + 4 * (size_t)child[j], 32);
+            const int32_t k = sidx ? sidx[j] : -1;
+            if (k >= 0) {
+                fe<Fr> o;
+                memcpy(o.v, snap + 4 * (size_t)k, 32);
+                s = fe_sub<Fr>(s, o);  // canonical in, canonical out
+            }
+        }
+        int32_t d = 0;
+        for_each_digit_fb<Fr>(s, fg, [&](int ww, int32_t dd) {
+            if (ww == w) d = dd;
+        });
+        if (d != 0 && !inf[col])
+            fa = FC::madd(fa, tab[(size_t)col * fg.stride() + fg.off(w) + (uint32_t)(d < 0 ? -d : d) - 1].u, d < 0);
+    }
+    fb_block_sum_store<C, NT>(fa, &part[blockIdx.x]);
+}
+
+size_t sparse_small_pairs(const Table* t, size_t nnz) {
+    const int W = t->fb_c ? t->fb_geom().W : 32;
+    return nnz * (size_t)W;
+}
+
+int sparse_small_items_dev(vc_ctx* ctx, Table* t, const SmallRows& in, const std::function<void()>* overlap) {
+    using C = BN254G1;
+    using Fr = BN254Fr;
+    using Acc = C::Acc;
+    if (t->curve != VC_CURVE_BN254) return VC_E_INVALID;
+    const size_t batch = in.batch;
+    if (batch == 0) return VC_OK;
+    if (t->fb_c == 0) VK_TRY(fixed_base_precompute(ctx, t, 8));
+    const FbGeom fg = t->fb_geom();
+    const uint64_t W = (uint64_t)fg.W;
+    const uint64_t* rp = in.row_ptr;
+    if (rp[batch] * W >= (1ull << 32)) return VC_E_RANGE;
+    // chunks of NT pairs: a wave (7 dependent quad adds) while every row fits one (<= 2 non-zeros at
+    // W = 32: the extension c1 / c2 rows), else 256 threads (9 adds; rows of <= 8 non-zeros -- the
+    // extension rows [1, stem, c1, c2], an update's delta rows -- need no k_sparse_combine, whose
+    // one full add per level costs ~30 us, profiles/r05/verkle/)
+    uint64_t maxp = 0;
+    for (size_t g = 0; g < batch; g++) maxp = std::max<uint64_t>(maxp, (rp[g + 1] - rp[g]) * W);
+    const uint32_t NT = maxp <= 64 ? 64 : 256;
+    // chunk table (host, page-locked: one upload) and, when a row has several chunks, rc
+    size_t nch = 0;
+    bool multi = false;
+    for (size_t g = 0; g < batch; g++) {
+        const uint64_t np = (rp[g + 1] - rp[g]) * W;
+        const size_t k = np == 0 ? 1 : (size_t)((np + NT - 1) / NT);
+        multi |= k > 1;
+        nch += k;
+    }
+    const size_t ck_bytes = nch * sizeof(SmallChunk), rc_bytes = multi ? (batch + 1) * 4 : 0;
+    VK_TRY(ctx->pin_sparse_ck.ensure(ck_bytes + rc_bytes));
+    SmallChunk* hck = ctx->pin_sparse_ck.as<SmallChunk>();
+    uint32_t* hrc = reinterpret_cast<uint32_t*>(ctx->pin_sparse_ck.as<uint8_t>() + ck_bytes);
+    size_t b = 0;
+    for (size_t g = 0; g < batch; g++) {
+        const uint32_t np = (uint32_t)((rp[g + 1] - rp[g]) * W);
+        if (multi) hrc[g] = (uint32_t)b;
+        uint32_t p0 = 0;
+        do {
+            hck[b++] = SmallChunk{(uint32_t)rp[g], np, p0, 0};
+            p0 += NT;
+        } while (p0 < np);
+    }
+    if (multi) hrc[batch] = (uint32_t)b;
+    hipStream_t st = ctx->stream;
+    DevBuf d_ck(ctx), d_part(ctx), d_rows(ctx);
+    VK_TRY(d_ck.ensure(ck_bytes + rc_bytes));
+    VK_TRY(d_part.ensure(nch * sizeof(Acc)));
+    if (multi) VK_TRY(d_rows.ensure(batch * sizeof(Acc)));
+    VK_CHECK_HIP(hipMemcpyAsync(d_ck.p, hck, ck_bytes + rc_bytes, hipMemcpyHostToDevice, st));
+    using FA = FbE<C>;
+    const FA* tab = t->fb.as<FA>();
+    const uint8_t* tinf = t->inf.as<uint8_t>();
+    const SmallChunk* dck = d_ck.as<SmallChunk>();
+#define VK_SMALL_(MODE, NTV)                                                                                  \
+    VK_LAUNCH(ctx, "sparse_small", (k_fb_sparse_small<C, Fr, MODE, NTV>), nch, NTV, 0, tab, tinf, fg, dck, in.d_cols, \
+              in.d_vals, in.d_item, in.d_child, in.d_sidx, in.d_snap, d_part.as<Acc>())
+    if (NT == 64) {
+        if (in.mode == 0) VK_SMALL_(0, 64);
+        else if (in.mode == 1) VK_SMALL_(1, 64);
+        else VK_SMALL_(2, 64);
+    } else {
+        if (in.mode == 0) VK_SMALL_(0, 256);
+        else if (in.mode == 1) VK_SMALL_(1, 256);
+        else VK_SMALL_(2, 256);
+    }
+#undef VK_SMALL_
+    Acc* rows = d_part.as<Acc>();
+    if (multi) {
+        VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<C::Inl>), batch, 64, 0, d_part.as<Acc>(),
+                  reinterpret_cast<const uint32_t*>(d_ck.as<uint8_t>() + ck_bytes), d_rows.as<Acc>());
+        rows = d_rows.as<Acc>();
+    }
+    return normalize_rows_items(ctx, rows, batch, in.d_add_ids, in.d_add_xy, in.d_add_inf, in.d_dst, in.d_out_xy,
+                                in.d_out_inf, in.d_out_item, overlap);
 }
 
 // BN254 sparse commits with device inputs and outputs (the verkle tree's device-resident levels)

@@ -134,20 +134,24 @@ static bool verify_timing() {
 
 // width-w fixed-base commitments of Montgomery scalars (host) -> canonical affine (host)
 // overlap: host work run while the commit kernel runs (fb_commit_t)
+// cols (optional, latency path only -- fb_small_path): compacted rows, item i of commit g is base
+// cols[g width + i]
 static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
-                        uint8_t* out_inf, const std::function<void()>* overlap = nullptr) {
-    const size_t in_bytes = batch * width * 32, out_bytes = batch * 65;
+                        uint8_t* out_inf, const std::function<void()>* overlap = nullptr,
+                        const uint32_t* cols = nullptr) {
+    const size_t in_bytes = batch * width * 32, col_bytes = cols ? batch * width * 4 : 0, out_bytes = batch * 65;
     VK_TRY(ctx->ws[WS_MISC].ensure(out_bytes));
     uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
     uint8_t* dinf = dxy + batch * 64;
     // pinned staging both ways (the IPA rounds call this 8 times per proof: pageable copies went
     // through bounce buffers), points and flags read back in one copy; the scalars are uploaded by
     // msm_batch_run, or read in place by its latency path
-    VK_TRY(ctx->pin_io.ensure(std::max(in_bytes, out_bytes)));
+    VK_TRY(ctx->pin_io.ensure(std::max(in_bytes + col_bytes, out_bytes)));
     memcpy(ctx->pin_io.p, sc, in_bytes);
+    if (cols) memcpy(static_cast<uint8_t*>(ctx->pin_io.p) + in_bytes, cols, col_bytes);
     bool on_host = false;
     VK_TRY(msm_batch_run(ctx, t, width, nullptr, batch, 1, dxy, dinf, out_xy, out_inf, &on_host, &ctx->pin_io,
-                         overlap));
+                         overlap, cols != nullptr));
     if (on_host) return VC_OK;
     VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_io.p, dxy, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
@@ -275,34 +279,61 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
         s.w = transcript_digest(s.tr, "w");
         s.coeff.assign(N, fe_one<F>());
     });
-    const size_t W = N + 1;
+    // L (R) of a round has non-zeros only at the N / 2 bases i with i mod m >= m / 2 (< m / 2) and
+    // at q: on the latency path the rows are compacted to those N / 2 + 1 bases (half the threads
+    // and half the block partials the host adds per round); otherwise full width-(N + 1) rows
+    static const bool compact_env = !(getenv("VKZG_IPA_COMPACT") && atoi(getenv("VKZG_IPA_COMPACT")) == 0);
+    const bool compact = compact_env && fb_small_path(ctx, t, N / 2 + 1, 2 * B);
+    const size_t W = compact ? N / 2 + 1 : N + 1;
     std::vector<Fr> sc(2 * B * W);
+    std::vector<uint32_t> cols(compact ? 2 * B * W : 0);
     std::vector<uint64_t> oxy(2 * B * 8);
     std::vector<uint8_t> oinf(2 * B);
     double lap_fill = 0, lap_commit = 0, lap_fold = 0;
     for (size_t r = 0; r < K; r++) {
         const size_t m = N >> r, half = m / 2;
         const double c0 = verify_timing() ? verify_clock_us() : 0.0;
+        if (compact) {  // the same base lists for every proof of the batch
+            uint32_t* cL = cols.data();
+            uint32_t* cR = cols.data() + W;
+            size_t kl = 0, kr = 0;
+            for (size_t i = 0; i < N; i++) {
+                if (i % m >= half) cL[kl++] = (uint32_t)i;
+                else cR[kr++] = (uint32_t)i;
+            }
+            cL[kl] = cR[kr] = (uint32_t)N;
+            for (size_t p = 1; p < B; p++) memcpy(&cols[2 * p * W], cols.data(), 2 * W * 4);
+        }
         par_for([&](size_t p) {
             IpaState& s = st[p];
             Fr* sL = &sc[(2 * p) * W];
             Fr* sR = &sc[(2 * p + 1) * W];
-            for (size_t i = 0; i < N; i++) {
-                size_t j = i % m;
-                if (j >= half) {
-                    sL[i] = fe_mul<F>(s.a[j - half], s.coeff[i]);
-                    sR[i] = fe_zero<F>();
-                } else {
-                    sR[i] = fe_mul<F>(s.a[j + half], s.coeff[i]);
-                    sL[i] = fe_zero<F>();
+            if (compact) {
+                size_t kl = 0, kr = 0;
+                for (size_t i = 0; i < N; i++) {
+                    size_t j = i % m;
+                    if (j >= half) sL[kl++] = fe_mul<F>(s.a[j - half], s.coeff[i]);
+                    else sR[kr++] = fe_mul<F>(s.a[j + half], s.coeff[i]);
+                }
+            } else {
+                for (size_t i = 0; i < N; i++) {
+                    size_t j = i % m;
+                    if (j >= half) {
+                        sL[i] = fe_mul<F>(s.a[j - half], s.coeff[i]);
+                        sR[i] = fe_zero<F>();
+                    } else {
+                        sR[i] = fe_mul<F>(s.a[j + half], s.coeff[i]);
+                        sL[i] = fe_zero<F>();
+                    }
                 }
             }
             // q' * <a_L, b_R> = q * (w <a_L, b_R>)
-            sL[N] = fe_mul<F>(s.w, inner(&s.a[0], &s.b[half], half));
-            sR[N] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
+            sL[W - 1] = fe_mul<F>(s.w, inner(&s.a[0], &s.b[half], half));
+            sR[W - 1] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
         });
         const double c1 = verify_timing() ? verify_clock_us() : 0.0;
-        VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data()));
+        VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data(), nullptr,
+                            compact ? cols.data() : nullptr));
         const double c2 = verify_timing() ? verify_clock_us() : 0.0;
         par_for([&](size_t p) {
             IpaState& s = st[p];
@@ -822,23 +853,7 @@ __global__ void k_to_data_item(const fe<BN254Fq>* __restrict__ xy, const uint8_t
                                fe<F>* __restrict__ out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    fe<F> r = fe_zero<F>();
-    if (!inf[i]) {
-        fe<BN254Fq> x = xy[2 * i], y = xy[2 * i + 1];
-        fe<BN254Fq> ny = fe_sub<BN254Fq>(fe_zero<BN254Fq>(), y);
-        bool neg = false;  // y > p - y (canonical)
-        for (int k = 7; k >= 0; k--) {
-            if (y.v[k] != ny.v[k]) {
-                neg = y.v[k] > ny.v[k];
-                break;
-            }
-        }
-        for (int k = 0; k < 8; k++) r.v[k] = x.v[k];
-        if (neg) r.v[7] |= 0x80000000u;
-        // value < 2^256 < 6r: subtract r while >= r
-        for (int it = 0; it < 6; it++) r = fe_reduce_once<F>(r);
-    }
-    out[i] = r;
+    out[i] = to_data_item_canon(xy[2 * i], xy[2 * i + 1], inf[i] != 0);
 }
 
 }  // namespace vk

@@ -9,6 +9,7 @@
 #include <array>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -165,6 +166,18 @@ struct vc_verkle {
     std::vector<std::vector<int>> dirty_int;
     VerkleDev dev;
     bool host_valid = true;  // false: the device mirror holds newer results than cxy / cinf / item
+    // delta updates (verkle_commitment_dev): base[id] = the node's stored commitment is its last
+    // successful one, and every change of its slots since is in slog as (parent, slot, the child the
+    // slot held then: -1 = empty) -- logged at insert time for base parents only
+    struct SlotLog {
+        int parent, old;
+        uint8_t slot;
+    };
+    std::vector<uint8_t> base;
+    std::vector<SlotLog> slog;
+    void log_slot(int parent, uint8_t slot, int old) {
+        if (base[parent]) slog.push_back({parent, old, slot});
+    }
     int add(VNode&& n) {
         nodes.push_back(std::move(n));
         cxy.resize(cxy.size() + 8, 0);
@@ -172,6 +185,7 @@ struct vc_verkle {
         item.resize(item.size() + 4, 0);
         has_commit.push_back(0);
         queued.push_back(0);
+        base.push_back(0);
         return (int)nodes.size() - 1;
     }
     void mark(int id) {  // commitment cleared (node.rs:150-152 commitment = None)
@@ -192,13 +206,33 @@ struct vc_verkle {
         return c;
     }
     void clear_dirty() {  // after a commitment: every listed node is committed
-        for (int id : dirty_ext) has_commit[id] = 1, queued[id] = 0;
+        for (int id : dirty_ext) has_commit[id] = 1, queued[id] = 0, base[id] = 1;
         for (auto& lv : dirty_int)
-            for (int id : lv) has_commit[id] = 1, queued[id] = 0;
+            for (int id : lv) has_commit[id] = 1, queued[id] = 0, base[id] = 1;
         dirty_ext.clear();
         dirty_int.clear();
+        slog.clear();
+    }
+    // a failed commitment may have stored some dirty nodes' new results already: their stored
+    // commitments are no delta bases any more (the retry recommits them in full)
+    void drop_delta() {
+        for (int id : dirty_ext) base[id] = 0;
+        for (auto& lv : dirty_int)
+            for (int id : lv) base[id] = 0;
+        slog.clear();
     }
 };
+
+namespace {
+// drop_delta unless the commitment reached its end (ok = true)
+struct DeltaGuard {
+    vc_verkle* t;
+    bool ok = false;
+    ~DeltaGuard() {
+        if (!ok) t->drop_delta();
+    }
+};
+}  // namespace
 
 namespace {
 
@@ -290,6 +324,8 @@ int vc_verkle_insert(vc_verkle* t, const uint8_t* key, const uint8_t* value) {
         depth++;
     }
     for (int p : path) t->mark(p);  // clear the commitments on the path
+    // the path's slots (their children's items change) -- internal path[i] sits at depth i
+    for (size_t i = 0; i + 1 < path.size(); i++) t->log_slot(path[i], stem[i], path[i + 1]);
     VNode* n = &t->nodes[cur];
     if (action == INTO_EXT) {
         std::array<uint8_t, 32> v;
@@ -298,6 +334,7 @@ int vc_verkle_insert(vc_verkle* t, const uint8_t* key, const uint8_t* value) {
         return VC_OK;
     }
     if (action == NEW_EXT) {
+        t->log_slot(cur, (uint8_t)parent_k, -1);
         int e = new_ext(t, stem, unit, value);
         t->nodes[cur].children[(uint8_t)parent_k] = e;
         return VC_OK;
@@ -305,6 +342,7 @@ int vc_verkle_insert(vc_verkle* t, const uint8_t* key, const uint8_t* value) {
     // SPLIT: new internal keyed by the first differing unit d (which may skip levels, as in
     // the reference: node.rs:176-185)
     const int old = t->nodes[cur].children[(uint8_t)parent_k];
+    t->log_slot(cur, (uint8_t)parent_k, old);
     const std::array<uint8_t, 32> old_stem = t->nodes[old].stem;
     const int d = next_diff_depth(old_stem.data(), stem, depth, N);
     int e = new_ext(t, stem, unit, value);
@@ -675,6 +713,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
         vc_verkle* t;
         ~DropMirror() { t->dev.release(); }
     } drop{t};
+    DeltaGuard delta_guard{t};
     const int N = t->N;
     static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
     auto tic = std::chrono::steady_clock::now();
@@ -918,6 +957,7 @@ int verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, ui
     memcpy(out_xy, &t->cxy[0], 64);
     *out_inf = t->cinf[0];
     t->clear_dirty();
+    delta_guard.ok = true;
     return VC_OK;
 }
 
@@ -936,6 +976,20 @@ __global__ void k_vk_gather(const uint64_t* __restrict__ item, const uint32_t* _
     o[1] = s[1];
     o[2] = s[2];
     o[3] = s[3];
+}
+// a level's row values: item(child) - (sidx < 0 ? 0 : snap[sidx]) mod r (canonical Fr words) --
+// a full row's entries have no old value, a delta row's the child's item at the last commitment
+__global__ void k_vk_delta(const uint64_t* __restrict__ item, const uint32_t* __restrict__ child,
+                           const int32_t* __restrict__ sidx, const uint64_t* __restrict__ snap, size_t n,
+                           uint64_t* __restrict__ out) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    fe<BN254Fr> a, b = fe_zero<BN254Fr>();
+    memcpy(a.v, item + 4 * (size_t)child[j], 32);
+    const int32_t k = sidx[j];
+    if (k >= 0) memcpy(b.v, snap + 4 * (size_t)k, 32);
+    const fe<BN254Fr> d = fe_sub<BN254Fr>(a, b);  // (canonical in, canonical out)
+    memcpy(out + 4 * j, d.v, 32);
 }
 // 16-byte leaf halves -> 4-word scalars
 __global__ void k_vk_widen16(const uint64_t* __restrict__ in, size_t n, uint64_t* __restrict__ out) {
@@ -1011,6 +1065,7 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         fprintf(stderr, "[verkle-dev] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tic).count());
         tic = now;
     };
+    DeltaGuard delta_guard{t};
     VK_TRY(mirror_prepare(ctx, t));
     VerkleDev& D = t->dev;
     uint64_t* m_item = static_cast<uint64_t*>(D.item);
@@ -1022,15 +1077,151 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     auto grid = [](size_t n) { return (unsigned)((n + 255) / 256); };
     lap("mirror");
     // results of one level's B rows (device) -> the mirror at the nodes' ids
-    auto scatter = [&](const std::vector<int>& ids, const void* d_xy, const uint8_t* d_inf, const void* d_it) -> int {
-        const size_t B = ids.size();
-        DevBuf d_ids(ctx);
-        VK_TRY(d_ids.ensure(B * 4));
-        VK_CHECK_HIP(hipMemcpyAsync(d_ids.p, ids.data(), B * 4, hipMemcpyHostToDevice, st));
-        VK_LAUNCH(ctx, "verkle_scatter", k_vk_scatter, grid(B), 256, 0, d_ids.as<uint32_t>(), B,
-                  static_cast<const uint64_t*>(d_xy), d_inf, static_cast<const uint64_t*>(d_it), m_cxy, m_inf, m_item);
+    auto scatter = [&](const uint32_t* d_ids, size_t B, const void* d_xy, const uint8_t* d_inf, const void* d_it) -> int {
+        VK_LAUNCH(ctx, "verkle_scatter", k_vk_scatter, grid(B), 256, 0, d_ids, B, static_cast<const uint64_t*>(d_xy),
+                  d_inf, static_cast<const uint64_t*>(d_it), m_cxy, m_inf, m_item);
         return VC_OK;
     };
+    // levels of at most this many (non-zero, window) pairs take the sparse commits' latency path
+    // (a wave per 64 pairs, msm.hip k_fb_sparse_small) instead of the sort-based one: an update's
+    // levels; VKZG_SPARSE_SMALL_MAX (pairs, read per call; 0 = never) is the A/B knob
+    const char* small_env = getenv("VKZG_SPARSE_SMALL_MAX");
+    const size_t small_max = small_env ? (size_t)atoll(small_env) : (size_t)1 << 18;
+    auto small_ok = [&](size_t nnz) { return sparse_small_pairs(tab, nnz) <= small_max; };
+    // delta rows: an updated internal node whose last commitment is in the mirror (base) is
+    // C_old + sum over its changed slots of (item(child now) - item(child then)) L_slot, instead of
+    // its full row (~160 children per level-1 node of a 65,536-key tree, ~2 of them changed by a
+    // 1 % update). The changed slots are the insert-time slot log's (first entry per slot: the child
+    // at the last commitment); their old items are snapshotted here, before this call's scatters
+    // overwrite them. VKZG_VERKLE_DELTA=0 (read per call, A/B probe) recommits every row in full.
+    const char* delta_env = getenv("VKZG_VERKLE_DELTA");
+    const bool use_delta = !(delta_env && atoi(delta_env) == 0);
+    struct DPlan {
+        uint64_t seen[4];
+        std::vector<std::pair<uint8_t, int32_t>> e;  // (slot, snapshot index; -1: the slot was empty)
+    };
+    std::unordered_map<int, size_t> plan_of;
+    std::vector<DPlan> plans;
+    std::vector<uint32_t> snap_ids;
+    std::unordered_map<int, int32_t> snap_of;
+    if (use_delta) {
+        for (const auto& L : t->slog) {
+            auto pi = plan_of.try_emplace(L.parent, plans.size());
+            if (pi.second) plans.push_back(DPlan{{0, 0, 0, 0}, {}});
+            DPlan& P = plans[pi.first->second];
+            if ((P.seen[L.slot >> 6] >> (L.slot & 63)) & 1) continue;
+            P.seen[L.slot >> 6] |= 1ull << (L.slot & 63);
+            int32_t k = -1;
+            if (L.old >= 0) {
+                auto si = snap_of.try_emplace(L.old, (int32_t)snap_ids.size());
+                if (si.second) snap_ids.push_back((uint32_t)L.old);
+                k = si.first->second;
+            }
+            P.e.push_back({L.slot, k});
+        }
+    }
+    DevBuf d_snap(ctx), d_snap_ids(ctx);
+    if (!snap_ids.empty()) {
+        const size_t S = snap_ids.size();
+        VK_TRY(d_snap_ids.ensure(S * 4));
+        VK_TRY(d_snap.ensure(S * 32));
+        VK_CHECK_HIP(hipMemcpyAsync(d_snap_ids.p, snap_ids.data(), S * 4, hipMemcpyHostToDevice, st));
+        VK_LAUNCH(ctx, "verkle_gather", k_vk_gather, grid(S), 256, 0, m_item, d_snap_ids.as<uint32_t>(), S,
+                  d_snap.as<uint64_t>());
+    }
+    lap("delta plan");
+    // one internal level's lists (column, child id[, snapshot index] per non-zero, node ids[, the
+    // delta rows' add ids]) in page-locked memory for one upload: ints only, the values are the
+    // children's items in the mirror (minus the snapshot for a delta row)
+    struct LevelLists {
+        int level = -1, status = VC_OK;
+        size_t B = 0, nnz = 0, o_child = 0, o_ids = 0, o_sidx = 0, o_add = 0, o_end = 0;
+        bool any_delta = false, dense = false;
+        uvec<uint64_t> ptr;
+        uint8_t* pin = nullptr;
+    };
+    const char* dense_env = getenv("VKZG_VERKLE_DENSE");
+    const int dense_mode = dense_env ? atoi(dense_env) : -1;
+    auto build_level = [&](int level, LevelLists& L, PinBuf& pinbuf) {
+        const std::vector<int>& lv = t->dirty_int[level];
+        const size_t B = lv.size();
+        L.level = level;
+        L.B = B;
+        std::vector<const DPlan*> rplan(B, nullptr);
+        bool any_delta = false;
+        // the fixed-base latency path with host results for <= 64 full rows (the root: 0.44 -> 0.11
+        // ms); VKZG_VERKLE_DENSE=0 / 1 (read per call, as the host path) forces sparse /
+        // dense levels. A level of <= 64 rows commits full rows (delta rows would not shorten the
+        // latency path's dependent adds).
+        L.dense = dense_mode == 1 || (dense_mode != 0 && B <= 64);
+        if (!plans.empty() && !L.dense)
+            for (size_t b = 0; b < B; b++) {
+                if (!t->base[lv[b]]) continue;
+                auto it = plan_of.find(lv[b]);
+                if (it == plan_of.end()) continue;
+                rplan[b] = &plans[it->second];
+                any_delta = true;
+            }
+        L.any_delta = any_delta;
+        L.ptr.resize(B + 1);
+        uvec<uint64_t>& ptr = L.ptr;
+        ptr[0] = 0;
+        for (size_t b = 0; b < B; b++)
+            ptr[b + 1] = ptr[b] + (rplan[b] ? rplan[b]->e.size() : t->nodes[lv[b]].children.v.size());
+        const size_t nnz = ptr[B], nz1 = std::max<size_t>(nnz, 1);
+        L.nnz = nnz;
+        // layout: cols | child | ids | (delta) sidx | add_ids
+        L.o_child = nz1 * 4;
+        L.o_ids = L.o_child + nz1 * 4;
+        L.o_sidx = L.o_ids + B * 4;
+        L.o_add = L.o_sidx + (any_delta ? nz1 * 4 : 0);
+        L.o_end = L.o_add + (any_delta ? B * 4 : 0);
+        L.status = pinbuf.ensure(L.o_end);
+        if (L.status != VC_OK) return;
+        uint8_t* pin = pinbuf.as<uint8_t>();
+        L.pin = pin;
+        uint32_t* cols = reinterpret_cast<uint32_t*>(pin);
+        uint32_t* child = reinterpret_cast<uint32_t*>(pin + L.o_child);
+        uint32_t* ids = reinterpret_cast<uint32_t*>(pin + L.o_ids);
+        int32_t* sidx = reinterpret_cast<int32_t*>(pin + L.o_sidx);
+        uint32_t* add_ids = reinterpret_cast<uint32_t*>(pin + L.o_add);
+        pool_for(0, B, 256, [&](size_t b) {
+            size_t j = ptr[b];
+            const VNode& n = t->nodes[lv[b]];
+            ids[b] = (uint32_t)lv[b];
+            if (rplan[b]) {
+                for (auto& e : rplan[b]->e) {
+                    cols[j] = e.first;
+                    child[j] = (uint32_t)n.children.find(e.first)->second;
+                    sidx[j] = e.second;
+                    j++;
+                }
+            } else {
+                for (auto& kv : n.children.v) {
+                    cols[j] = kv.first;
+                    child[j] = (uint32_t)kv.second;
+                    if (any_delta) sidx[j] = -1;
+                    j++;
+                }
+            }
+            if (any_delta) add_ids[b] = rplan[b] ? (uint32_t)lv[b] : 0xffffffffu;
+        });
+    };
+    // internal nodes, deepest level first (width 256: the reference's hard-coded HACK). A level's
+    // lists depend on the tree alone, so the next level's are built (into the other page-locked
+    // buffer) while the current level's kernels run -- in the wait of its normalisation
+    std::vector<int> order;
+    for (int level = (int)t->dirty_int.size() - 1; level >= 0; level--)
+        if (!t->dirty_int[level].empty()) order.push_back(level);
+    LevelLists lists[2];
+    size_t next_built = 0;  // levels of `order` whose lists are built
+    auto build_next = [&]() {
+        if (next_built < order.size()) {
+            build_level(order[next_built], lists[next_built & 1], ctx->pin_verkle_lv[next_built & 1]);
+            next_built++;
+        }
+    };
+    const std::function<void()> build_next_fn = build_next;
     // extension nodes: c1 / c2 rows (host: the leaves), then the width-4 rows on the device
     const std::vector<int>& exts = t->dirty_ext;
     const size_t E = exts.size();
@@ -1050,9 +1241,11 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             maxlen = std::max(maxlen, parts[k].maxlen);
         }
         const size_t nnz = noff[T];
-        // page-locked layout: row_ptr (2E + 1 u64) | stem items (E x 4 u64) | values (nnz x 2 u64) | cols
-        const size_t o_stem = (2 * E + 1) * 8, o_vals = o_stem + E * 32, o_cols = o_vals + nnz * 16;
-        VK_TRY(ctx->pin_verkle.ensure(o_cols + nnz * 4));
+        // page-locked layout: row_ptr (2E + 1 u64) | stem items (E x 4 u64) | values (nnz x 2 u64) |
+        // node ids (E u32) | cols (nnz u32); everything after row_ptr goes up in one copy
+        const size_t o_stem = (2 * E + 1) * 8, o_vals = o_stem + E * 32, o_ids = o_vals + nnz * 16,
+                     o_cols = o_ids + E * 4, o_end = o_cols + nnz * 4;
+        VK_TRY(ctx->pin_verkle.ensure(o_end));
         uint8_t* pin = ctx->pin_verkle.as<uint8_t>();
         uint64_t* rp = reinterpret_cast<uint64_t*>(pin);
         rp[0] = 0;
@@ -1068,96 +1261,109 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         };
         if (T == 1) merge(0);
         else pool.run(merge);
+        uint32_t* ids = reinterpret_cast<uint32_t*>(pin + o_ids);
+        for (size_t e = 0; e < E; e++) ids[e] = (uint32_t)exts[e];
         lap("ext rows (host)");
-        DevBuf d_cols(ctx), d_v16(ctx), d_vals(ctx), d_stem(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
-        VK_TRY(d_cols.ensure(std::max<size_t>(nnz, 1) * 4));
-        VK_TRY(d_v16.ensure(std::max<size_t>(nnz, 1) * 16));
-        VK_TRY(d_vals.ensure(std::max<size_t>(nnz, 1) * 32));
-        VK_TRY(d_stem.ensure(E * 32));
+        DevBuf d_up(ctx), d_vals(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
+        VK_TRY(d_up.ensure(o_end - o_stem));
         VK_TRY(d_xy.ensure(2 * E * 64));
         VK_TRY(d_inf.ensure(2 * E));
         VK_TRY(d_it.ensure(2 * E * 32));
-        if (nnz) {
-            VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, pin + o_cols, nnz * 4, hipMemcpyHostToDevice, st));
-            VK_CHECK_HIP(hipMemcpyAsync(d_v16.p, pin + o_vals, nnz * 16, hipMemcpyHostToDevice, st));
-            VK_LAUNCH(ctx, "verkle_widen", k_vk_widen16, grid(nnz), 256, 0, d_v16.as<uint64_t>(), nnz,
-                      d_vals.as<uint64_t>());
+        VK_CHECK_HIP(hipMemcpyAsync(d_up.p, pin + o_stem, o_end - o_stem, hipMemcpyHostToDevice, st));
+        const uint64_t* d_stem = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>());
+        const uint64_t* d_v16 = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>() + (o_vals - o_stem));
+        const uint32_t* d_ids = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (o_ids - o_stem));
+        const uint32_t* d_cols = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (o_cols - o_stem));
+        if (small_ok(nnz)) {  // the 16-byte values read as they are
+            SmallRows in;
+            in.batch = 2 * E;
+            in.row_ptr = rp;
+            in.mode = 1;
+            in.d_cols = d_cols;
+            in.d_vals = d_v16;
+            in.d_out_xy = d_xy.as<uint64_t>();
+            in.d_out_inf = d_inf.as<uint8_t>();
+            in.d_out_item = d_it.as<uint64_t>();
+            VK_TRY(sparse_small_items_dev(ctx, tab, in));
+        } else {
+            VK_TRY(d_vals.ensure(std::max<size_t>(nnz, 1) * 32));
+            if (nnz)
+                VK_LAUNCH(ctx, "verkle_widen", k_vk_widen16, grid(nnz), 256, 0, d_v16, nnz, d_vals.as<uint64_t>());
+            // rows of <= 4 non-zeros (random keys: one leaf per extension) are the sparse commit's
+            // chunks as they are (an empty row is an empty chunk: the identity), no chunk lists
+            VK_TRY(sparse_commit_items_dev(ctx, tab, 2 * E, rp, maxlen <= 4, d_cols, d_vals.p, d_xy.p,
+                                           d_inf.as<uint8_t>(), d_it.p));
         }
-        VK_CHECK_HIP(hipMemcpyAsync(d_stem.p, pin + o_stem, E * 32, hipMemcpyHostToDevice, st));
-        // rows of <= 4 non-zeros (random keys: one leaf per extension) are the sparse commit's chunks
-        // as they are (an empty row is an empty chunk: the identity), no chunk lists
-        VK_TRY(sparse_commit_items_dev(ctx, tab, 2 * E, rp, maxlen <= 4, d_cols.as<uint32_t>(), d_vals.p, d_xy.p,
-                                       d_inf.as<uint8_t>(), d_it.p));
         lap("ext c1 / c2 commits");
-        DevBuf d_c4(ctx), d_v4(ctx), d_xy4(ctx), d_inf4(ctx), d_it4(ctx);
+        DevBuf d_c4(ctx), d_v4(ctx);
         VK_TRY(d_c4.ensure(4 * E * 4));
         VK_TRY(d_v4.ensure(4 * E * 32));
-        VK_TRY(d_xy4.ensure(E * 64));
-        VK_TRY(d_inf4.ensure(E));
-        VK_TRY(d_it4.ensure(E * 32));
-        VK_LAUNCH(ctx, "verkle_ext_rows4", k_vk_ext_rows4, grid(4 * E), 256, 0, d_stem.as<uint64_t>(),
-                  d_it.as<uint64_t>(), E, d_c4.as<uint32_t>(), d_v4.as<uint64_t>());
+        VK_LAUNCH(ctx, "verkle_ext_rows4", k_vk_ext_rows4, grid(4 * E), 256, 0, d_stem, d_it.as<uint64_t>(), E,
+                  d_c4.as<uint32_t>(), d_v4.as<uint64_t>());
         uvec<uint64_t> rp4(E + 1);
         for (size_t k = 0; k <= E; k++) rp4[k] = 4 * k;
-        VK_TRY(sparse_commit_items_dev(ctx, tab, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, d_xy4.p,
-                                       d_inf4.as<uint8_t>(), d_it4.p));
-        VK_TRY(scatter(exts, d_xy4.p, d_inf4.as<uint8_t>(), d_it4.p));
+        if (small_ok(4 * E)) {  // results straight into the mirror
+            SmallRows in;
+            in.batch = E;
+            in.row_ptr = rp4.data();
+            in.mode = 0;
+            in.d_cols = d_c4.as<uint32_t>();
+            in.d_vals = d_v4.as<uint64_t>();
+            in.d_dst = d_ids;
+            in.d_out_xy = m_cxy;
+            in.d_out_inf = m_inf;
+            in.d_out_item = m_item;
+            VK_TRY(sparse_small_items_dev(ctx, tab, in, order.empty() ? nullptr : &build_next_fn));
+        } else {
+            DevBuf d_xy4(ctx), d_inf4(ctx), d_it4(ctx);
+            VK_TRY(d_xy4.ensure(E * 64));
+            VK_TRY(d_inf4.ensure(E));
+            VK_TRY(d_it4.ensure(E * 32));
+            VK_TRY(sparse_commit_items_dev(ctx, tab, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, d_xy4.p,
+                                           d_inf4.as<uint8_t>(), d_it4.p));
+            VK_TRY(scatter(d_ids, E, d_xy4.p, d_inf4.as<uint8_t>(), d_it4.p));
+        }
         lap("ext commits");
     }
-    // internal nodes, deepest level first (width 256: the reference's hard-coded HACK)
-    for (int level = (int)t->dirty_int.size() - 1; level >= 0; level--) {
-        const std::vector<int>& lv = t->dirty_int[level];
-        const size_t B = lv.size();
-        if (!B) continue;
-        // (column, child id) lists: ints only, the values are the children's items in the mirror
-        uvec<uint64_t> ptr(B + 1);
-        ptr[0] = 0;
-        for (size_t b = 0; b < B; b++) ptr[b + 1] = ptr[b] + t->nodes[lv[b]].children.v.size();
-        const size_t nnz = ptr[B];
-        uvec<uint32_t> cols(std::max<size_t>(nnz, 1)), child(std::max<size_t>(nnz, 1)), row;
-        pool_for(0, B, 256, [&](size_t b) {
-            size_t j = ptr[b];
-            for (auto& kv : t->nodes[lv[b]].children.v) {
-                cols[j] = kv.first;
-                child[j] = (uint32_t)kv.second;
-                j++;
-            }
-        });
-        DevBuf d_cols(ctx), d_child(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
-        VK_TRY(d_cols.ensure(std::max<size_t>(nnz, 1) * 4));
-        VK_TRY(d_child.ensure(std::max<size_t>(nnz, 1) * 4));
-        VK_TRY(d_xy.ensure(B * 64));
-        VK_TRY(d_inf.ensure(B));
-        VK_TRY(d_it.ensure(B * 32));
-        if (nnz) {
-            VK_CHECK_HIP(hipMemcpyAsync(d_cols.p, cols.data(), nnz * 4, hipMemcpyHostToDevice, st));
-            VK_CHECK_HIP(hipMemcpyAsync(d_child.p, child.data(), nnz * 4, hipMemcpyHostToDevice, st));
-        }
-        // the fixed-base latency path for <= 64 rows (the root: 0.44 -> 0.11 ms);
-        // VKZG_VERKLE_DENSE=0 / 1 (read per call, as the host path) forces sparse / dense levels
-        const char* dense_env = getenv("VKZG_VERKLE_DENSE");
-        const int dense_mode = dense_env ? atoi(dense_env) : -1;
-        const bool dense = dense_mode == 1 || (dense_mode != 0 && B <= 64);
-        if (dense) {
+    for (size_t oi = 0; oi < order.size(); oi++) {
+        if (next_built <= oi) build_next();
+        LevelLists& L = lists[oi & 1];
+        if (L.status != VC_OK) return L.status;
+        const size_t B = L.B, nnz = L.nnz, nz1 = std::max<size_t>(nnz, 1);
+        const uvec<uint64_t>& ptr = L.ptr;
+        DevBuf d_up(ctx);
+        VK_TRY(d_up.ensure(L.o_end));
+        VK_CHECK_HIP(hipMemcpyAsync(d_up.p, L.pin, L.o_end, hipMemcpyHostToDevice, st));
+        const uint32_t* d_cols = d_up.as<uint32_t>();
+        const uint32_t* d_child = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + L.o_child);
+        const uint32_t* d_ids = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + L.o_ids);
+        const int32_t* d_sidx = L.any_delta ? reinterpret_cast<const int32_t*>(d_up.as<uint8_t>() + L.o_sidx) : nullptr;
+        const uint32_t* d_add = L.any_delta ? reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + L.o_add) : nullptr;
+        // the next level's lists go into the other buffer while this level runs
+        const std::function<void()>* ov = next_built < order.size() ? &build_next_fn : nullptr;
+        if (L.dense) {
             // dense rows gathered on the device, committed on the latency path (host results), the
             // <= 64 items on the host, results uploaded into the mirror
-            row.resize(std::max<size_t>(nnz, 1));
+            uvec<uint32_t> row(nz1);
             for (size_t b = 0; b < B; b++)
                 for (uint64_t j = ptr[b]; j < ptr[b + 1]; j++) row[j] = (uint32_t)b;
-            DevBuf d_row(ctx), d_dense(ctx);
-            VK_TRY(d_row.ensure(std::max<size_t>(nnz, 1) * 4));
+            DevBuf d_row(ctx), d_dense(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
+            VK_TRY(d_row.ensure(nz1 * 4));
             VK_TRY(d_dense.ensure(B * 256 * 32));
+            VK_TRY(d_xy.ensure(B * 64));
+            VK_TRY(d_inf.ensure(B));
+            VK_TRY(d_it.ensure(B * 32));
             VK_CHECK_HIP(hipMemsetAsync(d_dense.p, 0, B * 256 * 32, st));
             if (nnz) {
                 VK_CHECK_HIP(hipMemcpyAsync(d_row.p, row.data(), nnz * 4, hipMemcpyHostToDevice, st));
-                VK_LAUNCH(ctx, "verkle_dense", k_vk_dense, grid(nnz), 256, 0, d_row.as<uint32_t>(),
-                          d_cols.as<uint32_t>(), d_child.as<uint32_t>(), nnz, m_item, 256u, d_dense.as<uint64_t>());
+                VK_LAUNCH(ctx, "verkle_dense", k_vk_dense, grid(nnz), 256, 0, d_row.as<uint32_t>(), d_cols, d_child,
+                          nnz, m_item, 256u, d_dense.as<uint64_t>());
             }
             std::vector<uint64_t> hxy(B * 8), hit(B * 4);
             std::vector<uint8_t> hinf(B);
             bool on_host = false;
             VK_TRY(msm_batch_run(ctx, tab, 256, d_dense.p, B, 0, d_xy.p, d_inf.as<uint8_t>(), hxy.data(), hinf.data(),
-                                 &on_host));
+                                 &on_host, nullptr, ov));
             if (!on_host) {
                 VK_CHECK_HIP(hipMemcpyAsync(hxy.data(), d_xy.p, B * 64, hipMemcpyDeviceToHost, st));
                 VK_CHECK_HIP(hipMemcpyAsync(hinf.data(), d_inf.p, B, hipMemcpyDeviceToHost, st));
@@ -1167,20 +1373,49 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             VK_CHECK_HIP(hipMemcpyAsync(d_xy.p, hxy.data(), B * 64, hipMemcpyHostToDevice, st));
             VK_CHECK_HIP(hipMemcpyAsync(d_inf.p, hinf.data(), B, hipMemcpyHostToDevice, st));
             VK_CHECK_HIP(hipMemcpyAsync(d_it.p, hit.data(), B * 32, hipMemcpyHostToDevice, st));
-            VK_TRY(scatter(lv, d_xy.p, d_inf.as<uint8_t>(), d_it.p));
+            VK_TRY(scatter(d_ids, B, d_xy.p, d_inf.as<uint8_t>(), d_it.p));
             VK_CHECK_HIP(hipStreamSynchronize(st));  // the host staging dies here
             lap("internal level (dense)");
             continue;
         }
-        DevBuf d_vals(ctx);
-        VK_TRY(d_vals.ensure(std::max<size_t>(nnz, 1) * 32));
-        if (nnz)
-            VK_LAUNCH(ctx, "verkle_gather", k_vk_gather, grid(nnz), 256, 0, m_item, d_child.as<uint32_t>(), nnz,
-                      d_vals.as<uint64_t>());
-        VK_TRY(sparse_commit_items_dev(ctx, tab, B, ptr.data(), false, d_cols.as<uint32_t>(), d_vals.p, d_xy.p,
-                                       d_inf.as<uint8_t>(), d_it.p));
-        VK_TRY(scatter(lv, d_xy.p, d_inf.as<uint8_t>(), d_it.p));
-        lap("internal level (sparse)");
+        if (small_ok(nnz)) {  // children's items gathered in the kernel; results into the mirror
+            SmallRows in;
+            in.batch = B;
+            in.row_ptr = ptr.data();
+            in.mode = 2;
+            in.d_cols = d_cols;
+            in.d_item = m_item;
+            in.d_child = d_child;
+            in.d_sidx = d_sidx;
+            in.d_snap = d_snap.as<uint64_t>();
+            in.d_add_ids = d_add;
+            in.d_add_xy = m_cxy;
+            in.d_add_inf = m_inf;
+            in.d_dst = d_ids;
+            in.d_out_xy = m_cxy;
+            in.d_out_inf = m_inf;
+            in.d_out_item = m_item;
+            VK_TRY(sparse_small_items_dev(ctx, tab, in, ov));
+            lap(L.any_delta ? "internal level (small, delta rows)" : "internal level (small)");
+            continue;
+        }
+        DevBuf d_vals(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
+        VK_TRY(d_vals.ensure(nz1 * 32));
+        VK_TRY(d_xy.ensure(B * 64));
+        VK_TRY(d_inf.ensure(B));
+        VK_TRY(d_it.ensure(B * 32));
+        if (L.any_delta) {
+            if (nnz)
+                VK_LAUNCH(ctx, "verkle_delta", k_vk_delta, grid(nnz), 256, 0, m_item, d_child, d_sidx,
+                          d_snap.as<uint64_t>(), nnz, d_vals.as<uint64_t>());
+        } else if (nnz) {
+            VK_LAUNCH(ctx, "verkle_gather", k_vk_gather, grid(nnz), 256, 0, m_item, d_child, nnz, d_vals.as<uint64_t>());
+        }
+        if (ov) (*ov)();  // (the sort-based path has no hook: build the next lists once its kernels are queued)
+        VK_TRY(sparse_commit_items_dev(ctx, tab, B, ptr.data(), false, d_cols, d_vals.p, d_xy.p, d_inf.as<uint8_t>(),
+                                       d_it.p, d_add, m_cxy, m_inf));
+        VK_TRY(scatter(d_ids, B, d_xy.p, d_inf.as<uint8_t>(), d_it.p));
+        lap(L.any_delta ? "internal level (sparse, delta rows)" : "internal level (sparse)");
     }
     // the root's commitment from the mirror (the rest stays there: host_valid = false)
     uint64_t rxy[8];
@@ -1192,6 +1427,7 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     *out_inf = rinf;
     t->clear_dirty();
     t->host_valid = false;
+    delta_guard.ok = true;
     lap("root");
     return VC_OK;
 }
