@@ -11,10 +11,19 @@
  * into one batched width-N commit (c1, c2), one batched to_data_item and one batched
  * width-4 commit; then every dirty internal node of one depth goes into one batched
  * width-256 commit, deepest level first -- instead of the reference's one recursive commit
- * per node. Rows are sparse (vc_msm_batch_sparse): an internal node has a few non-zero
- * children of 256, so only non-zeros are expanded into table points. The commitment scheme
- * is whatever `table` holds: the KZG Lagrange SRS (vc_kzg_setup) or an IPA CRS
- * (vc_bases_upload), BN254 G1.
+ * per node. Rows are sparse: an internal node has a few non-zero children of 256, so only
+ * non-zeros are expanded into table points. The commitment scheme is whatever `table` holds:
+ * the KZG Lagrange SRS (vc_kzg_setup) or an IPA CRS (vc_bases_upload), BN254 G1.
+ *
+ * Device residency (vc_verkle_commitment, one context): every node's commitment, identity flag
+ * and to_data_item live in a device mirror between calls (indexed by node id), so a level's
+ * rows read their children's items there and nothing returns to the host but the root; the
+ * host sends only the extension leaf values and each level's (column, child id) lists. An
+ * updated internal node whose last commitment is in the mirror is recommitted as a delta row,
+ * C_old + sum over the slots changed since of (item(new child) - item(old child)) L_slot (the
+ * slots are logged at insert time) -- the same group element as its full row. A call that
+ * fails leaves every dirty node to be recommitted in full by the next one. VKZG_VERKLE_DEV=0
+ * (read per call) takes the host-built path the sharded / group commitments use.
  *
  * Reference quirks kept: the extension commit width is the key length
  * N, not 256; the stem keeps the key's last unit; internal nodes commit at width 256;

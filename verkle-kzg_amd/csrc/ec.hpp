@@ -290,7 +290,7 @@ using Bandersnatch = TECurve<BLS381Fr, BandD>;
 // to_data_item (reference lib.rs:56-67) of a canonical affine BN254 G1 point: its compressed
 // encoding (x, the top bit set when y > p - y) read as a little-endian integer mod r -- canonical
 // Fr words; the identity maps to 0
-VK_HD inline fe<BN254Fr> to_data_item_canon(const fe<BN254Fq>& x, const fe<BN254Fq>& y, bool inf) {
+VK_HD fe<BN254Fr> to_data_item_canon(const fe<BN254Fq>& x, const fe<BN254Fq>& y, bool inf) {
     fe<BN254Fr> r = fe_zero<BN254Fr>();
     if (inf) return r;
     const fe<BN254Fq> ny = fe_sub<BN254Fq>(fe_zero<BN254Fq>(), y);

@@ -391,6 +391,7 @@ struct FbEntryLimbs {
 template <class C>
 using FbE = FbEntryLimbs<C>;
 
+#ifdef __HIPCC__
 // xor butterfly over the wave on the radix-29 accumulators (the add the tails run too). The
 // shuffle moves sizeof(Acc) / 4 words (shfl_xor_pod): SW29::Acc is 4 L limbs of 29 bits plus the
 // `inf` flag -- 37 words at BN254 (L = 9), 57 at BLS12-381 -- not the 4 N words of the ec.hpp
@@ -451,5 +452,7 @@ __device__ __forceinline__ void fb_block_sum_store(typename Fast29<C>::type::Acc
         }
     }
 }
+
+#endif  // __HIPCC__
 
 }  // namespace vk
