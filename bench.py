@@ -42,7 +42,7 @@ CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
 # (scripts/bench_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
-PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r04", "r03", "r02", "r01"))
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r05", "r04", "r03", "r02", "r01"))
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r04", "pmc_summary.json"))
 # the headline's accumulate instantiation in the PMC summary: the shared-window copies in the pair
 # layout (AffP, the default), else the (x, y, -y) records (AffN), else the packed tables
@@ -1195,6 +1195,7 @@ def main():
             traffic = ke.get("by_class", {}).get("1", ke).get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
 
+    prov = provenance()
     out = {
         "metric": METRIC,
         "value": a.steps / dt,
@@ -1241,7 +1242,9 @@ def main():
         "accumulate_clock_mhz": acc_mhz or None,
         "accumulate_clock_source": (f"s_memtime / s_memrealtime stamps around one lane's loop, {acc_clk_n} "
                                     "timed launches (vc_ctx_accumulate_clock)") if acc_clk_n else None,
-        "provenance": provenance(),
+        "provenance": prov,
+        "pmc_libvkzg_sha256": (pmc or {}).get("libvkzg_sha256"),
+        "pmc_same_library": bool(pmc) and (pmc or {}).get("libvkzg_sha256") == prov.get("libvkzg_sha256"),
         "result_inf": int(res[1]),
         "result_check": check,
         "variable_base": variable,

@@ -92,7 +92,8 @@ def main(d, out):
     except (OSError, IndexError, KeyError, ValueError):
         pass
     with open(out, "w") as f:
-        json.dump({"config": config, "bench_under_rocprof": bench, "note": "avg_ns from the kernel-trace pass; FETCH/WRITE from separate --pmc passes of the "
+        lib_sha = ((bench or {}).get("provenance") or {}).get("libvkzg_sha256")
+        json.dump({"config": config, "libvkzg_sha256": lib_sha, "bench_under_rocprof": bench, "note": "avg_ns from the kernel-trace pass; FETCH/WRITE from separate --pmc passes of the "
                            "same command; hbm_bytes_per_launch = 1024*(2*FETCH_KB + WRITE_KB) (gfx950 FETCH "
                            "correction, MI355X_MICROARCH.md HBM section); by_class (accumulate): launches grouped by "
                            "work in units of the smallest (1 = one MSM's bucket set: the headline; 2 = the KZG "
