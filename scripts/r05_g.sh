@@ -14,3 +14,4 @@ timeout -k 10 200 python -u verkle-kzg_amd/tools/verkle_ab.py 65536 6 >> $O/ab.t
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/vtrace -o vt -- python3 -u verkle-kzg_amd/tools/verkle_ab.py 65536 2 > $O/vtrace.log 2>&1 || exit $?
 VKZG_HOST_TIMING=1 timeout -k 10 200 python -u verkle-kzg_amd/tools/ipa_probe.py > $O/ipa.txt 2>&1 || exit $?
 VKZG_IPA_COMPACT=0 timeout -k 10 200 python -u verkle-kzg_amd/tools/ipa_probe.py > $O/ipa_nocompact.txt 2>&1 || exit $?
+VKZG_VERBOSE=1 timeout -k 10 200 python -u verkle-kzg_amd/tools/verkle_ab.py 65536 3 > $O/laps.txt 2>&1 || exit $?

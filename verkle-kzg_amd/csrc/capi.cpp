@@ -4,6 +4,7 @@
 
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "ctx.hpp"
@@ -52,6 +53,36 @@ void pool_put(vc_ctx* ctx, void* p, size_t cap) {
     }
     ctx->pool_free.emplace(cap, p);
     ctx->pool_bytes += cap;
+}
+
+// live contexts by uid: a verkle tree's device mirror outlives the calls that use it and goes back
+// to its context's pool when released -- if that context still exists and is not busy
+namespace {
+std::mutex g_live_mu;
+std::unordered_map<uint64_t, vc_ctx*>& live_ctx() {
+    static std::unordered_map<uint64_t, vc_ctx*> m;
+    return m;
+}
+}  // namespace
+void ctx_register(vc_ctx* ctx, bool live) {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    if (live) live_ctx()[ctx->uid] = ctx;
+    else live_ctx().erase(ctx->uid);
+}
+void pool_return_uid(uint64_t uid, int dev, void* p, size_t cap) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        auto it = live_ctx().find(uid);
+        // (try_lock: the caller may hold this or another context's lock; then the block is freed)
+        if (it != live_ctx().end() && it->second->mu.try_lock()) {
+            pool_put(it->second, p, cap);
+            it->second->mu.unlock();
+            return;
+        }
+    }
+    if (dev >= 0) (void)hipSetDevice(dev);
+    (void)hipFree(p);
 }
 
 int DevBuf::ensure(size_t bytes) {
@@ -229,12 +260,14 @@ int vc_ctx_create(int curve, int device, vc_ctx** out) {
         return VC_E_HIP;
     }
     c->stream = c->own_stream;
+    vk::ctx_register(c, true);
     *out = c;
     return VC_OK;
 }
 
 void vc_ctx_destroy(vc_ctx* ctx) {
     if (!ctx) return;
+    vk::ctx_register(ctx, false);  // before its lock: no mirror block comes back to it after this
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         (void)hipSetDevice(ctx->device);

@@ -31,6 +31,10 @@ namespace vk {
 hipError_t& last_hip_error();
 int pool_take(vc_ctx* ctx, size_t bytes, void** p, size_t* cap);
 void pool_put(vc_ctx* ctx, void* p, size_t cap);
+// the live-context registry (capi.cpp) and a block returned to the pool of context `uid` if it
+// still exists and its lock is free (else hipFree on device `dev`)
+void ctx_register(vc_ctx* ctx, bool live);
+void pool_return_uid(uint64_t uid, int dev, void* p, size_t cap);
 
 // Device buffer. DevBuf(ctx) draws from / returns to the context's stream-ordered block pool
 // (per-call scratch of the scheme paths: a hipMalloc + hipFree pair per buffer per call cost
