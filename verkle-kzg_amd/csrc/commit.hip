@@ -478,7 +478,7 @@ template <class C, class Fr>
 __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
                                                         const uint8_t* __restrict__ inf, uint32_t width, FbGeom fg,
                                                         const uint32_t* __restrict__ sc, int mont,
-                                                        uint32_t bpc, int wpt, const uint32_t* __restrict__ cols,
+                                                        uint32_t bpc, int wpt, StrideCols cols,
                                                         typename C::Acc* __restrict__ part) {
     using FC = typename Fast29<C>::type;
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
@@ -487,8 +487,9 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
     const uint32_t j = blk * 256 + threadIdx.x;
     const uint32_t i = j / WG, wg = j % WG;
     typename FC::Acc fa = FC::zero();
-    // cols (optional): commit g's item i is table base cols[g width + i] (compacted rows)
-    const uint32_t base = (i < width && cols) ? cols[(size_t)g * width + i] : i;
+    // compacted rows (cols.half != 0): commit g's item i is a table base of a strided pattern
+    // (computed: a list in host memory cost a dependent PCIe read per thread, +7 us per launch)
+    const uint32_t base = cols.half ? cols.base(g, i) : i;
     if (i < width && !inf[base]) {
         FbDigits<Fr> dg;
         dg.s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
@@ -580,10 +581,12 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                       const PinBuf* pin_sc, const std::function<void()>* overlap, bool with_cols) {
+                       const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* cols) {
     using Acc = typename C::Acc;
+    const bool with_cols = cols && cols->half;
     if (width > t->n && !with_cols) return VC_E_RANGE;
-    if (with_cols && !pin_sc) return VC_E_INVALID;
+    if (with_cols && (size_t)cols->extra >= t->n) return VC_E_RANGE;
+    if (with_cols && cols->base(0, cols->n_main - 1) >= t->n) return VC_E_RANGE;
     if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8, 0));
     if (batch == 0) {
         if (overlap && *overlap) (*overlap)();
@@ -626,22 +629,9 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         VK_TRY(ctx->pin_small.ensure(part_bytes));
         if (!(zc & 1)) VK_TRY(ctx->ws[WS_PIECE].ensure(part_bytes));
         Acc* d_part = (zc & 1) ? static_cast<Acc*>(ctx->pin_small.dp) : ctx->ws[WS_PIECE].as<Acc>();
-        // compacted rows: the base indices follow the scalars in the pinned staging
-        const uint32_t* d_cols = nullptr;
-        if (with_cols) {
-            const size_t off = items * 32;
-            if (zc & 2) {
-                d_cols = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(pin_sc->dp) + off);
-            } else {
-                VK_TRY(ctx->ws[WS_COLS].ensure(items * 4));
-                VK_CHECK_HIP(hipMemcpyAsync(ctx->ws[WS_COLS].p, static_cast<const uint8_t*>(pin_sc->p) + off,
-                                            items * 4, hipMemcpyHostToDevice, ctx->stream));
-                d_cols = ctx->ws[WS_COLS].as<uint32_t>();
-            }
-        }
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
                   t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
-                  bpc, wpt, d_cols, d_part);
+                  bpc, wpt, with_cols ? *cols : StrideCols{}, d_part);
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
         // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the
@@ -831,7 +821,7 @@ bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch) {
 
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                   void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                  const PinBuf* pin_sc, const std::function<void()>* overlap, bool with_cols) {
+                  const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* with_cols) {
     bool dummy = false;
     if (!on_host) on_host = &dummy;
     *on_host = false;

@@ -58,6 +58,16 @@ struct DevBuf {
 
 // page-locked host staging (one per lane): device->host copies into pageable memory go through a
 // bounce buffer and start late (measured ~25 us before the MSM's second small read-back)
+// compacted rows of the batched commit's latency path (the IPA rounds' L / R): item i < n_main of
+// commit g is table base (i / half) m + (g odd ? off_odd : off_even) + i % half, item n_main is
+// base `extra` (half = 0: plain rows, item i is base i)
+struct StrideCols {
+    uint32_t half = 0, m = 0, off_even = 0, off_odd = 0, n_main = 0, extra = 0;
+    __host__ __device__ uint32_t base(uint32_t g, uint32_t i) const {
+        return i < n_main ? (i / half) * m + ((g & 1) ? off_odd : off_even) + i % half : extra;
+    }
+};
+
 struct PinBuf {
     void* p = nullptr;
     void* dp = nullptr;     // the device's address of p (kernels read / write it over PCIe)
@@ -131,7 +141,6 @@ enum WsSlot {
     WS_SCALARS,
     WS_OUT,
     WS_MISC,
-    WS_COLS,
     WS_TREE,
     WS_TAIL,
     WS_PIECE,
@@ -341,13 +350,12 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 // the results are written there instead of d_out_* and *on_host is set
 // pin_sc: the scalars in ctx->pin_io (host, page-locked) instead of d_scalars (nullptr): uploaded
 // to WS_SCALARS here, or read in place over PCIe by the latency path. overlap: host work run once
-// the commit kernel is enqueued, before the call waits for it. with_cols: compacted rows -- item i
-// of commit g is table base cols[g width + i], the u32 cols following the batch x width scalars in
-// pin_sc (latency path only: VC_E_INVALID otherwise; fb_small_path says whether it runs)
+// the commit kernel is enqueued, before the call waits for it. cols: compacted rows (latency path
+// only: VC_E_INVALID otherwise; fb_small_path says whether it runs)
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
                   uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr,
-                  const std::function<void()>* overlap = nullptr, bool with_cols = false);
+                  const std::function<void()>* overlap = nullptr, const StrideCols* cols = nullptr);
 // whether msm_batch_run of `batch` width-`width` commits takes the latency path
 bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch);
 }  // namespace vk

@@ -134,24 +134,22 @@ static bool verify_timing() {
 
 // width-w fixed-base commitments of Montgomery scalars (host) -> canonical affine (host)
 // overlap: host work run while the commit kernel runs (fb_commit_t)
-// cols (optional, latency path only -- fb_small_path): compacted rows, item i of commit g is base
-// cols[g width + i]
+// cols (optional, latency path only -- fb_small_path): compacted rows (ctx.hpp StrideCols)
 static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
                         uint8_t* out_inf, const std::function<void()>* overlap = nullptr,
-                        const uint32_t* cols = nullptr) {
-    const size_t in_bytes = batch * width * 32, col_bytes = cols ? batch * width * 4 : 0, out_bytes = batch * 65;
+                        const StrideCols* cols = nullptr) {
+    const size_t in_bytes = batch * width * 32, out_bytes = batch * 65;
     VK_TRY(ctx->ws[WS_MISC].ensure(out_bytes));
     uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
     uint8_t* dinf = dxy + batch * 64;
     // pinned staging both ways (the IPA rounds call this 8 times per proof: pageable copies went
     // through bounce buffers), points and flags read back in one copy; the scalars are uploaded by
     // msm_batch_run, or read in place by its latency path
-    VK_TRY(ctx->pin_io.ensure(std::max(in_bytes + col_bytes, out_bytes)));
+    VK_TRY(ctx->pin_io.ensure(std::max(in_bytes, out_bytes)));
     memcpy(ctx->pin_io.p, sc, in_bytes);
-    if (cols) memcpy(static_cast<uint8_t*>(ctx->pin_io.p) + in_bytes, cols, col_bytes);
     bool on_host = false;
     VK_TRY(msm_batch_run(ctx, t, width, nullptr, batch, 1, dxy, dinf, out_xy, out_inf, &on_host, &ctx->pin_io,
-                         overlap, cols != nullptr));
+                         overlap, cols));
     if (on_host) return VC_OK;
     VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_io.p, dxy, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
@@ -286,23 +284,22 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     const bool compact = compact_env && fb_small_path(ctx, t, N / 2 + 1, 2 * B);
     const size_t W = compact ? N / 2 + 1 : N + 1;
     std::vector<Fr> sc(2 * B * W);
-    std::vector<uint32_t> cols(compact ? 2 * B * W : 0);
     std::vector<uint64_t> oxy(2 * B * 8);
     std::vector<uint8_t> oinf(2 * B);
     double lap_fill = 0, lap_commit = 0, lap_fold = 0;
     for (size_t r = 0; r < K; r++) {
         const size_t m = N >> r, half = m / 2;
         const double c0 = verify_timing() ? verify_clock_us() : 0.0;
-        if (compact) {  // the same base lists for every proof of the batch
-            uint32_t* cL = cols.data();
-            uint32_t* cR = cols.data() + W;
-            size_t kl = 0, kr = 0;
-            for (size_t i = 0; i < N; i++) {
-                if (i % m >= half) cL[kl++] = (uint32_t)i;
-                else cR[kr++] = (uint32_t)i;
-            }
-            cL[kl] = cR[kr] = (uint32_t)N;
-            for (size_t p = 1; p < B; p++) memcpy(&cols[2 * p * W], cols.data(), 2 * W * 4);
+        // L (even commits): bases i with i mod m >= half, R (odd): i mod m < half, in index order
+        // -- the k-th is (k / half) m + k mod half (+ half for L) --, then q
+        StrideCols cols;
+        if (compact) {
+            cols.half = (uint32_t)half;
+            cols.m = (uint32_t)m;
+            cols.off_even = (uint32_t)half;
+            cols.off_odd = 0;
+            cols.n_main = (uint32_t)(N / 2);
+            cols.extra = (uint32_t)N;
         }
         par_for([&](size_t p) {
             IpaState& s = st[p];
@@ -333,7 +330,7 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
         });
         const double c1 = verify_timing() ? verify_clock_us() : 0.0;
         VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data(), nullptr,
-                            compact ? cols.data() : nullptr));
+                            compact ? &cols : nullptr));
         const double c2 = verify_timing() ? verify_clock_us() : 0.0;
         par_for([&](size_t p) {
             IpaState& s = st[p];

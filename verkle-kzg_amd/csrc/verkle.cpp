@@ -176,6 +176,9 @@ struct vc_verkle {
     };
     std::vector<uint8_t> base;
     std::vector<SlotLog> slog;
+    // scratch of the commitment's delta plan, per node id (-1 outside a call): the node's plan /
+    // its snapshot index (persistent arrays: no hash maps per call)
+    std::vector<int32_t> plan_slot, snap_slot;
     void log_slot(int parent, uint8_t slot, int old) {
         if (base[parent]) slog.push_back({parent, old, slot});
     }
@@ -187,6 +190,8 @@ struct vc_verkle {
         has_commit.push_back(0);
         queued.push_back(0);
         base.push_back(0);
+        plan_slot.push_back(-1);
+        snap_slot.push_back(-1);
         return (int)nodes.size() - 1;
     }
     void mark(int id) {  // commitment cleared (node.rs:150-152 commitment = None)
@@ -453,8 +458,11 @@ struct Rows {
 // the node points to, its line now cached) -- the walks are chains of dependent DRAM misses
 // (~360 ns per extension node on 16 threads)
 // the per-worker parts of build_rows (one part when the range is small)
+// reuse (optional): parts of an earlier call, cleared and refilled -- their storage stays
+// allocated (a fresh 65,536-extension level's part vectors cost ~0.1 ms of page faults per worker)
 template <class R, class Fn, class Pf>
-std::vector<R> build_parts(HostPool& pool, size_t lo, size_t hi, size_t nnz_per, Fn fn, Pf pf) {
+std::vector<R> build_parts(HostPool& pool, size_t lo, size_t hi, size_t nnz_per, Fn fn, Pf pf,
+                           std::vector<R>* reuse = nullptr) {
     const size_t count = hi - lo;
     auto walk_range = [&](size_t a, size_t b, R& r) {
         for (size_t i = a; i < std::min(b, a + 16); i++) pf(i, 0);
@@ -468,10 +476,13 @@ std::vector<R> build_parts(HostPool& pool, size_t lo, size_t hi, size_t nnz_per,
     const unsigned T = (count >= 64 && count * nnz_per >= 16384)
                            ? (unsigned)std::min<size_t>(pool.size(), std::max<size_t>(1, count / 16))
                            : 1;
-    std::vector<R> part(T);
+    std::vector<R> part;
+    if (reuse) part.swap(*reuse);
+    part.resize(T);
     auto run = [&](unsigned k) {
         if (k >= T) return;
         const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
+        part[k].clear();
         part[k].reserve(b - a, (b - a) * std::min<size_t>(nnz_per, 4));
         walk_range(a, b, part[k]);
     };
@@ -578,6 +589,13 @@ struct ExtRows16 {
     uvec<uint64_t> vals;  // 2 u64 per non-zero
     uvec<uint64_t> stem;  // 4 u64 per extension node (its stem item)
     uint32_t maxlen = 0;  // longest row (<= 4: the sparse commit's chunks are the rows)
+    void clear() {  // (capacity kept)
+        ptr.assign(1, 0);
+        cols.clear();
+        vals.clear();
+        stem.clear();
+        maxlen = 0;
+    }
     void reserve(size_t rows, size_t nnz) {
         ptr.reserve(2 * rows + 1);
         cols.reserve(nnz);
@@ -1098,26 +1116,56 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     const bool use_delta = !(delta_env && atoi(delta_env) == 0);
     struct DPlan {
         uint64_t seen[4];
-        std::vector<std::pair<uint8_t, int32_t>> e;  // (slot, snapshot index; -1: the slot was empty)
+        uint32_t start, cnt;  // its entries in plan_e: (slot, snapshot index; -1: the slot was empty)
     };
-    std::unordered_map<int, size_t> plan_of;
     std::vector<DPlan> plans;
+    std::vector<std::pair<uint8_t, int32_t>> plan_e;
     std::vector<uint32_t> snap_ids;
-    std::unordered_map<int, int32_t> snap_of;
-    if (use_delta) {
-        for (const auto& L : t->slog) {
-            auto pi = plan_of.try_emplace(L.parent, plans.size());
-            if (pi.second) plans.push_back(DPlan{{0, 0, 0, 0}, {}});
-            DPlan& P = plans[pi.first->second];
+    std::vector<int> plan_nodes;  // nodes whose plan_slot is set (reset on exit)
+    struct PlanReset {
+        vc_verkle* t;
+        const std::vector<int>& pn;
+        const std::vector<uint32_t>& sn;
+        ~PlanReset() {
+            for (int id : pn) t->plan_slot[id] = -1;
+            for (uint32_t id : sn) t->snap_slot[id] = -1;
+        }
+    } plan_reset{t, plan_nodes, snap_ids};
+    if (use_delta && !t->slog.empty()) {
+        // pass 1: a plan per logged parent, the first entry per (parent, slot) kept; snapshot slots
+        std::vector<int32_t> kept(t->slog.size(), -1);  // its plan, or -1 for a repeated slot
+        for (size_t i = 0; i < t->slog.size(); i++) {
+            const auto& L = t->slog[i];
+            int32_t p = t->plan_slot[L.parent];
+            if (p < 0) {
+                p = (int32_t)plans.size();
+                plans.push_back(DPlan{{0, 0, 0, 0}, 0, 0});
+                t->plan_slot[L.parent] = p;
+                plan_nodes.push_back(L.parent);
+            }
+            DPlan& P = plans[p];
             if ((P.seen[L.slot >> 6] >> (L.slot & 63)) & 1) continue;
             P.seen[L.slot >> 6] |= 1ull << (L.slot & 63);
-            int32_t k = -1;
-            if (L.old >= 0) {
-                auto si = snap_of.try_emplace(L.old, (int32_t)snap_ids.size());
-                if (si.second) snap_ids.push_back((uint32_t)L.old);
-                k = si.first->second;
+            P.cnt++;
+            kept[i] = p;
+            if (L.old >= 0 && t->snap_slot[L.old] < 0) {
+                t->snap_slot[L.old] = (int32_t)snap_ids.size();
+                snap_ids.push_back((uint32_t)L.old);
             }
-            P.e.push_back({L.slot, k});
+        }
+        // pass 2: the entries grouped by plan
+        uint32_t run = 0;
+        for (auto& P : plans) {
+            P.start = run;
+            run += P.cnt;
+            P.cnt = 0;
+        }
+        plan_e.resize(run);
+        for (size_t i = 0; i < t->slog.size(); i++) {
+            if (kept[i] < 0) continue;
+            const auto& L = t->slog[i];
+            DPlan& P = plans[kept[i]];
+            plan_e[P.start + P.cnt++] = {L.slot, L.old >= 0 ? t->snap_slot[L.old] : -1};
         }
     }
     DevBuf d_snap(ctx), d_snap_ids(ctx);
@@ -1157,9 +1205,9 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         if (!plans.empty() && !L.dense)
             for (size_t b = 0; b < B; b++) {
                 if (!t->base[lv[b]]) continue;
-                auto it = plan_of.find(lv[b]);
-                if (it == plan_of.end()) continue;
-                rplan[b] = &plans[it->second];
+                const int32_t pi = t->plan_slot[lv[b]];
+                if (pi < 0) continue;
+                rplan[b] = &plans[pi];
                 any_delta = true;
             }
         L.any_delta = any_delta;
@@ -1167,7 +1215,7 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         uvec<uint64_t>& ptr = L.ptr;
         ptr[0] = 0;
         for (size_t b = 0; b < B; b++)
-            ptr[b + 1] = ptr[b] + (rplan[b] ? rplan[b]->e.size() : t->nodes[lv[b]].children.v.size());
+            ptr[b + 1] = ptr[b] + (rplan[b] ? rplan[b]->cnt : t->nodes[lv[b]].children.v.size());
         const size_t nnz = ptr[B], nz1 = std::max<size_t>(nnz, 1);
         L.nnz = nnz;
         // layout: cols | child | ids | (delta) sidx | add_ids
@@ -1190,7 +1238,8 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             const VNode& n = t->nodes[lv[b]];
             ids[b] = (uint32_t)lv[b];
             if (rplan[b]) {
-                for (auto& e : rplan[b]->e) {
+                for (uint32_t q = 0; q < rplan[b]->cnt; q++) {
+                    const auto& e = plan_e[rplan[b]->start + q];
                     cols[j] = e.first;
                     child[j] = (uint32_t)n.children.find(e.first)->second;
                     sidx[j] = e.second;
@@ -1228,9 +1277,15 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     if (E) {
         // the rows are built in per-worker parts (with each node's stem item), then merged straight
         // into page-locked memory: the uploads are plain DMA, and no fresh pageable buffer is touched
+        static thread_local std::vector<ExtRows16> parts_cache;  // storage kept between calls
         std::vector<ExtRows16> parts = build_parts<ExtRows16>(
             pool, 0, E, (size_t)N, [&](size_t e, ExtRows16& r) { ext_rows16(t, exts[e], r); },
-            [&](size_t e, int stage) { ext_prefetch(t, exts[e], stage); });
+            [&](size_t e, int stage) { ext_prefetch(t, exts[e], stage); }, &parts_cache);
+        struct KeepParts {
+            std::vector<ExtRows16>& p;
+            std::vector<ExtRows16>& cache;
+            ~KeepParts() { cache.swap(p); }
+        } keep_parts{parts, parts_cache};
         const size_t T = parts.size();
         std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0), eoff(T + 1, 0);
         uint32_t maxlen = 0;
