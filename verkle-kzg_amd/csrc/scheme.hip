@@ -278,9 +278,12 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
         s.coeff.assign(N, fe_one<F>());
     });
     // L (R) of a round has non-zeros only at the N / 2 bases i with i mod m >= m / 2 (< m / 2) and
-    // at q: on the latency path the rows are compacted to those N / 2 + 1 bases (half the threads
-    // and half the block partials the host adds per round); otherwise full width-(N + 1) rows
-    static const bool compact_env = !(getenv("VKZG_IPA_COMPACT") && atoi(getenv("VKZG_IPA_COMPACT")) == 0);
+    // at q. VKZG_IPA_COMPACT=1 (A/B probe) compacts the rows to those N / 2 + 1 bases on the latency
+    // path: half the threads and half the block partials the host adds, but measured slower (prove
+    // 0.80 vs 0.77 ms, kernel 62 vs 56 us per round: profiles/r05/ipa_compact/) -- the zero lanes of
+    // the full rows make the first adds of the block tree identity adds, which the compacted rows
+    // replace by real ones. Off by default.
+    static const bool compact_env = getenv("VKZG_IPA_COMPACT") && atoi(getenv("VKZG_IPA_COMPACT")) == 1;
     const bool compact = compact_env && fb_small_path(ctx, t, N / 2 + 1, 2 * B);
     const size_t W = compact ? N / 2 + 1 : N + 1;
     std::vector<Fr> sc(2 * B * W);
