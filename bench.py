@@ -1255,7 +1255,7 @@ def main():
     if not a.no_secondary:
         # config 3: batched width-256 commits (fixed-base tables), batch split across ranks; timed
         # on the commit_window / commit_windows table (172 GB at 19 / 13), the c = 16 one (17.2 GB), the c = 18 x 14
-        # one (68.7 GB) and the deployable c = 17 one (32.2 GB)
+        # one (68.7 GB) and the deployable 15-window one (31.1 GB)
         cstate = {}
 
         def cengine():  # (re)create: closing the engine frees a table a peer rank could not fit
@@ -1329,8 +1329,9 @@ def main():
         small = ctime(16) if a.commit_window != 16 else big
         # the <= 70 GB table: 14 windows (12 of 18 bits, 2 of 19), 68.7 GB
         mixed = ctime(18, 14)
-        # the deployable <= 32 GB table: 15 windows of 17 bits, 32.2 GB (30 GiB)
-        deploy = ctime(17)
+        # the deployable <= 32 GB table: 15 windows (14 of 17 bits, one of 16), 31.1 GB -- the adds
+        # of c = 17's 15 windows from a smaller table (c = 17 x 15 is 32.2 GB)
+        deploy = ctime(16, 15)
         head = big or small
         if head is None:  # neither table fits beside the rest on every rank
             out["secondary"] = {"workload": f"{B} batched width-256 Bandersnatch commits (configs[2])",
@@ -1343,7 +1344,7 @@ def main():
                 **head,
                 "c16": small,
                 "mixed_c18_w14": mixed,
-                "c17_w15_deployable": deploy,
+                "deployable_w15_31GB": deploy,
             }
         cstate["eng"].close()
 
