@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-5 rehearsal on one MI355X, in the order that ties the bench line to its counters: every
+# -m gpu test, smoke(), the rocprofv3 kernel trace + PMC passes of the bench (scripts/bench_profile.sh),
+# their summary installed as profiles/r05/pmc_summary.json (so the bench line reads counters taken on
+# this library), then the default bench line with the CPU baselines.
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r05_final}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1
+echo tests-done
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1
+echo smoke-done
+bash $R/scripts/bench_profile.sh $TAG
+cp $R/gpurun_out/prof_$TAG/summary.json $R/profiles/r05/pmc_summary.json
+mkdir -p $O/profiles_r05 && cp $R/profiles/r05/pmc_summary.json $O/profiles_r05/
+cd $R
+timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
+echo bench-done
