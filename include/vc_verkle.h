@@ -58,6 +58,9 @@ int vc_verkle_commitment(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy,
 /* diagnostics: per node id (up to max) its type (0 internal, 1 extension), level and committed
  * to_data_item (4 u64, canonical); *n = the node count */
 int vc_verkle_debug_nodes(vc_verkle* t, size_t max, uint8_t* type, int32_t* level, uint64_t* items, size_t* n);
+/* diagnostics (no GPU): the device path's extension host stage -- c1 / c2 rows of every
+ * extension node built and merged into one buffer -- run `reps` times; *us = the median (us) */
+int vc_verkle_debug_ext_stage(vc_verkle* t, int reps, double* us);
 /* node counts (diagnostics): internal, extension, dirty */
 int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, size_t* dirty);
 

@@ -47,6 +47,7 @@ int kzg_share_finish(KzgShare* s, const uint64_t* total, uint32_t* out_acc, uint
 void kzg_share_free(KzgShare* s);
 int kzg_share_sum(int curve, const uint64_t* parts, int G, uint64_t* total);
 int verkle_pull_host(vc_verkle* t);
+int verkle_debug_ext_stage(vc_verkle* t, int reps, double* us);
 // one context, every level device-resident (verkle.cpp; vc_verkle_commitment's default)
 int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf);
 

@@ -106,21 +106,25 @@ static void item_of_bytes(const uint8_t* b, size_t len, uint64_t out[4]) {
         memcpy(out, w, 32);
         static const uint64_t R[4] = {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
                                       0x30644e72e131a029ULL};  // BN254 r
-        for (int k = 0; k < 6; k++) {
-            bool ge = false;
-            for (int i = 3; i >= 0; i--)
-                if (out[i] != R[i]) {
-                    ge = out[i] > R[i];
-                    break;
-                } else if (i == 0) {
-                    ge = true;
-                }
-            if (!ge) break;
-            unsigned __int128 br = 0;
+        // v mod r with one quotient estimate: q = floor(v_3 / r_3) (<= 5) is floor(v / r) or one
+        // more (r_3 ~ 2^61.6 dwarfs the lower limbs' share), so v - q r lies in [-r, r): one
+        // conditional add (the compare-and-subtract loop it replaces mispredicted ~48 ns per stem)
+        const uint64_t q = out[3] / R[3];
+        typedef unsigned __int128 u128;
+        u128 mc = 0, br = 0;
+        for (int i = 0; i < 4; i++) {
+            mc += (u128)q * R[i];
+            const u128 d = (u128)out[i] - (uint64_t)mc - (uint64_t)br;
+            out[i] = (uint64_t)d;
+            br = (d >> 64) & 1;
+            mc >>= 64;
+        }
+        if ((uint64_t)mc + (uint64_t)br) {  // negative: add r back
+            u128 c = 0;
             for (int i = 0; i < 4; i++) {
-                unsigned __int128 d = (unsigned __int128)out[i] - R[i] - (uint64_t)br;
-                out[i] = (uint64_t)d;
-                br = (d >> 64) & 1;
+                c += (u128)out[i] + R[i];
+                out[i] = (uint64_t)c;
+                c >>= 64;
             }
         }
         return;
@@ -407,6 +411,13 @@ int vc_verkle_debug_nodes(vc_verkle* t, size_t max, uint8_t* type, int32_t* leve
     return VC_OK;
 }
 
+// diagnostics (tools/verkle_host_probe.py, no GPU): the device path's extension host stage (rows
+// built and merged into a plain buffer) over every extension node, `reps` times; *us = the median
+int vc_verkle_debug_ext_stage(vc_verkle* t, int reps, double* us) {
+    if (!t || !us || reps < 1) return VC_E_INVALID;
+    return vk::verkle_debug_ext_stage(t, reps, us);
+}
+
 int vc_verkle_stats(const vc_verkle* t, size_t* internal, size_t* extension, size_t* dirty) {
     if (!t) return VC_E_INVALID;
     size_t a = 0, b = 0, c = 0;
@@ -482,9 +493,13 @@ std::vector<R> build_parts(HostPool& pool, size_t lo, size_t hi, size_t nnz_per,
     auto run = [&](unsigned k) {
         if (k >= T) return;
         const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
-        part[k].clear();
-        part[k].reserve(b - a, (b - a) * std::min<size_t>(nnz_per, 4));
-        walk_range(a, b, part[k]);
+        // filled in a local object: the parts' vector headers share cache lines, and every
+        // push_back updates its header (false sharing made 8 threads 1.6x one)
+        R local = std::move(part[k]);
+        local.clear();
+        local.reserve(b - a, (b - a) * std::min<size_t>(nnz_per, 4));
+        walk_range(a, b, local);
+        part[k] = std::move(local);
     };
     if (T == 1) run(0);
     else pool.run(run);
@@ -518,8 +533,10 @@ R build_rows(HostPool& pool, size_t lo, size_t hi, size_t nnz_per, Fn fn, Pf pf)
     pool.run([&](unsigned k) {  // the pool runs k < pool.size(): workers past T have no part
         if (k >= T) return;
         const size_t a = lo + count * k / T, b = lo + count * (k + 1) / T;
-        part[k].reserve(b - a, (b - a) * nnz_per);
-        walk_range(a, b, part[k]);
+        R local;  // (a local object: no false sharing on the parts' vector headers)
+        local.reserve(b - a, (b - a) * nnz_per);
+        walk_range(a, b, local);
+        part[k] = std::move(local);
     });
     std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0);
     for (unsigned k = 0; k < T; k++) {
@@ -655,6 +672,114 @@ static void ext_prefetch(const vc_verkle* t, int id, int stage) {
     } else if (!n.leaves.v.empty()) {
         __builtin_prefetch(n.leaves.v.data());
     }
+}
+
+// The extension level's host stage (verkle_commitment_dev): c1 / c2 rows built in per-worker parts
+// (with each node's stem item), then merged in parallel straight into one buffer (page-locked in the
+// commitment: the upload is plain DMA) laid out as row_ptr (2E + 1 u64) | stem items (E x 4 u64) |
+// values (nnz x 2 u64) | node ids (E u32) | cols (nnz u32) -- everything after row_ptr goes up in one
+// copy. `cache`: part storage kept between calls (no page faults on fresh vectors).
+struct ExtStage {
+    size_t nnz = 0, o_stem = 0, o_vals = 0, o_ids = 0, o_cols = 0, o_end = 0;
+    uint32_t maxlen = 0;
+    uint8_t* base = nullptr;
+};
+static int ext_stage(const vc_verkle* t, const std::vector<int>& exts, HostPool& pool, std::vector<ExtRows16>& cache,
+                     const std::function<uint8_t*(size_t)>& buffer, ExtStage* out, double* t_build = nullptr) {
+    const size_t E = exts.size();
+    const auto tb0 = std::chrono::steady_clock::now();
+    std::vector<ExtRows16> parts = build_parts<ExtRows16>(
+        pool, 0, E, (size_t)t->N, [&](size_t e, ExtRows16& r) { ext_rows16(t, exts[e], r); },
+        [&](size_t e, int stage) { ext_prefetch(t, exts[e], stage); }, &cache);
+    struct KeepParts {
+        std::vector<ExtRows16>& p;
+        std::vector<ExtRows16>& cache;
+        ~KeepParts() { cache.swap(p); }
+    } keep_parts{parts, cache};
+    if (t_build) *t_build = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tb0).count();
+    const size_t T = parts.size();
+    std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0), eoff(T + 1, 0);
+    uint32_t maxlen = 0;
+    for (size_t k = 0; k < T; k++) {
+        roff[k + 1] = roff[k] + parts[k].n();
+        noff[k + 1] = noff[k] + parts[k].cols.size();
+        eoff[k + 1] = eoff[k] + parts[k].stem.size() / 4;
+        maxlen = std::max(maxlen, parts[k].maxlen);
+    }
+    const size_t nnz = noff[T];
+    ExtStage& X = *out;
+    X.nnz = nnz;
+    X.maxlen = maxlen;
+    X.o_stem = (2 * E + 1) * 8;
+    X.o_vals = X.o_stem + E * 32;
+    X.o_ids = X.o_vals + nnz * 16;
+    X.o_cols = X.o_ids + E * 4;
+    X.o_end = X.o_cols + nnz * 4;
+    uint8_t* pin = buffer(X.o_end);
+    if (!pin) return VC_E_OOM;
+    X.base = pin;
+    uint64_t* rp = reinterpret_cast<uint64_t*>(pin);
+    uint32_t* ids = reinterpret_cast<uint32_t*>(pin + X.o_ids);
+    rp[0] = 0;
+    auto merge = [&](unsigned k) {  // part k holds extensions [eoff[k], eoff[k + 1]) in order
+        if (k >= T) return;
+        const ExtRows16& r = parts[k];
+        for (size_t i = 1; i < r.ptr.size(); i++) rp[roff[k] + i] = noff[k] + r.ptr[i];
+        memcpy(pin + X.o_stem + eoff[k] * 32, r.stem.data(), r.stem.size() * 8);
+        if (!r.cols.empty()) {
+            memcpy(pin + X.o_vals + noff[k] * 16, r.vals.data(), r.vals.size() * 8);
+            memcpy(pin + X.o_cols + noff[k] * 4, r.cols.data(), r.cols.size() * 4);
+        }
+        for (size_t e = eoff[k]; e < eoff[k + 1]; e++) ids[e] = (uint32_t)exts[e];
+    };
+    if (T == 1) merge(0);
+    else pool.run(merge);
+    return VC_OK;
+}
+
+int verkle_debug_ext_stage(vc_verkle* t, int reps, double* us) {
+    std::vector<int> exts;
+    for (size_t i = 0; i < t->nodes.size(); i++)
+        if (t->nodes[i].ext) exts.push_back((int)i);
+    std::vector<ExtRows16> cache;
+    std::vector<uint8_t> buf;
+    std::vector<double> ts, tbs;
+    for (int r = 0; r < reps; r++) {
+        const auto t0 = std::chrono::steady_clock::now();
+        ExtStage X;
+        double tb = 0;
+        VK_TRY(ext_stage(t, exts, host_pool(), cache,
+                         [&](size_t bytes) -> uint8_t* {
+                             if (buf.size() < bytes) buf.resize(bytes);
+                             return buf.data();
+                         },
+                         &X, &tb));
+        ts.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        tbs.push_back(tb);
+    }
+    if (getenv("VKZG_VERBOSE")) {  // one thread over the whole level, and the stem items alone
+        ExtRows16 r;
+        r.reserve(exts.size(), exts.size() * 4);
+        auto c0 = std::chrono::steady_clock::now();
+        for (size_t e = 0; e < exts.size(); e++) ext_rows16(t, exts[e], r);
+        auto c1 = std::chrono::steady_clock::now();
+        uint64_t acc = 0, w[4];
+        for (size_t e = 0; e < exts.size(); e++) {
+            item_of_bytes(t->nodes[exts[e]].stem.data(), t->N, w);
+            acc ^= w[0];
+        }
+        auto c2 = std::chrono::steady_clock::now();
+        fprintf(stderr, "[ext stage] one thread: rows %.1f us, stem items alone %.1f us (%llu), sizeof(VNode) %zu\n",
+                std::chrono::duration<double, std::micro>(c1 - c0).count(),
+                std::chrono::duration<double, std::micro>(c2 - c1).count(), (unsigned long long)(acc & 1), sizeof(VNode));
+    }
+    std::sort(ts.begin(), ts.end());
+    std::sort(tbs.begin(), tbs.end());
+    *us = ts[ts.size() / 2];
+    if (getenv("VKZG_VERBOSE"))
+        fprintf(stderr, "[ext stage] %zu extensions, %u threads: build %.1f us, total %.1f us (medians)\n", exts.size(),
+                host_pool().size(), tbs[tbs.size() / 2], *us);
+    return VC_OK;
 }
 
 // vc_msm_batch_sparse + vc_to_data_item_batch in one call (capi.cpp vc_msm_batch_sparse_items)
@@ -1275,49 +1400,18 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     const std::vector<int>& exts = t->dirty_ext;
     const size_t E = exts.size();
     if (E) {
-        // the rows are built in per-worker parts (with each node's stem item), then merged straight
-        // into page-locked memory: the uploads are plain DMA, and no fresh pageable buffer is touched
         static thread_local std::vector<ExtRows16> parts_cache;  // storage kept between calls
-        std::vector<ExtRows16> parts = build_parts<ExtRows16>(
-            pool, 0, E, (size_t)N, [&](size_t e, ExtRows16& r) { ext_rows16(t, exts[e], r); },
-            [&](size_t e, int stage) { ext_prefetch(t, exts[e], stage); }, &parts_cache);
-        struct KeepParts {
-            std::vector<ExtRows16>& p;
-            std::vector<ExtRows16>& cache;
-            ~KeepParts() { cache.swap(p); }
-        } keep_parts{parts, parts_cache};
-        const size_t T = parts.size();
-        std::vector<size_t> roff(T + 1, 0), noff(T + 1, 0), eoff(T + 1, 0);
-        uint32_t maxlen = 0;
-        for (size_t k = 0; k < T; k++) {
-            roff[k + 1] = roff[k] + parts[k].n();
-            noff[k + 1] = noff[k] + parts[k].cols.size();
-            eoff[k + 1] = eoff[k] + parts[k].stem.size() / 4;
-            maxlen = std::max(maxlen, parts[k].maxlen);
-        }
-        const size_t nnz = noff[T];
-        // page-locked layout: row_ptr (2E + 1 u64) | stem items (E x 4 u64) | values (nnz x 2 u64) |
-        // node ids (E u32) | cols (nnz u32); everything after row_ptr goes up in one copy
-        const size_t o_stem = (2 * E + 1) * 8, o_vals = o_stem + E * 32, o_ids = o_vals + nnz * 16,
-                     o_cols = o_ids + E * 4, o_end = o_cols + nnz * 4;
-        VK_TRY(ctx->pin_verkle.ensure(o_end));
-        uint8_t* pin = ctx->pin_verkle.as<uint8_t>();
+        ExtStage X;
+        VK_TRY(ext_stage(t, exts, pool, parts_cache,
+                         [&](size_t bytes) -> uint8_t* {
+                             return ctx->pin_verkle.ensure(bytes) == VC_OK ? ctx->pin_verkle.as<uint8_t>() : nullptr;
+                         },
+                         &X));
+        const size_t nnz = X.nnz, o_stem = X.o_stem, o_vals = X.o_vals, o_ids = X.o_ids, o_cols = X.o_cols,
+                     o_end = X.o_end;
+        const uint32_t maxlen = X.maxlen;
+        uint8_t* pin = X.base;
         uint64_t* rp = reinterpret_cast<uint64_t*>(pin);
-        rp[0] = 0;
-        auto merge = [&](unsigned k) {
-            if (k >= T) return;
-            const ExtRows16& r = parts[k];
-            for (size_t i = 1; i < r.ptr.size(); i++) rp[roff[k] + i] = noff[k] + r.ptr[i];
-            memcpy(pin + o_stem + eoff[k] * 32, r.stem.data(), r.stem.size() * 8);
-            if (!r.cols.empty()) {
-                memcpy(pin + o_vals + noff[k] * 16, r.vals.data(), r.vals.size() * 8);
-                memcpy(pin + o_cols + noff[k] * 4, r.cols.data(), r.cols.size() * 4);
-            }
-        };
-        if (T == 1) merge(0);
-        else pool.run(merge);
-        uint32_t* ids = reinterpret_cast<uint32_t*>(pin + o_ids);
-        for (size_t e = 0; e < E; e++) ids[e] = (uint32_t)exts[e];
         lap("ext rows (host)");
         DevBuf d_up(ctx), d_vals(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
         VK_TRY(d_up.ensure(o_end - o_stem));

@@ -51,6 +51,7 @@ SIGNATURES = {
     "vc_verkle_path": (c_int, [c_void_p, P, c_size_t, P, P]),
     "vc_verkle_commitment": (c_int, [c_void_p, c_int, c_void_p, P, P]),
     "vc_verkle_debug_nodes": (c_int, [c_void_p, c_size_t, P, P, P, P]),
+    "vc_verkle_debug_ext_stage": (c_int, [c_void_p, c_int, P]),
     "vc_verkle_stats": (c_int, [c_void_p, P, P, P]),
     "vc_transcript_reserve": (None, [c_void_p, c_size_t]),
     "vc_msm_windows": (c_int, [c_int, c_size_t, P, P, P]),

@@ -53,6 +53,12 @@ class VerkleTree:
               "vc_verkle_path")
         return [(tuple(key[:d + 1]), key[d]) for d in range(n.value)]
 
+    def debug_ext_stage(self, reps=5):
+        """median us of the device path's extension host stage over every extension (no GPU)"""
+        us = ctypes.c_double()
+        check(lib().vc_verkle_debug_ext_stage(self.h, reps, ctypes.byref(us)), "vc_verkle_debug_ext_stage")
+        return us.value
+
     def debug_nodes(self):
         """per node id: (type 0 internal / 1 extension, level, committed item as int)"""
         n = ctypes.c_size_t()
