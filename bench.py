@@ -931,10 +931,15 @@ def verkle_line(a, local, stream):
     keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
     vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
     veng.fixed_base_precompute(kzg.table, 8)  # the SRS fixed-base tables, untimed (setup)
-    # warm-up: one full commitment of an identical tree (first-use workspace allocations)
+    # warm-up: one full commitment of an identical tree and one 1 % update of it (first-use
+    # workspace and page-locked staging allocations of both paths; other keys than the timed update's)
     w = VerkleTree(32)
     for i in range(nk):
         w.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    w.commitment(veng, kzg.table)
+    wrng = np.random.default_rng(17)
+    for i in wrng.integers(0, nk, size=max(1, nk // 100)):
+        w.insert_single(keys[i].tobytes(), wrng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
     w.commitment(veng, kzg.table)
     del w
     # the kernel totals of a full commitment: an identical tree committed with per-kernel events
