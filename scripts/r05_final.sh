@@ -19,3 +19,6 @@ mkdir -p $O/profiles_r05 && cp $R/profiles/r05/pmc_summary.json $O/profiles_r05/
 cd $R
 timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
 echo bench-done
+# the N > 1 flow end to end (two ranks on this one card, gloo + host-callback exchange)
+timeout -k 10 900 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline > $O/rehearse_2rank.json 2> $O/rehearse_2rank.err
+echo rehearse-done
