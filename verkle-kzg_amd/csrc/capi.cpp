@@ -1,4 +1,5 @@
 // extern "C" entry points of libvkzg.so (declared in include/vc_msm.h).
+#include <algorithm>
 #include <atomic>
 #include <hip/hip_runtime.h>
 
@@ -103,8 +104,12 @@ int DevBuf::ensure(size_t bytes) {
 
 int PinBuf::ensure(size_t bytes) {
     if (bytes <= cap && p) return VC_OK;
+    // grow by half at least (and to 64 KiB): a page-locked re-allocation costs ~0.1-0.3 ms, and
+    // callers whose sizes creep up call by call (the verkle levels of successive updates) would
+    // otherwise pay it again and again
+    if (p) bytes = std::max(bytes, cap + cap / 2);
+    bytes = std::max<size_t>(bytes, 64 << 10);
     release();
-    if (bytes == 0) bytes = 16;
     hipError_t e = hipHostMalloc(&p, bytes, flags ? flags : hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
     if (e != hipSuccess) {
