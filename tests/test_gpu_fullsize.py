@@ -230,8 +230,8 @@ def test_msm_chunk_option_small(oracle_c):
 
 
 def test_commit_10k_width256_c20(oracle_c):
-    """configs[2]: 10,000 width-256 Bandersnatch commits on the c = 20 table (13 windows, 188.4 GB:
-    256 x 13 x 2^19 x 108 B; c = 16 if it does not fit next to the rest), 16 sampled commits
+    """configs[2]: 10,000 width-256 Bandersnatch commits on the c = 20 table (13 windows, 223 GB:
+    256 x 13 x 2^19 x 128-B entries; c = 16 if it does not fit next to the rest), 16 sampled commits
     against the oracle."""
     import torch
     import vkzg
@@ -258,11 +258,51 @@ def test_commit_10k_width256_c20(oracle_c):
         e.close()
 
 
+def test_commit_10k_all_by_linearity(oracle_c):
+    """configs[2], every one of the 10,000 commits at once, on the bench's deployable table (15
+    windows, 14 of 17 bits, 31.1 GB): sum_j rho_j C_j over random 64-bit rho_j, computed by the
+    GPU's variable-base Pippenger over the 10,000 output points, == the oracle's MSM of the combined
+    scalars S_i = sum_j rho_j s_ji mod r over the 256 bases (a commit that is wrong anywhere moves
+    the sum, except with probability ~2^-64)."""
+    import torch
+    import vkzg
+    from pyoracle.curves import BAND_R
+    e = vkzg.Engine("bandersnatch")
+    try:
+        tab = e.random_bases(256, seed=3)
+        xy, inf = e.download_bases(tab)
+        e.fixed_base_precompute(tab, 16, 15)
+        assert e.fixed_base_geometry(tab) == (16, 15, 14)
+        B = 10_000
+        sc = vkzg.random_scalars("bandersnatch", B * 256, np.random.default_rng(25))
+        d_sc = torch.from_numpy(sc.view(np.int64).copy()).cuda()
+        d_xy = torch.zeros((B, 8), dtype=torch.int64, device="cuda")
+        d_inf = torch.zeros(B, dtype=torch.uint8, device="cuda")
+        e.msm_batch_device(tab, 256, d_sc.data_ptr(), B, d_xy.data_ptr(), d_inf.data_ptr())
+        got_xy = d_xy.cpu().numpy().view(np.uint64)
+        got_inf = d_inf.cpu().numpy()
+        rho = [int(x) for x in np.random.default_rng(26).integers(1, 1 << 63, size=B, dtype=np.int64)]
+        # S_i = sum_j rho_j s_ji mod r, with exact integers (the scalars are 4 canonical u64 limbs)
+        raw = np.ascontiguousarray(sc, dtype="<u8").tobytes()  # row-major: commit j, base i, 4 limbs
+        S = [0] * 256
+        for j in range(B):
+            rj, base = rho[j], j * 256 * 32
+            for i in range(256):
+                S[i] += rj * int.from_bytes(raw[base + 32 * i:base + 32 * i + 32], "little")
+        S = [v % BAND_R for v in S]
+        want = oracle_c.msm_arrays("bandersnatch", xy, inf, vkzg.ints_to_limbs(S, 4), 1)
+        outs = e.upload_bases(got_xy, got_inf)  # the 10,000 commitments as a base table
+        got = e.msm(outs, vkzg.ints_to_limbs(rho, 4))
+        assert got[1] == want[1] and np.array_equal(got[0], want[0])
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("c,windows,wide", [(18, 14, 2), (19, 13, 7)])
 def test_commit_10k_width256_mixed(oracle_c, c, windows, wide):
-    """configs[2] on the mixed tables: 14 windows (12 of 18 bits, 2 of 19), 58 GB, and the bench's
-    13 windows (6 of 19 bits, 7 of 20), 145 GB, for 256 Bandersnatch bases; 8 sampled commits
-    against the oracle."""
+    """configs[2] on the mixed tables: 14 windows (12 of 18 bits, 2 of 19), 68.7 GB, and the bench's
+    13 windows (6 of 19 bits, 7 of 20), 172 GB (128-B entries), for 256 Bandersnatch bases; 8 sampled
+    commits against the oracle."""
     import torch
     import vkzg
     e = vkzg.Engine("bandersnatch")
