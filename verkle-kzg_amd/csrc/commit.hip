@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <immintrin.h>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -479,7 +481,8 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
                                                         const uint8_t* __restrict__ inf, uint32_t width, FbGeom fg,
                                                         const uint32_t* __restrict__ sc, int mont,
                                                         uint32_t bpc, int wpt, StrideCols cols,
-                                                        typename C::Acc* __restrict__ part) {
+                                                        typename C::Acc* __restrict__ part,
+                                                        uint32_t* __restrict__ flags, uint32_t epoch) {
     using FC = typename Fast29<C>::type;
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
     const int W = fg.W;
@@ -502,6 +505,13 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
         }
     }
     fb_block_sum_store<C>(fa, &part[blockIdx.x]);
+    // zero-copy completion: the block's partial (written by thread 0 above) is made visible system
+    // wide, then its flag takes this launch's epoch -- the host polls the flags instead of waiting
+    // for the stream (fb_commit_t)
+    if (flags != nullptr && threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&flags[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <class C>
@@ -626,12 +636,23 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         };
         const double t0 = timing ? now_us() : 0.0;
         const size_t part_bytes = (size_t)batch * bpc * sizeof(Acc);
-        VK_TRY(ctx->pin_small.ensure(part_bytes));
+        const uint32_t nblk = (uint32_t)(batch * bpc);
+        // zero-copy partials: the blocks' completion flags follow them in the fine-grained buffer
+        // (VKZG_SMALL_POLL=0, read once: wait for the stream instead)
+        static const bool poll_env = !(getenv("VKZG_SMALL_POLL") && atoi(getenv("VKZG_SMALL_POLL")) == 0);
+        const bool poll = poll_env && (zc & 1);
+        const size_t flag_off = (part_bytes + 63) / 64 * 64;
+        VK_TRY(ctx->pin_small.ensure(flag_off + (size_t)nblk * 4));
         if (!(zc & 1)) VK_TRY(ctx->ws[WS_PIECE].ensure(part_bytes));
         Acc* d_part = (zc & 1) ? static_cast<Acc*>(ctx->pin_small.dp) : ctx->ws[WS_PIECE].as<Acc>();
+        volatile uint32_t* hflags = reinterpret_cast<volatile uint32_t*>(static_cast<uint8_t*>(ctx->pin_small.p) + flag_off);
+        uint32_t* dflags = poll ? reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->pin_small.dp) + flag_off) : nullptr;
+        const uint32_t epoch = ++ctx->small_epoch == 0 ? ++ctx->small_epoch : ctx->small_epoch;  // never 0
+        if (poll)  // (fresh page-locked memory holds anything: no stale flag may match)
+            for (uint32_t b = 0; b < nblk; b++) hflags[b] = 0;
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
                   t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
-                  bpc, wpt, with_cols ? *cols : StrideCols{}, d_part);
+                  bpc, wpt, with_cols ? *cols : StrideCols{}, d_part, dflags, epoch);
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
         // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the
@@ -641,7 +662,26 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
             VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_small.p, ctx->ws[WS_PIECE].p, part_bytes, hipMemcpyDeviceToHost,
                                         ctx->stream));
         if (overlap && *overlap) (*overlap)();
-        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        bool seen = false;
+        if (poll) {  // every block's flag at this epoch: the partials are in host memory
+            const auto w0 = std::chrono::steady_clock::now();
+            for (uint32_t spins = 0;; spins++) {
+                uint32_t b = 0;
+                while (b < nblk && hflags[b] == epoch) b++;
+                if (b == nblk) {
+                    seen = true;
+                    break;
+                }
+                // bounded: past 20 ms (a first launch loading its code, or a fault) wait for the
+                // stream, which also reports any error
+                if ((spins & 1023) == 1023 &&
+                    std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(20))
+                    break;
+                _mm_pause();
+            }
+            std::atomic_thread_fence(std::memory_order_acquire);
+        }
+        if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         const double t1 = timing ? now_us() : 0.0;
         const int nl = (int)(C::F::N / 2);
         std::vector<uint64_t> oxy(h_out_xy ? 0 : (size_t)batch * 2 * nl);
