@@ -251,6 +251,7 @@ int vc_ctx_create(int curve, int device, vc_ctx** out) {
     c->curve = curve;
     c->device = device;
     c->pin_small.flags = hipHostMallocCoherent;
+    c->pin_norm_vk.flags = hipHostMallocCoherent;  // written by kernels, polled by the host
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         vk::last_hip_error() = e;

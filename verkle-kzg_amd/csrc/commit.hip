@@ -242,7 +242,8 @@ __global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__
                                                      const uint32_t* __restrict__ add_ids,
                                                      const uint64_t* __restrict__ add_xy,
                                                      const uint8_t* __restrict__ add_inf,
-                                                     fe<BN254Fq>* __restrict__ others, fe<BN254Fq>* __restrict__ tot) {
+                                                     fe<BN254Fq>* __restrict__ others, fe<BN254Fq>* __restrict__ tot,
+                                                     uint32_t* __restrict__ flags, uint32_t epoch) {
     using C = BN254G1;
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     C::Acc a = j < count ? rows[j] : C::zero();
@@ -259,6 +260,12 @@ __global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__
         }
     }
     norm_prep_block<C>(a, j, count, others, tot);
+    // tot in fine-grained host memory (normalize_rows_items): the block product is made visible
+    // system wide, then the block's flag takes this launch's epoch (the host polls the flags)
+    if (flags != nullptr && threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&flags[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <class C>
@@ -790,20 +797,47 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     using F = BN254Fq;
     if (n == 0) return VC_OK;
     const size_t nblk = (n + 255) / 256;
-    DevBuf others(ctx), tot(ctx);
+    DevBuf others(ctx);
     VK_TRY(others.ensure(n * sizeof(fe<F>)));
-    VK_TRY(tot.ensure(nblk * sizeof(fe<F>)));
-    // its own pinned staging (the previous call's H2D may still be queued: grow it only after a sync)
-    if (ctx->pin_norm_vk.cap < 2 * nblk * sizeof(fe<F>)) {
+    // fine-grained page-locked staging of its own, two halves used by alternate calls, each
+    // [block products | inverses | flags]: the prep kernel writes the products and per-block flags
+    // straight into it, the host polls the flags, writes the inverses there and the finish kernel
+    // reads them in place -- no copies, no stream wait (a bounded spin; the stream wait is the
+    // fallback). The previous call's finish may still read its inverses, so this call takes the
+    // other half (the call before that finished: its successor's prep, queued after it, was seen
+    // complete); the buffer grows only after a sync.
+    const size_t flag_off = 2 * nblk * sizeof(fe<F>), half_bytes = (flag_off + nblk * 4 + 255) / 256 * 256;
+    if (ctx->pin_norm_vk.cap < 2 * half_bytes) {
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-        VK_TRY(ctx->pin_norm_vk.ensure(std::max<size_t>(2 * nblk, 64) * sizeof(fe<F>)));
+        VK_TRY(ctx->pin_norm_vk.ensure(2 * half_bytes));
     }
-    fe<F>* h = ctx->pin_norm_vk.as<fe<F>>();
+    const size_t half = ctx->pin_norm_vk.cap / 2 / 256 * 256;  // (>= half_bytes)
+    ctx->norm_vk_parity ^= 1u;
+    uint8_t* hbase = ctx->pin_norm_vk.as<uint8_t>() + ctx->norm_vk_parity * half;
+    uint8_t* dbase = static_cast<uint8_t*>(ctx->pin_norm_vk.dp) + ctx->norm_vk_parity * half;
+    fe<F>* h = reinterpret_cast<fe<F>*>(hbase);
+    fe<F>* dh = reinterpret_cast<fe<F>*>(dbase);
+    volatile uint32_t* hflags = reinterpret_cast<volatile uint32_t*>(hbase + flag_off);
+    uint32_t* dflags = reinterpret_cast<uint32_t*>(dbase + flag_off);
+    const uint32_t epoch = ++ctx->small_epoch == 0 ? ++ctx->small_epoch : ctx->small_epoch;  // never 0
+    for (size_t b = 0; b < nblk; b++) hflags[b] = 0;
     VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids, add_xy,
-              add_inf, others.as<fe<F>>(), tot.as<fe<F>>());
-    VK_CHECK_HIP(hipMemcpyAsync(h, tot.p, nblk * sizeof(fe<F>), hipMemcpyDeviceToHost, ctx->stream));
+              add_inf, others.as<fe<F>>(), dh, dflags, epoch);
     if (overlap && *overlap) (*overlap)();
-    VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    bool seen = false;
+    const auto w0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 0;; spins++) {
+        size_t b = 0;
+        while (b < nblk && hflags[b] == epoch) b++;
+        if (b == nblk) {
+            seen = true;
+            break;
+        }
+        if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(20)) break;
+        _mm_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     fe<F>* inv = h + nblk;
     inv[0] = h[0];
     for (size_t b = 1; b < nblk; b++) inv[b] = fe_mul<F>(inv[b - 1], h[b]);
@@ -814,9 +848,9 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
         inv[b] = ib;
     }
     inv[0] = run;
-    VK_CHECK_HIP(hipMemcpyAsync(tot.p, inv, nblk * sizeof(fe<F>), hipMemcpyHostToDevice, ctx->stream));
+    std::atomic_thread_fence(std::memory_order_release);  // the inverses before the launch that reads them
     VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
-              others.as<fe<F>>(), tot.as<fe<F>>(), dst, out_xy, out_inf, out_item);
+              others.as<fe<F>>(), dh + nblk, dst, out_xy, out_inf, out_item);
     return VC_OK;
 }
 
