@@ -24,7 +24,6 @@
 #include "ctx.hpp"
 #include "ec.hpp"
 #include "ec29.hpp"
-#include "host/pool.hpp"
 
 namespace vk {
 
@@ -599,8 +598,7 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                       const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* cols,
-                       SpinTeam* team) {
+                       const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* cols) {
     using Acc = typename C::Acc;
     const bool with_cols = cols && cols->half;
     if (width > t->n && !with_cols) return VC_E_RANGE;
@@ -711,35 +709,12 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         uint64_t* rxy = h_out_xy ? h_out_xy : oxy.data();
         uint8_t* rinf = h_out_xy ? h_out_inf : oinf.data();
         // the partials serially (the host pool's wake-up cost more than the ~23 us of adds of the
-        // IPA prover's 2 x 33 partials: prove 0.89 -> 1.07 ms) -- or, given a caller's spinning team
-        // (the IPA prover), in T contiguous ranges of the flattened (commit, partial) list, each
-        // thread's sums per commit it touches, folded here -- then one batched inversion
+        // IPA prover's 2 x 33 partials: prove 0.89 -> 1.07 ms), then one batched inversion
         std::vector<Acc> sums(batch);
-        if (team && team->size() > 1 && (size_t)batch * bpc >= 32) {
-            const unsigned T = team->size();
-            const size_t M = (size_t)batch * bpc;
-            std::vector<Acc> ps((size_t)T * batch, C::zero());
-            team->run([&](unsigned k) {
-                const size_t lo = M * k / T, hi = M * (k + 1) / T;
-                for (size_t a = lo; a < hi;) {
-                    const size_t g = a / bpc, e = std::min(hi, (g + 1) * (size_t)bpc);
-                    Acc v = parts[a];
-                    for (size_t b = a + 1; b < e; b++) v = C::add(v, parts[b]);
-                    ps[(size_t)k * batch + g] = v;
-                    a = e;
-                }
-            });
-            for (size_t g = 0; g < batch; g++) {
-                Acc a = ps[g];
-                for (unsigned k = 1; k < T; k++) a = C::add(a, ps[(size_t)k * batch + g]);
-                sums[g] = a;
-            }
-        } else {
-            for (size_t g = 0; g < batch; g++) {
-                Acc a = parts[g * bpc];
-                for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
-                sums[g] = a;
-            }
+        for (size_t g = 0; g < batch; g++) {
+            Acc a = parts[g * bpc];
+            for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
+            sums[g] = a;
         }
         const double t2 = timing ? now_us() : 0.0;
         VK_TRY(acc_to_affine_batch(ctx->curve, reinterpret_cast<const uint32_t*>(sums.data()), batch, rxy, rinf));
@@ -933,8 +908,7 @@ bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch) {
 
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                   void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                  const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* with_cols,
-                  SpinTeam* team) {
+                  const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* with_cols) {
     bool dummy = false;
     if (!on_host) on_host = &dummy;
     *on_host = false;
@@ -942,13 +916,13 @@ int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t 
     switch (t->curve) {
         case VC_CURVE_BN254:
             return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                 h_out_inf, on_host, pin_sc, overlap, with_cols, team);
+                                                 h_out_inf, on_host, pin_sc, overlap, with_cols);
         case VC_CURVE_BLS12_381:
             return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                   h_out_inf, on_host, pin_sc, overlap, with_cols, team);
+                                                   h_out_inf, on_host, pin_sc, overlap, with_cols);
         case VC_CURVE_BANDERSNATCH:
             return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                     h_out_inf, on_host, pin_sc, overlap, with_cols, team);
+                                                     h_out_inf, on_host, pin_sc, overlap, with_cols);
     }
     return VC_E_INVALID;
 }

@@ -58,7 +58,6 @@ struct DevBuf {
 
 // page-locked host staging (one per lane): device->host copies into pageable memory go through a
 // bounce buffer and start late (measured ~25 us before the MSM's second small read-back)
-class SpinTeam;  // host/pool.hpp
 // compacted rows of the batched commit's latency path (the IPA rounds' L / R): item i < n_main of
 // commit g is table base (i / half) m + (g odd ? off_odd : off_even) + i % half, item n_main is
 // base `extra` (half = 0: plain rows, item i is base i)
@@ -358,8 +357,7 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
                   uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr,
-                  const std::function<void()>* overlap = nullptr, const StrideCols* cols = nullptr,
-                  SpinTeam* team = nullptr);
+                  const std::function<void()>* overlap = nullptr, const StrideCols* cols = nullptr);
 // whether msm_batch_run of `batch` width-`width` commits takes the latency path
 bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch);
 }  // namespace vk

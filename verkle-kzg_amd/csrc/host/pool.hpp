@@ -4,7 +4,6 @@
 // are never joined (the pool lives until process exit). Header-only: one pool per process.
 #pragma once
 #include <algorithm>
-#include <atomic>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -85,51 +84,6 @@ private:
     std::exception_ptr err_;
     unsigned pending_ = 0, gen_ = 0;
 };
-// A short-lived team of helper threads that spin between jobs (no condition-variable wake-up:
-// the host pool's ~10-50 us wake-up is longer than the jobs this is for -- the latency path's
-// block partials, a few us of adds per IPA round). Created for one prover call and joined at its
-// end; run(f) calls f(k) for k < size(), k == 0 on the calling thread, and spins until all return.
-class SpinTeam {
-public:
-    explicit SpinTeam(unsigned helpers) : n_(helpers + 1) {
-        for (unsigned k = 1; k < n_; k++) th_.emplace_back([this, k] { loop(k); });
-    }
-    ~SpinTeam() {
-        stop_.store(true, std::memory_order_release);
-        for (auto& t : th_) t.join();
-    }
-    SpinTeam(const SpinTeam&) = delete;
-    SpinTeam& operator=(const SpinTeam&) = delete;
-    unsigned size() const { return n_; }
-    void run(const std::function<void(unsigned)>& f) {
-        job_ = &f;
-        done_.store(0, std::memory_order_relaxed);
-        gen_.fetch_add(1, std::memory_order_release);
-        f(0);
-        while (done_.load(std::memory_order_acquire) < n_ - 1) __builtin_ia32_pause();
-    }
-
-private:
-    void loop(unsigned k) {
-        uint32_t seen = 0;
-        for (;;) {
-            uint32_t g;
-            while ((g = gen_.load(std::memory_order_acquire)) == seen) {
-                if (stop_.load(std::memory_order_acquire)) return;
-                __builtin_ia32_pause();
-            }
-            seen = g;
-            (*job_)(k);
-            done_.fetch_add(1, std::memory_order_acq_rel);
-        }
-    }
-    unsigned n_;
-    std::vector<std::thread> th_;
-    std::atomic<uint32_t> gen_{0}, done_{0};
-    std::atomic<bool> stop_{false};
-    const std::function<void(unsigned)>* job_ = nullptr;
-};
-
 inline HostPool& host_pool() {
     static HostPool* p = new HostPool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
     return *p;

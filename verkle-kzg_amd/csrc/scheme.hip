@@ -137,7 +137,7 @@ static bool verify_timing() {
 // cols (optional, latency path only -- fb_small_path): compacted rows (ctx.hpp StrideCols)
 static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_t batch, uint64_t* out_xy,
                         uint8_t* out_inf, const std::function<void()>* overlap = nullptr,
-                        const StrideCols* cols = nullptr, SpinTeam* team = nullptr) {
+                        const StrideCols* cols = nullptr) {
     const size_t in_bytes = batch * width * 32, out_bytes = batch * 65;
     VK_TRY(ctx->ws[WS_MISC].ensure(out_bytes));
     uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
@@ -149,7 +149,7 @@ static int commit_batch(vc_ctx* ctx, Table* t, size_t width, const Fr* sc, size_
     memcpy(ctx->pin_io.p, sc, in_bytes);
     bool on_host = false;
     VK_TRY(msm_batch_run(ctx, t, width, nullptr, batch, 1, dxy, dinf, out_xy, out_inf, &on_host, &ctx->pin_io,
-                         overlap, cols, team));
+                         overlap, cols));
     if (on_host) return VC_OK;
     VK_CHECK_HIP(hipMemcpyAsync(ctx->pin_io.p, dxy, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
@@ -287,11 +287,6 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     const bool compact = compact_env && fb_small_path(ctx, t, N / 2 + 1, 2 * B);
     const size_t W = compact ? N / 2 + 1 : N + 1;
     std::vector<Fr> sc(2 * B * W);
-    // helper threads spinning for the rounds' host partial sums (VKZG_IPA_TEAM, read once: helpers,
-    // 0 = the sums on this thread); only for the latency path's few commits
-    static const int team_env = getenv("VKZG_IPA_TEAM") ? atoi(getenv("VKZG_IPA_TEAM")) : 0;
-    const int team_helpers = (B <= 4 && fb_small_path(ctx, t, W, 2 * B)) ? std::max(0, std::min(team_env, 15)) : 0;
-    std::unique_ptr<SpinTeam> team;
     std::vector<uint64_t> oxy(2 * B * 8);
     std::vector<uint8_t> oinf(2 * B);
     double lap_fill = 0, lap_commit = 0, lap_fold = 0;
@@ -337,12 +332,8 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
             sR[W - 1] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
         });
         const double c1 = verify_timing() ? verify_clock_us() : 0.0;
-        // round 0 starts the spinning team once its kernel is queued (thread start-up under the kernel)
-        const std::function<void()> start_team = [&] {
-            if (team_helpers > 0 && !team) team.reset(new SpinTeam((unsigned)team_helpers));
-        };
-        VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data(), r == 0 ? &start_team : nullptr,
-                            compact ? &cols : nullptr, team.get()));
+        VK_TRY(commit_batch(ctx, t, W, sc.data(), 2 * B, oxy.data(), oinf.data(), nullptr,
+                            compact ? &cols : nullptr));
         const double c2 = verify_timing() ? verify_clock_us() : 0.0;
         par_for([&](size_t p) {
             IpaState& s = st[p];
