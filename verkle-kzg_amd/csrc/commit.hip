@@ -483,8 +483,8 @@ __global__ void __launch_bounds__(64) k_fb_combine_wave(const typename Fast29<C>
 constexpr int FB_WPT = 1;
 static int fb_wpt() { return FB_WPT; }
 
-template <class C, class Fr, int NT = 256>
-__global__ void __launch_bounds__(NT) k_fb_commit_small(const FbE<C>* __restrict__ tab,
+template <class C, class Fr>
+__global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
                                                         const uint8_t* __restrict__ inf, uint32_t width, FbGeom fg,
                                                         const uint32_t* __restrict__ sc, int mont,
                                                         uint32_t bpc, int wpt, StrideCols cols,
@@ -494,7 +494,7 @@ __global__ void __launch_bounds__(NT) k_fb_commit_small(const FbE<C>* __restrict
     const uint32_t g = blockIdx.x / bpc, blk = blockIdx.x % bpc;
     const int W = fg.W;
     const uint32_t WG = (uint32_t)(W + wpt - 1) / wpt;
-    const uint32_t j = blk * NT + threadIdx.x;
+    const uint32_t j = blk * 256 + threadIdx.x;
     const uint32_t i = j / WG, wg = j % WG;
     typename FC::Acc fa = FC::zero();
     // compacted rows (cols.half != 0): commit g's item i is a table base of a strided pattern
@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(NT) k_fb_commit_small(const FbE<C>* __restrict
             if (w >= wb && d != 0) fa = FC::madd(fa, ti[fg.off(w) + (uint32_t)(d < 0 ? -d : d) - 1].u, d < 0);
         }
     }
-    fb_block_sum_store<C, NT>(fa, &part[blockIdx.x]);
+    fb_block_sum_store<C>(fa, &part[blockIdx.x]);
     // zero-copy completion: the block's partial (written by thread 0 above) is made visible system
     // wide, then its flag takes this launch's epoch -- the host polls the flags instead of waiting
     // for the stream (fb_commit_t)
@@ -635,15 +635,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         }
     }
     if (small) {  // small batch: latency path
-        // threads per block: each level of the block's add tree is one dependent quad add (~6 us on a
-        // lone wave) while the host adds a partial in ~0.2 us -- smaller blocks move levels to the
-        // host (VKZG_SMALL_NT = 64 / 128 / 256, read once; A/B probe)
-        static const uint32_t NTs = [] {
-            const char* e = getenv("VKZG_SMALL_NT");
-            const int v = e ? atoi(e) : 256;
-            return (uint32_t)(v == 64 || v == 128 ? v : 256);
-        }();
-        const uint32_t bpc = (uint32_t)((width * WG + NTs - 1) / NTs);
+        const uint32_t bpc = (uint32_t)((width * WG + 255) / 256);
         // VKZG_HOST_TIMING=1: launch-to-readback, host adds and normalisation on stderr (probe)
         static const bool timing = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
         auto now_us = [] {
@@ -665,14 +657,9 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
         const uint32_t epoch = ++ctx->small_epoch == 0 ? ++ctx->small_epoch : ctx->small_epoch;  // never 0
         if (poll)  // (fresh page-locked memory holds anything: no stale flag may match)
             for (uint32_t b = 0; b < nblk; b++) hflags[b] = 0;
-#define VK_FBS_(NTV)                                                                                            \
-    VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr, NTV>), batch * bpc, NTV, 0, t->fb.as<FbE<C>>(),   \
-              t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont, bpc, wpt, \
-              with_cols ? *cols : StrideCols{}, d_part, dflags, epoch)
-        if (NTs == 64) VK_FBS_(64);
-        else if (NTs == 128) VK_FBS_(128);
-        else VK_FBS_(256);
-#undef VK_FBS_
+        VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
+                  t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
+                  bpc, wpt, with_cols ? *cols : StrideCols{}, d_part, dflags, epoch);
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
         // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the

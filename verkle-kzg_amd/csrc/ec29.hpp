@@ -413,13 +413,13 @@ __device__ __forceinline__ typename FC::Acc fb_wave_sum29(typename FC::Acc v) {
 // of ~13 us plus 3 more on one thread. Every thread of the block must call it.
 template <class C, int NT = 256>
 __device__ __forceinline__ void fb_block_sum_store(typename Fast29<C>::type::Acc fa, typename C::Acc* out) {
-    static_assert(NT == 256 || NT == 128 || NT == 64, "one, two or four waves");
+    static_assert(NT == 256 || NT == 64, "a wave or four");
     using FC = typename Fast29<C>::type;
     using Acc = typename C::Acc;
     if constexpr (FC::quad) {
         __shared__ typename FC::Acc wq[NT / 64];
         const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, role = lane & 3, q0 = lane & ~3u;
-        constexpr uint32_t ITS = NT == 256 ? 9 : NT == 128 ? 8 : 7;
+        constexpr uint32_t ITS = NT == 256 ? 9 : 7;
         typename FC::Acc v = shfl_idx_pod(fa, q0);
         for (uint32_t it = 0; it < ITS; it++) {  // one add call site
             typename FC::Acc o;
@@ -432,7 +432,7 @@ __device__ __forceinline__ void fb_block_sum_store(typename Fast29<C>::type::Acc
                     if (lane == 0) wq[wave] = v;
                     __syncthreads();
                     if (wave != 0) break;
-                    v = (lane >> 2) < (uint32_t)(NT / 64) ? wq[lane >> 2] : FC::zero();
+                    v = (lane >> 2) < 4 ? wq[lane >> 2] : FC::zero();
                 }
                 o = shfl_xor_pod(v, 4u << (it - 7));
             }
@@ -444,15 +444,11 @@ __device__ __forceinline__ void fb_block_sum_store(typename Fast29<C>::type::Acc
         if constexpr (NT == 64) {
             if (threadIdx.x == 0) *out = acc;
         } else {
-            __shared__ Acc wsum[NT / 64];
+            __shared__ Acc wsum[4];
             const int wave = threadIdx.x / 64;
             if ((threadIdx.x & 63) == 0) wsum[wave] = acc;
             __syncthreads();
-            if (threadIdx.x == 0) {
-                Acc t = C::add(wsum[0], wsum[1]);
-                if constexpr (NT == 256) t = C::add(t, C::add(wsum[2], wsum[3]));
-                *out = t;
-            }
+            if (threadIdx.x == 0) *out = C::add(C::add(wsum[0], wsum[1]), C::add(wsum[2], wsum[3]));
         }
     }
 }
