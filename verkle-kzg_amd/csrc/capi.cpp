@@ -3,6 +3,9 @@
 #include <atomic>
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -252,6 +255,7 @@ int vc_ctx_create(int curve, int device, vc_ctx** out) {
     c->device = device;
     c->pin_small.flags = hipHostMallocCoherent;
     c->pin_norm_vk.flags = hipHostMallocCoherent;  // written by kernels, polled by the host
+    c->pin[0].flags = c->pin[1].flags = hipHostMallocCoherent;  // the MSM tails' points and flags
     hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         vk::last_hip_error() = e;
@@ -458,7 +462,13 @@ int vc_msm_device(vc_ctx* ctx, int id, size_t offset, const void* d_sc, size_t n
     Guard g(ctx);
     std::vector<uint32_t> acc(vk::point_words(ctx->curve));
     VK_TRY(msm_device_acc(ctx, id, offset, d_sc, n, mont, acc.data()));
-    return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
+    static const bool timing = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+    if (!timing) return vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
+    const auto a0 = std::chrono::steady_clock::now();
+    const int st = vk::acc_to_affine(ctx->curve, acc.data(), out_xy, out_inf);
+    fprintf(stderr, "msm_affine_us=%.1f\n",
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a0).count());
+    return st;
 }
 
 int vc_msm_device_many(vc_ctx* ctx, int id, const void* const* d_scalars, const int* mont, size_t n, size_t count,

@@ -215,6 +215,7 @@ struct vc_ctx {
     int opt_host_chunks = 2;                 // vc_msm: scalar copies in this many chunks (msm_run_host)
     uint32_t fb_lanes = 0;                // resident lanes of k_fb_commit_cm (cached per context)
     uint32_t small_epoch = 0;             // completion-flag epoch of the latency path's launches
+    uint32_t tail_epoch = 0;              // the same for the MSM tails' direct completion (pin[0 / 1])
     uint32_t norm_vk_parity = 0;          // the half of pin_norm_vk the last verkle normalisation used
     // geometry of the last MSM (vc_msm_last_plan): window bits c, windows W (of the whole MSM),
     // terms per point (2 with the GLV split), radix multiplier m (radix m 2^c; 1 = 2^c), shared

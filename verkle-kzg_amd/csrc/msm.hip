@@ -15,7 +15,9 @@
 // thread is fixed (M entries) even when every scalar hits one bucket.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
+#include <immintrin.h>
 #include <cstdio>
 #include <hipcub/hipcub.hpp>
 
@@ -1313,6 +1315,12 @@ struct MsmSlice {
     FAcc<C>* bucket_dst = nullptr;
     uint32_t* chain_dst = nullptr;
     bool skip_reduce = false;
+    // direct completion (TailDirect): the final stage wrote the points and the chain word into the
+    // lane's fine-grained page-locked buffer, then `nflags` flags at flag_off took `epoch`
+    bool direct = false;
+    uint32_t epoch = 0, nflags = 0;
+    size_t flag_off = 0;
+    double t_launch0 = 0.0;  // VKZG_HOST_TIMING: when the slice's first kernel was launched (us)
     // BLS12-381 radix digits still to be made (msm_run_t leaves the GLV split to slice_enqueue,
     // which fuses the sort histogram into it when the geometry allows): sc == nullptr otherwise
     struct {
@@ -1469,6 +1477,10 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
     sl.tail = ws[WS_TAIL].as<Acc>();
 
     bool counts_ready = false;
+    static const bool timing = getenv("VKZG_HOST_TIMING") && atoi(getenv("VKZG_HOST_TIMING")) != 0;
+    if (timing)
+        sl.t_launch0 =
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
     if constexpr (std::is_same<C, BLS381G1>::value) {
         if (!sl.radix.sc.empty()) {
             // whole bucket sets over all their windows, whole sort blocks of scalars: the GLV split
@@ -1519,8 +1531,32 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
         VK_TRY(msm_tail_fixup_walk<C>(ctx, L, sl.offsets, NBtot, M, sl.buckets, sl.carry, sl.owner, 1u << sl.guard,
                                       sl.owner_b, sl.through, Tmax));
     if (sl.skip_reduce) return VC_OK;
-    VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, Wr, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part,
-                              sl.tail, nU > 1));
+    // direct completion: the final stage writes its W (J + nU) points and the chain word straight
+    // into the lane's fine-grained page-locked buffer and flags each block; the host polls the flags
+    // (slice_finish) -- no read-back copy (a ~4-us blit plus its dispatch) and no stream wake-up
+    // (~10-20 us). VKZG_TAIL_POLL=0 (A/B probe): copy and wait.
+    static const bool poll_env = !(getenv("VKZG_TAIL_POLL") && atoi(getenv("VKZG_TAIL_POLL")) == 0);
+    TailDirect td;
+    Acc* out = sl.tail;
+    sl.direct = false;
+    if (poll_env && L.pin->flags == hipHostMallocCoherent) {
+        sl.nflags = (uint32_t)Wr * (J + nU);
+        sl.flag_off = tail_bytes + 16;
+        VK_TRY(L.pin->ensure(sl.flag_off + (size_t)sl.nflags * 4));
+        // (fresh page-locked memory holds anything: no stale flag may match)
+        volatile uint32_t* hf = reinterpret_cast<volatile uint32_t*>(static_cast<uint8_t*>(L.pin->p) + sl.flag_off);
+        for (uint32_t k = 0; k < sl.nflags; k++) hf[k] = 0;
+        sl.epoch = ++ctx->tail_epoch == 0 ? ++ctx->tail_epoch : ctx->tail_epoch;  // never 0
+        uint8_t* dbase = static_cast<uint8_t*>(L.pin->dp);
+        td.flags = reinterpret_cast<uint32_t*>(dbase + sl.flag_off);
+        td.epoch = sl.epoch;
+        td.chain_src = sl.chain_max;
+        td.chain_dst = reinterpret_cast<uint32_t*>(dbase + tail_bytes);
+        out = reinterpret_cast<Acc*>(dbase);
+        sl.direct = true;
+    }
+    VK_TRY(msm_tail_reduce<C>(ctx, L, sl.buckets, sl.offsets, NB, Wr, Lseg, S, J, sl.seg, sl.rs, sl.bsum_part, out,
+                              nU > 1, sl.direct ? &td : nullptr));
     return VC_OK;
 }
 
@@ -1528,8 +1564,32 @@ static int slice_enqueue(vc_ctx* ctx, MsmSlice<C>& sl, Src src, size_t nv, const
 template <class C>
 static int slice_fetch(MsmSlice<C>& sl) {
     sl.ht.resize((size_t)sl.Wr * (sl.J + sl.nU));
+    if (sl.direct) return VC_OK;  // written in place by the final stage
     VK_TRY(sl.L.pin->ensure(sl.tail_bytes + 16));
     VK_CHECK_HIP(hipMemcpyAsync(sl.L.pin->p, sl.tail, sl.tail_bytes + 4, hipMemcpyDeviceToHost, sl.L.st));
+    return VC_OK;
+}
+
+// the wait for a slice's results: its flags at this epoch (direct completion), bounded -- past
+// 20 ms (a first launch loading its code, or a fault) the stream wait, which also reports errors
+template <class C>
+static int slice_wait(const MsmSlice<C>& sl) {
+    if (sl.direct) {
+        const volatile uint32_t* hf =
+            reinterpret_cast<const volatile uint32_t*>(static_cast<const uint8_t*>(sl.L.pin->p) + sl.flag_off);
+        const auto w0 = std::chrono::steady_clock::now();
+        for (uint32_t spins = 0;; spins++) {
+            uint32_t k = 0;
+            while (k < sl.nflags && hf[k] == sl.epoch) k++;
+            if (k == sl.nflags) {
+                std::atomic_thread_fence(std::memory_order_acquire);
+                return VC_OK;
+            }
+            if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(20)) break;
+            _mm_pause();
+        }
+    }
+    VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
     return VC_OK;
 }
 
@@ -1564,7 +1624,7 @@ static typename C::Acc shared_set_sum(const MsmSlice<C>& sl, int set) {
 template <class C>
 static int slice_finish(vc_ctx* ctx, MsmSlice<C>& sl, typename C::Acc* res) {
     using Acc = typename C::Acc;
-    VK_CHECK_HIP(hipStreamSynchronize(sl.L.st));
+    VK_TRY(slice_wait<C>(sl));
     memcpy(sl.ht.data(), sl.L.pin->p, sl.ht.size() * sizeof(Acc));
     memcpy(&sl.Lmax, static_cast<const uint8_t*>(sl.L.pin->p) + sl.tail_bytes, 4);
     if (sl.Lmax > (1u << sl.guard)) {  // rare (heavily repeated scalars): pointer jumping, redo the tail
@@ -1827,8 +1887,8 @@ static int msm_run_t(vc_ctx* ctx, Table* t, size_t offset, const uint32_t* d_sc,
         res = C::add(res, r);
     }
     if (host_timing())
-        fprintf(stderr, "msm_host n=%zu enqueue_us=%.1f wait_us=%.1f fold_us=%.1f\n", n, t_enq - t_entry,
-                t_sync - t_enq, now_us() - t_sync);
+        fprintf(stderr, "msm_host n=%zu first_launch_us=%.1f enqueue_us=%.1f wait_us=%.1f fold_us=%.1f\n", n,
+                sl[0].t_launch0 - t_entry, t_enq - t_entry, t_sync - t_enq, now_us() - t_sync);
     if (nsl == 2) {  // later work on the context's stream stays ordered after lane 1
         join = ctx->get_event();
         VK_CHECK_HIP(hipEventRecord(join, ctx->side_stream));

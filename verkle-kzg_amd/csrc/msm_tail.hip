@@ -449,12 +449,22 @@ struct PartLoc {
     }
 };
 
+// the final stage's completion in direct mode (TailDirect): the block's point (and, for block 0,
+// the chain word) reach host memory before its flag does
+__device__ __forceinline__ void tail_flag(TailDirect d, uint32_t sum) {
+    if (d.flags == nullptr) return;
+    if (sum == 0 && d.chain_dst) *d.chain_dst = *d.chain_src;
+    __threadfence_system();
+    __hip_atomic_store(&d.flags[sum], d.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // stage 2: one wave per (w, q) sum folds its partials (nb1 or nb2: ceil(n/64) per lane, then
 // the butterfly)
 template <class C, class A>
 __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __restrict__ partial, uint32_t J,
                                                    uint32_t h, uint32_t nU, uint32_t nb1, uint32_t nb2,
-                                                   uint32_t pL, uint32_t urow, typename C::Acc* __restrict__ out) {
+                                                   uint32_t pL, uint32_t urow, typename C::Acc* __restrict__ out,
+                                                   TailDirect dir) {
     using Acc = typename A::Acc;
     const uint32_t sum = blockIdx.x, lane = threadIdx.x;
     const PartLoc loc(sum, J, h, nU, nb1, nb2, pL, urow != 0);
@@ -476,7 +486,10 @@ __global__ void __launch_bounds__(64) k_msm_sumpart(const typename A::Acc* __res
         }
         v = A::add(v, o);
     }
-    if (lane == 0) out[sum] = A::store(v);
+    if (lane == 0) {
+        out[sum] = A::store(v);
+        tail_flag(dir, sum);
+    }
 }
 
 // the same on quads (SW curves): 16 logical lanes per wave, each a quad running the 4-lane
@@ -490,7 +503,8 @@ template <class C, class A>
 __global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const typename A::Acc* __restrict__ partial,
                                                                      uint32_t J, uint32_t h, uint32_t nU,
                                                                      uint32_t nb1, uint32_t nb2, uint32_t pL,
-                                                                     uint32_t urow, typename C::Acc* __restrict__ out) {
+                                                                     uint32_t urow, typename C::Acc* __restrict__ out,
+                                                                     TailDirect dir) {
     using Acc = typename A::Acc;
     constexpr uint32_t QPB = 16 * SUMPART_WAVES, LGW = SUMPART_WAVES == 4 ? 2 : SUMPART_WAVES == 2 ? 1 : 0;
     static_assert((1u << LGW) == SUMPART_WAVES, "SUMPART_WAVES: 1, 2 or 4");
@@ -518,7 +532,10 @@ __global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const type
         }
         v = A::add_quad(v, o, role);
     }
-    if (tid == 0) out[sum] = A::store(v);
+    if (tid == 0) {
+        out[sum] = A::store(v);
+        tail_flag(dir, sum);
+    }
 }
 
 // pointer-jumping rounds r0 <= r < r1 (span 2^r) for a host-known Lmax, or -- guarded -- rounds
@@ -623,8 +640,9 @@ int msm_tail_fixup_more(vc_ctx* ctx, Lane L, uint32_t T, const uint32_t* Lp, uin
 template <class C>
 int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
-                    typename C::Acc* out, bool residue) {
+                    typename C::Acc* out, bool residue, const TailDirect* direct) {
     using A = typename Fast29<C>::type;
+    const TailDirect dir = direct ? *direct : TailDirect{};
     const uint32_t* toff = nullptr;
     const uint32_t* uoff = nullptr;
     const FAcc<C>* usrc = accs;
@@ -670,10 +688,10 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
                  nU, tp.K, tp.nb1, tp.nb2, tp.pL, tp.gL, tp.gH, n_waves, toff, uoff, partial);
     if constexpr (A::quad)
         VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart_q<C, A>), sums, 64 * SUMPART_WAVES, 0, partial, J, tp.h,
-                     nU, tp.nb1, tp.nb2, tp.pL, tp.urow ? 1u : 0u, out);
+                     nU, tp.nb1, tp.nb2, tp.pL, tp.urow ? 1u : 0u, out, dir);
     else
         VK_LAUNCH_ON(ctx, L.st, "msm_sumpart", (k_msm_sumpart<C, A>), sums, 64, 0, partial, J, tp.h, nU, tp.nb1,
-                     tp.nb2, tp.pL, tp.urow ? 1u : 0u, out);
+                     tp.nb2, tp.pL, tp.urow ? 1u : 0u, out, dir);
     return VC_OK;
 }
 
@@ -685,7 +703,7 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
     template int msm_tail_fixup_walk<C>(vc_ctx*, Lane, const uint32_t*, uint32_t, uint32_t, FAcc<C>*, const FAcc<C>*, \
                                         const FAcc<C>*, uint32_t, const uint32_t*, const uint8_t*, uint32_t);                                             \
     template int msm_tail_reduce<C>(vc_ctx*, Lane, const FAcc<C>*, const uint32_t*, uint32_t, int, uint32_t, uint32_t, \
-                                    uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*, bool);
+                                    uint32_t, FAcc<C>*, FAcc<C>*, FAcc<C>*, C::Acc*, bool, const TailDirect*);
 VK_INST_TAIL(BN254G1)
 VK_INST_TAIL(BLS381G1)
 VK_INST_TAIL(Bandersnatch)

@@ -155,8 +155,18 @@ inline uint32_t msm_fixup_guard_rounds(size_t nv, uint32_t NB, uint32_t M) {
     while ((1ull << r) < chain && r < 6) r++;
     return r;
 }
+// Direct completion of the reduction: `out` is the device address of fine-grained page-locked
+// memory, each final-stage block writes its point there, block 0 also copies *chain_src (the
+// accumulate's longest chain) to *chain_dst, and then the block's flag takes `epoch` (system-scope
+// release). The host polls the flags instead of a read-back copy and a stream wait.
+struct TailDirect {
+    uint32_t* flags = nullptr;
+    uint32_t epoch = 0;
+    const uint32_t* chain_src = nullptr;
+    uint32_t* chain_dst = nullptr;
+};
 template <class C>
 int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t* offsets, uint32_t NB, int W,
                     uint32_t Lseg, uint32_t S, uint32_t J, FAcc<C>* accs, FAcc<C>* Rs, FAcc<C>* partial,
-                    typename C::Acc* out, bool residue = false);
+                    typename C::Acc* out, bool residue = false, const TailDirect* direct = nullptr);
 }  // namespace vk
