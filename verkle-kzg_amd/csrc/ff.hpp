@@ -346,82 +346,190 @@ VK_HD bool fe_is_one_raw(const fe<F>& a) {
     return o == 0;
 }
 #ifndef __HIP_DEVICE_COMPILE__
-// Host inverse: the binary extended Euclid below on 64-bit limbs (half the limb steps of the
-// 32-bit version). On the GPU box's host, BLS12-381 Fq: 7.4 us against 13.2 us (32-bit limbs) and
-// 15 us for Fermat with a 5-bit window (tools/hostinv.cpp). It is the last serial step of every
-// MSM call (acc_to_affine) and of every IPA round's normalisation.
+// Host inverse by Bernstein-Yang divsteps (variable time), 62 at a time on signed 62-bit limbs:
+// each batch is found from the low 64 bits of f and g alone (a 2x2 transition matrix with entries
+// below 2^62), then applied to the full-size f, g (exact division by 2^62) and to the Bezout
+// coefficients d, e (kept in (-2p, p); a multiple of p added so the division by 2^62 is exact).
+// ~12-18 batches for a 381-bit modulus. It is the last serial step of every MSM call
+// (acc_to_affine) and of every IPA round's normalisation: on the GPU box's host the 64-bit binary
+// Euclid it replaces took ~8 us for BLS12-381 Fq (tools/hostinv.cpp; tests/cpp/inv_check.cpp
+// checks both against a^(p-2)).
 template <class F>
-inline fe<F> fe_inv_host(const fe<F>& a_mont) {
-    constexpr int M = F::N / 2;
-    typedef unsigned __int128 u128;
-    uint64_t p[M], u[M], v[M], x1[M] = {1}, x2[M] = {0};
-    for (int i = 0; i < M; i++) p[i] = (uint64_t)F::p(2 * i) | ((uint64_t)F::p(2 * i + 1) << 32);
-    memcpy(u, a_mont.v, sizeof u);
-    memcpy(v, p, sizeof v);
-    auto one = [](const uint64_t* a) {
-        if (a[0] != 1) return false;
-        for (int i = 1; i < M; i++)
-            if (a[i]) return false;
-        return true;
-    };
-    auto shr1 = [](uint64_t* a, uint64_t top) {
-        for (int i = 0; i < M - 1; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 63);
-        a[M - 1] = (a[M - 1] >> 1) | (top << 63);
-    };
-    auto addp = [&](uint64_t* a) {
-        u128 c = 0;
-        for (int i = 0; i < M; i++) {
-            c += (u128)a[i] + p[i];
-            a[i] = (uint64_t)c;
-            c >>= 64;
+struct Sg62 {
+    static constexpr int M = F::N / 2;                      // 64-bit words of the field
+    static constexpr int L = (64 * M + 2 + 61) / 62;        // signed 62-bit limbs (value and sign)
+    static constexpr uint64_t M62 = ~(uint64_t)0 >> 2;
+    int64_t mod[L];
+    uint64_t inv62;                                         // p^-1 mod 2^62
+    constexpr Sg62() : mod(), inv62(0) {
+        uint64_t w[M] = {};
+        for (int i = 0; i < M; i++) w[i] = (uint64_t)F::p(2 * i) | ((uint64_t)F::p(2 * i + 1) << 32);
+        for (int k = 0; k < L; k++) {
+            const int o = 62 * k, wi = o / 64, sh = o % 64;
+            uint64_t x = wi < M ? w[wi] >> sh : 0;
+            if (sh > 2 && wi + 1 < M) x |= w[wi + 1] << (64 - sh);
+            mod[k] = (int64_t)(x & M62);
         }
-        return (uint64_t)c;
-    };
-    auto geq = [](const uint64_t* a, const uint64_t* b) {
-        for (int i = M - 1; i >= 0; i--)
-            if (a[i] != b[i]) return a[i] > b[i];
-        return true;
-    };
-    auto sub = [](uint64_t* a, const uint64_t* b) {
-        uint64_t br = 0;
-        for (int i = 0; i < M; i++) {
-            const u128 d = (u128)a[i] - b[i] - br;
-            a[i] = (uint64_t)d;
-            br = (uint64_t)(d >> 64) & 1;
-        }
-    };
-    auto subm = [&](uint64_t* a, const uint64_t* b) {  // a - b mod p, both in [0, p)
-        if (geq(a, b)) {
-            sub(a, b);
+        uint64_t x = 1;
+        for (int i = 0; i < 7; i++) x *= 2 - w[0] * x;  // p^-1 mod 2^64 (Newton)
+        inv62 = x & M62;
+    }
+};
+struct SgT {
+    int64_t u, v, q, r;
+};
+// 62 divsteps on the low bits: returns the new eta (= -delta), the matrix in t
+inline int64_t sg_divsteps62(int64_t eta, uint64_t f, uint64_t g, SgT& t) {
+    uint64_t u = 1, v = 0, q = 0, r = 1;
+    int i = 62;
+    for (;;) {
+        const int zeros = __builtin_ctzll(g | (~(uint64_t)0 << i));  // sentinel at bit i
+        g >>= zeros;
+        u <<= zeros;
+        v <<= zeros;
+        eta -= zeros;
+        i -= zeros;
+        if (i == 0) break;
+        uint64_t w;
+        int limit;
+        if (eta < 0) {  // swap: (f, g) <- (g, -f)
+            eta = -eta;
+            uint64_t tmp = f;
+            f = g;
+            g = 0 - tmp;
+            tmp = u;
+            u = q;
+            q = 0 - tmp;
+            tmp = v;
+            v = r;
+            r = 0 - tmp;
+            limit = ((int)eta + 1) > i ? i : ((int)eta + 1);
+            const uint64_t m = (~(uint64_t)0 >> (64 - limit)) & 63u;
+            w = (f * g * (f * f - 2)) & m;  // -g / f mod 2^6 (f (2 - f^2) = f^-1 mod 64)
         } else {
-            uint64_t t[M];
-            memcpy(t, b, sizeof t);
-            sub(t, a);
-            memcpy(a, p, sizeof t);
-            sub(a, t);
+            limit = ((int)eta + 1) > i ? i : ((int)eta + 1);
+            const uint64_t m = (~(uint64_t)0 >> (64 - limit)) & 15u;
+            w = f + (((f + 1) & 4) << 1);  // f^-1 mod 16
+            w = (0 - w * g) & m;
         }
-    };
-    while (!one(u) && !one(v)) {
-        while ((u[0] & 1) == 0) {
-            shr1(u, 0);
-            const uint64_t c = (x1[0] & 1) ? addp(x1) : 0;
-            shr1(x1, c);
-        }
-        while ((v[0] & 1) == 0) {
-            shr1(v, 0);
-            const uint64_t c = (x2[0] & 1) ? addp(x2) : 0;
-            shr1(x2, c);
-        }
-        if (geq(u, v)) {
-            sub(u, v);
-            subm(x1, x2);
-        } else {
-            sub(v, u);
-            subm(x2, x1);
+        g += f * w;
+        q += u * w;
+        r += v * w;
+    }
+    t.u = (int64_t)u;
+    t.v = (int64_t)v;
+    t.q = (int64_t)q;
+    t.r = (int64_t)r;
+    return eta;
+}
+// canonical a (not Montgomery; 0 < a < p) -> a^-1 mod p, canonical
+template <class F>
+inline fe<F> fe_inv_canon_host(const fe<F>& a) {
+    typedef __int128 i128;
+    static constexpr Sg62<F> S{};
+    constexpr int L = Sg62<F>::L, M = Sg62<F>::M;
+    constexpr int64_t M62 = (int64_t)Sg62<F>::M62;
+    int64_t d[L] = {}, e[L] = {}, f[L], g[L] = {};
+    e[0] = 1;
+    for (int k = 0; k < L; k++) f[k] = S.mod[k];
+    {
+        uint64_t w[M];
+        memcpy(w, a.v, sizeof w);
+        for (int k = 0; k < L; k++) {
+            const int o = 62 * k, wi = o / 64, sh = o % 64;
+            uint64_t x = wi < M ? w[wi] >> sh : 0;
+            if (sh > 2 && wi + 1 < M) x |= w[wi + 1] << (64 - sh);
+            g[k] = (int64_t)(x & (uint64_t)M62);
         }
     }
-    fe<F> r, r2;
-    memcpy(r.v, one(u) ? x1 : x2, sizeof u);  // (aR)^-1
+    int len = L;
+    int64_t eta = -1;
+    for (;;) {
+        SgT t;
+        eta = sg_divsteps62(eta, (uint64_t)f[0], (uint64_t)g[0], t);
+        // (d, e) <- (t [d, e] + p [md, me]) / 2^62
+        {
+            const int64_t sd = d[L - 1] >> 63, se = e[L - 1] >> 63;
+            int64_t md = (t.u & sd) + (t.v & se), me = (t.q & sd) + (t.r & se);
+            i128 cd = (i128)t.u * d[0] + (i128)t.v * e[0], ce = (i128)t.q * d[0] + (i128)t.r * e[0];
+            md -= (int64_t)((S.inv62 * (uint64_t)cd + (uint64_t)md) & (uint64_t)M62);
+            me -= (int64_t)((S.inv62 * (uint64_t)ce + (uint64_t)me) & (uint64_t)M62);
+            cd += (i128)S.mod[0] * md;
+            ce += (i128)S.mod[0] * me;
+            cd >>= 62;
+            ce >>= 62;
+            for (int i = 1; i < L; i++) {
+                cd += (i128)t.u * d[i] + (i128)t.v * e[i] + (i128)S.mod[i] * md;
+                ce += (i128)t.q * d[i] + (i128)t.r * e[i] + (i128)S.mod[i] * me;
+                d[i - 1] = (int64_t)cd & M62;
+                cd >>= 62;
+                e[i - 1] = (int64_t)ce & M62;
+                ce >>= 62;
+            }
+            d[L - 1] = (int64_t)cd;
+            e[L - 1] = (int64_t)ce;
+        }
+        // (f, g) <- t [f, g] / 2^62 over the live limbs
+        {
+            i128 cf = (i128)t.u * f[0] + (i128)t.v * g[0], cg = (i128)t.q * f[0] + (i128)t.r * g[0];
+            cf >>= 62;
+            cg >>= 62;
+            for (int i = 1; i < len; i++) {
+                cf += (i128)t.u * f[i] + (i128)t.v * g[i];
+                cg += (i128)t.q * f[i] + (i128)t.r * g[i];
+                f[i - 1] = (int64_t)cf & M62;
+                cf >>= 62;
+                g[i - 1] = (int64_t)cg & M62;
+                cg >>= 62;
+            }
+            f[len - 1] = (int64_t)cf;
+            g[len - 1] = (int64_t)cg;
+        }
+        if (g[0] == 0) {
+            int64_t c = 0;
+            for (int j = 1; j < len; j++) c |= g[j];
+            if (c == 0) break;  // g = 0: f = +-1
+        }
+        // shorten when the top limbs of f and g are both 0 or -1
+        const int64_t fn = f[len - 1], gn = g[len - 1];
+        if (len > 1 && (fn ^ (fn >> 63)) == 0 && (gn ^ (gn >> 63)) == 0) {
+            f[len - 2] |= (int64_t)((uint64_t)fn << 62);
+            g[len - 2] |= (int64_t)((uint64_t)gn << 62);
+            len--;
+        }
+    }
+    // d in (-2p, p) -> d sign(f) in [0, p)
+    {
+        int64_t c = d[L - 1] >> 63;
+        for (int i = 0; i < L; i++) d[i] += S.mod[i] & c;
+        const int64_t neg = f[len - 1] >> 63;
+        for (int i = 0; i < L; i++) d[i] = (d[i] ^ neg) - neg;
+        for (int i = 0; i < L - 1; i++) {
+            d[i + 1] += d[i] >> 62;
+            d[i] &= M62;
+        }
+        c = d[L - 1] >> 63;
+        for (int i = 0; i < L; i++) d[i] += S.mod[i] & c;
+        for (int i = 0; i < L - 1; i++) {
+            d[i + 1] += d[i] >> 62;
+            d[i] &= M62;
+        }
+    }
+    uint64_t w[M] = {};
+    for (int k = 0; k < L; k++) {  // 62-bit limbs back to 64-bit words
+        const int o = 62 * k, wi = o / 64, sh = o % 64;
+        const uint64_t x = (uint64_t)d[k];
+        if (wi < M) w[wi] |= x << sh;
+        if (sh > 2 && wi + 1 < M) w[wi + 1] |= x >> (64 - sh);
+    }
+    fe<F> r;
+    memcpy(r.v, w, sizeof w);
+    return r;
+}
+// for aR (Montgomery form of a != 0) returns a^-1 R
+template <class F>
+inline fe<F> fe_inv_host(const fe<F>& a_mont) {
+    fe<F> r = fe_inv_canon_host<F>(a_mont), r2;  // (aR)^-1
     for (int i = 0; i < F::N; i++) r2.v[i] = F::r2(i);
     return fe_mul<F>(fe_mul<F>(r, r2), r2);  // (aR)^-1 R^2 = a^-1 R
 }

@@ -1,8 +1,8 @@
 // Host Montgomery inversion variants for BLS12-381 Fq (the last serial step of every MSM call:
-// acc_to_affine): the library's host fe_inv_bin (now the 64-bit-limb binary Euclid, fe_inv_host),
-// the 32-bit-limb binary Euclid it replaced, and a standalone 64-bit-limb binary Euclid. Measured
-// on the GPU box's host before the switch: Fermat with a 5-bit window 15 us, 32-bit binary 13.2 us,
-// 64-bit binary 7.4 us.
+// acc_to_affine): the library's host fe_inv_bin (since round 5 the divstep inverse, fe_inv_host in
+// csrc/ff.hpp), the 32-bit-limb binary Euclid and the standalone 64-bit-limb binary Euclid it
+// replaced. Measured on the GPU box's host: Fermat with a 5-bit window 15 us, 32-bit binary 13.2
+// us, 64-bit binary 7.4 us, divsteps 1.2 us (tools/hostops.cpp, profiles/r05/host_ops/).
 // build: hipcc -O3 --offload-arch=gfx950 -I.. hostinv.cpp -o hostinv   (host code only)
 #include <hip/hip_runtime.h>
 #include <chrono>
