@@ -670,12 +670,30 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
                                         ctx->stream));
         if (overlap && *overlap) (*overlap)();
         bool seen = false;
+        // the partials serially on this thread (the host pool's wake-up cost more than the ~23 us
+        // of adds of the IPA prover's 2 x 33 partials: prove 0.89 -> 1.07 ms); while polling, each
+        // block's partial is added as soon as its flag arrives, so the adds overlap the blocks
+        // that finish later. Then one batched inversion.
+        std::vector<Acc> sums(batch);
+        // VKZG_SMALL_INCR=0 (read once; A/B probe): add the partials after the last flag instead
+        static const bool incr = !(getenv("VKZG_SMALL_INCR") && atoi(getenv("VKZG_SMALL_INCR")) == 0);
         if (poll) {  // every block's flag at this epoch: the partials are in host memory
+            std::vector<uint8_t> done(nblk, 0), have(batch, 0);
+            uint32_t ndone = 0;
             const auto w0 = std::chrono::steady_clock::now();
             for (uint32_t spins = 0;; spins++) {
-                uint32_t b = 0;
-                while (b < nblk && hflags[b] == epoch) b++;
-                if (b == nblk) {
+                for (uint32_t b = 0; b < nblk; b++) {
+                    if (done[b] || hflags[b] != epoch) continue;
+                    if (incr) {
+                        std::atomic_thread_fence(std::memory_order_acquire);
+                        const uint32_t g = b / bpc;
+                        sums[g] = have[g] ? C::add(sums[g], parts[b]) : parts[b];
+                        have[g] = 1;
+                    }
+                    done[b] = 1;
+                    ndone++;
+                }
+                if (ndone == nblk) {
                     seen = true;
                     break;
                 }
@@ -686,27 +704,26 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
                     break;
                 _mm_pause();
             }
-            std::atomic_thread_fence(std::memory_order_acquire);
         }
-        if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         const double t1 = timing ? now_us() : 0.0;
+        if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        if (!seen || !incr) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            for (size_t g = 0; g < batch; g++) {
+                Acc a = parts[g * bpc];
+                for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
+                sums[g] = a;
+            }
+        }
         const int nl = (int)(C::F::N / 2);
         std::vector<uint64_t> oxy(h_out_xy ? 0 : (size_t)batch * 2 * nl);
         std::vector<uint8_t> oinf(h_out_xy ? 0 : batch);
         uint64_t* rxy = h_out_xy ? h_out_xy : oxy.data();
         uint8_t* rinf = h_out_xy ? h_out_inf : oinf.data();
-        // the partials serially (the host pool's wake-up cost more than the ~23 us of adds of the
-        // IPA prover's 2 x 33 partials: prove 0.89 -> 1.07 ms), then one batched inversion
-        std::vector<Acc> sums(batch);
-        for (size_t g = 0; g < batch; g++) {
-            Acc a = parts[g * bpc];
-            for (uint32_t b = 1; b < bpc; b++) a = C::add(a, parts[g * bpc + b]);
-            sums[g] = a;
-        }
         const double t2 = timing ? now_us() : 0.0;
         VK_TRY(acc_to_affine_batch(ctx->curve, reinterpret_cast<const uint32_t*>(sums.data()), batch, rxy, rinf));
         if (timing)
-            fprintf(stderr, "[fb_small] %zu x %u partials: launch..readback %.1f us, adds %.1f us, affine %.1f us\n",
+            fprintf(stderr, "[fb_small] %zu x %u partials: launch..last flag (adds overlapped) %.1f us, rest %.1f us, affine %.1f us\n",
                     batch, bpc, t1 - t0, t2 - t1, now_us() - t2);
         if (h_out_xy) {
             *on_host = true;
