@@ -1474,6 +1474,14 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         }
         lap("ext commits");
     }
+    // the dense (host-result) levels' staging stays alive until the one sync at the end, and the
+    // root's point is taken from them when the root was on such a level (no read-back)
+    std::vector<std::vector<uint64_t>> keep64;
+    std::vector<std::vector<uint8_t>> keep8;
+    std::vector<uvec<uint32_t>> keep32;
+    uint64_t root_xy[8];
+    uint8_t root_inf = 1;
+    bool root_known = false;
     for (size_t oi = 0; oi < order.size(); oi++) {
         if (next_built <= oi) build_next();
         LevelLists& L = lists[oi & 1];
@@ -1523,7 +1531,18 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             VK_CHECK_HIP(hipMemcpyAsync(d_inf.p, hinf.data(), B, hipMemcpyHostToDevice, st));
             VK_CHECK_HIP(hipMemcpyAsync(d_it.p, hit.data(), B * 32, hipMemcpyHostToDevice, st));
             VK_TRY(scatter(d_ids, B, d_xy.p, d_inf.as<uint8_t>(), d_it.p));
-            VK_CHECK_HIP(hipStreamSynchronize(st));  // the host staging dies here
+            const uint32_t* h_ids = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(L.pin) + L.o_ids);
+            for (size_t b = 0; b < B; b++)
+                if (h_ids[b] == 0) {  // the root (node id 0)
+                    memcpy(root_xy, &hxy[8 * b], 64);
+                    root_inf = hinf[b];
+                    root_known = true;
+                }
+            // the uploads above read these host vectors: kept (not synchronised) until the end
+            keep64.push_back(std::move(hxy));
+            keep64.push_back(std::move(hit));
+            keep8.push_back(std::move(hinf));
+            keep32.push_back(std::move(row));
             lap("internal level (dense)");
             continue;
         }
@@ -1569,10 +1588,15 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     // the root's commitment from the mirror (the rest stays there: host_valid = false)
     uint64_t rxy[8];
     uint8_t rinf = 1;
-    VK_CHECK_HIP(hipMemcpyAsync(rxy, m_cxy, 64, hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipMemcpyAsync(&rinf, m_inf, 1, hipMemcpyDeviceToHost, st));
+    if (root_known) {  // the root's level ran on the host-result path
+        memcpy(rxy, root_xy, 64);
+        rinf = root_inf;
+    } else {
+        VK_CHECK_HIP(hipMemcpyAsync(rxy, m_cxy, 64, hipMemcpyDeviceToHost, st));
+        VK_CHECK_HIP(hipMemcpyAsync(&rinf, m_inf, 1, hipMemcpyDeviceToHost, st));
+    }
     VK_CHECK_HIP(hipStreamSynchronize(st));  // also: every staging vector above may die now
-    lap("root read-back");
+    lap(root_known ? "final sync (root from the dense level)" : "root read-back");
     memcpy(out_xy, rxy, 64);
     *out_inf = rinf;
     t->clear_dirty();
