@@ -198,6 +198,7 @@ struct vc_ctx {
                                     // the kernel writes them straight to host memory)
     vk::PinBuf pin_norm;            // block products / inverses of the split normalisation
     vk::PinBuf pin_y;               // the KZG opening's y, copied back asynchronously
+    vk::PinBuf pin_mp;              // the multiproof finish's h - g, copied back ahead of the E commit
     vk::PinBuf pin_verkle;          // the verkle extension rows, merged straight into page-locked memory
     vk::PinBuf pin_verkle_lv[2];    // verkle levels' lists (one upload per level; the next level's are
                                     // built into the other one while the current level runs)

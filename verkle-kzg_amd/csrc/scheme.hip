@@ -817,7 +817,7 @@ __global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, co
     if (threadIdx.x == 0) Q[(size_t)zi * N + z] = fe_neg<F>(fe_mul<F>(sh[0], pw_inv[z]));
 }
 
-// g[k] = sum_z Q[z][k] ; h[k] = sum_z invt[z] S[z][k] ; hmg = h - g
+// g[k] = sum_z Q[z][k] ; h[k] = sum_z invt[z] S[z][k] ; hmg = h - g (when invt_z and hmg are given)
 // g[k] = sum_z Q[z][k], h[k] = sum_z invt_z[z] S[z][k]: a block per MP_CB_K columns, its 256
 // threads split the Z rows MP_CB_R ways (row-groups strided by MP_CB_R), partials added in LDS --
 // the one-thread-per-column form ran 256 dependent multiplies per thread on 4 waves (~0.15 ms of
@@ -825,7 +825,8 @@ __global__ void __launch_bounds__(256) k_mp_quot(const fe<F>* __restrict__ S, co
 constexpr uint32_t MP_CB_K = 16, MP_CB_R = 16;
 __global__ void __launch_bounds__(256) k_mp_combine(const fe<F>* __restrict__ S, const fe<F>* __restrict__ Q,
                                                     const fe<F>* __restrict__ invt_z, size_t N, uint32_t Z,
-                                                    fe<F>* __restrict__ g, fe<F>* __restrict__ h) {
+                                                    fe<F>* __restrict__ g, fe<F>* __restrict__ h,
+                                                    fe<F>* __restrict__ hmg) {
     __shared__ fe<F> pg[MP_CB_R][MP_CB_K], ph[MP_CB_R][MP_CB_K];
     const uint32_t kc = threadIdx.x % MP_CB_K, rg = threadIdx.x / MP_CB_K;
     const size_t k = (size_t)blockIdx.x * MP_CB_K + kc;
@@ -845,6 +846,7 @@ __global__ void __launch_bounds__(256) k_mp_combine(const fe<F>* __restrict__ S,
         }
         g[k] = gg;
         if (invt_z) h[k] = hh;
+        if (invt_z && hmg) hmg[k] = fe_sub<F>(hh, gg);
     }
 }
 
@@ -1813,34 +1815,51 @@ static int mp_finish(vc_ctx* ctx, int scheme, Table* t, size_t N, const std::vec
     VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, d_S.as<fe<F>>(), inv1, pw, pwi, d_zv.as<uint32_t>(), N,
               d_Q.as<fe<F>>());
     VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
-              (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
-    std::vector<Fr> g(N), h(N);
-    VK_CHECK_HIP(hipMemcpyAsync(g.data(), d_g.p, N * 32, hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipStreamSynchronize(st));
+              (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>(), (fe<F>*)nullptr);
+    // D = commit(g) and E = commit(h) read g / h in device memory (Montgomery scalars) on the latency
+    // path, which completes by polled flags: no read-back of g or h and no stream wait; h - g (the
+    // inner proof's data) is made on the device and copied into page-locked memory ahead of the E
+    // commit, so it is on the host when E's flags are
+    auto commit_dev = [&](const void* d_sc, uint64_t* xy, uint8_t* inf) -> int {
+        VK_TRY(ctx->ws[WS_MISC].ensure(65));
+        uint8_t* dxy_ = ctx->ws[WS_MISC].as<uint8_t>();
+        bool on_host = false;
+        VK_TRY(msm_batch_run(ctx, t, N, d_sc, 1, 1, dxy_, dxy_ + 64, xy, inf, &on_host, nullptr, nullptr));
+        if (on_host) return VC_OK;
+        uint8_t tmp[65];
+        VK_CHECK_HIP(hipMemcpyAsync(tmp, dxy_, 65, hipMemcpyDeviceToHost, st));
+        VK_CHECK_HIP(hipStreamSynchronize(st));
+        memcpy(xy, tmp, 64);
+        *inf = tmp[64];
+        return VC_OK;
+    };
     lap("sums, quotients, g");
-    // D = commit(g)
     uint64_t dxy[8];
     uint8_t dinf;
-    VK_TRY(commit_batch(ctx, t, N, g.data(), 1, dxy, &dinf));
+    VK_TRY(commit_dev(d_g.p, dxy, &dinf));
     lap("D");
     transcript_append_point(tr, dxy, dinf, "D");
     Fr tt = transcript_digest(tr, "t");
     std::vector<Fr> invs = invert_domain_at(tt, N);  // 1/(t - z), z an integer (utils.rs:57-62)
     std::vector<Fr> invz(Z);
     for (uint32_t k = 0; k < Z; k++) invz[k] = invs[zval[k]];
-    VK_CHECK_HIP(hipMemcpyAsync(d_it.p, invz.data(), Z * 32, hipMemcpyHostToDevice, st));
+    VK_TRY(ctx->pin_mp.ensure(N * 32 + (size_t)Z * 32));
+    uint8_t* pin_hmg = static_cast<uint8_t*>(ctx->pin_mp.p);
+    memcpy(pin_hmg + N * 32, invz.data(), Z * 32);
+    VK_CHECK_HIP(hipMemcpyAsync(d_it.p, pin_hmg + N * 32, Z * 32, hipMemcpyHostToDevice, st));
+    DevBuf d_hmg(ctx);
+    VK_TRY(d_hmg.ensure(N * 32));
     VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, d_S.as<fe<F>>(), d_Q.as<fe<F>>(),
-              d_it.as<fe<F>>(), N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>());
-    VK_CHECK_HIP(hipMemcpyAsync(h.data(), d_h.p, N * 32, hipMemcpyDeviceToHost, st));
-    VK_CHECK_HIP(hipStreamSynchronize(st));
+              d_it.as<fe<F>>(), N, Z, d_g.as<fe<F>>(), d_h.as<fe<F>>(), d_hmg.as<fe<F>>());
+    VK_CHECK_HIP(hipMemcpyAsync(pin_hmg, d_hmg.p, N * 32, hipMemcpyDeviceToHost, st));
     lap("t, h");
     uint64_t exy[8];
     uint8_t einf;
-    VK_TRY(commit_batch(ctx, t, N, h.data(), 1, exy, &einf));
+    VK_TRY(commit_dev(d_h.p, exy, &einf));  // (its completion follows the copy above in the stream)
     lap("E");
     transcript_append_point(tr, exy, einf, "E");
     std::vector<Fr> hmg(N);
-    for (size_t k = 0; k < N; k++) hmg[k] = fe_sub<F>(h[k], g[k]);
+    memcpy(hmg.data(), pin_hmg, N * 32);
     Acc mc = C::add(acc_of(exy, einf), C::neg(acc_of(dxy, dinf)));
     memcpy(d_xy, dxy, 64);
     *d_inf = dinf;
@@ -1985,7 +2004,8 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
             VK_LAUNCH(ctx, "mp_quot", k_mp_quot, Z, 256, 0, Sm[p]->as<fe<F>>(), inv1, pw, pwi, zv[p]->as<uint32_t>(), N,
                       Qb[p]->as<fe<F>>());
             VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
-                      (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N);
+                      (const fe<F>*)nullptr, N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N,
+                      (fe<F>*)nullptr);
             return VC_OK;
         };
         st = launch();
@@ -2011,7 +2031,8 @@ static int mp_prove_many(vc_ctx* ctx, int scheme, Table* t, size_t N, size_t Q, 
         }
         auto launch = [&]() -> int {
             VK_LAUNCH(ctx, "mp_combine", k_mp_combine, (N + MP_CB_K - 1) / MP_CB_K, 256, 0, Sm[p]->as<fe<F>>(), Qb[p]->as<fe<F>>(),
-                      it[p]->as<fe<F>>(), N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N);
+                      it[p]->as<fe<F>>(), N, Z, d_g.as<fe<F>>() + p * N, d_h.as<fe<F>>() + p * N,
+                      (fe<F>*)nullptr);
             return VC_OK;
         };
         st = launch();
