@@ -937,7 +937,10 @@ def verkle_line(a, local, stream):
     nk = a.verkle_keys
     keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
     vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
-    veng.fixed_base_precompute(kzg.table, 8)  # the SRS fixed-base tables, untimed (setup)
+    # the SRS fixed-base tables, untimed (setup): 16-bit windows (16 per scalar, 17.2 GB for the 256
+    # Lagrange points) -- half the table points per non-zero of c = 8's 32 windows: full commitment
+    # 3.47-3.60 -> 3.03-3.07 ms (profiles/r05/verkle/fb_c/)
+    veng.fixed_base_precompute(kzg.table, 16)
     # warm-up: one full commitment of an identical tree and one 1 % update of it (first-use
     # workspace and page-locked staging allocations of both paths; other keys than the timed update's)
     w = VerkleTree(32)
@@ -985,6 +988,7 @@ def verkle_line(a, local, stream):
     t_upd = time.perf_counter() - t0
     veng.close()
     return {"workload": f"verkle tree, {nk} random 32-unit keys, KZG(256) BN254 (8(f) rank 1)",
+            "srs_fixed_base": "16-bit windows, 16 per scalar, 17.2 GB (setup, untimed)",
             "nodes": st, "insert_s": t_ins, "full_commitment_ms": t_full * 1e3,
             "nodes_per_s_full": st["dirty"] / t_full, "full_kernel_ms_total": kms,
             "full_split_ms": {"gpu_kernels": gpu_ms, "host_and_transfers": t_full * 1e3 - gpu_ms},

@@ -164,7 +164,10 @@ int vc_msm_batch_device(vc_ctx* ctx, int table_id, size_t width, const void* d_s
 int vc_msm_batch_sparse(vc_ctx* ctx, int table_id, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                         const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);
 /* Build fixed-base window tables for a table (used by vc_msm_batch*); window_bits in [4, 20]
- * (n x ceil(bits/c) x 2^(c-1) entries of 108 B: 188 GB for 256 Bandersnatch bases at c = 20). */
+ * (n x ceil(bits/c) x 2^(c-1) entries of 128 B, one cache line each: 223 GB for 256 Bandersnatch
+ * bases at c = 20). A table that reaches a batched commit without them gets them on first use at
+ * the widest c <= 16 that fits what is left of the context's 20 GB budget for such tables
+ * (VKZG_FB_BUDGET_GB), at least 8: c = 16 (17.2 GB) for the first 257-point IPA CRS. */
 int vc_fixed_base_precompute(vc_ctx* ctx, int table_id, int window_bits);
 /* The same with `windows` signed-digit windows of window_bits or window_bits + 1 bits (the
  * last bits + 1 - window_bits * windows windows are the wider ones; window_bits in [4, 19]).

@@ -22,3 +22,6 @@ echo bench-done
 # the N > 1 flow end to end (two ranks on this one card, gloo + host-callback exchange)
 timeout -k 10 900 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline > $O/rehearse_2rank.json 2> $O/rehearse_2rank.err
 echo rehearse-done
+# one-card per-rank slices of the 2^20 MSM (point ranges / window parts at G = 2 and 8)
+timeout -k 10 300 python -u verkle-kzg_amd/tools/split_probe.py 1,2,8 > $O/split_probe.txt 2>&1
+echo split-done

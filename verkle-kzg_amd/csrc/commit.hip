@@ -595,6 +595,29 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
     return VC_OK;
 }
 
+// window bits of the fixed-base tables a commit builds on first use (a table without
+// vc_fixed_base_precompute: the IPA CRS of the prover / verifier, the multiproof's D / E): the
+// widest c <= 16 whose table fits what is left of the context's budget for such tables
+// (VKZG_FB_BUDGET_GB, default 20 GB of the card's 288, less the ones built before), at least 8.
+// Fewer windows mean fewer table points per commit, hence fewer latency-path blocks and block
+// partials: the 257-point IPA CRS at c = 16 (16 windows, 17.2 GB) proves in 0.64 ms against 0.73 at
+// c = 8 (32 windows, 134 MB), the multiproof finish 0.99 against 1.15 ms (profiles/r05/fb_default_c/).
+// VKZG_FB_C_DEFAULT (read once; A/B probe) fixes c.
+template <class Fr>
+static double fb_auto_bytes(size_t n, int c) {
+    const size_t W = (size_t)(Fr::BITS + 1 + c - 1) / c;
+    return (double)n * (double)W * (double)(1u << (c - 1)) * 128.0;
+}
+template <class Fr>
+static int fb_default_c(size_t n, size_t used) {
+    static const int forced = getenv("VKZG_FB_C_DEFAULT") ? atoi(getenv("VKZG_FB_C_DEFAULT")) : 0;
+    static const double budget_gb = getenv("VKZG_FB_BUDGET_GB") ? atof(getenv("VKZG_FB_BUDGET_GB")) : 20.0;
+    if (forced >= 4 && forced <= 20) return forced;
+    for (int c = 16; c > 8; c--)
+        if ((double)used + fb_auto_bytes<Fr>(n, c) <= budget_gb * 1e9) return c;
+    return 8;
+}
+
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
@@ -604,7 +627,11 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (width > t->n && !with_cols) return VC_E_RANGE;
     if (with_cols && (size_t)cols->extra >= t->n) return VC_E_RANGE;
     if (with_cols && cols->base(0, cols->n_main - 1) >= t->n) return VC_E_RANGE;
-    if (t->fb_c == 0) VK_TRY(fb_precompute_t<C>(ctx, t, 8, 0));
+    if (t->fb_c == 0) {
+        const int c = fb_default_c<Fr>(t->n, ctx->fb_auto_bytes);
+        VK_TRY(fb_precompute_t<C>(ctx, t, c, 0));
+        ctx->fb_auto_bytes += (size_t)fb_auto_bytes<Fr>(t->n, c);
+    }
     if (batch == 0) {
         if (overlap && *overlap) (*overlap)();
         return VC_OK;
@@ -905,8 +932,16 @@ bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch) {
         }
     }
     const size_t lanes = ctx->fb_lanes ? ctx->fb_lanes : 131072;
-    const int c = t->fb_c ? t->fb_c : 8;
-    const size_t W = t->fb_c ? (size_t)t->fb_W : (size_t)((255 + 1 + c - 1) / c);  // (before the default tables exist)
+    size_t W = (size_t)t->fb_W;
+    if (!t->fb_c) {  // before the default tables exist: the geometry fb_commit_t will build
+        int c = 8, bits = 255;
+        switch (t->curve) {
+            case VC_CURVE_BN254: c = fb_default_c<BN254Fr>(t->n, ctx->fb_auto_bytes), bits = BN254Fr::BITS; break;
+            case VC_CURVE_BLS12_381: c = fb_default_c<BLS381Fr>(t->n, ctx->fb_auto_bytes), bits = BLS381Fr::BITS; break;
+            default: c = fb_default_c<BandFr>(t->n, ctx->fb_auto_bytes), bits = BandFr::BITS; break;
+        }
+        W = (size_t)(bits + 1 + c - 1) / c;
+    }
     return batch * width * W <= lanes;
 }
 

@@ -217,6 +217,7 @@ struct vc_ctx {
     uint32_t fb_lanes = 0;                // resident lanes of k_fb_commit_cm (cached per context)
     uint32_t small_epoch = 0;             // completion-flag epoch of the latency path's launches
     uint32_t tail_epoch = 0;              // the same for the MSM tails' direct completion (pin[0 / 1])
+    size_t fb_auto_bytes = 0;             // fixed-base tables built on first use (commit.hip fb_default_c)
     uint32_t norm_vk_parity = 0;          // the half of pin_norm_vk the last verkle normalisation used
     // geometry of the last MSM (vc_msm_last_plan): window bits c, windows W (of the whole MSM),
     // terms per point (2 with the GLV split), radix multiplier m (radix m 2^c; 1 = 2^c), shared

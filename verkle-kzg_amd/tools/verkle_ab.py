@@ -18,7 +18,7 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 eng = vkzg.Engine("bn254", 0)
 eng.set_stream(torch.cuda.current_stream().cuda_stream)
 kzg = scheme.KZG(eng, 256)
-eng.fixed_base_precompute(kzg.table, 8)
+eng.fixed_base_precompute(kzg.table, int(os.environ.get("VKZG_AB_FB_C", "8")))  # window bits (A/B)
 rng = np.random.default_rng(91)
 keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
 vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
