@@ -292,6 +292,7 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         ctx->pin_norm.release();
         ctx->pin_y.release();
         ctx->pin_mp.release();
+        ctx->pin_ipa.release();
         ctx->pin_verkle.release();
         for (auto& b : ctx->pin_verkle_lv) b.release();
         ctx->pin_norm_vk.release();

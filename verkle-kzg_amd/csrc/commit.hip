@@ -487,7 +487,7 @@ template <class C, class Fr>
 __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restrict__ tab,
                                                         const uint8_t* __restrict__ inf, uint32_t width, FbGeom fg,
                                                         const uint32_t* __restrict__ sc, int mont,
-                                                        uint32_t bpc, int wpt, StrideCols cols,
+                                                        uint32_t bpc, int wpt, StrideCols cols, IpaRows ipa,
                                                         typename C::Acc* __restrict__ part,
                                                         uint32_t* __restrict__ flags, uint32_t epoch) {
     using FC = typename Fast29<C>::type;
@@ -500,9 +500,30 @@ __global__ void __launch_bounds__(256) k_fb_commit_small(const FbE<C>* __restric
     // compacted rows (cols.half != 0): commit g's item i is a table base of a strided pattern
     // (computed: a list in host memory cost a dependent PCIe read per thread, +7 us per launch)
     const uint32_t base = cols.half ? cols.base(g, i) : i;
+    // the IPA rows (IpaRows): this round's coefficient of item i, folded and stored by L's window-0
+    // thread for the next round -- identity bases included -- then the item's scalar
+    fe<Fr> ipa_s = fe_zero<Fr>();
+    if (ipa.a != nullptr && i < width) {
+        const uint32_t p = g >> 1;
+        if (i < ipa.N) {
+            fe<Fr> c = load_scalar_fb<Fr>(ipa.coeff_in, (size_t)p * ipa.N + i);
+            if (ipa.fold && (i % ipa.m_prev) < ipa.h_prev) c = fe_mul<Fr>(c, load_scalar_fb<Fr>(ipa.x, p));
+            if ((g & 1) == 0 && wg == 0) {
+                uint4* o = reinterpret_cast<uint4*>(ipa.coeff_out + 8 * ((size_t)p * ipa.N + i));
+                o[0] = make_uint4(c.v[0], c.v[1], c.v[2], c.v[3]);
+                o[1] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
+            }
+            const uint32_t jj = i % ipa.m;
+            const bool on = (g & 1) ? jj < ipa.h : jj >= ipa.h;
+            if (on)
+                ipa_s = fe_mul<Fr>(load_scalar_fb<Fr>(ipa.a, (size_t)p * ipa.N + ((g & 1) ? jj + ipa.h : jj - ipa.h)), c);
+        } else {
+            ipa_s = load_scalar_fb<Fr>(ipa.q, g);
+        }
+    }
     if (i < width && !inf[base]) {
         FbDigits<Fr> dg;
-        dg.s = load_scalar_fb<Fr>(sc, (size_t)g * width + i);
+        dg.s = ipa.a != nullptr ? ipa_s : load_scalar_fb<Fr>(sc, (size_t)g * width + i);
         if (mont) dg.s = fe_from_mont<Fr>(dg.s);
         const FbE<C>* ti = tab + (size_t)base * fg.stride();
         const int wb = (int)wg * wpt, we = min(W, wb + wpt);
@@ -621,7 +642,8 @@ static int fb_default_c(size_t n, size_t used) {
 template <class C, class Fr>
 static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                        void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                       const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* cols) {
+                       const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* cols,
+                       const IpaRows* ipa) {
     using Acc = typename C::Acc;
     const bool with_cols = cols && cols->half;
     if (width > t->n && !with_cols) return VC_E_RANGE;
@@ -646,7 +668,8 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     const int wpt = fb_wpt();
     const size_t WG = (size_t)(W + wpt - 1) / wpt;
     const bool small = items * WG <= lanes && batch <= 64;
-    if (with_cols && !small) return VC_E_INVALID;  // compacted rows: the latency path only
+    if ((with_cols || ipa) && !small) return VC_E_INVALID;  // compacted / IPA rows: the latency path only
+    if (ipa && (with_cols || width != (size_t)ipa->N + 1 || batch % 2)) return VC_E_INVALID;
     // zero-copy on the latency path (VKZG_ZERO_COPY, A/B probe: bit 0 partials, bit 1 scalars):
     // the kernel reads host-pinned scalars and writes its block partials to fine-grained host
     // memory over PCIe instead of a copy engine moving them before / after it
@@ -686,7 +709,7 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
             for (uint32_t b = 0; b < nblk; b++) hflags[b] = 0;
         VK_LAUNCH(ctx, "fb_commit_small", (k_fb_commit_small<C, Fr>), batch * bpc, 256, 0, t->fb.as<FbE<C>>(),
                   t->inf.as<uint8_t>(), (uint32_t)width, fg, reinterpret_cast<const uint32_t*>(d_sc), mont,
-                  bpc, wpt, with_cols ? *cols : StrideCols{}, d_part, dflags, epoch);
+                  bpc, wpt, with_cols ? *cols : StrideCols{}, ipa ? *ipa : IpaRows{}, d_part, dflags, epoch);
         // the few block partials are added and normalised on the host: a lone GPU lane pays
         // ~10 us per serial EC add and ~160 us per field inversion, the host ~1 us / ~20 us
         // (pinned read-back; a caller that wants host results -- h_out_xy -- gets them without the
@@ -947,7 +970,8 @@ bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch) {
 
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t batch, int mont,
                   void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy, uint8_t* h_out_inf, bool* on_host,
-                  const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* with_cols) {
+                  const PinBuf* pin_sc, const std::function<void()>* overlap, const StrideCols* with_cols,
+                  const IpaRows* ipa) {
     bool dummy = false;
     if (!on_host) on_host = &dummy;
     *on_host = false;
@@ -955,13 +979,13 @@ int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, size_t 
     switch (t->curve) {
         case VC_CURVE_BN254:
             return fb_commit_t<BN254G1, BN254Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                 h_out_inf, on_host, pin_sc, overlap, with_cols);
+                                                 h_out_inf, on_host, pin_sc, overlap, with_cols, ipa);
         case VC_CURVE_BLS12_381:
             return fb_commit_t<BLS381G1, BLS381Fr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                   h_out_inf, on_host, pin_sc, overlap, with_cols);
+                                                   h_out_inf, on_host, pin_sc, overlap, with_cols, ipa);
         case VC_CURVE_BANDERSNATCH:
             return fb_commit_t<Bandersnatch, BandFr>(ctx, t, width, d_sc, batch, mont, d_out_xy, d_out_inf, h_out_xy,
-                                                     h_out_inf, on_host, pin_sc, overlap, with_cols);
+                                                     h_out_inf, on_host, pin_sc, overlap, with_cols, ipa);
     }
     return VC_E_INVALID;
 }

@@ -68,6 +68,22 @@ struct StrideCols {
     }
 };
 
+// The IPA prover's L / R rows made inside the latency-path commit (commit.hip k_fb_commit_small)
+// instead of on the host: commit g (proof p = g / 2, L even, R odd), item i < n_main is
+// a[p][i % m - h] * coeff[i] for L when i % m >= h, a[p][i % m + h] * coeff[i] for R when i % m < h,
+// zero otherwise; item n_main is q[g] (the q' <a, b> term). coeff is this round's coefficient row:
+// coeff_in[p] folded by the previous round's challenge x[p] where (i % m_prev) < h_prev (fold != 0),
+// written to coeff_out[p] by L's window-0 threads. Montgomery BN254 Fr, 8 words each; a, x and q
+// in page-locked host memory (the host folds a and b), coeff in device memory (ping-pong).
+struct IpaRows {
+    const uint32_t* a = nullptr;  // [B][N] (a_stride = N entries per proof)
+    const uint32_t* coeff_in = nullptr;
+    uint32_t* coeff_out = nullptr;
+    const uint32_t* x = nullptr;  // [B]
+    const uint32_t* q = nullptr;  // [2B]
+    uint32_t N = 0, m = 0, h = 0, fold = 0, m_prev = 0, h_prev = 0;
+};
+
 struct PinBuf {
     void* p = nullptr;
     void* dp = nullptr;     // the device's address of p (kernels read / write it over PCIe)
@@ -199,6 +215,7 @@ struct vc_ctx {
     vk::PinBuf pin_norm;            // block products / inverses of the split normalisation
     vk::PinBuf pin_y;               // the KZG opening's y, copied back asynchronously
     vk::PinBuf pin_mp;              // the multiproof finish's h - g, copied back ahead of the E commit
+    vk::PinBuf pin_ipa;             // the IPA prover's a, x and q terms read by the round kernel (IpaRows)
     vk::PinBuf pin_verkle;          // the verkle extension rows, merged straight into page-locked memory
     vk::PinBuf pin_verkle_lv[2];    // verkle levels' lists (one upload per level; the next level's are
                                     // built into the other one while the current level runs)
@@ -360,7 +377,8 @@ int table_from_acc(vc_ctx* ctx, Table* t, const void* d_acc, size_t n);
 int msm_batch_run(vc_ctx* ctx, Table* t, size_t width, const void* d_scalars, size_t batch,
                   int mont, void* d_out_xy, uint8_t* d_out_inf, uint64_t* h_out_xy = nullptr,
                   uint8_t* h_out_inf = nullptr, bool* on_host = nullptr, const PinBuf* pin_sc = nullptr,
-                  const std::function<void()>* overlap = nullptr, const StrideCols* cols = nullptr);
+                  const std::function<void()>* overlap = nullptr, const StrideCols* cols = nullptr,
+                  const IpaRows* ipa = nullptr);
 // whether msm_batch_run of `batch` width-`width` commits takes the latency path
 bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch);
 }  // namespace vk

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "../ec.hpp"
@@ -107,7 +108,7 @@ inline fe<F> fe_from_be_bytes_mod(const uint8_t* b, size_t len) {
 }
 
 // domain generator w_n = 5^((r-1)/n) (GeneralEvaluationDomain radix-2)
-inline Fr bn254_group_gen(uint64_t n) {
+inline Fr bn254_group_gen_uncached(uint64_t n) {
     // (r - 1) / n for power-of-two n <= 2^28: shift r - 1 right by log2 n
     Fr e;
     for (int i = 0; i < 8; i++) e.v[i] = BN254Fr::p(i);
@@ -119,6 +120,22 @@ inline Fr bn254_group_gen(uint64_t n) {
         e.v[7] >>= 1;
     }
     return fe_pow_fe<BN254Fr, BN254Fr>(mont_from_u64<BN254Fr>(5), e);
+}
+// the same, one exponentiation per domain size and process (~7 us each: every IPA prove / verify
+// and multiproof finish asked for it)
+inline Fr bn254_group_gen(uint64_t n) {
+    int lg = 0;
+    while ((1ull << lg) < n) lg++;
+    if (lg > 28) return bn254_group_gen_uncached(n);
+    static std::mutex mu;
+    static Fr cache[29];
+    static bool have[29] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (!have[lg]) {
+        cache[lg] = bn254_group_gen_uncached(n);
+        have[lg] = true;
+    }
+    return cache[lg];
 }
 
 }  // namespace vk

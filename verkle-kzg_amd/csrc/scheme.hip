@@ -115,9 +115,12 @@ static bool barycentric_panics(size_t size, const Fr& point) {
     return fe_eq<F>(fe_pow_u64<F>(point, size), fe_one<F>());
 }
 
+// (zero b entries skipped: the in-domain barycentric weights are one-hot, so the IPA prover's
+// evaluation and its first round's inner products are one product instead of N and N / 2)
 static Fr inner(const Fr* a, const Fr* b, size_t n) {
     Fr s = fe_zero<F>();
-    for (size_t i = 0; i < n; i++) s = fe_add<F>(s, fe_mul<F>(a[i], b[i]));
+    for (size_t i = 0; i < n; i++)
+        if (!fe_is_zero<F>(b[i])) s = fe_add<F>(s, fe_mul<F>(a[i], b[i]));
     return s;
 }
 
@@ -286,13 +289,89 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
     static const bool compact_env = getenv("VKZG_IPA_COMPACT") && atoi(getenv("VKZG_IPA_COMPACT")) == 1;
     const bool compact = compact_env && fb_small_path(ctx, t, N / 2 + 1, 2 * B);
     const size_t W = compact ? N / 2 + 1 : N + 1;
-    std::vector<Fr> sc(2 * B * W);
+    // the rows on the device (IpaRows, the latency path's commit kernel): the host keeps a, b and
+    // the q' <a, b> terms; the coefficient rows live in device memory and are folded there.
+    // VKZG_IPA_DEV_ROWS=0 (read once; A/B probe): the host builds every row.
+    static const bool dev_rows_env = !(getenv("VKZG_IPA_DEV_ROWS") && atoi(getenv("VKZG_IPA_DEV_ROWS")) == 0);
+    const bool dev_rows = dev_rows_env && !compact && fb_small_path(ctx, t, N + 1, 2 * B);
+    DevBuf d_coeff(ctx);
+    std::vector<Fr> ones;  // round 0's coefficients (the upload reads it until the first round ends)
+    Fr *pa = nullptr, *px = nullptr, *pq = nullptr;
+    const uint8_t* dbase = nullptr;
+    if (dev_rows) {
+        VK_TRY(d_coeff.ensure(2 * B * N * 32));
+        ones.assign(B * N, fe_one<F>());
+        VK_CHECK_HIP(hipMemcpyAsync(d_coeff.p, ones.data(), B * N * 32, hipMemcpyHostToDevice, ctx->stream));
+        VK_TRY(ctx->pin_ipa.ensure((B * N + 3 * B) * 32));
+        pa = ctx->pin_ipa.as<Fr>();
+        px = pa + B * N;
+        pq = px + B;
+        dbase = static_cast<const uint8_t*>(ctx->pin_ipa.dp);
+    }
+    std::vector<Fr> sc(dev_rows ? 0 : 2 * B * W);
     std::vector<uint64_t> oxy(2 * B * 8);
     std::vector<uint8_t> oinf(2 * B);
     double lap_fill = 0, lap_commit = 0, lap_fold = 0;
     for (size_t r = 0; r < K; r++) {
         const size_t m = N >> r, half = m / 2;
         const double c0 = verify_timing() ? verify_clock_us() : 0.0;
+        if (dev_rows) {
+            par_for([&](size_t p) {
+                IpaState& s = st[p];
+                memcpy(pa + p * N, s.a.data(), m * 32);
+                pq[2 * p] = fe_mul<F>(s.w, inner(&s.a[0], &s.b[half], half));
+                pq[2 * p + 1] = fe_mul<F>(s.w, inner(&s.a[half], &s.b[0], half));
+            });
+            IpaRows ir;
+            ir.a = reinterpret_cast<const uint32_t*>(dbase);
+            ir.x = reinterpret_cast<const uint32_t*>(dbase + (size_t)B * N * 32);
+            ir.q = reinterpret_cast<const uint32_t*>(dbase + (size_t)(B * N + B) * 32);
+            ir.coeff_in = reinterpret_cast<const uint32_t*>(d_coeff.as<uint8_t>() + (r & 1) * B * N * 32);
+            ir.coeff_out = reinterpret_cast<uint32_t*>(d_coeff.as<uint8_t>() + ((r + 1) & 1) * B * N * 32);
+            ir.N = (uint32_t)N;
+            ir.m = (uint32_t)m;
+            ir.h = (uint32_t)half;
+            ir.fold = r > 0 ? 1u : 0u;
+            ir.m_prev = (uint32_t)(2 * m);
+            ir.h_prev = (uint32_t)m;
+            const double c1 = verify_timing() ? verify_clock_us() : 0.0;
+            VK_TRY(ctx->ws[WS_MISC].ensure(2 * B * 65));
+            uint8_t* dxy = ctx->ws[WS_MISC].as<uint8_t>();
+            bool on_host = false;
+            VK_TRY(msm_batch_run(ctx, t, N + 1, nullptr, 2 * B, 1, dxy, dxy + 2 * B * 64, oxy.data(), oinf.data(),
+                                 &on_host, nullptr, nullptr, nullptr, &ir));
+            if (!on_host) {  // (the latency path returns host results: not expected)
+                VK_CHECK_HIP(hipMemcpyAsync(oxy.data(), dxy, 2 * B * 64, hipMemcpyDeviceToHost, ctx->stream));
+                VK_CHECK_HIP(hipMemcpyAsync(oinf.data(), dxy + 2 * B * 64, 2 * B, hipMemcpyDeviceToHost, ctx->stream));
+                VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+            }
+            const double c2 = verify_timing() ? verify_clock_us() : 0.0;
+            par_for([&](size_t p) {
+                IpaState& s = st[p];
+                const uint64_t* Lxy = &oxy[(2 * p) * 8];
+                const uint64_t* Rxy = &oxy[(2 * p + 1) * 8];
+                memcpy(proofs[p].l_xy + r * 8, Lxy, 64);
+                memcpy(proofs[p].r_xy + r * 8, Rxy, 64);
+                proofs[p].l_inf[r] = oinf[2 * p];
+                proofs[p].r_inf[r] = oinf[2 * p + 1];
+                transcript_append_point(s.tr, Lxy, oinf[2 * p], "L");
+                transcript_append_point(s.tr, Rxy, oinf[2 * p + 1], "R");
+                Fr x = transcript_digest(s.tr, "x");
+                // a <- a_L + x a_R ; b <- b_R + x b_L (the coefficients fold on the device)
+                for (size_t j = 0; j < half; j++) {
+                    s.a[j] = fe_add<F>(s.a[j], fe_mul<F>(x, s.a[j + half]));
+                    s.b[j] = fe_add<F>(s.b[j + half], fe_mul<F>(x, s.b[j]));
+                }
+                s.a.resize(half);
+                s.b.resize(half);
+                px[p] = x;  // the next round's kernel folds the coefficients by it
+            });
+            if (verify_timing()) {
+                const double c3 = verify_clock_us();
+                lap_fill += c1 - c0, lap_commit += c2 - c1, lap_fold += c3 - c2;
+            }
+            continue;
+        }
         // L (even commits): bases i with i mod m >= half, R (odd): i mod m < half, in index order
         // -- the k-th is (k / half) m + k mod half (+ half for L) --, then q
         StrideCols cols;
@@ -316,13 +395,14 @@ int ipa_prove_impl(vc_ctx* ctx, Table* t, size_t N, const std::vector<std::vecto
                     else sR[kr++] = fe_mul<F>(s.a[j + half], s.coeff[i]);
                 }
             } else {
+                // (round 0: every coefficient is one -- the rows are a's halves as they are)
                 for (size_t i = 0; i < N; i++) {
                     size_t j = i % m;
                     if (j >= half) {
-                        sL[i] = fe_mul<F>(s.a[j - half], s.coeff[i]);
+                        sL[i] = r == 0 ? s.a[j - half] : fe_mul<F>(s.a[j - half], s.coeff[i]);
                         sR[i] = fe_zero<F>();
                     } else {
-                        sR[i] = fe_mul<F>(s.a[j + half], s.coeff[i]);
+                        sR[i] = r == 0 ? s.a[j + half] : fe_mul<F>(s.a[j + half], s.coeff[i]);
                         sL[i] = fe_zero<F>();
                     }
                 }

@@ -114,7 +114,9 @@ class LagrangeBasis:
     """Evaluations over a radix-2 domain (possibly shorter than it: `max`)."""
 
     def __init__(self, evals, domain_size=None):
-        self.evals = [int(e) % R_BN254 for e in evals]
+        # a tuple: the limbs below are cached per padded length, so the values must not change
+        self.evals = tuple(int(e) % R_BN254 for e in evals)
+        self._limbs = {}
         ds = 1
         while ds < len(self.evals):
             ds <<= 1
@@ -131,10 +133,16 @@ class LagrangeBasis:
         return len(self.evals) - 1
 
     def limbs(self, n=None):
-        arr = ints_to_limbs(self.evals, 4)
-        if n is not None and arr.shape[0] < n:
-            arr = np.vstack([arr, np.zeros((n - arr.shape[0], 4), dtype=np.uint64)])
-        return np.ascontiguousarray(arr)
+        """(max(len, n), 4) canonical u64 limbs, converted once per n (read-only array)."""
+        arr = self._limbs.get(n)
+        if arr is None:
+            arr = ints_to_limbs(self.evals, 4)
+            if n is not None and arr.shape[0] < n:
+                arr = np.vstack([arr, np.zeros((n - arr.shape[0], 4), dtype=np.uint64)])
+            arr = np.ascontiguousarray(arr)
+            arr.flags.writeable = False
+            self._limbs[n] = arr
+        return arr
 
 
 # ---------------------------------------------------------------- proofs
