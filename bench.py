@@ -850,6 +850,13 @@ def kzg_reference_shapes(local, stream, cpu=True):
     return out
 
 
+def _log2_int(n):
+    k = 0
+    while (1 << k) < n:
+        k += 1
+    return k
+
+
 def ipa_line(local, stream, batch=256, cpu=False):
     """The reference's IPA bench shapes (vector-commit/benches/ipa.rs:79-109, N = 256, BN254,
     data r + i): single commit, prove in / out of domain, verify in domain -- latency of one
@@ -875,6 +882,22 @@ def ipa_line(local, stream, batch=256, cpu=False):
     out = {"workload": "IPA N = 256 on BN254 (benches/ipa.rs shapes, data r + i)"}
     out["commit_ms"], _ = timed(lambda: ipa.commit(datas[0]))
     out["prove_in_domain_ms"], prf = timed(lambda: ipa.prove_point(coms[0], 77, datas[0]))
+    # the same proof through the bare C ABI (vc_ipa_prove on inputs marshalled once): the library's
+    # latency without the Python mirror's conversions (tools/ipa_abi_probe.py)
+    import ctypes
+    from vkzg._lib import lib as _lib, check as _check
+    d0 = np.ascontiguousarray(datas[0].limbs(N)[:N])
+    cxy0, cinf0 = scheme._pt_arrays([coms[0]])
+    pt0 = vkzg.ints_to_limbs([77], 4)
+    pbuf, parrs = scheme.IPAProof._alloc(_log2_int(N))
+    parr = (scheme._ProofBuf * 1)(pbuf)
+
+    def abi_prove():
+        _check(_lib().vc_ipa_prove(ieng.h, ipa.table, N, scheme._p(d0), scheme._p(cxy0), scheme._p(cinf0),
+                                   scheme._p(pt0), 1, None, ctypes.cast(parr, scheme._P)), "ipa_prove")
+    out["prove_in_domain_ms_c_abi"], _ = timed(abi_prove)
+    if scheme.IPAProof._from(parr[0], parrs).as_dict() != prf.as_dict():
+        raise SystemExit("bench: the bare vc_ipa_prove call gave a different proof")
     out["prove_out_domain_ms"], _ = timed(lambda: ipa.prove_point(coms[0], N * 7 + 3, datas[0]))
     out["verify_in_domain_ms"], ok = timed(lambda: ipa.verify_point(coms[0], 77, prf))
     assert ok
