@@ -31,15 +31,22 @@ def _fr(x):
     return ints_to_limbs([int(x) % R_BN254], 4)[0].copy()
 
 
+_M256 = (1 << 256) - 1
+
+
 def _pt_arrays(pts):
-    xy = np.zeros((len(pts), 8), dtype=np.uint64)
-    inf = np.zeros(len(pts), dtype=np.uint8)
+    """[(x, y) | None] -> ((n, 8) u64 limbs, (n,) identity flags): one bytes buffer for all points
+    (per-point numpy assignments cost ~10 us per call of the IPA prover's Python mirror)"""
+    n = len(pts)
+    buf = bytearray(64 * n)
+    inf = np.zeros(n, dtype=np.uint8)
     for i, P in enumerate(pts):
         if P is None:
             inf[i] = 1
         else:
-            xy[i, :4] = ints_to_limbs([P[0]], 4)[0]
-            xy[i, 4:] = ints_to_limbs([P[1]], 4)[0]
+            buf[64 * i:64 * i + 32] = (int(P[0]) & _M256).to_bytes(32, "little")
+            buf[64 * i + 32:64 * i + 64] = (int(P[1]) & _M256).to_bytes(32, "little")
+    xy = np.frombuffer(buf, dtype="<u8").reshape(n, 8).astype(np.uint64)
     return xy, inf
 
 
@@ -160,17 +167,27 @@ class IPAProof:
 
     @staticmethod
     def _alloc(rounds):
-        arrs = {"lxy": np.zeros((rounds, 8), dtype=np.uint64), "linf": np.zeros(rounds, dtype=np.uint8),
-                "rxy": np.zeros((rounds, 8), dtype=np.uint64), "rinf": np.zeros(rounds, dtype=np.uint8)}
-        b = _ProofBuf(rounds, _p(arrs["lxy"]), _p(arrs["linf"]), _p(arrs["rxy"]), _p(arrs["rinf"]))
+        # one buffer, four views (the caller keeps `arrs`, hence the buffer, alive while the struct's
+        # raw pointers are in use): four allocations and four data_as pointers cost ~19 us a call
+        k = rounds
+        raw = np.zeros(128 * k + 2 * k, dtype=np.uint8)
+        base = raw.ctypes.data
+        arrs = {"lxy": raw[:64 * k].view(np.uint64).reshape(k, 8), "rxy": raw[64 * k:128 * k].view(np.uint64).reshape(k, 8),
+                "linf": raw[128 * k:128 * k + k], "rinf": raw[128 * k + k:], "_raw": raw}
+        b = _ProofBuf(k, base, base + 128 * k, base + 64 * k, base + 128 * k + k)
         return b, arrs
 
     @staticmethod
     def _from(b, arrs):
         k = b.rounds
-        return IPAProof([_pt(arrs["lxy"][i], arrs["linf"][i]) for i in range(k)],
-                        [_pt(arrs["rxy"][i], arrs["rinf"][i]) for i in range(k)],
-                        limbs_to_int(list(b.tip)), limbs_to_int(list(b.y)))
+        fb = int.from_bytes
+
+        def pts(xy, inf):  # whole arrays to bytes once, then one int.from_bytes per coordinate
+            raw, flags = np.ascontiguousarray(xy[:k], dtype="<u8").tobytes(), inf[:k].tolist()
+            return [None if flags[i] else (fb(raw[64 * i:64 * i + 32], "little"), fb(raw[64 * i + 32:64 * i + 64], "little"))
+                    for i in range(k)]
+        return IPAProof(pts(arrs["lxy"], arrs["linf"]), pts(arrs["rxy"], arrs["rinf"]),
+                        fb(bytes(b.tip), "little"), fb(bytes(b.y), "little"))
 
     def _to(self):
         k = len(self.l)
@@ -226,7 +243,7 @@ class IPA:
 
     def prove_batch_points(self, commitments, points, datas, transcripts=None):
         B = len(datas)
-        d = np.concatenate([x.limbs(self.N)[: self.N] for x in datas])
+        d = datas[0].limbs(self.N)[: self.N] if B == 1 else np.concatenate([x.limbs(self.N)[: self.N] for x in datas])
         cxy, cinf = _pt_arrays(commitments)
         pts = ints_to_limbs([int(p) % R_BN254 for p in points], 4)
         K = _log2(self.N)
