@@ -256,11 +256,13 @@ class Engine:
         return arrays_to_points(self.curve, xy[None, :], np.array([inf]))[0]
 
     def msm_device(self, table, d_scalars_ptr, n, offset=0, mont=False):
-        out = np.zeros(2 * self.nl, dtype=np.uint64)
-        oinf = np.zeros(1, dtype=np.uint8)
+        # ctypes buffers passed as they are (two numpy arrays and two data_as pointers cost a few us
+        # per call: the bench's timed step); the result is a numpy view of the output buffer
+        out = (ctypes.c_uint64 * (2 * self.nl))()
+        oinf = ctypes.c_uint8(0)
         check(lib().vc_msm_device(self.h, table, offset, ctypes.c_void_p(d_scalars_ptr), n,
-                                  1 if mont else 0, _ptr(out), _ptr(oinf)), "vc_msm_device")
-        return out, int(oinf[0])
+                                  1 if mont else 0, out, ctypes.byref(oinf)), "vc_msm_device")
+        return np.frombuffer(out, dtype=np.uint64), int(oinf.value)
 
     def msm_device_many(self, table, d_scalars_ptrs, n, mont=None):
         """len(d_scalars_ptrs) MSMs over one table (vc_msm_device_many): one batched pipeline on
