@@ -352,7 +352,7 @@ template <class T>
 __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, const uint32_t* __restrict__ base,
                                                    uint32_t nblk, uint32_t bins, uint32_t FB,
                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
-                                                   uint32_t* __restrict__ zero_word, uint32_t cap) {
+                                                   uint32_t* __restrict__ zero_word, uint32_t cap, uint32_t regs_ok) {
     __shared__ uint32_t h[256], x[256];
     extern __shared__ uint32_t stage[];
     const uint32_t g = blockIdx.x, F = 1u << FB, t = threadIdx.x;
@@ -362,7 +362,21 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
     const uint32_t end = base[(size_t)(g + 1) * nblk];  // base has bins*nblk + 1 entries
     if (cnt_lane) h[t] = 0;
     __syncthreads();
-    {  // RH loads in flight per thread before their counter atomics
+    // a staged bin of at most RMAX entries per thread keeps its entries in registers from the
+    // counting pass to the scatter: the bin is read from HBM once, not twice (uniform per block)
+    constexpr uint32_t RMAX = 16;
+    T er[RMAX];
+    const bool regs = regs_ok != 0 && cap != 0 && end - start <= cap && end - start <= RMAX * blockDim.x;
+    if (regs) {
+#pragma unroll
+        for (uint32_t k = 0; k < RMAX; k++) {
+            const uint32_t p = start + t + k * blockDim.x;
+            er[k] = p < end ? tmp[p] : T(0);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < RMAX; k++)
+            if (start + t + k * blockDim.x < end) atomicAdd(&h[sort_fine_of<T>(er[k], FB)], 1u);
+    } else {  // RH loads in flight per thread before their counter atomics
         constexpr uint32_t RH = 4;
         for (uint32_t p0 = start + t; p0 < end; p0 += RH * blockDim.x) {
             T e[RH];
@@ -396,6 +410,14 @@ __global__ void __launch_bounds__(1024) k_sort_fine(const T* __restrict__ tmp, c
     // the scatter RS entries at a time (loads, then LDS cursor atomics, then stores: RS atomics in
     // flight per thread)
     constexpr uint32_t RS = 4;
+    if (regs) {
+#pragma unroll
+        for (uint32_t k = 0; k < RMAX; k++)
+            if (start + t + k * blockDim.x < end) stage[atomicAdd(&h[sort_fine_of<T>(er[k], FB)], 1u)] = sort_entry_of<T>(er[k], FB);
+        __syncthreads();
+        for (uint32_t p = t; p < end - start; p += blockDim.x) sorted[start + p] = stage[p];
+        return;
+    }
     if (end - start <= cap) {  // uniform over the block
         for (uint32_t p0 = start + t; p0 < end; p0 += RS * blockDim.x) {
             T e[RS];
@@ -1177,6 +1199,9 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
     // LDS staging of the fine scatter (16K entries, 64 KB: two blocks per CU, 1024 threads) when the
     // mean bin leaves it ~40 % headroom (radix 2^20: 11.5K); a bin beyond it scatters directly
     static const int stage_env = getenv("VKZG_SORT_STAGE") ? atoi(getenv("VKZG_SORT_STAGE")) : 1;  // A/B probe
+    // staged bins of <= 16 entries per thread keep their entries in registers (k_sort_fine);
+    // VKZG_SORT_FINE_REGS=0: A/B probe
+    static const uint32_t fine_regs = !(getenv("VKZG_SORT_FINE_REGS") && atoi(getenv("VKZG_SORT_FINE_REGS")) == 0);
     uint32_t cap = 0;
     if (stage_env && total / bins <= 12000) {
         cap = 16384;
@@ -1201,17 +1226,17 @@ static int sort_entries(vc_ctx* ctx, Lane L, Src src, uint32_t nv, int c, int wb
                          NBC, nblk, stride, wps, chunk, counts, base, static_cast<uint32_t*>(tmp), s * bins_l, bins_l);
         }
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, cap * 4,
-                     static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
+                     static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap, fine_regs);
     } else if (narrow) {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint32_t>), nblk, sblk, lds, src, nv, c, wb, we,
                      FB, NBC, nblk, stride, wps, chunk, base, static_cast<uint32_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint32_t>, bins, fblk, cap * 4,
-                     static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
+                     static_cast<const uint32_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap, fine_regs);
     } else {
         VK_LAUNCH_ON(ctx, st, "msm_sort_coarse", (k_sort_coarse<Src, uint64_t>), nblk, sblk, lds, src, nv, c, wb, we,
                      FB, NBC, nblk, stride, wps, chunk, base, static_cast<uint64_t*>(tmp));
         VK_LAUNCH_ON(ctx, st, "msm_sort_fine", k_sort_fine<uint64_t>, bins, fblk, cap * 4,
-                     static_cast<const uint64_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap);
+                     static_cast<const uint64_t*>(tmp), base, nblk, bins, FB, offsets, sorted, zero_word, cap, fine_regs);
     }
     return VC_OK;
 }
