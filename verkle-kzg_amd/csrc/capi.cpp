@@ -297,6 +297,7 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         for (auto& b : ctx->pin_verkle_lv) b.release();
         ctx->pin_norm_vk.release();
         ctx->pin_sparse_ck.release();
+        ctx->pin_sparse_ch.release();
         for (auto& kv : ctx->pool_free) (void)hipFree(kv.second);
         ctx->pool_free.clear();
         for (auto& p : ctx->pending) {

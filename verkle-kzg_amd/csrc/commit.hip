@@ -243,7 +243,9 @@ __global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__
                                                      const uint64_t* __restrict__ add_xy,
                                                      const uint8_t* __restrict__ add_inf,
                                                      fe<BN254Fq>* __restrict__ others, fe<BN254Fq>* __restrict__ tot,
-                                                     uint32_t* __restrict__ flags, uint32_t epoch) {
+                                                     uint32_t* __restrict__ flags, uint32_t epoch,
+                                                     uint32_t* __restrict__ counter, fe<BN254Fq>* __restrict__ cof,
+                                                     fe<BN254Fq>* __restrict__ total) {
     using C = BN254G1;
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     C::Acc a = j < count ? rows[j] : C::zero();
@@ -260,11 +262,66 @@ __global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__
         }
     }
     norm_prep_block<C>(a, j, count, others, tot);
-    // tot in fine-grained host memory (normalize_rows_items): the block product is made visible
-    // system wide, then the block's flag takes this launch's epoch (the host polls the flags)
-    if (flags != nullptr && threadIdx.x == 0) {
+    if (counter == nullptr) {
+        // tot in fine-grained host memory (normalize_rows_items): the block product is made visible
+        // system wide, then the block's flag takes this launch's epoch (the host polls the flags)
+        if (flags != nullptr && threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(&flags[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+    // device scan (tot in device memory): the last block to arrive turns the nblk block products
+    // into per-block cofactors cof[b] = prod_{k != b} tot[k] and hands the host only their total
+    // (one inversion there, ~1 us, instead of Montgomery's trick over every block product: ~3
+    // multiplies per block, 40 us for 512 blocks, with the GPU idle)
+    using F = BN254Fq;
+    __shared__ uint32_t s_last;
+    __shared__ fe<F> spre[256], ssuf[256];
+    const uint32_t tid = threadIdx.x, nb = gridDim.x;
+    if (tid == 0) {
+        __threadfence();  // this block's product before its arrival
+        s_last = atomicAdd(counter, 1u) == nb - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    auto load = [&](uint32_t b) {  // another block's product: through the coherent path
+        fe<F> v;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&tot[b]);
+#pragma unroll
+        for (int k = 0; k < F::N; k++) v.v[k] = __hip_atomic_load(&src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+    };
+    const uint32_t per = (nb + 255) / 256, b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+    fe<F> seg = fe_one<F>();
+    for (uint32_t b = b1; b-- > b0;) {  // suffix products inside the segment, parked in cof
+        cof[b] = seg;
+        seg = fe_mul<F>(load(b), seg);
+    }
+    spre[tid] = seg;
+    ssuf[tid] = seg;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256; off <<= 1) {
+        fe<F> p = spre[tid], q = ssuf[tid];
+        if (tid >= off) p = fe_mul<F>(spre[tid - off], p);
+        if (tid + off < 256) q = fe_mul<F>(q, ssuf[tid + off]);
+        __syncthreads();
+        spre[tid] = p;
+        ssuf[tid] = q;
+        __syncthreads();
+    }
+    fe<F> run = tid > 0 ? spre[tid - 1] : fe_one<F>();           // the segments before this one
+    const fe<F> after = tid < 255 ? ssuf[tid + 1] : fe_one<F>();  // and after it
+    for (uint32_t b = b0; b < b1; b++) {
+        cof[b] = fe_mul<F>(fe_mul<F>(run, cof[b]), after);
+        run = fe_mul<F>(run, load(b));
+    }
+    if (tid == 0) {
+        *total = spre[255];
+        *counter = 0;  // for the next launch (stream-ordered after this one)
         __threadfence_system();
-        __hip_atomic_store(&flags[blockIdx.x], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&flags[0], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -318,13 +375,16 @@ __global__ void __launch_bounds__(256) k_norm_finish_vk(const BN254G1::Acc* __re
                                                        const fe<BN254Fq>* __restrict__ others,
                                                        const fe<BN254Fq>* __restrict__ binv,
                                                        const uint32_t* __restrict__ dst, uint64_t* __restrict__ out_xy,
-                                                       uint8_t* __restrict__ out_inf, uint64_t* __restrict__ out_item) {
+                                                       uint8_t* __restrict__ out_inf, uint64_t* __restrict__ out_item,
+                                                       const fe<BN254Fq>* __restrict__ tinv) {
     using F = BN254Fq;
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= count) return;
     const BN254G1::Acc a = rows[j];
     const bool ident = BN254G1::is_zero(a);
-    const fe<F> iz = fe_mul<F>(binv[blockIdx.x], others[j]);
+    // the block's inverse: binv[b], or (device scan) the cofactor times the total's inverse
+    const fe<F> bi = tinv ? fe_mul<F>(*tinv, binv[blockIdx.x]) : binv[blockIdx.x];
+    const fe<F> iz = fe_mul<F>(bi, others[j]);
     const fe<F> t = fe_mul<F>(iz, a.zz);  // 1/Z
     fe<F> cx = fe_from_mont<F>(fe_mul<F>(a.x, fe_sqr<F>(t))), cy = fe_from_mont<F>(fe_mul<F>(a.y, iz));
     if (ident) cx = cy = fe_zero<F>();
@@ -887,27 +947,75 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     volatile uint32_t* hflags = reinterpret_cast<volatile uint32_t*>(hbase + flag_off);
     uint32_t* dflags = reinterpret_cast<uint32_t*>(dbase + flag_off);
     const uint32_t epoch = ++ctx->small_epoch == 0 ? ++ctx->small_epoch : ctx->small_epoch;  // never 0
+    // the last block's scan costs ~17 us of serial multiplies whatever nblk is; the host's trick
+    // ~54 ns per block: the scan pays from ~128 blocks on (c1 / c2 rows: 88 -> 74 us of prep + gap,
+    // width-4 rows 76 -> 58 us; a 256-row level 24 -> 43 us: profiles/r05/verkle/sparse_norm_vk/)
+    static const size_t scan_min = getenv("VKZG_NORM_DEVSCAN") ? (size_t)atol(getenv("VKZG_NORM_DEVSCAN")) : 128;  // A/B
+    if (scan_min != 0 && nblk >= scan_min) {
+        // the block products scanned on the device (k_norm_prep_vk's last block): the host inverts
+        // their total only; page-locked [total | its inverse | flag] in the same alternating halves
+        DevBuf& cnt = ctx->ws[WS_NORM_CNT];
+        DevBuf& dt = ctx->ws[WS_NORM_TOT];
+        if (cnt.p == nullptr) {
+            VK_TRY(cnt.ensure(256));
+            VK_CHECK_HIP(hipMemsetAsync(cnt.p, 0, 256, ctx->stream));
+        }
+        VK_TRY(dt.ensure(2 * nblk * sizeof(fe<F>)));
+        fe<F>* dtot = dt.as<fe<F>>();
+        hflags[0] = 0;
+        VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids,
+                  add_xy, add_inf, others.as<fe<F>>(), dtot, dflags, epoch, cnt.as<uint32_t>(), dtot + nblk, dh);
+        if (overlap && *overlap) (*overlap)();
+        bool seen = false;
+        const auto w0 = std::chrono::steady_clock::now();
+        for (uint32_t spins = 0;; spins++) {
+            if (hflags[0] == epoch) {
+                seen = true;
+                break;
+            }
+            if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(20)) break;
+            _mm_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        h[1] = fe_inv_bin<F>(h[0]);  // never zero: identities count as 1
+        std::atomic_thread_fence(std::memory_order_release);  // the inverse before the launch that reads it
+        VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
+                  others.as<fe<F>>(), dtot + nblk, dst, out_xy, out_inf, out_item, dh + 1);
+        return VC_OK;
+    }
     for (size_t b = 0; b < nblk; b++) hflags[b] = 0;
     VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids, add_xy,
-              add_inf, others.as<fe<F>>(), dh, dflags, epoch);
+              add_inf, others.as<fe<F>>(), dh, dflags, epoch, (uint32_t*)nullptr, (fe<F>*)nullptr, (fe<F>*)nullptr);
     if (overlap && *overlap) (*overlap)();
+    // Montgomery's trick over the block products: the forward products are taken as the blocks'
+    // flags arrive (blocks finish roughly in order), so only the inversion and the backward pass
+    // follow the last block
+    fe<F>* inv = h + nblk;
+    size_t done = 0;  // blocks [0, done) seen and multiplied in
+    auto take = [&](size_t upto) {
+        for (; done < upto; done++) inv[done] = done ? fe_mul<F>(inv[done - 1], h[done]) : h[done];
+    };
     bool seen = false;
     const auto w0 = std::chrono::steady_clock::now();
     for (uint32_t spins = 0;; spins++) {
-        size_t b = 0;
+        size_t b = done;
         while (b < nblk && hflags[b] == epoch) b++;
-        if (b == nblk) {
+        if (b > done) {
+            std::atomic_thread_fence(std::memory_order_acquire);  // the products after their flags
+            take(b);
+        }
+        if (done == nblk) {
             seen = true;
             break;
         }
         if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - w0 > std::chrono::milliseconds(20)) break;
         _mm_pause();
     }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    fe<F>* inv = h + nblk;
-    inv[0] = h[0];
-    for (size_t b = 1; b < nblk; b++) inv[b] = fe_mul<F>(inv[b - 1], h[b]);
+    if (!seen) {
+        VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        take(nblk);
+    }
     fe<F> run = fe_inv_bin<F>(inv[nblk - 1]);
     for (size_t b = nblk - 1; b > 0; b--) {
         const fe<F> ib = fe_mul<F>(run, inv[b - 1]);
@@ -917,7 +1025,7 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     inv[0] = run;
     std::atomic_thread_fence(std::memory_order_release);  // the inverses before the launch that reads them
     VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
-              others.as<fe<F>>(), dh + nblk, dst, out_xy, out_inf, out_item);
+              others.as<fe<F>>(), dh + nblk, dst, out_xy, out_inf, out_item, (const fe<F>*)nullptr);
     return VC_OK;
 }
 

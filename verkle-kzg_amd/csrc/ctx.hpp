@@ -179,6 +179,8 @@ enum WsSlot {
     WS_GLV_FLAG,
     WS_RAW_B,  // radix-29 row sums of the sparse accumulate (converted by k_fast_store)
     WS_SP_ITEMS,  // to_data_item of the sparse commits' rows (msm_batch_sparse_items)
+    WS_NORM_CNT,  // the verkle normalisation's arrival counter (zero between launches)
+    WS_NORM_TOT,  // its block products and per-block cofactors (device scan)
     WS_COUNT_
 };
 
@@ -221,6 +223,7 @@ struct vc_ctx {
                                     // built into the other one while the current level runs)
     vk::PinBuf pin_norm_vk;         // block products / inverses of the verkle rows' normalisation
     vk::PinBuf pin_sparse_ck;       // chunk tables of the sparse commits' latency path
+    vk::PinBuf pin_sparse_ch;       // chunk lists of the sort-based sparse commits
     // free blocks of DevBuf(ctx) scratch (size -> pointer); all their users run on `stream`
     // (or are synchronised), so a block freed by one call is safely reused by the next in
     // stream order; vc_ctx_set_stream drains the old stream first
@@ -359,11 +362,14 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
                          const uint8_t* add_inf, const uint32_t* dst, uint64_t* out_xy, uint8_t* out_inf,
                          uint64_t* out_item, const std::function<void()>* overlap = nullptr);
 // d_add_ids (optional): row g also adds the canonical affine point (d_add_xy, d_add_inf)[d_add_ids[g]]
-// before the normalisation (0xffffffff: nothing) -- a verkle row that updates its old commitment
+// before the normalisation (0xffffffff: nothing) -- a verkle row that updates its old commitment.
+// d_dst (optional): row g's outputs go to index d_dst[g] (the tree's mirror). The normalisation is
+// normalize_rows_items' (polled, no stream wait; `overlap` runs once every kernel is queued).
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
                             const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items,
                             const uint32_t* d_add_ids = nullptr, const uint64_t* d_add_xy = nullptr,
-                            const uint8_t* d_add_inf = nullptr);
+                            const uint8_t* d_add_inf = nullptr, const uint32_t* d_dst = nullptr,
+                            const std::function<void()>* overlap = nullptr);
 // k_to_data_item over device points (canonical affine u64 x 8 + flags) into device items, on the
 // ctx stream (scheme.hip)
 int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, size_t n, void* d_items);

@@ -2120,42 +2120,44 @@ __global__ void k_iota(uint32_t* __restrict__ o, uint32_t n);
 // the rows (identity: rc = 0..batch, cptr = row_ptr; nothing is built).
 constexpr size_t SPARSE_CHNZ = 4;
 struct SparseChunks {
-    uvec<uint32_t> rc;
-    uvec<uint64_t> cptr;
+    const uint32_t* rc = nullptr;    // row g's chunks are [rc[g], rc[g + 1])
+    const uint64_t* cptr = nullptr;  // chunk k's non-zeros are [cptr[k], cptr[k + 1])
     size_t nch = 0;
     bool identity = false;
 };
-static void sparse_chunks(const uint64_t* row_ptr, size_t batch, bool rows_fit, SparseChunks* out) {
+// The chunk lists in one serial pass, straight into page-locked staging (one upload each): the two
+// pooled passes into fresh vectors they replace cost ~0.1 ms of idle GPU on a 17k-row verkle level
+// (the pool's wake-ups and page faults; profiles/r05/verkle/sparse_norm_vk/). The previous call's
+// uploads from the staging have completed: every sparse commit ends in a normalisation that saw its
+// first kernel finish (or waited for the stream).
+static int sparse_chunks(vc_ctx* ctx, const uint64_t* row_ptr, size_t batch, bool rows_fit, SparseChunks* out) {
     const size_t CHNZ = SPARSE_CHNZ;
     if (rows_fit) {  // the caller knows every row has 1..CHNZ non-zeros
         out->identity = true;
         out->nch = batch;
-        return;
+        return VC_OK;
     }
-    auto& rc = out->rc;
-    rc.resize(batch + 1);
-    pool_for(0, batch, 4096, [&](size_t g) {
-        const uint64_t len = row_ptr[g + 1] - row_ptr[g];
-        rc[g] = (uint32_t)(len == 0 ? 1 : (len + CHNZ - 1) / CHNZ);
-    });
-    uint32_t run = 0;
-    for (size_t g = 0; g <= batch; g++) {
-        const uint32_t c = g < batch ? rc[g] : 0u;
-        rc[g] = run;
-        run += c;
-    }
-    out->nch = run;
-    auto& cptr = out->cptr;
-    cptr.resize(out->nch + 1);
+    // max(1, ceil(len / CHNZ)) <= 1 + floor(len / CHNZ) chunks per row
+    const size_t cap = batch + row_ptr[batch] / CHNZ;
+    VK_TRY(ctx->pin_sparse_ch.ensure((cap + 1) * 8 + (batch + 1) * 4));
+    uint64_t* cptr = ctx->pin_sparse_ch.as<uint64_t>();
+    uint32_t* rc = reinterpret_cast<uint32_t*>(cptr + cap + 1);
+    size_t run = 0;
     cptr[0] = 0;
-    pool_for(0, batch, 4096, [&](size_t g) {
-        uint64_t* o = &cptr[rc[g] + 1];
-        if (row_ptr[g + 1] == row_ptr[g]) {
-            o[0] = row_ptr[g];
-            return;
+    for (size_t g = 0; g < batch; g++) {
+        rc[g] = (uint32_t)run;
+        const uint64_t lo = row_ptr[g], hi = row_ptr[g + 1];
+        if (lo == hi) {  // an empty row is one empty chunk (the identity)
+            cptr[++run] = lo;
+            continue;
         }
-        for (uint64_t j = row_ptr[g]; j < row_ptr[g + 1]; j += CHNZ) *o++ = std::min<uint64_t>(j + CHNZ, row_ptr[g + 1]);
-    });
+        for (uint64_t j = lo; j < hi; j += CHNZ) cptr[++run] = std::min<uint64_t>(j + CHNZ, hi);
+    }
+    rc[batch] = (uint32_t)run;
+    out->rc = rc;
+    out->cptr = cptr;
+    out->nch = run;
+    return VC_OK;
 }
 
 // The sparse commit on the device: columns d_cols (u32) and scalars d_sc (4 u64, canonical unless
@@ -2184,7 +2186,8 @@ template <class C, class Fr>
 static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
                              const uint32_t* d_cols_in, const void* d_sc_in, int mont, void* d_xy, uint8_t* d_inf,
                              void* d_items, const uint32_t* d_add_ids = nullptr, const uint64_t* d_add_xy = nullptr,
-                             const uint8_t* d_add_inf = nullptr) {
+                             const uint8_t* d_add_inf = nullptr, const uint32_t* d_dst = nullptr,
+                             const std::function<void()>* overlap = nullptr) {
     using Acc = typename C::Acc;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
@@ -2202,7 +2205,7 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     const FbGeom fg = t->fb_geom();
     const int W = fg.W;
     SparseChunks ch;
-    sparse_chunks(row_ptr, batch, rows_fit, &ch);
+    VK_TRY(sparse_chunks(ctx, row_ptr, batch, rows_fit, &ch));
     const size_t nch = ch.nch;
     if ((uint64_t)t->n * fg.stride() >= (1ull << 31)) return VC_E_RANGE;  // entry index + sign bit
     const size_t maxL = nnz * (size_t)W;
@@ -2243,8 +2246,8 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
         VK_LAUNCH(ctx, "sparse_iota", k_iota, (uint32_t)((batch + 1 + 255) / 256), 256, 0, d_rc.as<uint32_t>(),
                   (uint32_t)batch);
     } else {
-        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, ch.cptr.data(), (nch + 1) * 8, hipMemcpyHostToDevice, st));
-        VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, ch.rc.data(), (batch + 1) * 4, hipMemcpyHostToDevice, st));
+        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, ch.cptr, (nch + 1) * 8, hipMemcpyHostToDevice, st));
+        VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, ch.rc, (batch + 1) * 4, hipMemcpyHostToDevice, st));
     }
     const uint32_t* d_cols = d_cols_in;
     const uint32_t* d_sc = static_cast<const uint32_t*>(d_sc_in);
@@ -2290,6 +2293,18 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     }
     VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
               d_rc.as<uint32_t>(), d_rows.as<Acc>());
+    if constexpr (std::is_same<C, BN254G1>::value) {
+        // BN254 rows with items (the verkle levels): the old-commitment adds, the canonical points,
+        // their items and the placement at d_dst in normalize_rows_items' two kernels, the block
+        // products polled from page-locked memory (no copies, no stream wait, no separate item /
+        // scatter launches: ~40 us of idle GPU per level before, profiles/r05/verkle/)
+        if (d_items) {
+            lap("kernels");
+            return normalize_rows_items(ctx, d_rows.p, batch, d_add_ids, d_add_xy, d_add_inf, d_dst,
+                                        static_cast<uint64_t*>(d_xy), d_inf, static_cast<uint64_t*>(d_items), overlap);
+        }
+    }
+    if (d_dst || overlap) return VC_E_INVALID;  // (BN254 with items only)
     if (d_add_ids)  // rows that update a previous commitment: C_old + sum (delta_k) L_k
         VK_LAUNCH(ctx, "sparse_add_base", (k_rows_add_base<C>), (unsigned)((batch + 255) / 256), 256, 0,
                   d_rows.as<Acc>(), batch, d_add_ids, d_add_xy, d_add_inf);
@@ -2479,10 +2494,11 @@ int sparse_small_items_dev(vc_ctx* ctx, Table* t, const SmallRows& in, const std
 // BN254 sparse commits with device inputs and outputs (the verkle tree's device-resident levels)
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
                             const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items,
-                            const uint32_t* d_add_ids, const uint64_t* d_add_xy, const uint8_t* d_add_inf) {
-    if (t->curve != VC_CURVE_BN254) return VC_E_INVALID;
+                            const uint32_t* d_add_ids, const uint64_t* d_add_xy, const uint8_t* d_add_inf,
+                            const uint32_t* d_dst, const std::function<void()>* overlap) {
+    if (t->curve != VC_CURVE_BN254 || !d_items) return VC_E_INVALID;
     return sparse_commit_dev<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, rows_fit, d_cols, d_sc, 0, d_xy, d_inf, d_items,
-                                               d_add_ids, d_add_xy, d_add_inf);
+                                               d_add_ids, d_add_xy, d_add_inf, d_dst, overlap);
 }
 
 int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,

@@ -1389,8 +1389,12 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         if (!t->dirty_int[level].empty()) order.push_back(level);
     LevelLists lists[2];
     size_t next_built = 0;  // levels of `order` whose lists are built
+    // level cur's lists are in use: the other buffer takes order[cur + 1] (before the first level,
+    // cur = 0 and both buffers are free: order[0] and order[1] may be built during the extension
+    // commits' kernels)
+    size_t cur = 0;
     auto build_next = [&]() {
-        if (next_built < order.size()) {
+        if (next_built < order.size() && next_built <= cur + 1) {
             build_level(order[next_built], lists[next_built & 1], ctx->pin_verkle_lv[next_built & 1]);
             next_built++;
         }
@@ -1441,7 +1445,8 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             // rows of <= 4 non-zeros (random keys: one leaf per extension) are the sparse commit's
             // chunks as they are (an empty row is an empty chunk: the identity), no chunk lists
             VK_TRY(sparse_commit_items_dev(ctx, tab, 2 * E, rp, maxlen <= 4, d_cols, d_vals.p, d_xy.p,
-                                           d_inf.as<uint8_t>(), d_it.p));
+                                           d_inf.as<uint8_t>(), d_it.p, nullptr, nullptr, nullptr, nullptr,
+                                           order.empty() ? nullptr : &build_next_fn));
         }
         lap("ext c1 / c2 commits");
         DevBuf d_c4(ctx), d_v4(ctx);
@@ -1463,14 +1468,10 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             in.d_out_inf = m_inf;
             in.d_out_item = m_item;
             VK_TRY(sparse_small_items_dev(ctx, tab, in, order.empty() ? nullptr : &build_next_fn));
-        } else {
-            DevBuf d_xy4(ctx), d_inf4(ctx), d_it4(ctx);
-            VK_TRY(d_xy4.ensure(E * 64));
-            VK_TRY(d_inf4.ensure(E));
-            VK_TRY(d_it4.ensure(E * 32));
-            VK_TRY(sparse_commit_items_dev(ctx, tab, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, d_xy4.p,
-                                           d_inf4.as<uint8_t>(), d_it4.p));
-            VK_TRY(scatter(d_ids, E, d_xy4.p, d_inf4.as<uint8_t>(), d_it4.p));
+        } else {  // results straight into the mirror as well
+            VK_TRY(sparse_commit_items_dev(ctx, tab, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, m_cxy, m_inf,
+                                           m_item, nullptr, nullptr, nullptr, d_ids,
+                                           order.empty() ? nullptr : &build_next_fn));
         }
         lap("ext commits");
     }
@@ -1483,6 +1484,7 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     uint8_t root_inf = 1;
     bool root_known = false;
     for (size_t oi = 0; oi < order.size(); oi++) {
+        cur = oi;
         if (next_built <= oi) build_next();
         LevelLists& L = lists[oi & 1];
         if (L.status != VC_OK) return L.status;
@@ -1567,11 +1569,8 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             lap(L.any_delta ? "internal level (small, delta rows)" : "internal level (small)");
             continue;
         }
-        DevBuf d_vals(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
+        DevBuf d_vals(ctx);
         VK_TRY(d_vals.ensure(nz1 * 32));
-        VK_TRY(d_xy.ensure(B * 64));
-        VK_TRY(d_inf.ensure(B));
-        VK_TRY(d_it.ensure(B * 32));
         if (L.any_delta) {
             if (nnz)
                 VK_LAUNCH(ctx, "verkle_delta", k_vk_delta, grid(nnz), 256, 0, m_item, d_child, d_sidx,
@@ -1579,10 +1578,11 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         } else if (nnz) {
             VK_LAUNCH(ctx, "verkle_gather", k_vk_gather, grid(nnz), 256, 0, m_item, d_child, nnz, d_vals.as<uint64_t>());
         }
-        if (ov) (*ov)();  // (the sort-based path has no hook: build the next lists once its kernels are queued)
-        VK_TRY(sparse_commit_items_dev(ctx, tab, B, ptr.data(), false, d_cols, d_vals.p, d_xy.p, d_inf.as<uint8_t>(),
-                                       d_it.p, d_add, m_cxy, m_inf));
-        VK_TRY(scatter(d_ids, B, d_xy.p, d_inf.as<uint8_t>(), d_it.p));
+        // results straight into the mirror (a delta row's old commitment is read there by the first
+        // normalisation kernel, its new one written by the second); the next level's lists are built
+        // once this level's kernels are queued
+        VK_TRY(sparse_commit_items_dev(ctx, tab, B, ptr.data(), false, d_cols, d_vals.p, m_cxy, m_inf, m_item, d_add,
+                                       m_cxy, m_inf, d_ids, ov));
         lap(L.any_delta ? "internal level (sparse, delta rows)" : "internal level (sparse)");
     }
     // the root's commitment from the mirror (the rest stays there: host_valid = false)
