@@ -101,9 +101,9 @@ def parse():
 
 # N > 1 split of the headline MSM, chosen per N from the one-card per-rank probe
 # (verkle-kzg_amd/tools/split_probe.py: the slowest rank's share of a 2^20 MSM, point range vs
-# window part; profiles/r04/split_probe.txt: G = 2 points 1.70 ms against windows 1.80, G = 4 a tie
-# at 1.09 / 1.08, G = 8 windows 0.75 against points 1.81 -- an eighth of the points is too few for
-# the radix copies' 163,840-bucket tail)
+# window part, wall time without per-kernel events; profiles/r05/split_walltime/: G = 2 points
+# 1.41-1.42 ms against windows 1.54-1.58, G = 8 windows 0.60-0.62 against points 0.70-0.71 -- an
+# eighth of the points still pays the radix copies' whole bucket tail; G = 4 a tie in round 4)
 AUTO_SPLIT = {2: "points", 3: "points"}
 
 

@@ -1454,8 +1454,13 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         VK_TRY(d_v4.ensure(4 * E * 32));
         VK_LAUNCH(ctx, "verkle_ext_rows4", k_vk_ext_rows4, grid(4 * E), 256, 0, d_stem, d_it.as<uint64_t>(), E,
                   d_c4.as<uint32_t>(), d_v4.as<uint64_t>());
-        uvec<uint64_t> rp4(E + 1);
-        for (size_t k = 0; k <= E; k++) rp4[k] = 4 * k;
+        // rows of 4: row_ptr[k] = 4 k, kept between calls (a fresh 0.5 MB vector's page faults and
+        // fill were ~30 us of idle GPU before the width-4 commits)
+        static thread_local uvec<uint64_t> rp4;
+        if (rp4.size() < E + 1) {
+            rp4.resize(E + 1);
+            for (size_t k = 0; k <= E; k++) rp4[k] = 4 * k;
+        }
         if (small_ok(4 * E)) {  // results straight into the mirror
             SmallRows in;
             in.batch = E;
