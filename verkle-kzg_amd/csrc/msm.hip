@@ -939,9 +939,12 @@ __global__ void __launch_bounds__(1024) k_glv_radix_hist(const uint32_t* __restr
             skip[k] = i >= hi || (inf != nullptr && inf[i]);
             f[k] = i < hi ? load_scalar<Fr>(sc, i) : fe_zero<Fr>();
         }
+        // unrolled (no break): f[k] / skip[k] stay in registers -- a rolled loop indexed them
+        // dynamically, i.e. through scratch memory
+#pragma unroll
         for (int k = 0; k < PRE; k++) {
             const uint32_t i = i0 + (uint32_t)k * blockDim.x;
-            if (i >= hi) break;
+            if (i >= hi) continue;
             if (skip[k]) {
                 for (int w = 0; w < W; w++) dig[(size_t)w * nv + i] = dig[(size_t)w * nv + n + i] = 0;
                 continue;
