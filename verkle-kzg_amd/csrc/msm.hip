@@ -2294,8 +2294,14 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
         VK_LAUNCH(ctx, "sparse_store", (k_fast_store<C>), (nch + 255) / 256, 256, 0, d_raw.as<RAcc>(), (uint32_t)nch,
                   d_off.as<uint32_t>(), d_chunks.as<Acc>());
     }
-    VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
-              d_rc.as<uint32_t>(), d_rows.as<Acc>());
+    // one chunk per row (identity): the chunk sums are the rows -- no combine launch (a one-wave
+    // block per row only copied them: ~60 us for the 131,072 extension c1 / c2 rows)
+    Acc* rows_p = d_rows.as<Acc>();
+    if (ch.identity)
+        rows_p = d_chunks.as<Acc>();
+    else
+        VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
+                  d_rc.as<uint32_t>(), rows_p);
     if constexpr (std::is_same<C, BN254G1>::value) {
         // BN254 rows with items (the verkle levels): the old-commitment adds, the canonical points,
         // their items and the placement at d_dst in normalize_rows_items' two kernels, the block
@@ -2303,16 +2309,16 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
         // scatter launches: ~40 us of idle GPU per level before, profiles/r05/verkle/)
         if (d_items) {
             lap("kernels");
-            return normalize_rows_items(ctx, d_rows.p, batch, d_add_ids, d_add_xy, d_add_inf, d_dst,
+            return normalize_rows_items(ctx, rows_p, batch, d_add_ids, d_add_xy, d_add_inf, d_dst,
                                         static_cast<uint64_t*>(d_xy), d_inf, static_cast<uint64_t*>(d_items), overlap);
         }
     }
     if (d_dst || overlap) return VC_E_INVALID;  // (BN254 with items only)
     if (d_add_ids)  // rows that update a previous commitment: C_old + sum (delta_k) L_k
         VK_LAUNCH(ctx, "sparse_add_base", (k_rows_add_base<C>), (unsigned)((batch + 255) / 256), 256, 0,
-                  d_rows.as<Acc>(), batch, d_add_ids, d_add_xy, d_add_inf);
+                  rows_p, batch, d_add_ids, d_add_xy, d_add_inf);
     lap("kernels");
-    VK_TRY(normalize_to_canon(ctx, ctx->curve, d_rows.p, batch, d_xy, d_inf));
+    VK_TRY(normalize_to_canon(ctx, ctx->curve, rows_p, batch, d_xy, d_inf));
     lap("normalise");
     if (d_items) VK_TRY(to_data_item_device(ctx, d_xy, d_inf, batch, d_items));
     return VC_OK;
