@@ -14,6 +14,9 @@ the reference's naive MSM restated in C (oracle/c/ref_curve.c) timed on a bounde
 this host.
 
     python bench.py [--gpus N --steps K --warmup W]
+
+--gpus N > 1 starts N rank processes itself (torch.distributed.run on 127.0.0.1) unless a launcher
+already set WORLD_SIZE (then --gpus must equal it); --rehearse-one-gpu puts every rank on device 0.
 """
 import argparse
 import json
@@ -42,7 +45,7 @@ CURVE_TAG = {"bls12_381": "BLS381Fq", "bn254": "BN254Fq", "bandersnatch": "BandD
 SCALAR_BITS = {"bls12_381": 255, "bn254": 254, "bandersnatch": 253}
 # HBM bytes of the dominant kernel from rocprofv3 PMC passes of this same command
 # (scripts/bench_profile.sh -> verkle-kzg_amd/tools/prof_summary.py), refreshed each profiling round
-PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r05", "r04", "r03", "r02", "r01"))
+PMC_SUMMARY = next((p for p in (os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r06", "r05", "r04", "r03", "r02", "r01"))
                     if os.path.exists(p)), os.path.join(ROOT, "profiles", "r04", "pmc_summary.json"))
 # the headline's accumulate instantiation in the PMC summary: the shared-window copies in the pair
 # layout (AffP, the default), else the (x, y, -y) records (AffN), else the packed tables
@@ -60,7 +63,8 @@ def progress(msg):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 without a launcher's WORLD_SIZE starts N ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     # 20 untimed steps (~55 ms) before the timed region: measured 2.58-2.60 ms per step after 3,
     # 2.56 after 20, 2.53-2.55 after 100 on one box (the clock settles; profiles/r05/warmup/)
@@ -82,6 +86,7 @@ def parse():
     ap.add_argument("--no-verkle", action="store_true", help="skip the verkle-tree commitment line (8(f) rank 1)")
     ap.add_argument("--no-ipa", action="store_true", help="skip the single IPA prove/verify line (benches/ipa.rs)")
     ap.add_argument("--verkle-keys", type=int, default=1 << 16)
+    ap.add_argument("--verkle-reps", type=int, default=5, help="fresh trees / 1 % update rounds timed (medians)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the Pippenger CPU baseline (0: min(16, cpu_count), one GPU's CPU share)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 16, help="terms of the CPU naive MSM sample (~15 s)")
@@ -92,6 +97,8 @@ def parse():
                     help="multi-rank rehearsal on a 1-GPU box: every rank on device 0, gloo process group, "
                          "vc_comm host-callback exchange (RCCL refuses two ranks on one device); timings are "
                          "not scaling numbers")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank bookkeeping only (gloo, no GPU): rank 0 prints the world it ran in")
     ap.add_argument("--comm", choices=["capi", "torch"], default="capi",
                     help="N > 1 exchange: vc_comm (C ABI, RCCL) or torch.distributed all-gather")
     ap.add_argument("--msm-split", choices=["auto", "windows", "points"], default="auto",
@@ -950,9 +957,10 @@ def ipa_concurrent(N, datas, coms, per=16):
 def verkle_line(a, local, stream):
     """verkle-tree commitment (lib.rs:127-129 / node.rs:205-277) over a
     KZG(256) Lagrange SRS on BN254, 32-unit keys (Ethereum-style 31-byte stem + suffix), random
-    32-byte values: the full commitment of a fresh tree (after an untimed warm-up commitment of an
-    identical tree), then after 1% of the keys are updated
-    (only the dirty nodes of each level are recommitted, one batched launch per level)."""
+    32-byte values: the median full commitment of --verkle-reps fresh trees (after an untimed
+    warm-up commitment of an identical tree) and the median of --verkle-reps rounds of 1 % key
+    updates (only the dirty nodes of each level recommitted, one batched launch per level); every
+    root checked (result_check)."""
     from vkzg import scheme
     from vkzg.verkle import VerkleTree
     veng = vkzg.Engine("bn254", local)
@@ -977,52 +985,136 @@ def verkle_line(a, local, stream):
         w.insert_single(keys[i].tobytes(), wrng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
     w.commitment(veng, kzg.table)
     del w
-    # the kernel totals of a full commitment: an identical tree committed with per-kernel events
+    # the kernel totals of a full commitment: an identical tree committed with per-kernel events;
+    # its root is the reference every timed commitment below is checked against
     k = VerkleTree(32)
     for i in range(nk):
         k.insert_single(keys[i].tobytes(), vals[i].tobytes())
     veng.enable_timing(True)
     veng.reset_timing()
-    k.commitment(veng, kzg.table)
+    root_k = k.commitment(veng, kzg.table)
     veng.enable_timing(False)
     del k
+    kms = {}
+    for kn in ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup_init", "msm_fixup_jump",
+               "msm_fixup", "sparse_store", "sparse_combine", "norm_prep", "norm_finish", "fb_normalize",
+               "fb_commit", "fb_combine", "fb_commit_small", "to_data_item", "sparse_iota", "verkle_widen",
+               "verkle_ext_rows4", "verkle_gather", "verkle_dense", "verkle_scatter"):
+        ms, cnt = veng.kernel_time(kn)
+        if cnt:
+            kms[kn] = round(ms, 3)
+    gpu_ms = sum(kms.values())
+    # full commitments: FRESH trees (nothing committed yet), timed without per-kernel events, each
+    # root compared with tree k's
+    fulls, t_ins, st, same_full = [], [], None, True
+    for _ in range(a.verkle_reps):
+        t = VerkleTree(32)
+        t0 = time.perf_counter()
+        for i in range(nk):
+            t.insert_single(keys[i].tobytes(), vals[i].tobytes())
+        t_ins.append(time.perf_counter() - t0)
+        st = t.stats()
+        t0 = time.perf_counter()
+        root = t.commitment(veng, kzg.table)
+        fulls.append(time.perf_counter() - t0)
+        same_full &= root == root_k
+        del t
+    # 1 % updates: rounds of nk / 100 rewritten keys on one tree (dirty nodes only, delta rows)
     t = VerkleTree(32)
-    t0 = time.perf_counter()
     for i in range(nk):
         t.insert_single(keys[i].tobytes(), vals[i].tobytes())
-    t_ins = time.perf_counter() - t0
-    st = t.stats()
-    t0 = time.perf_counter()  # timed without per-kernel events
     t.commitment(veng, kzg.table)
-    t_full = time.perf_counter() - t0
-    kms = {}
-    for k in ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup_init", "msm_fixup_jump",
-              "msm_fixup", "sparse_store", "sparse_combine", "norm_prep", "norm_finish", "fb_normalize",
-              "fb_commit", "fb_combine", "fb_commit_small", "to_data_item", "sparse_iota", "verkle_widen",
-              "verkle_ext_rows4", "verkle_gather", "verkle_dense", "verkle_scatter"):
-        ms, cnt = veng.kernel_time(k)
-        if cnt:
-            kms[k] = round(ms, 3)
-    gpu_ms = sum(kms.values())
     upd = max(1, nk // 100)
-    for i in rng.integers(0, nk, size=upd):
-        t.insert_single(keys[i].tobytes(), rng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
-    dirty = t.stats()["dirty"]
-    t0 = time.perf_counter()
-    t.commitment(veng, kzg.table)
-    t_upd = time.perf_counter() - t0
+    upds, dirty = [], []
+    cur = vals.copy()
+    for _ in range(a.verkle_reps):
+        for i in rng.integers(0, nk, size=upd):
+            cur[i] = rng.integers(0, 256, size=32, dtype=np.uint8)
+            t.insert_single(keys[i].tobytes(), cur[i].tobytes())
+        dirty.append(t.stats()["dirty"])
+        t0 = time.perf_counter()
+        root_u = t.commitment(veng, kzg.table)
+        upds.append(time.perf_counter() - t0)
+    # the last update's root == a fresh tree of the final contents committed in full (untimed)
+    f = VerkleTree(32)
+    for i in range(nk):
+        f.insert_single(keys[i].tobytes(), cur[i].tobytes())
+    same_upd = f.commitment(veng, kzg.table) == root_u
+    del f, t
     veng.close()
+    if not (same_full and same_upd):
+        raise SystemExit(f"bench: verkle result check FAILED (full {same_full}, update {same_upd})")
+    full_med = float(np.median(fulls))
     return {"workload": f"verkle tree, {nk} random 32-unit keys, KZG(256) BN254 (8(f) rank 1)",
             "srs_fixed_base": "16-bit windows, 16 per scalar, 17.2 GB (setup, untimed)",
-            "nodes": st, "insert_s": t_ins, "full_commitment_ms": t_full * 1e3,
-            "nodes_per_s_full": st["dirty"] / t_full, "full_kernel_ms_total": kms,
-            "full_split_ms": {"gpu_kernels": gpu_ms, "host_and_transfers": t_full * 1e3 - gpu_ms},
-            "updated_keys": upd, "dirty_nodes": dirty, "update_commitment_ms": t_upd * 1e3}
+            "nodes": st, "insert_s": float(np.median(t_ins)),
+            "reps": a.verkle_reps,
+            "full_commitment_ms": full_med * 1e3,
+            "full_commitment_ms_all": [round(x * 1e3, 3) for x in fulls],
+            "nodes_per_s_full": st["dirty"] / full_med, "full_kernel_ms_total": kms,
+            "full_split_ms": {"gpu_kernels": gpu_ms, "host_and_transfers": full_med * 1e3 - gpu_ms,
+                              "host_and_transfers_frac": 1 - gpu_ms / (full_med * 1e3),
+                              "note": "kernels from one commitment with per-kernel events; wall = median of the fresh trees"},
+            "updated_keys": upd, "dirty_nodes": int(np.median(dirty)),
+            "update_commitment_ms": float(np.median(upds)) * 1e3,
+            "update_commitment_ms_all": [round(x * 1e3, 3) for x in upds],
+            "result_check": {"ok": True,
+                             "method": "every fresh tree's root == tree k's (committed with events); the last "
+                                       "update's root == a fresh tree of the final contents committed in full"}}
+
+
+def launch_ranks(a, argv):
+    """`--gpus N` (N > 1) without a launcher: start N rank processes under torch.distributed.run
+    (127.0.0.1, a free port) running this same command line, and return their exit status. Runs
+    BEFORE anything touches HIP in this process (no vkzg.lib(), no torch.cuda call): the ranks are
+    children, never an exec of a process that initialised the GPU. Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    progress(f"--gpus {a.gpus} without WORLD_SIZE: launching {a.gpus} ranks ({' '.join(cmd[1:7])} ...)")
+    return subprocess.call(cmd)
+
+
+def launch_check(a):
+    """--launch-check: the rank bookkeeping alone (gloo, no GPU): rank 0 prints the world and the
+    ranks that reported (tests/test_bench_launch.py runs `bench.py --gpus 2 --launch-check`)"""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+        got = [None] * world
+        dist.all_gather_object(got, {"rank": rank, "pid": os.getpid()})
+        dist.destroy_process_group()
+    else:
+        got = [{"rank": rank, "pid": os.getpid()}]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "gpus_flag": a.gpus, "ranks": got}), flush=True)
+
+
+def world_from_env(a):
+    """the world this process belongs to; refuses a --gpus that disagrees with a launcher's WORLD_SIZE"""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and a.gpus != world:
+        raise SystemExit(f"bench: --gpus {a.gpus} disagrees with WORLD_SIZE={world} set by the launcher")
+    if not a.rehearse_one_gpu and not a.launch_check and world > 1:
+        ndev = torch.cuda.device_count()  # (counting devices does not initialise HIP on this image)
+        if world > ndev:
+            raise SystemExit(f"bench: {world} ranks but {ndev} visible GPU(s); --rehearse-one-gpu puts every rank on device 0")
+    return world
 
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
+    world = world_from_env(a)
+    if a.launch_check:
+        launch_check(a)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.rehearse_one_gpu:  # every rank on device 0, gloo + host-callback exchange (see --help)
@@ -1373,19 +1465,23 @@ def main():
         # the deployable <= 32 GB table: 15 windows (14 of 17 bits, one of 16), 31.1 GB -- the adds
         # of c = 17's 15 windows from a smaller table (c = 17 x 15 is 32.2 GB)
         deploy = ctime(16, 15)
-        head = big or small
-        if head is None:  # neither table fits beside the rest on every rank
+        # the headline is the deployable <= 32 GB table: a 256-point CRS served
+        # from ~11 % of the card; the larger tables are named sub-lines
+        head = deploy or small or big
+        if head is None:  # no table fits beside the rest on every rank
             out["secondary"] = {"workload": f"{B} batched width-256 Bandersnatch commits (configs[2])",
                                 "skipped": "no fixed-base table fits on every rank"}
         else:
             out["secondary"] = {
                 "workload": f"{B} batched width-256 Bandersnatch commits (configs[2]), fixed-base "
                             f"c={head['window_bits']} ({head['windows']} windows, {head['wide_windows']} of them "
-                            f"{head['window_bits'] + 1} bits), batch split over {world} rank(s)",
+                            f"{head['window_bits'] + 1} bits, {head['table_bytes'] / 1e9:.1f} GB table), "
+                            f"batch split over {world} rank(s)",
                 **head,
+                "table_choice": "the deployable table (<= 32 GB) leads; larger tables below as sub-lines",
                 "c16": small,
                 "mixed_c18_w14": mixed,
-                "deployable_w15_31GB": deploy,
+                f"large_c{a.commit_window}_w{a.commit_windows}": big if big is not small else None,
             }
         cstate["eng"].close()
 

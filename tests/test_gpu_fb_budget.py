@@ -28,3 +28,24 @@ def test_auto_windows_follow_the_context_budget():
             assert np.array_equal(out, outs[0][0]) and np.array_equal(inf, outs[0][1])
     finally:
         e.close()
+
+
+def test_auto_budget_returns_when_a_table_is_precomputed_explicitly():
+    """a first-use table that is later precomputed explicitly (vc_fixed_base_precompute) stops
+    counting against the budget: the next first-use table gets 16-bit windows again"""
+    import vkzg
+    e = vkzg.Engine("bn254")
+    try:
+        n = 257
+        sc = vkzg.random_scalars("bn254", n, np.random.default_rng(9))
+        a = e.random_bases(n, seed=3)
+        want = e.msm_batch(a, sc, n)
+        assert e.fixed_base_geometry(a)[0] == 16
+        e.fixed_base_precompute(a, 8)               # explicit: 134 MB, outside the budget
+        assert e.fixed_base_geometry(a)[0] == 8
+        b = e.random_bases(n, seed=3)
+        got = e.msm_batch(b, sc, n)
+        assert e.fixed_base_geometry(b)[0] == 16
+        assert np.array_equal(got[0], want[0]) and np.array_equal(e.msm_batch(a, sc, n)[0], want[0])
+    finally:
+        e.close()

@@ -190,3 +190,33 @@ def test_verkle_paths_and_contexts_interleave(oracle_c):
     finally:
         e1.close()
         e2.close()
+
+
+def test_verkle_mirror_moves_between_devices(oracle_c):
+    """one tree committed alternately on contexts of devices 0 and 1: the mirror moves with the
+    context (mirror_pull reads the old device's mirror and leaves the caller's device current,
+    so the new mirror and scratch are allocated on the new context's device). Needs 2 GPUs."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    import vkzg
+    from pyoracle import verkle as ov
+    from vkzg.verkle import VerkleTree
+    e0, e1 = vkzg.Engine("bn254", 0), vkzg.Engine("bn254", 1)
+    try:
+        s0, s1 = _schemes(e0)["kzg"], _schemes(e1)["kzg"]
+        rng = random.Random(5)
+        N = 4
+        t, o = VerkleTree(N), ov.VerkleTree(N)
+        for step, (eng_, (table, commit)) in enumerate([(e0, s0), (e1, s1), (e0, s0), (e1, s1)]):
+            for _ in range(40):
+                k, v = _key(rng, N, 8), _val(rng)
+                try:
+                    o.insert_single(k, v)
+                except ov.VerklePanic:
+                    continue
+                t.insert_single(k, v)
+            assert t.commitment(eng_, table) == o.commitment(commit), step
+    finally:
+        e0.close()
+        e1.close()

@@ -98,3 +98,18 @@ def test_tree_semantics_match_oracle(N, arity, n):
         assert t.path_to_stem(k) == want
     if arity <= 4:
         assert rejected > 0   # the panic path is exercised
+
+
+def test_key32_sets_reach_every_reduction():
+    """tests/verkle32_keys.py (the key-length-32 GPU parity tests' stems) reaches stems >= r with
+    every quotient 0..5 of bytes_to_item's reduction (lagrange_basis.rs:175-176), leaf units on
+    both sides of N / 2 = 16 (c1 / c2, node.rs:226-239), and the oracle tree inserts them all
+    without the reference's panic"""
+    from verkle32_keys import R, key_set, value
+    from pyoracle import verkle as ov
+    keys = key_set(11)
+    assert {int.from_bytes(k, "little") // R for k in keys} >= {0, 1, 2, 3, 4, 5}
+    assert any(k[-1] < 16 for k in keys) and any(k[-1] >= 16 for k in keys)
+    o, rng = ov.VerkleTree(32), random.Random(3)
+    for k in keys:
+        o.insert_single(k, value(rng))

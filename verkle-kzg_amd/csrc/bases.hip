@@ -171,7 +171,9 @@ static int fill_t(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf,
     using F = typename C::F;
     t->curve = ctx->curve;
     t->n = n;
-    t->fb_c = t->fb_W = 0;  // any fixed-base tables are stale now
+    t->fb_c = t->fb_W = 0;  // any fixed-base tables are stale now: give their memory back
+    t->fb_auto = false;
+    t->fb.release();
     t->subgroup = -1;
     t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff)));

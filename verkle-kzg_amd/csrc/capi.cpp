@@ -78,14 +78,15 @@ void pool_return_uid(uint64_t uid, int dev, void* p, size_t cap) {
     {
         std::lock_guard<std::mutex> lk(g_live_mu);
         auto it = live_ctx().find(uid);
-        // (try_lock: the caller may hold this or another context's lock; then the block is freed)
+        // (try_lock: another thread may hold the context's lock, then the block is freed; the
+        // calling thread may hold it too -- the lock is recursive, so that try_lock succeeds)
         if (it != live_ctx().end() && it->second->mu.try_lock()) {
             pool_put(it->second, p, cap);
             it->second->mu.unlock();
             return;
         }
     }
-    if (dev >= 0) (void)hipSetDevice(dev);
+    DeviceScope on(dev);  // hipFree on the block's device; the caller's current device is restored
     (void)hipFree(p);
 }
 
@@ -165,7 +166,10 @@ void vc_ctx::timer_end(const char* name, hipEvent_t a, hipStream_t s) {
 
 uint64_t* vc_ctx::clk_slot() {
     constexpr uint32_t SLOTS = 256;
+    const bool fresh = clk.p == nullptr;
     if (!timing || clk.ensure(SLOTS * 4 * sizeof(uint64_t)) != VC_OK) return nullptr;
+    if (fresh && (hipMemsetAsync(clk.p, 0, clk.cap, stream) != hipSuccess || hipStreamSynchronize(stream) != hipSuccess))
+        return nullptr;
     if (clk_pending.size() >= SLOTS) return nullptr;  // uncollected slots would be overwritten
     const uint32_t s = clk_next++ % SLOTS;
     clk_pending.push_back(s);
@@ -174,8 +178,15 @@ uint64_t* vc_ctx::clk_slot() {
 
 void vc_ctx::collect_timers() {
     if (!clk_pending.empty()) {
+        // the stamping kernels ran on the context's (non-blocking) streams: wait for both before the
+        // read-back, and clear the slots after it, so a reused slot never shows an older launch
+        (void)hipStreamSynchronize(stream);
+        (void)hipStreamSynchronize(side_stream);
         std::vector<uint64_t> h(clk.cap / sizeof(uint64_t));
-        if (hipMemcpy(h.data(), clk.p, clk.cap, hipMemcpyDeviceToHost) == hipSuccess)
+        const bool ok = hipMemcpyAsync(h.data(), clk.p, clk.cap, hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                        hipMemsetAsync(clk.p, 0, clk.cap, stream) == hipSuccess &&
+                        hipStreamSynchronize(stream) == hipSuccess;
+        if (ok)
             for (uint32_t s : clk_pending) {
                 const uint64_t* v = &h[4 * (size_t)s];
                 if (v[2] > v[0] && v[3] > v[1]) {
@@ -203,7 +214,7 @@ namespace {
 
 struct Guard {
     vc_ctx* c;
-    std::lock_guard<std::mutex> lk;
+    std::lock_guard<std::recursive_mutex> lk;
     explicit Guard(vc_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); }
     ~Guard() {
         if (c->timing) c->collect_timers();
@@ -279,7 +290,7 @@ void vc_ctx_destroy(vc_ctx* ctx) {
     if (!ctx) return;
     vk::ctx_register(ctx, false);  // before its lock: no mirror block comes back to it after this
     {
-        std::lock_guard<std::mutex> lk(ctx->mu);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         (void)hipSetDevice(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (auto* t : ctx->tables) delete t;

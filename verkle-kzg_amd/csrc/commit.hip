@@ -649,6 +649,7 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
     if (t->fb_c == c && t->fb_W == W && t->fb_big == big && t->fb.p) return VC_OK;
     t->fb.release();
     t->fb_c = 0;
+    t->fb_auto = false;  // (fb_commit_t marks its own first-use builds)
     VK_TRY(t->fb.ensure(std::max<size_t>((size_t)n * g.stride(), 1) * sizeof(FbE<C>)));
     DevBuf Q, tmp, aff_w;
     VK_TRY(Q.ensure(std::max<uint32_t>(n, 1) * sizeof(Acc)));
@@ -679,7 +680,9 @@ static int fb_precompute_t(vc_ctx* ctx, Table* t, int c, int windows) {
 // window bits of the fixed-base tables a commit builds on first use (a table without
 // vc_fixed_base_precompute: the IPA CRS of the prover / verifier, the multiproof's D / E): the
 // widest c <= 16 whose table fits what is left of the context's budget for such tables
-// (VKZG_FB_BUDGET_GB, default 20 GB of the card's 288, less the ones built before), at least 8.
+// (VKZG_FB_BUDGET_GB, default 20 GB of the card's 288, less the ones built before and still held)
+// and into the device's free memory less a 4 GB margin (hipMemGetInfo), at least 8; a build that
+// still fails for memory retries one window bit narrower, down to 8 (fb_commit_t).
 // Fewer windows mean fewer table points per commit, hence fewer latency-path blocks and block
 // partials: the 257-point IPA CRS at c = 16 (16 windows, 17.2 GB) proves in 0.64 ms against 0.73 at
 // c = 8 (32 windows, 134 MB), the multiproof finish 0.99 against 1.15 ms (profiles/r05/fb_default_c/).
@@ -694,8 +697,11 @@ static int fb_default_c(size_t n, size_t used) {
     static const int forced = getenv("VKZG_FB_C_DEFAULT") ? atoi(getenv("VKZG_FB_C_DEFAULT")) : 0;
     static const double budget_gb = getenv("VKZG_FB_BUDGET_GB") ? atof(getenv("VKZG_FB_BUDGET_GB")) : 20.0;
     if (forced >= 4 && forced <= 20) return forced;
+    double limit = budget_gb * 1e9 - (double)used;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) limit = std::min(limit, (double)free_b - 4e9);
     for (int c = 16; c > 8; c--)
-        if ((double)used + fb_auto_bytes<Fr>(n, c) <= budget_gb * 1e9) return c;
+        if (fb_auto_bytes<Fr>(n, c) <= limit) return c;
     return 8;
 }
 
@@ -710,9 +716,14 @@ static int fb_commit_t(vc_ctx* ctx, Table* t, size_t width, const void* d_sc, si
     if (with_cols && (size_t)cols->extra >= t->n) return VC_E_RANGE;
     if (with_cols && cols->base(0, cols->n_main - 1) >= t->n) return VC_E_RANGE;
     if (t->fb_c == 0) {
-        const int c = fb_default_c<Fr>(t->n, ctx->fb_auto_bytes);
-        VK_TRY(fb_precompute_t<C>(ctx, t, c, 0));
-        ctx->fb_auto_bytes += (size_t)fb_auto_bytes<Fr>(t->n, c);
+        int c = fb_default_c<Fr>(t->n, ctx->fb_auto_used());
+        int st = fb_precompute_t<C>(ctx, t, c, 0);
+        while (st == VC_E_OOM && c > 8) {  // another context or caller took the memory: narrower
+            (void)hipGetLastError();
+            st = fb_precompute_t<C>(ctx, t, --c, 0);
+        }
+        VK_TRY(st);
+        t->fb_auto = true;
     }
     if (batch == 0) {
         if (overlap && *overlap) (*overlap)();
@@ -894,6 +905,8 @@ static int table_from_acc_t(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) 
     t->curve = ctx->curve;
     t->n = n;
     t->fb_c = t->fb_W = t->fb_big = 0;
+    t->fb_auto = false;
+    t->fb.release();
     t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(typename C::Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
@@ -1067,9 +1080,9 @@ bool fb_small_path(vc_ctx* ctx, Table* t, size_t width, size_t batch) {
     if (!t->fb_c) {  // before the default tables exist: the geometry fb_commit_t will build
         int c = 8, bits = 255;
         switch (t->curve) {
-            case VC_CURVE_BN254: c = fb_default_c<BN254Fr>(t->n, ctx->fb_auto_bytes), bits = BN254Fr::BITS; break;
-            case VC_CURVE_BLS12_381: c = fb_default_c<BLS381Fr>(t->n, ctx->fb_auto_bytes), bits = BLS381Fr::BITS; break;
-            default: c = fb_default_c<BandFr>(t->n, ctx->fb_auto_bytes), bits = BandFr::BITS; break;
+            case VC_CURVE_BN254: c = fb_default_c<BN254Fr>(t->n, ctx->fb_auto_used()), bits = BN254Fr::BITS; break;
+            case VC_CURVE_BLS12_381: c = fb_default_c<BLS381Fr>(t->n, ctx->fb_auto_used()), bits = BLS381Fr::BITS; break;
+            default: c = fb_default_c<BandFr>(t->n, ctx->fb_auto_used()), bits = BandFr::BITS; break;
         }
         W = (size_t)(bits + 1 + c - 1) / c;
     }

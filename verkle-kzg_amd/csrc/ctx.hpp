@@ -36,6 +36,21 @@ void pool_put(vc_ctx* ctx, void* p, size_t cap);
 void ctx_register(vc_ctx* ctx, bool live);
 void pool_return_uid(uint64_t uid, int dev, void* p, size_t cap);
 
+// hipSetDevice(dev) for a scope, the thread's previous current device restored at its end (helpers
+// that touch another context's memory must not leave the caller allocating on that device)
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        if (dev >= 0 && hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 // Device buffer. DevBuf(ctx) draws from / returns to the context's stream-ordered block pool
 // (per-call scratch of the scheme paths: a hipMalloc + hipFree pair per buffer per call cost
 // tens of us each, and hipFree synchronises the device); DevBuf() owns its memory outright.
@@ -122,6 +137,7 @@ struct Table {
     DevBuf inf;    // n x u8
     // fixed-base window tables for batched commits
     int fb_c = 0, fb_W = 0, fb_big = 0;
+    bool fb_auto = false;  // built on first use by a commit (counts against the context's budget)
     DevBuf fb;
     FbGeom fb_geom() const { return FbGeom{fb_c, fb_W, fb_big}; }
     // 1: every base lies in the prime-order subgroup (the GLV endomorphism acts as lambda, so
@@ -206,7 +222,10 @@ struct vc_ctx {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     hipStream_t side_stream = nullptr;  // second queue for latency-bound tails
-    std::mutex mu;
+    // recursive: pool_return_uid try_locks the context a released verkle mirror belongs to, and
+    // the releasing thread may already own that lock (try_lock by the owner of a plain std::mutex
+    // is undefined; on a recursive one it succeeds)
+    std::recursive_mutex mu;
     std::vector<vk::Table*> tables;
     vk::DevBuf ws[vk::WS_COUNT_];
     vk::DevBuf ws2[vk::WS_COUNT_];  // workspace of lane 1 (side_stream)
@@ -237,7 +256,6 @@ struct vc_ctx {
     uint32_t fb_lanes = 0;                // resident lanes of k_fb_commit_cm (cached per context)
     uint32_t small_epoch = 0;             // completion-flag epoch of the latency path's launches
     uint32_t tail_epoch = 0;              // the same for the MSM tails' direct completion (pin[0 / 1])
-    size_t fb_auto_bytes = 0;             // fixed-base tables built on first use (commit.hip fb_default_c)
     uint32_t norm_vk_parity = 0;          // the half of pin_norm_vk the last verkle normalisation used
     // geometry of the last MSM (vc_msm_last_plan): window bits c, windows W (of the whole MSM),
     // terms per point (2 with the GLV split), radix multiplier m (radix m 2^c; 1 = 2^c), shared
@@ -265,6 +283,14 @@ struct vc_ctx {
     void timer_end(const char* name, hipEvent_t a, hipStream_t s = nullptr);
     void collect_timers();  // call after the stream is synchronised
     vk::Lane lane(int i) { return i == 0 ? vk::Lane{stream, ws, &pin[0]} : vk::Lane{side_stream, ws2, &pin[1]}; }
+    // bytes of the fixed-base tables built on first use that this context still holds (commit.hip
+    // fb_default_c's budget; a table refilled or re-precomputed explicitly stops counting)
+    size_t fb_auto_used() const {
+        size_t s = 0;
+        for (const vk::Table* t : tables)
+            if (t && t->fb_auto && t->fb.p) s += t->fb.cap;
+        return s;
+    }
     vk::Table* table(int id) {
         if (id < 0 || id >= (int)tables.size() || !tables[id]) return nullptr;
         return tables[id];

@@ -946,7 +946,7 @@ using namespace vk;
 namespace {
 struct Guard {
     vc_ctx* c;
-    std::lock_guard<std::mutex> lk;
+    std::lock_guard<std::recursive_mutex> lk;
     explicit Guard(vc_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); }
     ~Guard() {
         if (c->timing) c->collect_timers();

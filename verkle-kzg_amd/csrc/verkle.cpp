@@ -796,7 +796,8 @@ static int mirror_pull(vc_verkle* t) {
     if (t->host_valid) return VC_OK;
     const size_t n = std::min(t->nodes.size(), D.cap);
     if (D.ctx_uid && n) {
-        VK_CHECK_HIP(hipSetDevice(D.dev));
+        DeviceScope on(D.dev);  // the mirror's device, the caller's restored on return (a move to
+                                // another context allocates the new mirror on that one's device)
         VK_CHECK_HIP(hipMemcpy(t->item.data(), D.item, n * 32, hipMemcpyDeviceToHost));
         VK_CHECK_HIP(hipMemcpy(t->cxy.data(), D.cxy, n * 64, hipMemcpyDeviceToHost));
         VK_CHECK_HIP(hipMemcpy(t->cinf.data(), D.inf, n, hipMemcpyDeviceToHost));
@@ -812,6 +813,7 @@ static int mirror_prepare(vc_ctx* ctx, vc_verkle* t) {
     if (D.ctx_uid != ctx->uid) {  // first use, or another context: rebuild from the host arrays
         VK_TRY(mirror_pull(t));
         D.release();
+        VK_CHECK_HIP(hipSetDevice(ctx->device));  // (both restore it; allocations below are ctx's)
     }
     const bool fresh = D.ctx_uid == 0;
     if (D.cap < n) {  // (with room: a tree that grows by an update's splits keeps its buffers)
@@ -1188,7 +1190,7 @@ __global__ void k_vk_dense(const uint32_t* __restrict__ row, const uint32_t* __r
 
 int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy, uint8_t* out_inf) {
     if (!ctx || !t || !out_xy || !out_inf) return VC_E_INVALID;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     VK_CHECK_HIP(hipSetDevice(ctx->device));
     struct Collect {  // the per-kernel timers (vc_ctx_enable_timing), as the C ABI's Guard does
         vc_ctx* c;
