@@ -1025,20 +1025,25 @@ def verkle_line(a, local, stream):
         t.insert_single(keys[i].tobytes(), vals[i].tobytes())
     t.commitment(veng, kzg.table)
     upd = max(1, nk // 100)
-    upds, dirty = [], []
-    cur = vals.copy()
+    upds, dirty, history = [], [], []
     for _ in range(a.verkle_reps):
-        for i in rng.integers(0, nk, size=upd):
-            cur[i] = rng.integers(0, 256, size=32, dtype=np.uint8)
-            t.insert_single(keys[i].tobytes(), cur[i].tobytes())
+        for i in rng.choice(nk, size=upd, replace=False):
+            history.append((keys[i].tobytes(), rng.integers(0, 256, size=32, dtype=np.uint8).tobytes()))
+            t.insert_single(*history[-1])
         dirty.append(t.stats()["dirty"])
         t0 = time.perf_counter()
         root_u = t.commitment(veng, kzg.table)
         upds.append(time.perf_counter() - t0)
-    # the last update's root == a fresh tree of the final contents committed in full (untimed)
+    # the last update's root == a fresh tree with the same insertion history committed in full
+    # (untimed). Not the final contents inserted once: the reference's level-skipping splits
+    # (node.rs:176-185) make the trie depend on the order, and re-inserting a key below such a
+    # split can add a second extension for it (an oracle replay of this bench's first round: 65,537
+    # extensions against 65,536), so that tree may have another shape and root
     f = VerkleTree(32)
     for i in range(nk):
-        f.insert_single(keys[i].tobytes(), cur[i].tobytes())
+        f.insert_single(keys[i].tobytes(), vals[i].tobytes())
+    for kv in history:
+        f.insert_single(*kv)
     same_upd = f.commitment(veng, kzg.table) == root_u
     del f, t
     veng.close()
@@ -1060,7 +1065,8 @@ def verkle_line(a, local, stream):
             "update_commitment_ms_all": [round(x * 1e3, 3) for x in upds],
             "result_check": {"ok": True,
                              "method": "every fresh tree's root == tree k's (committed with events); the last "
-                                       "update's root == a fresh tree of the final contents committed in full"}}
+                                       "update's root == a fresh tree with the same insertion history "
+                                       "committed in full"}}
 
 
 def launch_ranks(a, argv):

@@ -7,7 +7,8 @@ of tests/verkle32_keys.py cover every quotient estimate of verkle.cpp's item_of_
 k r, k r + 1 for k = 1..5, 2^256 - 1, stems below k r with k r's top limb) and random stems >= r;
 leaf units < 16 and >= 16 fill c1 and c2 (node.rs:226-239). Each tree is committed fresh, then
 after two update rounds (~1 % of the keys rewritten plus a few new keys: dirty nodes only, delta
-rows on the device path), on the device path (default, every sparse level on the sort-based path,
+rows on the device path; one rewrite lands below a level-skipping split and adds a second extension
+for its stem, as the reference does -- tests/verkle32_keys.py quirk_keys), on the device path (default, every sparse level on the sort-based path,
 every level dense), the host path, a 2-member vc_group and 2 SPMD ranks (node slices per level),
 over KZG(256) (the bench's scheme) and IPA(256)."""
 import json
@@ -16,7 +17,7 @@ import random
 
 import pytest
 
-from verkle32_keys import key_set, value
+from verkle32_keys import key_set, quirk_keys, value
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -27,11 +28,14 @@ def _rounds(seed=11):
     """[(key, value)] per round: the full tree, then two update rounds of ~1 % rewrites + new keys"""
     rng = random.Random(seed)
     keys = key_set(seed)
-    rounds = [[(k, value(rng)) for k in keys]]
+    first, again = quirk_keys()
+    rounds = [[(k, value(rng)) for k in keys + first]]
     extra = key_set(seed + 1, n_random=12)
     for r in range(2):
         upd = [(k, value(rng)) for k in rng.sample(keys, max(3, len(keys) // 100))]
         upd += [(k, value(rng)) for k in extra[r * 6:(r + 1) * 6]]
+        if r == 0:  # the update that adds a second extension for one stem (the reference's quirk)
+            upd.append((again, value(rng)))
         rounds.append(upd)
     return rounds
 

@@ -113,3 +113,26 @@ def test_key32_sets_reach_every_reduction():
     o, rng = ov.VerkleTree(32), random.Random(3)
     for k in keys:
         o.insert_single(k, value(rng))
+
+
+def test_key32_quirk_update_adds_an_extension():
+    """the reference's level-skipping split (node.rs:176-185) makes a later re-insert of a key add a
+    second extension for its stem: the oracle and the engine's host trie agree on the shape"""
+    from verkle32_keys import quirk_keys, value
+    from pyoracle import verkle as ov
+    from vkzg.verkle import VerkleTree
+    first, again = quirk_keys()
+    o, t, rng = ov.VerkleTree(32), VerkleTree(32), random.Random(4)
+    for k in first:
+        v = value(rng)
+        o.insert_single(k, v)
+        t.insert_single(k, v)
+    n_before = t.stats()["extension"]
+    v = value(rng)
+    o.insert_single(again, v)
+    t.insert_single(again, v)
+    assert t.stats()["extension"] == n_before + 1 == 4
+
+    def exts(node):
+        return 1 if node.ext else sum(exts(c) for c in node.children.values())
+    assert exts(o.root) == 4

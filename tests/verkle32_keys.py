@@ -50,5 +50,17 @@ def key_set(seed, n_random=300):
     return keys
 
 
+def quirk_keys():
+    """A, B, C in this order, then A again: A and B share units 0-1, so their split puts an
+    internal node at root slot 200 keyed by unit 2 (the reference's level-skipping split,
+    node.rs:176-185); C (unit 1 = A's unit 2) then reaches A's extension through that node at depth
+    1 and splits it; re-inserting A walks slot 200 -> unit A[1] = 7, finds nothing and adds a second
+    extension for A's stem. Returned as (first-round keys, the key to re-insert later)."""
+    a = bytes([200, 7, 1]) + bytes(range(3, 32))
+    b = bytes([200, 7, 2]) + bytes(range(3, 32))
+    c = bytes([200, 1, 9]) + bytes(range(40, 69))
+    return [a, b, c], a
+
+
 def value(rng):
     return bytes(rng.randrange(256) for _ in range(32))
