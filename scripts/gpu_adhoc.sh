@@ -1,10 +1,9 @@
 set -eu
-O=gpurun_out/r06_e; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_verkle32.py tests/test_gpu_verkle.py -k "verkle32 or update_equals" > $O/tests.txt 2>&1
-echo tests-ok; tail -2 $O/tests.txt
-timeout -k 10 300 python -u verkle-kzg_amd/tools/verkle_update_check.py 65536 5 91 0 > $O/update_check.txt 2>&1
-echo check-ok; tail -5 $O/update_check.txt
-timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-secondary --no-kzg --no-mp --no-ipa > $O/bench_verkle.json 2> $O/bench_verkle.err
-echo bench-ok
-timeout -k 10 300 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --no-kzg --no-mp --no-ipa --no-verkle > $O/rehearse_2rank.json 2> $O/rehearse_2rank.err
-echo rehearse-ok
+R=$(pwd)
+O=$R/gpurun_out/r06_h; mkdir -p $O
+timeout -k 10 120 $R/verkle-kzg_amd/tools/affine_probe 32 3 > $O/affine_probe.txt 2>&1
+echo probe-ok; cat $O/affine_probe.txt
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv -d $O/pmc -o run -- $R/verkle-kzg_amd/tools/affine_probe 32 1 > $O/affine_probe_pmc_run.txt 2>&1
+echo pmc-ok
+find $O/pmc -name "*.csv" | head

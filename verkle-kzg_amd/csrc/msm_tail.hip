@@ -6,6 +6,7 @@
 // back to the ec.hpp form (for the host Horner pass).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "ctx.hpp"
@@ -16,6 +17,37 @@
 namespace vk {
 
 constexpr uint32_t NONE_T = 0xffffffffu;
+
+// Diagnostic build only (-DVKZG_TAIL_TRACE, tools/tail_trace.py): every lane of the tail kernels
+// records its entry and exit on the 100 MHz s_memrealtime clock, its wave's hardware slot (HW_ID,
+// XCC_ID) and a kernel-specific word (the fix-up's chain length, the bit sums' kind and item count)
+// into g_tail_trace[kernel][global thread] (4 x u64, vector stores); the default build has none.
+#ifdef VKZG_TAIL_TRACE
+constexpr uint32_t TT_KERNELS = 4, TT_MAXT = 1u << 18;
+__device__ unsigned long long g_tail_trace[(size_t)TT_KERNELS * TT_MAXT * 4];
+struct TTLane {
+    unsigned long long t0;
+    uint32_t kid, info = 0;
+    __device__ explicit TTLane(uint32_t k) : t0(__builtin_amdgcn_s_memrealtime()), kid(k) {}
+    __device__ ~TTLane() {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+        if (g >= TT_MAXT) return;
+        unsigned long long* p = g_tail_trace + ((size_t)kid * TT_MAXT + g) * 4;
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        p[0] = t0;
+        p[1] = t1;
+        p[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        p[3] = (unsigned long long)info | (1ull << 63);
+    }
+};
+#define TT_BEGIN(k) TTLane tt_lane_(k)
+#define TT_INFO(x) (tt_lane_.info = (uint32_t)(x))
+#else
+#define TT_BEGIN(k) ((void)0)
+#define TT_INFO(x) ((void)0)
+#endif
 
 // ---- fix-up of buckets that straddle accumulate threads. Thread u's carry piece (through[u]
 // = 1: the bucket ends in u; 2: it continues into u + 1) belongs to the bucket whose owner
@@ -105,6 +137,7 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk_q(typename A::Acc* __res
                                                          const typename A::Acc* __restrict__ owner_piece,
                                                          const uint32_t* __restrict__ offsets, uint32_t NBtot,
                                                          uint32_t M, uint32_t limit, const uint32_t* __restrict__ owner_b) {
+    TT_BEGIN(0);
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, b = gid >> 2, role = gid & 3;
     if (b >= NBtot) return;  // whole quads (NBtot * 4 threads)
     const uint32_t lo = offsets[b], hi = offsets[b + 1];
@@ -112,6 +145,7 @@ __global__ void __launch_bounds__(256) k_msm_fixup_walk_q(typename A::Acc* __res
     const uint32_t t0 = lo / M, t1 = (hi - 1) / M;
     if (t0 == t1 || t1 - t0 > limit) return;  // uniform over the quad
     if (owner_b && owner_b[t0] == NONE_T) return;  // merged inside the accumulate (written)
+    TT_INFO(t1 - t0);
     typename A::Acc acc = owner_piece[t0];
     for (uint32_t u = t0 + 1; u <= t1; u++) {
         const typename A::Acc o = carry[u];
@@ -133,6 +167,7 @@ __global__ void __launch_bounds__(256) k_msm_fixup_own(typename A::Acc* __restri
                                                       const uint32_t* __restrict__ owner_bucket,
                                                       const uint8_t* __restrict__ through, uint32_t Tmax,
                                                       const uint32_t* __restrict__ Lp, uint32_t M, uint32_t limit) {
+    TT_BEGIN(0);
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t T = (*Lp + M - 1) / M;
     if (t >= T || t >= Tmax) return;
@@ -156,6 +191,7 @@ __global__ void __launch_bounds__(256) k_msm_fixup_own(typename A::Acc* __restri
             u1++;
         }
     }
+    TT_INFO(u1 - t);
     // one add call site (an inlined add is ~34 KB of code: two would not share the I-cache)
     for (uint32_t u = t + 1;; u++) {
         acc = A::add(acc, c1);
@@ -284,9 +320,11 @@ __global__ void __launch_bounds__(256) k_msm_segr_q(const typename A::Acc* __res
                                                    const uint32_t* __restrict__ offsets, uint32_t NB, int W,
                                                    uint32_t Lseg, uint32_t S, typename A::Acc* __restrict__ Rs) {
     using Acc = typename A::Acc;
+    TT_BEGIN(1);
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, q = gid >> 2, role = gid & 3;
     const uint32_t w = q / S, s = q % S;
     if (w >= (uint32_t)W) return;  // whole quads
+    TT_INFO(Lseg);
     const size_t g0 = (size_t)w * NB + (size_t)s * Lseg;
     Acc R = A::zero();
     for (uint32_t r = 0; r < Lseg; r++) {
@@ -330,6 +368,7 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
                                                    const uint32_t* __restrict__ uoff,
                                                    typename A::Acc* __restrict__ partial) {
     using Acc = typename A::Acc;
+    TT_BEGIN(2);
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (gw >= n_waves) return;  // grid rounded up to whole blocks (uniform per wave)
     const uint32_t G = h ? 1u << h : 0u, Hn = h ? 1u << (J - h) : 0u;
@@ -366,6 +405,7 @@ __global__ void __launch_bounds__(256) k_msm_bitsum(const typename A::Acc* __res
     uint32_t lg_lanes = 0;  // xor levels of the fold inside a sum's lane group
     while ((1u << lg_lanes) < lanes) lg_lanes++;
     const size_t out = (size_t)w * (nTs + nU * nb2) + slot;
+    TT_INFO(kind << 24 | Kw);
     Acc v = A::zero();
     if constexpr (A::quad) {
         // Kw serial full adds per lane (every SIMD busy: issue-bound), then the wave's 64 lane sums
@@ -509,9 +549,11 @@ __global__ void __launch_bounds__(64 * SUMPART_WAVES) k_msm_sumpart_q(const type
     constexpr uint32_t QPB = 16 * SUMPART_WAVES, LGW = SUMPART_WAVES == 4 ? 2 : SUMPART_WAVES == 2 ? 1 : 0;
     static_assert((1u << LGW) == SUMPART_WAVES, "SUMPART_WAVES: 1, 2 or 4");
     __shared__ Acc wave_sum[SUMPART_WAVES];
+    TT_BEGIN(3);
     const uint32_t sum = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, role = lane & 3;
     const PartLoc loc(sum, J, h, nU, nb1, nb2, pL, urow != 0);
     const uint32_t cnt = loc.cnt;
+    TT_INFO(cnt);
     const uint32_t nk = (cnt + QPB - 1) / QPB;
     Acc v = A::zero();
     for (uint32_t it = 0; it < nk + 4 + LGW; it++) {  // one add call site
@@ -694,6 +736,21 @@ int msm_tail_reduce(vc_ctx* ctx, Lane L, const FAcc<C>* buckets, const uint32_t*
                      tp.nb2, tp.pL, tp.urow ? 1u : 0u, out, dir);
     return VC_OK;
 }
+
+#ifdef VKZG_TAIL_TRACE
+// the trace (TT_KERNELS x TT_MAXT x 4 u64) -> host, then cleared (diagnostic build only; not part
+// of the C ABI in include/)
+extern "C" int vkzg_tail_trace_fetch(unsigned long long* out, size_t words) {
+    const size_t all = sizeof(g_tail_trace) / sizeof(unsigned long long);
+    void* dp = nullptr;
+    VK_CHECK_HIP(hipGetSymbolAddress(&dp, HIP_SYMBOL(g_tail_trace)));
+    VK_CHECK_HIP(hipDeviceSynchronize());
+    if (out) VK_CHECK_HIP(hipMemcpy(out, dp, std::min(words, all) * 8, hipMemcpyDeviceToHost));
+    VK_CHECK_HIP(hipMemset(dp, 0, sizeof(g_tail_trace)));
+    VK_CHECK_HIP(hipDeviceSynchronize());
+    return VC_OK;
+}
+#endif
 
 #define VK_INST_TAIL(C)                                                                                      \
     template int msm_tail_fixup<C>(vc_ctx*, Lane, uint32_t, const uint32_t*, uint32_t, FAcc<C>*, FAcc<C>*,           \
