@@ -598,13 +598,13 @@ static void ext_rows(const vc_verkle* t, int id, Rows& r) {
     }
 }
 // the device path's extension rows: c1 / c2 as ext_rows, but with 16-byte values (a leaf half is
-// below 2^128: the device widens them) and the node's stem item computed while its lines are in
-// cache; stem[] is indexed by the row pair
+// below 2^128: the device widens them) and the node's raw stem bytes (the device reduces them mod r);
+// stem[] is indexed by the row pair
 struct ExtRows16 {
     uvec<uint64_t> ptr{0};
     uvec<uint32_t> cols;
     uvec<uint64_t> vals;  // 2 u64 per non-zero
-    uvec<uint64_t> stem;  // 4 u64 per extension node (its stem item)
+    uvec<uint64_t> stem;  // 4 u64 per extension node (its raw stem bytes, LE)
     uint32_t maxlen = 0;  // longest row (<= 4: the sparse commit's chunks are the rows)
     void clear() {  // (capacity kept)
         ptr.assign(1, 0);
@@ -660,8 +660,11 @@ static void ext_rows16(const vc_verkle* t, int id, ExtRows16& r) {
         r.maxlen = std::max<uint32_t>(r.maxlen, (uint32_t)(r.cols.size() - r.ptr.back()));
         r.ptr.push_back(r.cols.size());
     }
+    // the stem's raw LE bytes (zero beyond N): k_vk_ext_rows4 reduces them mod r on the device
+    // (bytes_to_item(stem.to_bytes()), node.rs:248-250 -> lagrange_basis.rs:175-176) -- the host's
+    // one-quotient reduction was ~35 % of this stage's single-thread time (profiles/r05/verkle/)
     r.stem.resize(r.stem.size() + 4);
-    item_of_bytes(n.stem.data(), N, r.stem.data() + r.stem.size() - 4);  // bytes_to_item(stem.to_bytes())
+    memcpy(r.stem.data() + r.stem.size() - 4, n.stem.data(), 32);
 }
 
 static void ext_prefetch(const vc_verkle* t, int id, int stage) {
@@ -675,8 +678,9 @@ static void ext_prefetch(const vc_verkle* t, int id, int stage) {
 }
 
 // The extension level's host stage (verkle_commitment_dev): c1 / c2 rows built in per-worker parts
-// (with each node's stem item), then merged in parallel straight into one buffer (page-locked in the
-// commitment: the upload is plain DMA) laid out as row_ptr (2E + 1 u64) | stem items (E x 4 u64) |
+// (with each node's raw stem bytes, reduced on the device), then merged in parallel straight into one
+// buffer (page-locked in the commitment: the upload is plain DMA) laid out as row_ptr (2E + 1 u64) |
+// stems (E x 32 B) |
 // values (nnz x 2 u64) | node ids (E u32) | cols (nnz u32) -- everything after row_ptr goes up in one
 // copy. `cache`: part storage kept between calls (no page faults on fresh vectors).
 struct ExtStage {
@@ -1145,7 +1149,9 @@ __global__ void k_vk_widen16(const uint64_t* __restrict__ in, size_t n, uint64_t
     out[4 * j + 2] = 0;
     out[4 * j + 3] = 0;
 }
-// extension commitment rows [1, stem item, c1 item, c2 item] (node.rs:245-256), columns 0..3
+// extension commitment rows [1, stem item, c1 item, c2 item] (node.rs:245-256), columns 0..3; the
+// stem arrives as its raw 32 LE bytes and is reduced mod r here (from_le_bytes_mod_order of a value
+// below 2^256 < 6 r: at most five subtractions)
 __global__ void k_vk_ext_rows4(const uint64_t* __restrict__ stem, const uint64_t* __restrict__ it12, size_t E,
                                uint32_t* __restrict__ cols, uint64_t* __restrict__ vals) {
     const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // entry 4 k + c
@@ -1155,11 +1161,28 @@ __global__ void k_vk_ext_rows4(const uint64_t* __restrict__ stem, const uint64_t
     cols[j] = c;
     const uint64_t one[4] = {1, 0, 0, 0};
     const uint64_t* v = c == 0 ? one : c == 1 ? stem + 4 * k : it12 + 4 * (2 * k + (c - 2));
+    uint64_t w[4] = {v[0], v[1], v[2], v[3]};
+    if (c == 1) {
+        constexpr uint64_t R[4] = {0x43e1f593f0000001ULL, 0x2833e84879b97091ULL, 0xb85045b68181585dULL,
+                                   0x30644e72e131a029ULL};  // BN254 r
+        for (int it = 0; it < 5; it++) {
+            uint64_t d[4], br = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint64_t a = w[i], b = R[i];
+                d[i] = a - b - br;
+                br = (a < b || (a == b && br)) ? 1 : 0;
+            }
+            if (br) break;  // w < r
+#pragma unroll
+            for (int i = 0; i < 4; i++) w[i] = d[i];
+        }
+    }
     uint64_t* o = vals + 4 * j;
-    o[0] = v[0];
-    o[1] = v[1];
-    o[2] = v[2];
-    o[3] = v[3];
+    o[0] = w[0];
+    o[1] = w[1];
+    o[2] = w[2];
+    o[3] = w[3];
 }
 // rows' results -> the mirror at their node ids
 __global__ void k_vk_scatter(const uint32_t* __restrict__ ids, size_t n, const uint64_t* __restrict__ xy,
