@@ -470,63 +470,27 @@ int vc_group_multiproof_prove_many(vc_group* g, int scheme, int id, size_t N, si
     if (!g->table_ok(id)) return VC_E_TABLE;
     const int G = g->size();
     std::vector<int> st(G, VC_OK);
-    // each member's proofs in up to 4 sub-batches over two device buffers: sub-batch b + 1's
-    // evaluations (Q N 32 B per proof, 512 MiB at 2^16 x 256) cross PCIe on an uploader thread
-    // while sub-batch b is proven, instead of one blocking copy of the member's whole slice before
-    // its first proof
+    // each member's proofs in ONE upload and one vc_multiproof_prove_many (its proofs' transcripts
+    // and GPU phases pipelined inside). Round 6 measured the alternative -- sub-batches over two
+    // device buffers, the next one's data crossing PCIe on an uploader thread while the current one
+    // is proven -- and it was slower (G = 1 / 2 on one card, 4 proofs of 2^14 x 256: 13.9-15.0 /
+    // 13.0-13.3 ms against 12.6 / 11.8-12.1, profiles/r06/group/): a proof's own latency (its
+    // transcript, ~3 ms) exceeds one proof's upload (128 MB in ~2.5 ms), so splitting the call
+    // costs the pipelining across proofs more than the overlap gives back
     return g->run(st, [&](int k) {
         auto share = [&]() -> int {
             size_t lo, hi;
             vk::shard_range(P, k, G, &lo, &hi);
             if (hi == lo) return VC_OK;
-            const size_t per = Q * N * 32, np = hi - lo;
-            const size_t nb = std::min<size_t>(np, 4), S = (np + nb - 1) / nb;
-            VK_TRY(g->data[k].ensure((np > S ? 2 : 1) * S * per));
+            const size_t bytes = (hi - lo) * Q * N * 32;
+            VK_TRY(g->data[k].ensure(bytes));
             VK_CHECK_HIP(hipSetDevice(g->ctx[k]->device));
-            uint8_t* buf[2] = {static_cast<uint8_t*>(g->data[k].p), static_cast<uint8_t*>(g->data[k].p) + S * per};
-            const int dev = g->ctx[k]->device;
-            auto upload = [&](size_t b) -> int {  // sub-batch b -> buf[b & 1], on its own stream
-                const size_t p0 = lo + b * S, cnt = std::min(S, hi - p0);
-                VK_CHECK_HIP(hipSetDevice(dev));
-                hipStream_t s = nullptr;
-                VK_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-                hipError_t e = hipMemcpyAsync(buf[b & 1], data + p0 * Q * N * 4, cnt * per, hipMemcpyHostToDevice, s);
-                if (e == hipSuccess) e = hipStreamSynchronize(s);
-                (void)hipStreamDestroy(s);
-                VK_CHECK_HIP(e);
-                return VC_OK;
-            };
-            const size_t nsub = (np + S - 1) / S;
-            VK_TRY(upload(0));
-            for (size_t b = 0; b < nsub; b++) {
-                int st_up = VC_OK;
-                std::thread up;
-                if (b + 1 < nsub) {
-                    try {
-                        up = std::thread([&, b] {
-                            try {
-                                st_up = upload(b + 1);
-                            } catch (...) {  // nothing may leave a thread function
-                                st_up = VC_E_OOM;
-                            }
-                        });
-                    } catch (const std::system_error&) {
-                        st_up = -1;  // no thread: upload after this sub-batch
-                    }
-                }
-                const size_t p0 = lo + b * S, cnt = std::min(S, hi - p0);
-                const int s = vc_multiproof_prove_many(
-                    g->ctx[k], scheme, g->tables[id][k], N, Q, cnt, buf[b & 1], com_xy + p0 * Q * 8, com_inf + p0 * Q,
-                    z + p0 * Q, y + p0 * Q * 4, d_xy + p0 * 8, d_inf + p0, scheme == 0 ? ipa_proofs + p0 : nullptr,
-                    scheme == 1 ? kzg_xy + p0 * 8 : nullptr, scheme == 1 ? kzg_inf + p0 : nullptr,
-                    scheme == 1 ? kzg_y + p0 * 4 : nullptr);
-                if (up.joinable()) up.join();
-                if (st_up == -1 && b + 1 < nsub) st_up = upload(b + 1);
-                VK_TRY(s);
-                VK_TRY(st_up);
-                VK_CHECK_HIP(hipSetDevice(dev));
-            }
-            return VC_OK;
+            VK_CHECK_HIP(hipMemcpy(g->data[k].p, data + lo * Q * N * 4, bytes, hipMemcpyHostToDevice));
+            return vc_multiproof_prove_many(g->ctx[k], scheme, g->tables[id][k], N, Q, hi - lo, g->data[k].p,
+                                            com_xy + lo * Q * 8, com_inf + lo * Q, z + lo * Q, y + lo * Q * 4,
+                                            d_xy + lo * 8, d_inf + lo, scheme == 0 ? ipa_proofs + lo : nullptr,
+                                            scheme == 1 ? kzg_xy + lo * 8 : nullptr,
+                                            scheme == 1 ? kzg_inf + lo : nullptr, scheme == 1 ? kzg_y + lo * 4 : nullptr);
         };
         st[k] = share();
     });
