@@ -227,3 +227,32 @@ def test_verkle_mirror_moves_between_devices(oracle_c):
     finally:
         e0.close()
         e1.close()
+
+
+@pytest.mark.parametrize("pieces", ["2", "3", "4"])
+def test_verkle_ext_rows_in_pieces(eng, pieces, monkeypatch):
+    """The extension rows built and uploaded in pieces (VKZG_VERKLE_EXT_PIECES, an A/B knob: the
+    default is one piece) == the one-buffer path (pieces = 1), fresh and after a 1 % update; a
+    20,000-key tree of 32-unit keys (uneven pieces at 3)."""
+    import numpy as np
+    from vkzg import scheme
+    from vkzg.verkle import VerkleTree
+    kzg = scheme.KZG(eng, 256)
+    rng = np.random.default_rng(12)
+    nk = 20_000
+    keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    upd = [(keys[i].tobytes(), rng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
+           for i in rng.choice(nk, size=nk // 100, replace=False)]
+
+    def roots(p):
+        monkeypatch.setenv("VKZG_VERKLE_EXT_PIECES", p)
+        t = VerkleTree(32)
+        for i in range(nk):
+            t.insert_single(keys[i].tobytes(), vals[i].tobytes())
+        a = t.commitment(eng, kzg.table)
+        for k, v in upd:
+            t.insert_single(k, v)
+        return a, t.commitment(eng, kzg.table)
+
+    assert roots(pieces) == roots("1")

@@ -305,6 +305,7 @@ void vc_ctx_destroy(vc_ctx* ctx) {
         ctx->pin_mp.release();
         ctx->pin_ipa.release();
         ctx->pin_verkle.release();
+        ctx->pin_verkle2.release();
         for (auto& b : ctx->pin_verkle_lv) b.release();
         ctx->pin_norm_vk.release();
         ctx->pin_sparse_ck.release();

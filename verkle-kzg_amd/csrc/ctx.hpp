@@ -238,6 +238,7 @@ struct vc_ctx {
     vk::PinBuf pin_mp;              // the multiproof finish's h - g, copied back ahead of the E commit
     vk::PinBuf pin_ipa;             // the IPA prover's a, x and q terms read by the round kernel (IpaRows)
     vk::PinBuf pin_verkle;          // the verkle extension rows, merged straight into page-locked memory
+    vk::PinBuf pin_verkle2;         // the second buffer of the rows built in pieces (odd pieces)
     vk::PinBuf pin_verkle_lv[2];    // verkle levels' lists (one upload per level; the next level's are
                                     // built into the other one while the current level runs)
     vk::PinBuf pin_norm_vk;         // block products / inverses of the verkle rows' normalisation

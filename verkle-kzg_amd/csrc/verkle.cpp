@@ -688,8 +688,11 @@ struct ExtStage {
     uint32_t maxlen = 0;
     uint8_t* base = nullptr;
 };
+// rp_out (optional): the row pointers go there instead, each plus nnz_base (one piece of a level
+// built in pieces: its rows' pointers in the level's array)
 static int ext_stage(const vc_verkle* t, const std::vector<int>& exts, HostPool& pool, std::vector<ExtRows16>& cache,
-                     const std::function<uint8_t*(size_t)>& buffer, ExtStage* out, double* t_build = nullptr) {
+                     const std::function<uint8_t*(size_t)>& buffer, ExtStage* out, double* t_build = nullptr,
+                     uint64_t* rp_out = nullptr, uint64_t nnz_base = 0) {
     const size_t E = exts.size();
     const auto tb0 = std::chrono::steady_clock::now();
     std::vector<ExtRows16> parts = build_parts<ExtRows16>(
@@ -722,13 +725,13 @@ static int ext_stage(const vc_verkle* t, const std::vector<int>& exts, HostPool&
     uint8_t* pin = buffer(X.o_end);
     if (!pin) return VC_E_OOM;
     X.base = pin;
-    uint64_t* rp = reinterpret_cast<uint64_t*>(pin);
+    uint64_t* rp = rp_out ? rp_out : reinterpret_cast<uint64_t*>(pin);
     uint32_t* ids = reinterpret_cast<uint32_t*>(pin + X.o_ids);
-    rp[0] = 0;
+    rp[0] = nnz_base;
     auto merge = [&](unsigned k) {  // part k holds extensions [eoff[k], eoff[k + 1]) in order
         if (k >= T) return;
         const ExtRows16& r = parts[k];
-        for (size_t i = 1; i < r.ptr.size(); i++) rp[roff[k] + i] = noff[k] + r.ptr[i];
+        for (size_t i = 1; i < r.ptr.size(); i++) rp[roff[k] + i] = nnz_base + noff[k] + r.ptr[i];
         memcpy(pin + X.o_stem + eoff[k] * 32, r.stem.data(), r.stem.size() * 8);
         if (!r.cols.empty()) {
             memcpy(pin + X.o_vals + noff[k] * 16, r.vals.data(), r.vals.size() * 8);
@@ -1429,29 +1432,97 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     const std::vector<int>& exts = t->dirty_ext;
     const size_t E = exts.size();
     if (E) {
-        static thread_local std::vector<ExtRows16> parts_cache;  // storage kept between calls
-        ExtStage X;
-        VK_TRY(ext_stage(t, exts, pool, parts_cache,
-                         [&](size_t bytes) -> uint8_t* {
-                             return ctx->pin_verkle.ensure(bytes) == VC_OK ? ctx->pin_verkle.as<uint8_t>() : nullptr;
-                         },
-                         &X));
-        const size_t nnz = X.nnz, o_stem = X.o_stem, o_vals = X.o_vals, o_ids = X.o_ids, o_cols = X.o_cols,
-                     o_end = X.o_end;
-        const uint32_t maxlen = X.maxlen;
-        uint8_t* pin = X.base;
-        uint64_t* rp = reinterpret_cast<uint64_t*>(pin);
-        lap("ext rows (host)");
+        static thread_local std::vector<ExtRows16> parts_cache[2];  // storage kept between calls
+        // the rows in pieces (VKZG_VERKLE_EXT_PIECES, read per call; A/B knob, default 1): piece p
+        // is built into page-locked buffer p & 1 while piece p - 1 crosses PCIe, each section of a
+        // piece copied to its place in the level's device arrays (vals / cols at the non-zeros
+        // before it: the device region holds the E 2 N upper bound). Measured slower at 65,536 keys
+        // (full commitment 2.17-2.23 ms in one piece, 2.33-2.40 in 2, 2.49-2.53 in 4, 3 alternating
+        // rounds, profiles/r06/verkle/pieces/): every piece pays the host pool's fork / join and
+        // merge, more than the ~0.05-0.08 ms of upload it hides. One piece: the level's one buffer
+        // in one copy.
+        const char* pe = getenv("VKZG_VERKLE_EXT_PIECES");
+        size_t NP = pe ? (size_t)std::max(1, atoi(pe)) : 1;
+        const size_t cap = E * 2 * (size_t)N;  // non-zeros: at most 2 N per extension
+        if (E < 4096 * NP || cap * 20 > ((size_t)256 << 20)) NP = 1;
         DevBuf d_up(ctx), d_vals(ctx), d_xy(ctx), d_inf(ctx), d_it(ctx);
-        VK_TRY(d_up.ensure(o_end - o_stem));
+        const uint64_t* d_stem = nullptr;
+        const uint64_t* d_v16 = nullptr;
+        const uint32_t* d_ids = nullptr;
+        const uint32_t* d_cols = nullptr;
+        const uint64_t* rp = nullptr;
+        size_t nnz = 0;
+        uint32_t maxlen = 0;
+        static thread_local uvec<uint64_t> rp_all;
+        if (NP == 1) {
+            ExtStage X;
+            VK_TRY(ext_stage(t, exts, pool, parts_cache[0],
+                             [&](size_t bytes) -> uint8_t* {
+                                 return ctx->pin_verkle.ensure(bytes) == VC_OK ? ctx->pin_verkle.as<uint8_t>() : nullptr;
+                             },
+                             &X));
+            nnz = X.nnz;
+            maxlen = X.maxlen;
+            uint8_t* pin = X.base;
+            rp = reinterpret_cast<const uint64_t*>(pin);
+            lap("ext rows (host)");
+            VK_TRY(d_up.ensure(X.o_end - X.o_stem));
+            VK_CHECK_HIP(hipMemcpyAsync(d_up.p, pin + X.o_stem, X.o_end - X.o_stem, hipMemcpyHostToDevice, st));
+            d_stem = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>());
+            d_v16 = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>() + (X.o_vals - X.o_stem));
+            d_ids = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (X.o_ids - X.o_stem));
+            d_cols = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (X.o_cols - X.o_stem));
+        } else {
+            // device: stems [E] x 32 B | ids [E] x 4 B | vals [cap] x 16 B | cols [cap] x 4 B
+            const size_t o_ids = E * 32, o_vals = o_ids + E * 4, o_cols = o_vals + cap * 16;
+            VK_TRY(d_up.ensure(o_cols + cap * 4));
+            uint8_t* du = d_up.as<uint8_t>();
+            rp_all.resize(2 * E + 1);
+            hipEvent_t ev[2] = {nullptr, nullptr};
+            struct Events {  // back to the pool on every exit, after the copies reading them finished
+                vc_ctx* c;
+                hipEvent_t* e;
+                ~Events() {
+                    for (int i = 0; i < 2; i++)
+                        if (e[i]) {
+                            (void)hipEventSynchronize(e[i]);
+                            c->event_pool.push_back(e[i]);
+                        }
+                }
+            } events{ctx, ev};
+            std::vector<int> sub;
+            for (size_t p = 0; p < NP; p++) {
+                const size_t e0 = E * p / NP, e1 = E * (p + 1) / NP;
+                sub.assign(exts.begin() + e0, exts.begin() + e1);
+                PinBuf& pb = (p & 1) ? ctx->pin_verkle2 : ctx->pin_verkle;
+                if (ev[p & 1]) VK_CHECK_HIP(hipEventSynchronize(ev[p & 1]));  // piece p - 2's copies are done
+                ExtStage X;
+                VK_TRY(ext_stage(t, sub, pool, parts_cache[p & 1],
+                                 [&](size_t bytes) -> uint8_t* { return pb.ensure(bytes) == VC_OK ? pb.as<uint8_t>() : nullptr; },
+                                 &X, nullptr, rp_all.data() + 2 * e0, nnz));
+                const size_t ep = e1 - e0;
+                uint8_t* pin = X.base;
+                VK_CHECK_HIP(hipMemcpyAsync(du + e0 * 32, pin + X.o_stem, ep * 32, hipMemcpyHostToDevice, st));
+                VK_CHECK_HIP(hipMemcpyAsync(du + o_ids + e0 * 4, pin + X.o_ids, ep * 4, hipMemcpyHostToDevice, st));
+                if (X.nnz) {
+                    VK_CHECK_HIP(hipMemcpyAsync(du + o_vals + nnz * 16, pin + X.o_vals, X.nnz * 16, hipMemcpyHostToDevice, st));
+                    VK_CHECK_HIP(hipMemcpyAsync(du + o_cols + nnz * 4, pin + X.o_cols, X.nnz * 4, hipMemcpyHostToDevice, st));
+                }
+                if (!ev[p & 1]) ev[p & 1] = ctx->get_event();
+                VK_CHECK_HIP(hipEventRecord(ev[p & 1], st));
+                nnz += X.nnz;
+                maxlen = std::max(maxlen, X.maxlen);
+            }
+            rp = rp_all.data();
+            lap("ext rows (host, in pieces)");
+            d_stem = reinterpret_cast<const uint64_t*>(du);
+            d_ids = reinterpret_cast<const uint32_t*>(du + o_ids);
+            d_v16 = reinterpret_cast<const uint64_t*>(du + o_vals);
+            d_cols = reinterpret_cast<const uint32_t*>(du + o_cols);
+        }
         VK_TRY(d_xy.ensure(2 * E * 64));
         VK_TRY(d_inf.ensure(2 * E));
         VK_TRY(d_it.ensure(2 * E * 32));
-        VK_CHECK_HIP(hipMemcpyAsync(d_up.p, pin + o_stem, o_end - o_stem, hipMemcpyHostToDevice, st));
-        const uint64_t* d_stem = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>());
-        const uint64_t* d_v16 = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>() + (o_vals - o_stem));
-        const uint32_t* d_ids = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (o_ids - o_stem));
-        const uint32_t* d_cols = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (o_cols - o_stem));
         if (small_ok(nnz)) {  // the 16-byte values read as they are
             SmallRows in;
             in.batch = 2 * E;
