@@ -1,9 +1,7 @@
 set -eu
 R=$(pwd)
-O=$R/gpurun_out/r06_final; mkdir -p $O
-timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
-echo bench-done; tail -3 $O/bench.err
-timeout -k 10 600 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-cpu-baseline > $O/rehearse_2rank.json 2> $O/rehearse_2rank.err
-echo rehearse-done
-timeout -k 10 300 python -u verkle-kzg_amd/tools/split_probe.py 1,2,8 > $O/split_probe.txt 2>&1
-echo split-done
+O=$R/gpurun_out/r06_n; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+VKZG_AB_FB_C=16 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/tr -o vk -- python3 -u $R/verkle-kzg_amd/tools/verkle_ab.py 65536 3 > $O/trace_run.txt 2>&1
+echo trace-done; tail -1 $O/trace_run.txt | cut -c1-200
+find $O/tr -name "*.csv" | head

@@ -201,86 +201,6 @@ __global__ void __launch_bounds__(256) k_msm_fixup_own(typename A::Acc* __restri
     buckets[b] = acc;
 }
 
-// The same walk with the rare long chains compacted (round 6, tools/tail_trace.py): every owner
-// adds its first carry piece (one add for all lanes), then the few lanes whose bucket spans more
-// threads (~1 % at the 2^20 radix MSM's 112 entries per thread and ~90 per bucket) hand their state
-// to the block through LDS and one wave per block -- rotated over the block's SIMDs by block index
-// -- finishes them. The per-lane walk made every wave holding one such lane run two adds at two
-// waves per SIMD (~25 us each): half the waves, a 66-us kernel; here the second round is one lone
-// wave's add. One add call site (a loop with the phase switch), as every tail kernel. Measured
-// slower (profiles/r06/tail_trace/: 0.076 vs 0.072 ms, 3 alternating rounds): round 1 itself got
-// longer (first exits at 30 us instead of 25; 250 VGPRs, the phase loop) and the block barrier holds
-// every wave to its block's slowest -- kept behind VKZG_FIXUP_COMPACT=1, off.
-template <class A>
-__global__ void __launch_bounds__(256) k_msm_fixup_own_c(typename A::Acc* __restrict__ buckets,
-                                                        const typename A::Acc* __restrict__ carry,
-                                                        const typename A::Acc* __restrict__ owner_piece,
-                                                        const uint32_t* __restrict__ owner_bucket,
-                                                        const uint8_t* __restrict__ through, uint32_t Tmax,
-                                                        const uint32_t* __restrict__ Lp, uint32_t M, uint32_t limit) {
-    using Acc = typename A::Acc;
-    __shared__ Acc q_acc[256];
-    __shared__ uint32_t q_u[256], q_u1[256], q_b[256];
-    __shared__ uint32_t q_n;
-    TT_BEGIN(0);
-    const uint32_t tid = threadIdx.x, t = blockIdx.x * blockDim.x + tid;
-    if (tid == 0) q_n = 0;
-    const uint32_t T = (*Lp + M - 1) / M;
-    bool act = t < T && t < Tmax;
-    uint32_t b = NONE_T, u = t + 1, u1 = t + 1;
-    Acc acc = A::zero(), c1 = A::zero();
-    if (act) {
-        const bool nx = t + 1 < T;
-        b = owner_bucket[t];
-        const uint8_t th1 = nx ? through[t + 1] : (uint8_t)0;
-        acc = owner_piece[t];
-        c1 = nx ? carry[t + 1] : A::zero();
-        act = b != NONE_T;
-        if (act && th1 == 2) {  // longer chains (rare)
-            u1++;
-            while (through[u1] == 2) {
-                if (u1 - t >= limit) {  // longer than the walk takes: host path
-                    act = false;
-                    break;
-                }
-                u1++;
-            }
-        }
-    }
-    TT_INFO(act ? u1 - t : 0);
-    __syncthreads();  // q_n = 0 before any push
-    for (int phase = 0;; phase++) {
-        if (act) acc = A::add(acc, c1);
-        if (phase == 0) {
-            if (act) {
-                if (u == u1) {
-                    buckets[b] = acc;
-                } else {
-                    const uint32_t k = atomicAdd(&q_n, 1u);
-                    q_acc[k] = acc;
-                    q_u[k] = u;
-                    q_u1[k] = u1;
-                    q_b[k] = b;
-                }
-            }
-            __syncthreads();
-            const uint32_t n = q_n, wv = tid >> 6;
-            const uint32_t e = (((wv + 4 - (blockIdx.x & 3)) & 3) << 6) + (tid & 63);
-            if (e >= n) return;
-            acc = q_acc[e];
-            u = q_u[e];
-            u1 = q_u1[e];
-            b = q_b[e];
-            act = true;
-        } else if (u == u1) {
-            buckets[b] = acc;
-            return;
-        }
-        c1 = carry[u + 1];
-        u++;
-    }
-}
-
 // c ? a : b word by word through masks: a plain select of two aggregates becomes a load through a
 // selected address, which keeps both in scratch memory for the whole loop
 template <class T>
@@ -721,16 +641,13 @@ int msm_tail_fixup_walk(vc_ctx* ctx, Lane L, const uint32_t* offsets, uint32_t N
     using A = typename Fast29<C>::type;
     static const int quad_env = getenv("VKZG_FIXUP_QUAD") ? atoi(getenv("VKZG_FIXUP_QUAD")) : 1;  // A/B probe
     static const int own_env = getenv("VKZG_FIXUP_OWN") ? atoi(getenv("VKZG_FIXUP_OWN")) : 1;     // A/B probe
-    // fewer accumulate threads than buckets: a lane per owner thread (k_msm_fixup_own; the long
-    // chains compacted through LDS with VKZG_FIXUP_COMPACT=1 -- measured 0.076 vs 0.072 ms, off)
-    static const int compact_env = getenv("VKZG_FIXUP_COMPACT") ? atoi(getenv("VKZG_FIXUP_COMPACT")) : 0;  // A/B probe
+    // fewer accumulate threads than buckets: a lane per owner thread (k_msm_fixup_own). Round 6
+    // built a variant with the rare long chains compacted through LDS (one wave per block finishing
+    // them) and measured it slower, 0.076 vs 0.072 ms (profiles/r06/tail_trace/; commit 9fc06f9's
+    // k_msm_fixup_own_c): removed
     if (own_env && owner_b && Tmax <= NBtot) {
-        if (compact_env)
-            VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_own_c<A>), (Tmax + 255) / 256, 256, 0, buckets, carry,
-                         owner, owner_b, through, Tmax, offsets + NBtot, M, limit);
-        else
-            VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_own<A>), (Tmax + 255) / 256, 256, 0, buckets, carry, owner,
-                         owner_b, through, Tmax, offsets + NBtot, M, limit);
+        VK_LAUNCH_ON(ctx, L.st, "msm_fixup", (k_msm_fixup_own<A>), (Tmax + 255) / 256, 256, 0, buckets, carry, owner,
+                     owner_b, through, Tmax, offsets + NBtot, M, limit);
         return VC_OK;
     }
     // quads while their waves fit ~2 per SIMD (one bucket set: 2^15 buckets -> 2048 waves); with
