@@ -390,13 +390,14 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
                          uint64_t* out_item, const std::function<void()>* overlap = nullptr);
 // d_add_ids (optional): row g also adds the canonical affine point (d_add_xy, d_add_inf)[d_add_ids[g]]
 // before the normalisation (0xffffffff: nothing) -- a verkle row that updates its old commitment.
-// d_dst (optional): row g's outputs go to index d_dst[g] (the tree's mirror). The normalisation is
+// d_dst (optional): row g's outputs go to index d_dst[g] (the tree's mirror). d_row_ptr (optional,
+// rows_fit only): a device copy of row_ptr the caller already has (no upload). The normalisation is
 // normalize_rows_items' (polled, no stream wait; `overlap` runs once every kernel is queued).
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
                             const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items,
                             const uint32_t* d_add_ids = nullptr, const uint64_t* d_add_xy = nullptr,
                             const uint8_t* d_add_inf = nullptr, const uint32_t* d_dst = nullptr,
-                            const std::function<void()>* overlap = nullptr);
+                            const std::function<void()>* overlap = nullptr, const uint64_t* d_row_ptr = nullptr);
 // k_to_data_item over device points (canonical affine u64 x 8 + flags) into device items, on the
 // ctx stream (scheme.hip)
 int to_data_item_device(vc_ctx* ctx, const void* d_xy, const uint8_t* d_inf, size_t n, void* d_items);

@@ -2190,7 +2190,7 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
                              const uint32_t* d_cols_in, const void* d_sc_in, int mont, void* d_xy, uint8_t* d_inf,
                              void* d_items, const uint32_t* d_add_ids = nullptr, const uint64_t* d_add_xy = nullptr,
                              const uint8_t* d_add_inf = nullptr, const uint32_t* d_dst = nullptr,
-                             const std::function<void()>* overlap = nullptr) {
+                             const std::function<void()>* overlap = nullptr, const uint64_t* d_row_ptr = nullptr) {
     using Acc = typename C::Acc;
     if (batch == 0) return VC_OK;
     const size_t nnz = row_ptr[batch];
@@ -2231,7 +2231,11 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     DevBuf& d_rc = ctx->ws[WS_SP_RC];
     DevBuf& d_chunks = ctx->ws[WS_SP_CHUNKS];
-    VK_TRY(d_rp.ensure((nch + 1) * 8));
+    // chunk lists: cptr and rc lie back to back in the page-locked staging (sparse_chunks), so they
+    // go up in one copy into d_rp (rc at the same offset); identity rows use d_rc for their iota
+    const size_t rc_off = ch.identity ? 0 : (size_t)(reinterpret_cast<const uint8_t*>(ch.rc) -
+                                                     reinterpret_cast<const uint8_t*>(ch.cptr));
+    VK_TRY(d_rp.ensure(ch.identity ? (nch + 1) * 8 : rc_off + (batch + 1) * 4));
     VK_TRY(d_rc.ensure((batch + 1) * 4));
     VK_TRY(d_chunks.ensure(nch * sizeof(Acc)));
     VK_TRY(d_cnt.ensure((nnz + 1) * 4));
@@ -2244,13 +2248,19 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     VK_TRY(d_own.ensure((size_t)(Tmax + 8) * sizeof(FAcc<C>)));
     VK_TRY(d_ownb.ensure((size_t)(Tmax + 8) * 4));
     lap("host chunk lists");
+    // rows as chunks: the row pointers are the chunk pointers -- the caller's device copy when it
+    // has one (d_row_ptr: the verkle extension rows upload theirs with the rows, or make them on the
+    // device), else one upload
+    const uint64_t* rp_dev = d_rp.as<uint64_t>();
+    const uint32_t* rc_dev = d_rc.as<uint32_t>();
     if (ch.identity) {
-        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, row_ptr, (batch + 1) * 8, hipMemcpyHostToDevice, st));
+        if (d_row_ptr) rp_dev = d_row_ptr;
+        else VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, row_ptr, (batch + 1) * 8, hipMemcpyHostToDevice, st));
         VK_LAUNCH(ctx, "sparse_iota", k_iota, (uint32_t)((batch + 1 + 255) / 256), 256, 0, d_rc.as<uint32_t>(),
                   (uint32_t)batch);
     } else {
-        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, ch.cptr, (nch + 1) * 8, hipMemcpyHostToDevice, st));
-        VK_CHECK_HIP(hipMemcpyAsync(d_rc.p, ch.rc, (batch + 1) * 4, hipMemcpyHostToDevice, st));
+        VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, ch.cptr, rc_off + (batch + 1) * 4, hipMemcpyHostToDevice, st));
+        rc_dev = reinterpret_cast<const uint32_t*>(d_rp.as<uint8_t>() + rc_off);
     }
     const uint32_t* d_cols = d_cols_in;
     const uint32_t* d_sc = static_cast<const uint32_t*>(d_sc_in);
@@ -2267,7 +2277,7 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     if (nnz)
         VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc, d_cols, nnz, mont, fg,
                   d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
-    VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, d_rp.as<uint64_t>(),
+    VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, rp_dev,
               d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
     // the fixed-base tables hold radix-2^29 limbs in 128-B entries (ec29.hpp FbE): the accumulate
     // reads the entries' limbs (is_fbe)
@@ -2301,7 +2311,7 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
         rows_p = d_chunks.as<Acc>();
     else
         VK_LAUNCH(ctx, "sparse_combine", (k_sparse_combine<typename C::Inl>), batch, 64, 0, d_chunks.as<Acc>(),
-                  d_rc.as<uint32_t>(), rows_p);
+                  rc_dev, rows_p);
     if constexpr (std::is_same<C, BN254G1>::value) {
         // BN254 rows with items (the verkle levels): the old-commitment adds, the canonical points,
         // their items and the placement at d_dst in normalize_rows_items' two kernels, the block
@@ -2504,10 +2514,10 @@ int sparse_small_items_dev(vc_ctx* ctx, Table* t, const SmallRows& in, const std
 int sparse_commit_items_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, bool rows_fit,
                             const uint32_t* d_cols, const void* d_sc, void* d_xy, uint8_t* d_inf, void* d_items,
                             const uint32_t* d_add_ids, const uint64_t* d_add_xy, const uint8_t* d_add_inf,
-                            const uint32_t* d_dst, const std::function<void()>* overlap) {
+                            const uint32_t* d_dst, const std::function<void()>* overlap, const uint64_t* d_row_ptr) {
     if (t->curve != VC_CURVE_BN254 || !d_items) return VC_E_INVALID;
     return sparse_commit_dev<BN254G1, BN254Fr>(ctx, t, batch, row_ptr, rows_fit, d_cols, d_sc, 0, d_xy, d_inf, d_items,
-                                               d_add_ids, d_add_xy, d_add_inf, d_dst, overlap);
+                                               d_add_ids, d_add_xy, d_add_inf, d_dst, overlap, d_row_ptr);
 }
 
 int msm_batch_sparse_items(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,

@@ -1187,6 +1187,11 @@ __global__ void k_vk_ext_rows4(const uint64_t* __restrict__ stem, const uint64_t
     o[2] = w[2];
     o[3] = w[3];
 }
+// row pointers of E rows of 4: rp[k] = 4 k, k <= E
+__global__ void k_vk_rp4(uint64_t* __restrict__ rp, size_t E) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k <= E) rp[k] = 4 * (uint64_t)k;
+}
 // rows' results -> the mirror at their node ids
 __global__ void k_vk_scatter(const uint32_t* __restrict__ ids, size_t n, const uint64_t* __restrict__ xy,
                              const uint8_t* __restrict__ inf, const uint64_t* __restrict__ it,
@@ -1451,6 +1456,7 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
         const uint32_t* d_ids = nullptr;
         const uint32_t* d_cols = nullptr;
         const uint64_t* rp = nullptr;
+        const uint64_t* d_rp_dev = nullptr;  // the row pointers on the device, when uploaded with the rows
         size_t nnz = 0;
         uint32_t maxlen = 0;
         static thread_local uvec<uint64_t> rp_all;
@@ -1466,12 +1472,15 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             uint8_t* pin = X.base;
             rp = reinterpret_cast<const uint64_t*>(pin);
             lap("ext rows (host)");
-            VK_TRY(d_up.ensure(X.o_end - X.o_stem));
-            VK_CHECK_HIP(hipMemcpyAsync(d_up.p, pin + X.o_stem, X.o_end - X.o_stem, hipMemcpyHostToDevice, st));
-            d_stem = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>());
-            d_v16 = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>() + (X.o_vals - X.o_stem));
-            d_ids = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (X.o_ids - X.o_stem));
-            d_cols = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + (X.o_cols - X.o_stem));
+            // the row pointers travel in the same copy: the sort-based commit reads them there
+            // instead of uploading them again (one 1-MB copy and its gap less, profiles/r06/verkle/)
+            VK_TRY(d_up.ensure(X.o_end));
+            VK_CHECK_HIP(hipMemcpyAsync(d_up.p, pin, X.o_end, hipMemcpyHostToDevice, st));
+            d_rp_dev = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>());
+            d_stem = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>() + X.o_stem);
+            d_v16 = reinterpret_cast<const uint64_t*>(d_up.as<uint8_t>() + X.o_vals);
+            d_ids = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + X.o_ids);
+            d_cols = reinterpret_cast<const uint32_t*>(d_up.as<uint8_t>() + X.o_cols);
         } else {
             // device: stems [E] x 32 B | ids [E] x 4 B | vals [cap] x 16 B | cols [cap] x 4 B
             const size_t o_ids = E * 32, o_vals = o_ids + E * 4, o_cols = o_vals + cap * 16;
@@ -1542,7 +1551,7 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             // chunks as they are (an empty row is an empty chunk: the identity), no chunk lists
             VK_TRY(sparse_commit_items_dev(ctx, tab, 2 * E, rp, maxlen <= 4, d_cols, d_vals.p, d_xy.p,
                                            d_inf.as<uint8_t>(), d_it.p, nullptr, nullptr, nullptr, nullptr,
-                                           order.empty() ? nullptr : &build_next_fn));
+                                           order.empty() ? nullptr : &build_next_fn, d_rp_dev));
         }
         lap("ext c1 / c2 commits");
         DevBuf d_c4(ctx), d_v4(ctx);
@@ -1569,10 +1578,13 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             in.d_out_inf = m_inf;
             in.d_out_item = m_item;
             VK_TRY(sparse_small_items_dev(ctx, tab, in, order.empty() ? nullptr : &build_next_fn));
-        } else {  // results straight into the mirror as well
+        } else {  // results straight into the mirror as well; row_ptr[k] = 4 k made on the device
+            DevBuf d_rp4(ctx);
+            VK_TRY(d_rp4.ensure((E + 1) * 8));
+            VK_LAUNCH(ctx, "verkle_rp4", k_vk_rp4, grid(E + 1), 256, 0, d_rp4.as<uint64_t>(), E);
             VK_TRY(sparse_commit_items_dev(ctx, tab, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, m_cxy, m_inf,
                                            m_item, nullptr, nullptr, nullptr, d_ids,
-                                           order.empty() ? nullptr : &build_next_fn));
+                                           order.empty() ? nullptr : &build_next_fn, d_rp4.as<uint64_t>()));
         }
         lap("ext commits");
     }
