@@ -256,3 +256,39 @@ def test_verkle_ext_rows_in_pieces(eng, pieces, monkeypatch):
         return a, t.commitment(eng, kzg.table)
 
     assert roots(pieces) == roots("1")
+
+
+@pytest.mark.parametrize("mode", ["late", "selfinv"])
+def test_verkle_norm_finish_modes(eng, mode, monkeypatch):
+    """The verkle levels' normalisation (commit.hip normalize_rows_items): by default the finish
+    kernel is queued behind the prep before the host has inverted the block products, its blocks
+    waiting on the host's go word. == the finish launched after the inversion (late,
+    VKZG_NORM_EARLY=0) and == blocks that stop waiting after 1 us and invert on their own
+    (selfinv, VKZG_NORM_EARLY_US=1); fresh and after a 1 % update of a 20,000-key tree (the c1 / c2
+    level's 40,000 rows take the device-scan form, the smaller levels the per-block form)."""
+    import numpy as np
+    from vkzg import scheme
+    from vkzg.verkle import VerkleTree
+    kzg = scheme.KZG(eng, 256)
+    rng = np.random.default_rng(13)
+    nk = 20_000
+    keys = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    vals = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+    upd = [(keys[i].tobytes(), rng.integers(0, 256, size=32, dtype=np.uint8).tobytes())
+           for i in rng.choice(nk, size=nk // 100, replace=False)]
+
+    def roots():
+        t = VerkleTree(32)
+        for i in range(nk):
+            t.insert_single(keys[i].tobytes(), vals[i].tobytes())
+        a = t.commitment(eng, kzg.table)
+        for k, v in upd:
+            t.insert_single(k, v)
+        return a, t.commitment(eng, kzg.table)
+
+    want = roots()
+    if mode == "late":
+        monkeypatch.setenv("VKZG_NORM_EARLY", "0")
+    else:
+        monkeypatch.setenv("VKZG_NORM_EARLY_US", "1")
+    assert roots() == want

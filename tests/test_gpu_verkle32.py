@@ -107,17 +107,21 @@ def eng():
     e.close()
 
 
-@pytest.mark.parametrize("mode", ["dev", "dev-sort", "dev-dense", "host"])
+@pytest.mark.parametrize("mode", ["dev", "dev-sort", "dev-dense", "dev-selfinv", "host"])
 @pytest.mark.parametrize("scheme_name", ["kzg", "ipa"])
 def test_verkle32_matches_oracle(eng, oracle_c, scheme_name, mode, monkeypatch):
     """one context: dev = the default device path; dev-sort = every sparse level on the sort-based
     path (VKZG_SPARSE_SMALL_MAX=0); dev-dense = every level as dense rows (VKZG_VERKLE_DENSE=1);
+    dev-selfinv = the normalisations' early-queued finish blocks time out at once (1 us) and invert
+    their products themselves (VKZG_NORM_EARLY_US=1: the path a stalled host thread takes);
     host = host-built rows (VKZG_VERKLE_DEV=0, the group / SPMD paths' code)"""
     from vkzg import scheme
     if mode == "dev-sort":
         monkeypatch.setenv("VKZG_SPARSE_SMALL_MAX", "0")
     elif mode == "dev-dense":
         monkeypatch.setenv("VKZG_VERKLE_DENSE", "1")
+    elif mode == "dev-selfinv":
+        monkeypatch.setenv("VKZG_NORM_EARLY_US", "1")
     elif mode == "host":
         monkeypatch.setenv("VKZG_VERKLE_DEV", "0")
     table = scheme.KZG(eng, 256).table if scheme_name == "kzg" else scheme.IPA(eng, 256, _ipa_points()).table

@@ -369,6 +369,39 @@ __global__ void __launch_bounds__(256) k_norm_finish(const typename C::Acc* __re
     if (out_inf) out_inf[j] = ident ? 1 : 0;
 }
 
+// A finish kernel queued before the host has its inverse(s) (normalize_rows_items): lane 0 of block
+// 0 waits for `flag` == epoch in fine-grained page-locked memory and hands it on through `relay` in
+// device memory, where the other blocks wait -- with the total's inverse itself in the device-scan
+// form: 512 blocks reading the same page-locked words over PCIe were served one after another,
+// ~0.8 us per block, 0.4 ms for the 131,072-row level (measured, profiles/r06/verkle/norm_early/).
+// In the per-block form each block reads its own inverse there. Every wait is bounded on the
+// 100 MHz clock: past `limit` ticks block 0 (or a block that never saw the relay) inverts the
+// value itself (prod: the block products or their total, written by the prep kernel), so the
+// kernel ends whatever the host does -- it only gets slower.
+struct NormGo {
+    const uint32_t* flag = nullptr;  // null: the inverses were written before the launch
+    uint64_t* relay = nullptr;       // 9 device words block 0 hands the go on through
+    uint32_t epoch = 0;
+    uint32_t per_block = 0;             // 1: inv[b] = 1 / prod[b] per block; 0: inv[0] = 1 / prod[0] (the total)
+    const fe<BN254Fq>* prod = nullptr;  // what the host inverts (device view of the page-locked staging)
+    const fe<BN254Fq>* inv = nullptr;   // where the host writes the inverse(s)
+    uint64_t limit = 0;
+    uint64_t* dbg = nullptr;  // VKZG_NORM_DEBUG: per block (start, seen or timed out, seen) on the 100 MHz clock
+};
+// (four 64-bit loads: page-locked host memory is read over PCIe uncached)
+__device__ __forceinline__ fe<BN254Fq> load_fe_sys(const fe<BN254Fq>* p) {
+    static_assert(BN254Fq::N == 8, "");
+    fe<BN254Fq> v;
+    uint64_t* src = const_cast<uint64_t*>(reinterpret_cast<const uint64_t*>(p));
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t w = __hip_atomic_load(&src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v.v[2 * k] = (uint32_t)w;
+        v.v[2 * k + 1] = (uint32_t)(w >> 32);
+    }
+    return v;
+}
+
 // verkle rows (BN254): canonical affine point, identity flag and to_data_item of row j stored at
 // dst[j] (dst null: at j) -- straight into the tree's device mirror
 __global__ void __launch_bounds__(256) k_norm_finish_vk(const BN254G1::Acc* __restrict__ rows, size_t count,
@@ -376,14 +409,82 @@ __global__ void __launch_bounds__(256) k_norm_finish_vk(const BN254G1::Acc* __re
                                                        const fe<BN254Fq>* __restrict__ binv,
                                                        const uint32_t* __restrict__ dst, uint64_t* __restrict__ out_xy,
                                                        uint8_t* __restrict__ out_inf, uint64_t* __restrict__ out_item,
-                                                       const fe<BN254Fq>* __restrict__ tinv) {
+                                                       const fe<BN254Fq>* __restrict__ tinv, NormGo go) {
     using F = BN254Fq;
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ fe<F> s_bi;
+    if (go.flag) {  // (uniform: every thread of the block reaches the barrier)
+        if (threadIdx.x == 0) {
+            const uint32_t k = go.per_block ? blockIdx.x : 0u;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            // relay words in device memory, each (epoch << 32) | payload, so a reader needs no ordering
+            // between them and the writer no release (an agent-scope release writes back the whole
+            // L2 of block 0's XCD first): [0, 8) the total's inverse, [8] whether the host answered
+            uint64_t* rl = go.relay;
+            const uint64_t tag = (uint64_t)go.epoch << 32;
+            bool host = false, have = false, seen = false;
+            fe<F> v;
+            if (blockIdx.x == 0) {
+                uint32_t* flag = const_cast<uint32_t*>(go.flag);
+                for (;;) {
+                    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == go.epoch) {
+                        host = true;
+                        break;
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > go.limit) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                seen = true;
+                if (!go.per_block) {  // the one inverse: read over PCIe once, handed on in device memory
+                    v = host ? load_fe_sys(go.inv) : fe_inv_bin<F>(load_fe_sys(go.prod));
+                    have = true;
+#pragma unroll
+                    for (int i = 0; i < F::N; i++)
+                        __hip_atomic_store(&rl[i], tag | v.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    __hip_atomic_store(&rl[8], tag | (host ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                const int nw = go.per_block ? 1 : F::N;
+                uint64_t* src = go.per_block ? rl + 8 : rl;
+                uint64_t w[F::N];
+                for (;;) {
+                    bool all = true;
+                    for (int i = 0; i < nw; i++) {
+                        w[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        all = all && (w[i] >> 32) == go.epoch;
+                    }
+                    if (all) {
+                        seen = true;
+                        break;
+                    }
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > go.limit) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (seen && go.per_block) host = (w[0] & 1u) != 0;
+                if (seen && !go.per_block) {
+#pragma unroll
+                    for (int i = 0; i < F::N; i++) v.v[i] = (uint32_t)w[i];
+                    have = true;
+                }
+            }
+            if (go.dbg) {
+                go.dbg[3 * blockIdx.x] = t0;
+                go.dbg[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+                go.dbg[3 * blockIdx.x + 2] = (seen ? 1u : 0u) | (host ? 2u : 0u);
+            }
+            // per block: its own inverse from the host (distinct addresses), or made here
+            if (!have) v = host ? load_fe_sys(go.inv + k) : fe_inv_bin<F>(load_fe_sys(go.prod + k));
+            s_bi = go.per_block ? v : fe_mul<F>(v, binv[blockIdx.x]);
+        }
+        __syncthreads();
+    }
     if (j >= count) return;
     const BN254G1::Acc a = rows[j];
     const bool ident = BN254G1::is_zero(a);
-    // the block's inverse: binv[b], or (device scan) the cofactor times the total's inverse
-    const fe<F> bi = tinv ? fe_mul<F>(*tinv, binv[blockIdx.x]) : binv[blockIdx.x];
+    // the block's inverse: binv[b], or (device scan) the cofactor times the total's inverse, or
+    // (queued early) what lane 0 got above
+    const fe<F> bi = go.flag ? s_bi : tinv ? fe_mul<F>(*tinv, binv[blockIdx.x]) : binv[blockIdx.x];
     const fe<F> iz = fe_mul<F>(bi, others[j]);
     const fe<F> t = fe_mul<F>(iz, a.zz);  // 1/Z
     fe<F> cx = fe_from_mont<F>(fe_mul<F>(a.x, fe_sqr<F>(t))), cy = fe_from_mont<F>(fe_mul<F>(a.y, iz));
@@ -946,7 +1047,9 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     // fallback). The previous call's finish may still read its inverses, so this call takes the
     // other half (the call before that finished: its successor's prep, queued after it, was seen
     // complete); the buffer grows only after a sync.
-    const size_t flag_off = 2 * nblk * sizeof(fe<F>), half_bytes = (flag_off + nblk * 4 + 255) / 256 * 256;
+    // [block products | inverses | the prep's flags | the host's go word]
+    const size_t flag_off = 2 * nblk * sizeof(fe<F>), go_off = flag_off + nblk * 4;
+    const size_t half_bytes = (go_off + 4 + 255) / 256 * 256;
     if (ctx->pin_norm_vk.cap < 2 * half_bytes) {
         VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         VK_TRY(ctx->pin_norm_vk.ensure(2 * half_bytes));
@@ -959,7 +1062,37 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     fe<F>* dh = reinterpret_cast<fe<F>*>(dbase);
     volatile uint32_t* hflags = reinterpret_cast<volatile uint32_t*>(hbase + flag_off);
     uint32_t* dflags = reinterpret_cast<uint32_t*>(dbase + flag_off);
+    volatile uint32_t* hgo = reinterpret_cast<volatile uint32_t*>(hbase + go_off);
     const uint32_t epoch = ++ctx->small_epoch == 0 ? ++ctx->small_epoch : ctx->small_epoch;  // never 0
+    // the finish kernel queued right behind the prep, before the host has the inverse (NormGo): its
+    // blocks wait on the host's go word, so the host's inversion is no longer followed by a launch
+    // (~10-20 us of idle GPU per level) and the host queues the next level's work while the prep
+    // runs. VKZG_NORM_EARLY=0: launch the finish after the inversion (A/B); VKZG_NORM_EARLY_US: the
+    // blocks' wait before they invert on their own.
+    // (both read per call: a test sets a 1-us bound to run the blocks' own inversions)
+    const char* ee = getenv("VKZG_NORM_EARLY");
+    const char* eu = getenv("VKZG_NORM_EARLY_US");
+    const bool early = !(ee && atoi(ee) == 0);
+    const uint64_t early_ticks = 100ull * (uint64_t)(eu ? std::max(1, atoi(eu)) : 2000);
+    // (per-kernel timing keeps the late launch: the finish's events would count the host's wait)
+    NormGo go;
+    const bool early_now = early && !ctx->timing;
+    DevBuf& cnt = ctx->ws[WS_NORM_CNT];  // word 0: the prep's arrival counter; bytes [128, 200): the relay
+    if (cnt.p == nullptr) {
+        VK_TRY(cnt.ensure(256));
+        VK_CHECK_HIP(hipMemsetAsync(cnt.p, 0, 256, ctx->stream));
+    }
+    if (early_now) {
+        *hgo = 0;
+        go.relay = reinterpret_cast<uint64_t*>(cnt.as<uint8_t>() + 128);
+        go.flag = reinterpret_cast<const uint32_t*>(dbase + go_off);
+        go.epoch = epoch;
+        go.limit = early_ticks;
+    }
+    auto release_go = [&]() {
+        std::atomic_thread_fence(std::memory_order_release);  // the inverses before the word that frees them
+        *hgo = epoch;
+    };
     // the last block's scan costs ~17 us of serial multiplies whatever nblk is; the host's trick
     // ~54 ns per block: the scan pays from ~128 blocks on (c1 / c2 rows: 88 -> 74 us of prep + gap,
     // width-4 rows 76 -> 58 us; a 256-row level 24 -> 43 us: profiles/r05/verkle/sparse_norm_vk/)
@@ -967,17 +1100,26 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     if (scan_min != 0 && nblk >= scan_min) {
         // the block products scanned on the device (k_norm_prep_vk's last block): the host inverts
         // their total only; page-locked [total | its inverse | flag] in the same alternating halves
-        DevBuf& cnt = ctx->ws[WS_NORM_CNT];
         DevBuf& dt = ctx->ws[WS_NORM_TOT];
-        if (cnt.p == nullptr) {
-            VK_TRY(cnt.ensure(256));
-            VK_CHECK_HIP(hipMemsetAsync(cnt.p, 0, 256, ctx->stream));
-        }
         VK_TRY(dt.ensure(2 * nblk * sizeof(fe<F>)));
         fe<F>* dtot = dt.as<fe<F>>();
         hflags[0] = 0;
         VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids,
                   add_xy, add_inf, others.as<fe<F>>(), dtot, dflags, epoch, cnt.as<uint32_t>(), dtot + nblk, dh);
+        static const bool dbg_on = getenv("VKZG_NORM_DEBUG") != nullptr;
+        DevBuf dbgbuf(ctx);
+        if (early_now && dbg_on) {
+            VK_TRY(dbgbuf.ensure(nblk * 24));
+            go.dbg = dbgbuf.as<uint64_t>();
+        }
+        if (early_now) {
+            go.per_block = 0;
+            go.prod = dh;
+            go.inv = dh + 1;
+            VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
+                      others.as<fe<F>>(), dtot + nblk, dst, out_xy, out_inf, out_item, (const fe<F>*)nullptr, go);
+        }
+        const auto d0 = std::chrono::steady_clock::now();
         if (overlap && *overlap) (*overlap)();
         bool seen = false;
         const auto w0 = std::chrono::steady_clock::now();
@@ -990,16 +1132,53 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
             _mm_pause();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        // (queued early: this wait also covers the finish, whose blocks invert on their own past their bound)
         if (!seen) VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         h[1] = fe_inv_bin<F>(h[0]);  // never zero: identities count as 1
+        const auto d1 = std::chrono::steady_clock::now();
+        if (early_now) release_go();
+        static const bool dbg = getenv("VKZG_NORM_DEBUG") != nullptr;
+        if (dbg)
+            fprintf(stderr, "[norm] n %zu nblk %zu early %d overlap %.1f us, flag wait + inverse %.1f us\n", n, nblk,
+                    (int)early_now, std::chrono::duration<double, std::micro>(w0 - d0).count(),
+                    std::chrono::duration<double, std::micro>(d1 - w0).count());
+        if (early_now) {
+            if (go.dbg) {
+                const auto g0 = std::chrono::steady_clock::now();
+                VK_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+                const double sync_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g0).count();
+                std::vector<uint64_t> hd(nblk * 3);
+                VK_CHECK_HIP(hipMemcpy(hd.data(), go.dbg, nblk * 24, hipMemcpyDeviceToHost));
+                uint64_t tmin = ~0ull, e0 = hd[1], emax = 0, smin = ~0ull, smax = 0;
+                size_t timed_out = 0;
+                for (size_t b = 0; b < nblk; b++) {
+                    tmin = std::min(tmin, hd[3 * b]);
+                    smin = std::min(smin, hd[3 * b]);
+                    smax = std::max(smax, hd[3 * b]);
+                    emax = std::max(emax, hd[3 * b + 1]);
+                    timed_out += hd[3 * b + 2] == 0;
+                }
+                fprintf(stderr, "[norm go] block 0 waited %.1f us (seen %d); starts span %.1f us; last block done waiting %.1f us after block 0; %zu timed out; host sync after go %.1f us\n",
+                        (hd[1] - hd[0]) / 100.0, (int)hd[2], (smax - smin) / 100.0, ((double)emax - (double)e0) / 100.0,
+                        timed_out, sync_us);
+            }
+            return VC_OK;
+        }
         std::atomic_thread_fence(std::memory_order_release);  // the inverse before the launch that reads it
         VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
-                  others.as<fe<F>>(), dtot + nblk, dst, out_xy, out_inf, out_item, dh + 1);
+                  others.as<fe<F>>(), dtot + nblk, dst, out_xy, out_inf, out_item, dh + 1, NormGo{});
         return VC_OK;
     }
     for (size_t b = 0; b < nblk; b++) hflags[b] = 0;
     VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids, add_xy,
               add_inf, others.as<fe<F>>(), dh, dflags, epoch, (uint32_t*)nullptr, (fe<F>*)nullptr, (fe<F>*)nullptr);
+    if (early_now) {
+        go.per_block = 1;
+        go.prod = dh;
+        go.inv = dh + nblk;
+        VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
+                  others.as<fe<F>>(), dh + nblk, dst, out_xy, out_inf, out_item, (const fe<F>*)nullptr, go);
+    }
     if (overlap && *overlap) (*overlap)();
     // Montgomery's trick over the block products: the forward products are taken as the blocks'
     // flags arrive (blocks finish roughly in order), so only the inversion and the backward pass
@@ -1036,9 +1215,13 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
         inv[b] = ib;
     }
     inv[0] = run;
+    if (early_now) {
+        release_go();
+        return VC_OK;
+    }
     std::atomic_thread_fence(std::memory_order_release);  // the inverses before the launch that reads them
     VK_LAUNCH(ctx, "norm_finish", k_norm_finish_vk, nblk, 256, 0, static_cast<const BN254G1::Acc*>(d_rows), n,
-              others.as<fe<F>>(), dh + nblk, dst, out_xy, out_inf, out_item, (const fe<F>*)nullptr);
+              others.as<fe<F>>(), dh + nblk, dst, out_xy, out_inf, out_item, (const fe<F>*)nullptr, NormGo{});
     return VC_OK;
 }
 
