@@ -258,14 +258,16 @@ def test_verkle_ext_rows_in_pieces(eng, pieces, monkeypatch):
     assert roots(pieces) == roots("1")
 
 
-@pytest.mark.parametrize("mode", ["late", "selfinv"])
+@pytest.mark.parametrize("mode", ["late", "selfinv", "unfused"])
 def test_verkle_norm_finish_modes(eng, mode, monkeypatch):
     """The verkle levels' normalisation (commit.hip normalize_rows_items): by default the finish
     kernel is queued behind the prep before the host has inverted the block products, its blocks
     waiting on the host's go word. == the finish launched after the inversion (late,
     VKZG_NORM_EARLY=0) and == blocks that stop waiting after 1 us and invert on their own
     (selfinv, VKZG_NORM_EARLY_US=1); fresh and after a 1 % update of a 20,000-key tree (the c1 / c2
-    level's 40,000 rows take the device-scan form, the smaller levels the per-block form)."""
+    level's 40,000 rows take the device-scan form, the smaller levels the per-block form). unfused:
+    the sort-based sparse commits' count / scan / expand / row offsets as separate launches
+    (VKZG_SPARSE_FUSED=0) instead of the two fused kernels."""
     import numpy as np
     from vkzg import scheme
     from vkzg.verkle import VerkleTree
@@ -289,6 +291,8 @@ def test_verkle_norm_finish_modes(eng, mode, monkeypatch):
     want = roots()
     if mode == "late":
         monkeypatch.setenv("VKZG_NORM_EARLY", "0")
+    elif mode == "unfused":
+        monkeypatch.setenv("VKZG_SPARSE_FUSED", "0")
     else:
         monkeypatch.setenv("VKZG_NORM_EARLY_US", "1")
     assert roots() == want

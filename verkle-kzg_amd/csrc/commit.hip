@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__
                                                      fe<BN254Fq>* __restrict__ others, fe<BN254Fq>* __restrict__ tot,
                                                      uint32_t* __restrict__ flags, uint32_t epoch,
                                                      uint32_t* __restrict__ counter, fe<BN254Fq>* __restrict__ cof,
-                                                     fe<BN254Fq>* __restrict__ total) {
+                                                     fe<BN254Fq>* __restrict__ total, uint64_t* __restrict__ tags) {
     using C = BN254G1;
     const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
     C::Acc a = j < count ? rows[j] : C::zero();
@@ -274,20 +274,47 @@ __global__ void __launch_bounds__(256) k_norm_prep_vk(BN254G1::Acc* __restrict__
     // device scan (tot in device memory): the last block to arrive turns the nblk block products
     // into per-block cofactors cof[b] = prod_{k != b} tot[k] and hands the host only their total
     // (one inversion there, ~1 us, instead of Montgomery's trick over every block product: ~3
-    // multiplies per block, 40 us for 512 blocks, with the GPU idle)
+    // multiplies per block, 40 us for 512 blocks, with the GPU idle).
+    // tags (round 6): each block publishes its product as eight (epoch << 32 | limb) words and
+    // arrives without a fence; the last block polls the words until they carry this launch's epoch.
+    // An agent-scope fence per block writes back its XCD's whole L2 first -- with 512 blocks that
+    // was most of the kernel (profiles/r06/verkle/fence_free/).
     using F = BN254Fq;
     __shared__ uint32_t s_last;
     __shared__ fe<F> spre[256], ssuf[256];
     const uint32_t tid = threadIdx.x, nb = gridDim.x;
+    const uint64_t tag = (uint64_t)epoch << 32;
     if (tid == 0) {
-        __threadfence();  // this block's product before its arrival
+        if (tags) {
+            const fe<F> mine = tot[blockIdx.x];  // (this thread's own store in norm_prep_block)
+#pragma unroll
+            for (int k = 0; k < F::N; k++)
+                __hip_atomic_store(&tags[(size_t)F::N * blockIdx.x + k], tag | mine.v[k], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __threadfence();  // this block's product before its arrival
+        }
         s_last = atomicAdd(counter, 1u) == nb - 1 ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();
+    if (!tags) __threadfence();
     auto load = [&](uint32_t b) {  // another block's product: through the coherent path
         fe<F> v;
+        if (tags) {  // every block stored its words before it arrived: the wait is short (bounded anyway)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                bool all = true;
+#pragma unroll
+                for (int k = 0; k < F::N; k++) {
+                    const uint64_t w = __hip_atomic_load(&tags[(size_t)F::N * b + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v.v[k] = (uint32_t)w;
+                    all = all && (w & 0xffffffff00000000ull) == tag;
+                }
+                if (all || __builtin_amdgcn_s_memrealtime() - t0 > 1000000ull) break;  // (10 ms)
+            }
+            return v;
+        }
         const uint32_t* src = reinterpret_cast<const uint32_t*>(&tot[b]);
 #pragma unroll
         for (int k = 0; k < F::N; k++) v.v[k] = __hip_atomic_load(&src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1077,7 +1104,7 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     // (per-kernel timing keeps the late launch: the finish's events would count the host's wait)
     NormGo go;
     const bool early_now = early && !ctx->timing;
-    DevBuf& cnt = ctx->ws[WS_NORM_CNT];  // word 0: the prep's arrival counter; bytes [128, 200): the relay
+    DevBuf& cnt = ctx->ws[WS_NORM_CNT];  // word 0: the prep's arrival counter; word 16: the sparse commits' (msm.hip k_sparse_count_scan); bytes [128, 200): the relay
     if (cnt.p == nullptr) {
         VK_TRY(cnt.ensure(256));
         VK_CHECK_HIP(hipMemsetAsync(cnt.p, 0, 256, ctx->stream));
@@ -1101,11 +1128,14 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
         // the block products scanned on the device (k_norm_prep_vk's last block): the host inverts
         // their total only; page-locked [total | its inverse | flag] in the same alternating halves
         DevBuf& dt = ctx->ws[WS_NORM_TOT];
-        VK_TRY(dt.ensure(2 * nblk * sizeof(fe<F>)));
+        VK_TRY(dt.ensure(2 * nblk * sizeof(fe<F>) + nblk * F::N * 8));
         fe<F>* dtot = dt.as<fe<F>>();
+        // VKZG_NORM_TAGS=0 (read per call, A/B): a fence per block before its arrival instead
+        const char* te = getenv("VKZG_NORM_TAGS");
+        uint64_t* tags = (te && atoi(te) == 0) ? nullptr : reinterpret_cast<uint64_t*>(dtot + 2 * nblk);
         hflags[0] = 0;
         VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids,
-                  add_xy, add_inf, others.as<fe<F>>(), dtot, dflags, epoch, cnt.as<uint32_t>(), dtot + nblk, dh);
+                  add_xy, add_inf, others.as<fe<F>>(), dtot, dflags, epoch, cnt.as<uint32_t>(), dtot + nblk, dh, tags);
         static const bool dbg_on = getenv("VKZG_NORM_DEBUG") != nullptr;
         DevBuf dbgbuf(ctx);
         if (early_now && dbg_on) {
@@ -1171,7 +1201,8 @@ int normalize_rows_items(vc_ctx* ctx, void* d_rows, size_t n, const uint32_t* ad
     }
     for (size_t b = 0; b < nblk; b++) hflags[b] = 0;
     VK_LAUNCH(ctx, "norm_prep", k_norm_prep_vk, nblk, 256, 0, static_cast<BN254G1::Acc*>(d_rows), n, add_ids, add_xy,
-              add_inf, others.as<fe<F>>(), dh, dflags, epoch, (uint32_t*)nullptr, (fe<F>*)nullptr, (fe<F>*)nullptr);
+              add_inf, others.as<fe<F>>(), dh, dflags, epoch, (uint32_t*)nullptr, (fe<F>*)nullptr, (fe<F>*)nullptr,
+              (uint64_t*)nullptr);
     if (early_now) {
         go.per_block = 1;
         go.prod = dh;

@@ -2067,6 +2067,131 @@ __global__ void k_sparse_expand(const uint32_t* __restrict__ sc, const uint32_t*
     });
 }
 
+// Fused form of count + scan + expand + rows (round 6): two launches instead of six (the hipcub
+// scan's two, the count, the expand, the row offsets and a fill) -- each tiny launch costs ~4.5 us
+// of GPU time even when the host is ahead (profiles/r06/verkle/norm_early/timeline_full_and_update.txt).
+// K1: elements [256 b, 256 b + 256) of block b (j <= nnz: the grid has nnz / 256 + 1 blocks, so
+// j = nnz is always some block's element, with count 0) -> local[j] = the exclusive count prefix
+// inside the block, bsum[b] = its total; the last block to arrive scans the block totals into
+// boff[0 .. nb] (boff[nb] = all entries) and resets the arrival counter for the next launch.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s_w, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < wv; k++) before += s_w[k];
+    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    return before + x - v;
+}
+template <class Fr>
+__global__ void __launch_bounds__(256) k_sparse_count_scan(const uint32_t* __restrict__ sc, size_t nnz, int mont,
+                                                          FbGeom g, uint32_t* __restrict__ local,
+                                                          uint64_t* __restrict__ bsum, uint32_t* __restrict__ boff,
+                                                          uint32_t* __restrict__ counter, uint32_t* __restrict__ chain_max,
+                                                          uint32_t epoch) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_last;
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t k = 0;
+    if (j < nnz) {
+        fe<Fr> s = load_scalar<Fr>(sc, j);
+        if (mont) s = fe_from_mont<Fr>(s);
+        for_each_digit_fb<Fr>(s, g, [&](int, int32_t d) { k += d != 0; });
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256(k, s_w, &tot);
+    if (j <= nnz) local[j] = ex;
+    if (chain_max && blockIdx.x == 0 && threadIdx.x == 0) *chain_max = 0;
+    const uint32_t nb = gridDim.x;
+    const uint64_t tag = (uint64_t)epoch << 32;
+    // the block total as one (epoch << 32 | total) word and no fence before the arrival: the last
+    // block polls the words until they carry this launch's epoch (a fence per block writes back its
+    // XCD's whole L2: ~28 us for the 1,025 blocks of a 262,144-non-zero level)
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&bsum[blockIdx.x], tag | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = atomicAdd(counter, 1u) == nb - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    auto total_of = [&](uint32_t b) -> uint32_t {  // (bounded: 10 ms)
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            const uint64_t w = __hip_atomic_load(&bsum[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((w & 0xffffffff00000000ull) == tag || __builtin_amdgcn_s_memrealtime() - t0 > 1000000ull)
+                return (uint32_t)w;
+        }
+    };
+    // the last block: exclusive scan of the nb block totals, ceil(nb / 256) consecutive per thread
+    // (the loads of a thread's totals go out together: one after another they cost ~1-2 us each,
+    // 30 us for the 1,025 blocks of a 262,144-non-zero level)
+    const uint32_t per = (nb + 255) / 256, b0 = min(threadIdx.x * per, nb), b1 = min(b0 + per, nb);
+    constexpr uint32_t PR = 8;
+    uint32_t v[PR];
+    uint32_t seg = 0;
+    if (per <= PR) {
+#pragma unroll
+        for (uint32_t q = 0; q < PR; q++) v[q] = b0 + q < b1 ? total_of(b0 + q) : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < PR; q++) seg += v[q];
+    } else {
+        for (uint32_t b = b0; b < b1; b++) seg += total_of(b);
+    }
+    uint32_t all;
+    uint32_t run = block_excl_scan256(seg, s_w, &all);
+    if (per <= PR) {
+#pragma unroll
+        for (uint32_t q = 0; q < PR; q++) {
+            if (b0 + q < b1) boff[b0 + q] = run;
+            run += v[q];
+        }
+    } else {
+        for (uint32_t b = b0; b < b1; b++) {
+            boff[b] = run;
+            run += total_of(b);
+        }
+    }
+    if (threadIdx.x == 0) {
+        boff[nb] = all;
+        *counter = 0;  // for the next launch (stream-ordered after this one)
+    }
+}
+// K2: thread i < nnz expands element i's digits at boff[i / 256] + local[i]; thread i <= nch sets
+// chunk i's entry offset (rp[i] is an element index <= nnz) and, for an empty chunk, its identity
+template <class Fr, class C>
+__global__ void __launch_bounds__(256) k_sparse_expand_rows(const uint32_t* __restrict__ sc,
+                                                           const uint32_t* __restrict__ cols, size_t nnz, int mont,
+                                                           FbGeom g, const uint32_t* __restrict__ local,
+                                                           const uint32_t* __restrict__ boff,
+                                                           uint32_t* __restrict__ entries,
+                                                           const uint64_t* __restrict__ rp, size_t nch,
+                                                           uint32_t* __restrict__ offsets,
+                                                           typename C::Acc* __restrict__ chunks) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nnz) {
+        fe<Fr> s = load_scalar<Fr>(sc, i);
+        if (mont) s = fe_from_mont<Fr>(s);
+        const uint32_t base = cols[i] * (uint32_t)g.stride();
+        uint32_t pos = boff[i >> 8] + local[i];
+        for_each_digit_fb<Fr>(s, g, [&](int w, int32_t d) {
+            if (d != 0)
+                entries[pos++] = (base + (uint32_t)g.off(w) + (uint32_t)(d < 0 ? -d : d) - 1) | (d < 0 ? 0x80000000u : 0u);
+        });
+    }
+    if (i <= nch) {
+        auto at = [&](uint64_t e) { return boff[e >> 8] + local[e]; };
+        const uint32_t o = at(rp[i]);
+        offsets[i] = o;
+        if (i < nch && at(rp[i + 1]) == o) chunks[i] = C::zero();
+    }
+}
+
 // row offsets in entry space; empty rows get the identity (the accumulate never writes them)
 template <class C>
 __global__ void k_sparse_rows(const uint64_t* __restrict__ row_ptr, const uint32_t* __restrict__ eoff, size_t batch,
@@ -2253,40 +2378,62 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     // device), else one upload
     const uint64_t* rp_dev = d_rp.as<uint64_t>();
     const uint32_t* rc_dev = d_rc.as<uint32_t>();
-    if (ch.identity) {
+    if (ch.identity) {  // (no chunk lists: the combine, their only reader, is skipped)
         if (d_row_ptr) rp_dev = d_row_ptr;
         else VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, row_ptr, (batch + 1) * 8, hipMemcpyHostToDevice, st));
-        VK_LAUNCH(ctx, "sparse_iota", k_iota, (uint32_t)((batch + 1 + 255) / 256), 256, 0, d_rc.as<uint32_t>(),
-                  (uint32_t)batch);
     } else {
         VK_CHECK_HIP(hipMemcpyAsync(d_rp.p, ch.cptr, rc_off + (batch + 1) * 4, hipMemcpyHostToDevice, st));
         rc_dev = reinterpret_cast<const uint32_t*>(d_rp.as<uint8_t>() + rc_off);
     }
     const uint32_t* d_cols = d_cols_in;
     const uint32_t* d_sc = static_cast<const uint32_t*>(d_sc_in);
-    VK_CHECK_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + nnz, 0, 4, st));
-    if (nnz)
-        VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc, nnz, mont, fg,
-                  d_cnt.as<uint32_t>());
-    size_t tmp_bytes = 0;
-    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
-                                                  nnz + 1, st));
-    VK_TRY(d_tmp.ensure(std::max<size_t>(tmp_bytes, 1)));
-    VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp.p, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
-                                                  nnz + 1, st));
-    if (nnz)
-        VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc, d_cols, nnz, mont, fg,
-                  d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
-    VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, rp_dev,
-              d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
+    VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
+    uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
+    // VKZG_SPARSE_FUSED=0 (read per call, A/B): the count, the hipcub scan, the expand and the row
+    // offsets as separate launches
+    const char* fe_env = getenv("VKZG_SPARSE_FUSED");
+    const bool fused = !(fe_env && atoi(fe_env) == 0);
+    if (fused) {
+        // the arrival counter: a word of the normalisation's zeroed counter buffer (commit.hip)
+        DevBuf& cntb = ctx->ws[WS_NORM_CNT];
+        if (cntb.p == nullptr) {
+            VK_TRY(cntb.ensure(256));
+            VK_CHECK_HIP(hipMemsetAsync(cntb.p, 0, 256, st));
+        }
+        const size_t nb = nnz / 256 + 1;  // elements 0 .. nnz
+        VK_TRY(d_eoff.ensure(nb * 8 + (nb + 1) * 4));
+        uint64_t* bsum = d_eoff.as<uint64_t>();
+        uint32_t* boff = reinterpret_cast<uint32_t*>(bsum + nb);
+        const uint32_t epoch = ++ctx->small_epoch == 0 ? ++ctx->small_epoch : ctx->small_epoch;  // never 0
+        VK_LAUNCH(ctx, "sparse_count_scan", (k_sparse_count_scan<Fr>), (unsigned)nb, 256, 0, d_sc, nnz, mont, fg,
+                  d_cnt.as<uint32_t>(), bsum, boff, cntb.as<uint32_t>() + 16, Tmax > 0 ? chain_max : (uint32_t*)nullptr,
+                  epoch);
+        VK_LAUNCH(ctx, "sparse_expand_rows", (k_sparse_expand_rows<Fr, C>), (unsigned)((std::max(nnz, nch + 1) + 255) / 256),
+                  256, 0, d_sc, d_cols, nnz, mont, fg, d_cnt.as<uint32_t>(), boff, d_ent.as<uint32_t>(), rp_dev, nch,
+                  d_off.as<uint32_t>(), d_chunks.as<Acc>());
+    } else {
+        VK_CHECK_HIP(hipMemsetAsync(d_cnt.as<uint32_t>() + nnz, 0, 4, st));
+        if (nnz)
+            VK_LAUNCH(ctx, "sparse_count", (k_sparse_count<Fr>), (nnz + 255) / 256, 256, 0, d_sc, nnz, mont, fg,
+                      d_cnt.as<uint32_t>());
+        size_t tmp_bytes = 0;
+        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
+                                                      nnz + 1, st));
+        VK_TRY(d_tmp.ensure(std::max<size_t>(tmp_bytes, 1)));
+        VK_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp.p, tmp_bytes, d_cnt.as<uint32_t>(), d_eoff.as<uint32_t>(),
+                                                      nnz + 1, st));
+        if (nnz)
+            VK_LAUNCH(ctx, "sparse_expand", (k_sparse_expand<Fr>), (nnz + 255) / 256, 256, 0, d_sc, d_cols, nnz, mont, fg,
+                      d_eoff.as<uint32_t>(), d_ent.as<uint32_t>());
+        VK_LAUNCH(ctx, "sparse_rows", (k_sparse_rows<C>), (nch + 1 + 255) / 256, 256, 0, rp_dev,
+                  d_eoff.as<uint32_t>(), nch, d_off.as<uint32_t>(), d_chunks.as<Acc>());
+        if (Tmax > 0) VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
+    }
     // the fixed-base tables hold radix-2^29 limbs in 128-B entries (ec29.hpp FbE): the accumulate
     // reads the entries' limbs (is_fbe)
     using FA = FbE<C>;
     const FA* tab = t->fb.as<FA>();
-    if (Tmax > 0) {  // all-zero rows only: k_sparse_rows already set every chunk to the identity
-        VK_TRY(ctx->ws[WS_CHAIN].ensure(4));
-        uint32_t* chain_max = ctx->ws[WS_CHAIN].as<uint32_t>();
-        VK_CHECK_HIP(hipMemsetAsync(chain_max, 0, 4, st));
+    if (Tmax > 0) {  // all-zero rows only: the row offsets already set every chunk to the identity
         using RAcc = FAcc<C>;
         DevBuf& d_raw = ctx->ws[WS_RAW_B];
         VK_TRY(d_raw.ensure(nch * sizeof(RAcc)));

@@ -1233,14 +1233,35 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
     if (!tab) return VC_E_TABLE;
     if (tab->curve != VC_CURVE_BN254) return VC_E_INVALID;
     static const bool verbose = getenv("VKZG_VERBOSE") != nullptr;
+    // VKZG_VERKLE_STAMPS=1: the host's time at each lap without synchronising (printed at the end)
+    static const bool stamps = getenv("VKZG_VERKLE_STAMPS") != nullptr;
     auto tic = std::chrono::steady_clock::now();
+    const auto t_entry = tic;
+    std::vector<std::pair<const char*, double>> marks;
     auto lap = [&](const char* what) {
+        if (stamps) {
+            marks.emplace_back(what, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_entry).count());
+            return;
+        }
         if (!verbose) return;
         (void)hipStreamSynchronize(ctx->stream);
         auto now = std::chrono::steady_clock::now();
         fprintf(stderr, "[verkle-dev] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(now - tic).count());
         tic = now;
     };
+    struct PrintMarks {
+        const std::vector<std::pair<const char*, double>>& m;
+        ~PrintMarks() {
+            if (m.empty()) return;
+            std::string line = "[verkle-stamps]";
+            char buf[96];
+            for (auto& x : m) {
+                snprintf(buf, sizeof buf, " %s@%.0f", x.first, x.second);
+                line += buf;
+            }
+            fprintf(stderr, "%s\n", line.c_str());
+        }
+    } print_marks{marks};
     DeltaGuard delta_guard{t};
     VK_TRY(mirror_prepare(ctx, t));
     VerkleDev& D = t->dev;
