@@ -996,10 +996,14 @@ def verkle_line(a, local, stream):
     veng.enable_timing(False)
     del k
     kms = {}
-    for kn in ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup_init", "msm_fixup_jump",
-               "msm_fixup", "sparse_store", "sparse_combine", "norm_prep", "norm_finish", "fb_normalize",
-               "fb_commit", "fb_combine", "fb_commit_small", "to_data_item", "sparse_iota", "verkle_widen",
-               "verkle_ext_rows4", "verkle_gather", "verkle_dense", "verkle_scatter"):
+    # every launch name the verkle paths time (csrc VK_LAUNCH names; the fused sparse kernels and the
+    # latency path's sparse_small were missing before round 6's last rehearsal, which overstated the
+    # host share by their ~0.1 ms)
+    for kn in ("sparse_count", "sparse_expand", "sparse_rows", "sparse_count_scan", "sparse_expand_rows",
+               "sparse_small", "sparse_accumulate", "msm_fixup_init", "msm_fixup_jump", "msm_fixup", "sparse_store",
+               "sparse_combine", "sparse_add_base", "norm_prep", "norm_finish", "fb_normalize", "fb_commit",
+               "fb_combine", "fb_commit_small", "to_data_item", "sparse_iota", "verkle_widen", "verkle_ext_rows4",
+               "verkle_rp4", "verkle_delta", "verkle_gather", "verkle_dense", "verkle_scatter"):
         ms, cnt = veng.kernel_time(kn)
         if cnt:
             kms[kn] = round(ms, 3)

@@ -12,9 +12,10 @@ import vkzg  # noqa: E402
 from vkzg import scheme  # noqa: E402
 from vkzg.verkle import VerkleTree  # noqa: E402
 
-NAMES = ("sparse_count", "sparse_expand", "sparse_rows", "sparse_accumulate", "msm_fixup", "sparse_store",
-         "sparse_combine", "normalize_out", "norm_prep", "norm_finish", "to_data_item", "fb_commit", "fb_combine", "fb_normalize_out",
-         "fb_commit_small")
+NAMES = ("sparse_count", "sparse_expand", "sparse_rows", "sparse_count_scan", "sparse_expand_rows", "sparse_small",
+         "sparse_accumulate", "msm_fixup", "sparse_store", "sparse_combine", "sparse_add_base", "normalize_out", "norm_prep",
+         "norm_finish", "to_data_item", "fb_commit", "fb_combine", "fb_normalize_out", "fb_commit_small", "verkle_widen",
+         "verkle_ext_rows4", "verkle_rp4", "verkle_delta", "verkle_gather", "verkle_dense", "verkle_scatter")
 nk = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 eng = vkzg.Engine("bn254", 0)
 eng.set_stream(torch.cuda.current_stream().cuda_stream)
