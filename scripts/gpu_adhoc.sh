@@ -1,9 +1,9 @@
+# second full parity run on the final library (another box)
 set -eu
 R=$(pwd)
-O=$R/gpurun_out/r06_smalltags; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_scheme.py tests/test_gpu_verkle.py tests/test_gpu_verkle32.py tests/test_gpu_multiproof_256.py -m gpu > $O/tests_default.txt 2>&1
-echo tests-default; tail -1 $O/tests_default.txt
-VKZG_SMALL_TAGS=1 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_scheme.py tests/test_gpu_verkle.py tests/test_gpu_verkle32.py tests/test_gpu_multiproof_256.py -m gpu > $O/tests_tags.txt 2>&1
-echo tests-tags; tail -1 $O/tests_tags.txt
-bash scripts/ab_probe.sh $O/ab_ipa VKZG_SMALL_TAGS "1 0" 3 120 python -u verkle-kzg_amd/tools/ipa_abi_probe.py
-VKZG_AB_FB_C=16 bash scripts/ab_probe.sh $O/ab_verkle VKZG_SMALL_TAGS "1 0" 3 180 python -u verkle-kzg_amd/tools/verkle_ab.py 65536 8
+O=$R/gpurun_out/r06_tests2; mkdir -p $O
+sha256sum verkle-kzg_amd/lib/libvkzg.so > $O/lib_sha.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1
+echo tests-done; tail -1 $O/gpu_tests.txt
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1
+echo smoke-done
