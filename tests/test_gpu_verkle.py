@@ -258,7 +258,7 @@ def test_verkle_ext_rows_in_pieces(eng, pieces, monkeypatch):
     assert roots(pieces) == roots("1")
 
 
-@pytest.mark.parametrize("mode", ["late", "selfinv", "unfused"])
+@pytest.mark.parametrize("mode", ["late", "selfinv", "unfused", "nolead"])
 def test_verkle_norm_finish_modes(eng, mode, monkeypatch):
     """The verkle levels' normalisation (commit.hip normalize_rows_items): by default the finish
     kernel is queued behind the prep before the host has inverted the block products, its blocks
@@ -267,7 +267,8 @@ def test_verkle_norm_finish_modes(eng, mode, monkeypatch):
     (selfinv, VKZG_NORM_EARLY_US=1); fresh and after a 1 % update of a 20,000-key tree (the c1 / c2
     level's 40,000 rows take the device-scan form, the smaller levels the per-block form). unfused:
     the sort-based sparse commits' count / scan / expand / row offsets as separate launches
-    (VKZG_SPARSE_FUSED=0) instead of the two fused kernels."""
+    (VKZG_SPARSE_FUSED=0) instead of the two fused kernels. nolead: the extension width-4 rows on the
+    SRS's own 16-bit fixed-base table instead of the 20-bit table of bases 0..3 (VKZG_VERKLE_LEAD_C=0)."""
     import numpy as np
     from vkzg import scheme
     from vkzg.verkle import VerkleTree
@@ -293,6 +294,8 @@ def test_verkle_norm_finish_modes(eng, mode, monkeypatch):
         monkeypatch.setenv("VKZG_NORM_EARLY", "0")
     elif mode == "unfused":
         monkeypatch.setenv("VKZG_SPARSE_FUSED", "0")
+    elif mode == "nolead":
+        monkeypatch.setenv("VKZG_VERKLE_LEAD_C", "0")
     else:
         monkeypatch.setenv("VKZG_NORM_EARLY_US", "1")
     assert roots() == want

@@ -174,6 +174,9 @@ static int fill_t(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf,
     t->fb_c = t->fb_W = 0;  // any fixed-base tables are stale now: give their memory back
     t->fb_auto = false;
     t->fb.release();
+    delete t->lead;  // (its bases are this table's first ones)
+    t->lead = nullptr;
+    t->lead_k = t->lead_c = 0;
     t->subgroup = -1;
     t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(Aff)));

@@ -1035,6 +1035,9 @@ static int table_from_acc_t(vc_ctx* ctx, Table* t, const void* d_acc, size_t n) 
     t->fb_c = t->fb_W = t->fb_big = 0;
     t->fb_auto = false;
     t->fb.release();
+    delete t->lead;
+    t->lead = nullptr;
+    t->lead_k = t->lead_c = 0;
     t->fast_ok = t->phi_ok = t->win_ok = 0;
     VK_TRY(t->bases.ensure(std::max<size_t>(n, 1) * sizeof(typename C::Aff)));
     VK_TRY(t->inf.ensure(std::max<size_t>(n, 1)));
@@ -1268,6 +1271,49 @@ int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void
         case VC_CURVE_BANDERSNATCH: return VK_NORM_(Bandersnatch);
     }
 #undef VK_NORM_
+    return VC_E_INVALID;
+}
+
+template <class C>
+static int lead_table_t(vc_ctx* ctx, Table* t, int k, int c, Table** out) {
+    using Aff = typename C::Aff;
+    *out = nullptr;
+    if (k <= 0 || (size_t)k > t->n) return VC_E_INVALID;
+    if (t->lead && t->lead_k == k && t->lead_c == c) {
+        *out = t->lead;
+        return VC_OK;
+    }
+    delete t->lead;
+    t->lead = nullptr;
+    Table* s = new Table();
+    s->curve = t->curve;
+    s->n = (size_t)k;
+    s->subgroup = t->subgroup;
+    int st = s->bases.ensure((size_t)k * sizeof(Aff));
+    if (st == VC_OK) st = s->inf.ensure((size_t)k);
+    if (st == VC_OK && (hipMemcpyAsync(s->bases.p, t->bases.p, (size_t)k * sizeof(Aff), hipMemcpyDeviceToDevice,
+                                       ctx->stream) != hipSuccess ||
+                        hipMemcpyAsync(s->inf.p, t->inf.p, (size_t)k, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess))
+        st = VC_E_HIP;
+    if (st == VC_OK) st = fixed_base_precompute(ctx, s, c);
+    if (st != VC_OK) {
+        delete s;
+        (void)hipGetLastError();
+        return st == VC_E_OOM ? VC_OK : st;  // out of memory: no lead table, the caller keeps t
+    }
+    t->lead = s;
+    t->lead_k = k;
+    t->lead_c = c;
+    *out = s;
+    return VC_OK;
+}
+int lead_table(vc_ctx* ctx, Table* t, int k, int c, Table** out) {
+    switch (t->curve) {
+        case VC_CURVE_BN254: return lead_table_t<BN254G1>(ctx, t, k, c, out);
+        case VC_CURVE_BLS12_381: return lead_table_t<BLS381G1>(ctx, t, k, c, out);
+        case VC_CURVE_BANDERSNATCH: return lead_table_t<Bandersnatch>(ctx, t, k, c, out);
+    }
+    *out = nullptr;
     return VC_E_INVALID;
 }
 

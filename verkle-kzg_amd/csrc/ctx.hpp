@@ -154,6 +154,15 @@ struct Table {
     int win_limbs = 1;  // copies in radix-2^29 limbs (1) or packed-29 (0, VKZG_WIN_PACKED probe)
     int win_pair = 0;   // radix copies in the pair layout (SW29::AffP, one 128-B record per signed copy)
     DevBuf win;
+    // the first few bases as a table of their own with wider fixed-base windows (lead_table in
+    // commit.hip: the verkle extension rows [1, stem, c1, c2] use bases 0..3 only); owned, built on
+    // first use, dropped when the bases are refilled
+    Table* lead = nullptr;
+    int lead_k = 0, lead_c = 0;
+    Table() = default;
+    Table(const Table&) = delete;
+    Table& operator=(const Table&) = delete;
+    ~Table() { delete lead; }
 };
 
 enum WsSlot {
@@ -341,6 +350,9 @@ int bases_fill(vc_ctx* ctx, Table* t, const uint64_t* xy, const uint8_t* inf, si
 int bases_random(vc_ctx* ctx, uint64_t seed, size_t n, int* id);
 int bases_download(vc_ctx* ctx, Table* t, uint64_t* xy, uint8_t* inf);
 int fixed_base_precompute(vc_ctx* ctx, Table* t, int c, int windows = 0);
+// t's first k bases as their own table with c-bit fixed-base windows (t->lead, built on first
+// use); *out = nullptr when it cannot be had (out of memory: the caller keeps t)
+int lead_table(vc_ctx* ctx, Table* t, int k, int c, Table** out);
 int normalize_to_canon(vc_ctx* ctx, int curve, const void* d_acc, size_t n, void* d_out_xy, uint8_t* d_out_inf);
 int msm_batch_sparse(vc_ctx* ctx, Table* t, size_t batch, const uint64_t* row_ptr, const uint32_t* cols,
                      const uint64_t* scalars, int mont, uint64_t* out_xy, uint8_t* out_inf);

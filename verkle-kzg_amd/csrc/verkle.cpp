@@ -1575,6 +1575,18 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
                                            order.empty() ? nullptr : &build_next_fn, d_rp_dev));
         }
         lap("ext c1 / c2 commits");
+        // the width-4 rows use bases 0..3 only: their own table with 20-bit windows (13 instead of
+        // 16 window adds per scalar, 3.5 GB; VKZG_VERKLE_LEAD_C: the window bits, 0 = the SRS's table)
+        Table* tab4 = tab;
+        {
+            const char* lc = getenv("VKZG_VERKLE_LEAD_C");
+            const int c4 = lc ? atoi(lc) : 20;
+            if (c4 > 0 && tab->n >= 4 && c4 > tab->fb_c) {
+                Table* lt = nullptr;
+                VK_TRY(lead_table(ctx, tab, 4, c4, &lt));
+                if (lt) tab4 = lt;
+            }
+        }
         DevBuf d_c4(ctx), d_v4(ctx);
         VK_TRY(d_c4.ensure(4 * E * 4));
         VK_TRY(d_v4.ensure(4 * E * 32));
@@ -1598,12 +1610,12 @@ int verkle_commitment_dev(vc_ctx* ctx, int table, vc_verkle* t, uint64_t* out_xy
             in.d_out_xy = m_cxy;
             in.d_out_inf = m_inf;
             in.d_out_item = m_item;
-            VK_TRY(sparse_small_items_dev(ctx, tab, in, order.empty() ? nullptr : &build_next_fn));
+            VK_TRY(sparse_small_items_dev(ctx, tab4, in, order.empty() ? nullptr : &build_next_fn));
         } else {  // results straight into the mirror as well; row_ptr[k] = 4 k made on the device
             DevBuf d_rp4(ctx);
             VK_TRY(d_rp4.ensure((E + 1) * 8));
             VK_LAUNCH(ctx, "verkle_rp4", k_vk_rp4, grid(E + 1), 256, 0, d_rp4.as<uint64_t>(), E);
-            VK_TRY(sparse_commit_items_dev(ctx, tab, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, m_cxy, m_inf,
+            VK_TRY(sparse_commit_items_dev(ctx, tab4, E, rp4.data(), true, d_c4.as<uint32_t>(), d_v4.p, m_cxy, m_inf,
                                            m_item, nullptr, nullptr, nullptr, d_ids,
                                            order.empty() ? nullptr : &build_next_fn, d_rp4.as<uint64_t>()));
         }
