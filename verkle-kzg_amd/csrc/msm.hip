@@ -2352,7 +2352,8 @@ static int sparse_commit_dev(vc_ctx* ctx, Table* t, size_t batch, const uint64_t
     DevBuf& d_own = ctx->ws[WS_OWNER];
     DevBuf& d_ownb = ctx->ws[WS_OWNER_B];
     DevBuf& d_tmp = ctx->ws[WS_SCAN_TMP];
-    const uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    uint32_t M = (uint32_t)std::min<size_t>(64, std::max<size_t>(16, maxL / 131072));
+    if (const char* em = getenv("VKZG_SPARSE_M")) M = (uint32_t)std::max(1, atoi(em));  // tuning probe (read per call)
     const uint32_t Tmax = (uint32_t)((maxL + M - 1) / M);
     DevBuf& d_rc = ctx->ws[WS_SP_RC];
     DevBuf& d_chunks = ctx->ws[WS_SP_CHUNKS];
