@@ -1,4 +1,6 @@
+# a second bench line on the round's final library (box-to-box spread; bench.py as the driver runs it)
 set -eu
 R=$(pwd)
-O=$R/gpurun_out/r06_partM; mkdir -p $O
-bash scripts/ab_probe.sh $O VKZG_MSM_M "16 24 32" 2 200 python -u verkle-kzg_amd/tools/split_probe.py 8
+O=$R/gpurun_out/r06_final6b; mkdir -p $O
+timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
+echo bench-done; tail -2 $O/bench.err
