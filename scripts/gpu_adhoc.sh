@@ -1,6 +1,7 @@
-# a second bench line on the round's final library (box-to-box spread; bench.py as the driver runs it)
 set -eu
 R=$(pwd)
-O=$R/gpurun_out/r06_final6b; mkdir -p $O
-timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
-echo bench-done; tail -2 $O/bench.err
+O=$R/gpurun_out/r06_mpomp; mkdir -p $O
+timeout -k 10 300 python -u verkle-kzg_amd/tools/mp_phase_probe.py 16 12 > $O/default.txt 2>&1
+OMP_WAIT_POLICY=PASSIVE timeout -k 10 300 python -u verkle-kzg_amd/tools/mp_phase_probe.py 16 12 > $O/omp_passive.txt 2>&1
+timeout -k 10 300 python -u verkle-kzg_amd/tools/mp_phase_probe.py 16 12 > $O/default2.txt 2>&1
+echo done
