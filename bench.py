@@ -1470,8 +1470,9 @@ def main():
 
         big = ctime(a.commit_window, a.commit_windows if a.commit_window != 16 else 0)
         small = ctime(16) if a.commit_window != 16 else big
-        # the <= 70 GB table: 14 windows (12 of 18 bits, 2 of 19), 68.7 GB
-        mixed = ctime(18, 14)
+        # the <= 70 GB table: 14 windows (12 of 18 bits, 2 of 19), 68.7 GB (not when more than two
+        # rehearsal ranks share one card: four of them do not fit its HBM beside the rest)
+        mixed = ctime(18, 14) if not (a.rehearse_one_gpu and world > 2) else None
         # the deployable <= 32 GB table: 15 windows (14 of 17 bits, one of 16), 31.1 GB -- the adds
         # of c = 17's 15 windows from a smaller table (c = 17 x 15 is 32.2 GB)
         deploy = ctime(16, 15)
