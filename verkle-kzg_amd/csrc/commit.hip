@@ -1285,6 +1285,15 @@ static int lead_table_t(vc_ctx* ctx, Table* t, int k, int c, Table** out) {
     }
     delete t->lead;
     t->lead = nullptr;
+    // only where it leaves the device 4 GB free (as the first-use tables, fb_default_c): otherwise
+    // no lead table and the caller keeps t; it then counts in the context's fb_auto_used()
+    {
+        using Fr = FrOf<C>;
+        const size_t W = (size_t)(Fr::BITS + 1 + c - 1) / c;
+        const double bytes = (double)k * (double)(W << (c - 1)) * (double)sizeof(FbE<C>);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && bytes > (double)free_b - 4e9) return VC_OK;
+    }
     Table* s = new Table();
     s->curve = t->curve;
     s->n = (size_t)k;

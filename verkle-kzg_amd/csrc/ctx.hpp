@@ -297,8 +297,10 @@ struct vc_ctx {
     // fb_default_c's budget; a table refilled or re-precomputed explicitly stops counting)
     size_t fb_auto_used() const {
         size_t s = 0;
-        for (const vk::Table* t : tables)
+        for (const vk::Table* t : tables) {
             if (t && t->fb_auto && t->fb.p) s += t->fb.cap;
+            if (t && t->lead && t->lead->fb.p) s += t->lead->fb.cap;  // (built on first use too)
+        }
         return s;
     }
     vk::Table* table(int id) {
